@@ -114,6 +114,346 @@ void sparse_scatter_add(const Tensor& val, const Tensor& idx, const Tensor& out,
                             out.data_ptr<float>(), (float)scale, accumulate, cur_stream());
 }
 
+// ------------------------------------------------------------------------------ random-k / threshold
+void randk_gather(const Tensor& x, const Tensor& seg_off, const Tensor& out_off, const Tensor& seeds,
+                  const Tensor& vals, const c10::optional<Tensor>& resid) {
+  CHECK_F32(x);
+  CHECK_I64(seg_off);
+  CHECK_I64(out_off);
+  CHECK_I64(seeds);
+  CHECK_F32(vals);
+  const int n_seg = (int)seeds.numel();
+  TORCH_CHECK(seg_off.numel() == n_seg + 1 && out_off.numel() == n_seg + 1, "offset tables must be n_seg+1");
+  float* rp = nullptr;
+  if (resid.has_value()) {
+    CHECK_F32((*resid));
+    TORCH_CHECK(resid->data_ptr() == x.data_ptr(), "residual zeroing requires x to be the residual buffer");
+    rp = resid->data_ptr<float>();
+  }
+  DevGuard guard(x.device());
+  grace::randk_gather(x.data_ptr<float>(), n_seg, seg_off.data_ptr<int64_t>(), out_off.data_ptr<int64_t>(),
+                      seeds.data_ptr<int64_t>(), vals.numel(), vals.data_ptr<float>(), rp, cur_stream());
+}
+
+// vals: [n_ranks, rank_stride] fp32 view (row r = rank r payload, first K entries used)
+void randk_scatter(const Tensor& vals, int64_t rank_stride, int64_t n_ranks, int64_t K, const Tensor& seg_off,
+                   const Tensor& out_off, const Tensor& seeds, const Tensor& out, double scale, bool accumulate) {
+  CHECK_DEV(vals);
+  CHECK_DT(vals, at::kFloat);
+  CHECK_I64(seg_off);
+  CHECK_I64(out_off);
+  CHECK_I64(seeds);
+  CHECK_F32(out);
+  TORCH_CHECK(vals.storage().nbytes() >= (size_t)(vals.storage_offset() + (n_ranks - 1) * rank_stride + K) * 4,
+              "vals view too small");
+  DevGuard guard(out.device());
+  grace::randk_scatter(vals.data_ptr<float>(), rank_stride, (int)n_ranks, (int)seeds.numel(),
+                       seg_off.data_ptr<int64_t>(), out_off.data_ptr<int64_t>(), seeds.data_ptr<int64_t>(), K,
+                       out.data_ptr<float>(), (float)scale, accumulate, cur_stream());
+}
+
+int64_t threshold_compact(const Tensor& g, const c10::optional<Tensor>& r, int64_t mode, double beta, double gamma,
+                          double thr, const Tensor& out_val, const Tensor& out_idx, const Tensor& counter,
+                          const c10::optional<Tensor>& resid) {
+  CHECK_F32(g);
+  CHECK_F32(out_val);
+  CHECK_I32(out_idx);
+  CHECK_I32(counter);
+  TORCH_CHECK(out_val.numel() >= g.numel() && out_idx.numel() >= g.numel(), "capacity must be >= numel");
+  const float* rp = nullptr;
+  if (mode == 1) {
+    TORCH_CHECK(r.has_value(), "mode 1 needs r");
+    CHECK_F32((*r));
+    rp = r->data_ptr<float>();
+  }
+  float* wp = nullptr;
+  if (resid.has_value()) {
+    CHECK_F32((*resid));
+    wp = resid->data_ptr<float>();
+  }
+  DevGuard guard(g.device());
+  grace::threshold_compact(g.data_ptr<float>(), rp, (int)mode, (float)beta, (float)gamma, g.numel(), (float)thr,
+                           out_val.data_ptr<float>(), out_idx.data_ptr<int32_t>(), counter.data_ptr<int32_t>(), wp,
+                           cur_stream());
+  return 0;
+}
+
+// ------------------------------------------------------------------------------ rank-strided payload rows
+// `base` is a uint8 view whose row r starts at r*rank_stride; validate the furthest byte read.
+void check_rows(const Tensor& base, int64_t rank_stride, int64_t n_ranks, int64_t last_byte) {
+  CHECK_DEV(base);
+  CHECK_DT(base, at::kByte);
+  TORCH_CHECK(n_ranks >= 1, "n_ranks >= 1");
+  const int64_t need = base.storage_offset() + (n_ranks - 1) * rank_stride + last_byte;
+  TORCH_CHECK((int64_t)base.storage().nbytes() >= need, "payload rows out of bounds");
+}
+
+inline const float* opt_f32(const c10::optional<Tensor>& t) {
+  if (!t.has_value()) return nullptr;
+  CHECK_F32((*t));
+  return t->data_ptr<float>();
+}
+inline float* opt_f32_mut(const c10::optional<Tensor>& t) {
+  if (!t.has_value()) return nullptr;
+  CHECK_F32((*t));
+  return t->data_ptr<float>();
+}
+
+// ------------------------------------------------------------------------------ sign bits
+void sign_pack(const Tensor& g, const c10::optional<Tensor>& r, int64_t ef_mode, double beta, double gamma,
+               const c10::optional<Tensor>& mom, double mom_beta, bool mom_valid, const c10::optional<Tensor>& vT,
+               const c10::optional<Tensor>& vF, const c10::optional<Tensor>& resid, bool neg, const Tensor& words,
+               const Tensor& seg, const Tensor& cb, const Tensor& ce, const Tensor& seg_start,
+               const Tensor& word_off, int64_t n_words) {
+  CHECK_F32(g);
+  CHECK_DEV(words);
+  CHECK_CONTIG(words);
+  CHECK_DT(words, at::kLong);
+  CHECK_I64(seg_start);
+  CHECK_I64(word_off);
+  TORCH_CHECK(words.numel() >= n_words, "words too small");
+  if (ef_mode == 1) TORCH_CHECK(r.has_value(), "ef_mode 1 needs r");
+  if (resid.has_value()) TORCH_CHECK(vT.has_value() && vF.has_value(), "residual needs vT/vF");
+  auto ct = make_ct(seg, cb, ce);
+  DevGuard guard(g.device());
+  grace::sign_pack(ct, seg_start.data_ptr<int64_t>(), word_off.data_ptr<int64_t>(), g.data_ptr<float>(), opt_f32(r),
+                   (int)ef_mode, (float)beta, (float)gamma, opt_f32_mut(mom), (float)mom_beta, mom_valid ? 1 : 0,
+                   opt_f32(vT), opt_f32(vF), opt_f32_mut(resid), neg,
+                   reinterpret_cast<uint64_t*>(words.data_ptr<int64_t>()), cur_stream());
+}
+
+void sign_unpack(const Tensor& base, int64_t rank_stride, int64_t words_off, int64_t vals_off, int64_t n_ranks,
+                 bool vote, double scale, const Tensor& out, bool accumulate, const Tensor& seg, const Tensor& cb,
+                 const Tensor& ce, const Tensor& seg_start, const Tensor& word_off, int64_t nw) {
+  CHECK_F32(out);
+  CHECK_I64(seg_start);
+  CHECK_I64(word_off);
+  const int n_seg = (int)seg_start.numel() - 1;
+  check_rows(base, rank_stride, n_ranks, std::max(words_off + nw * 8, vote ? (int64_t)0 : vals_off + 8 * n_seg));
+  auto ct = make_ct(seg, cb, ce);
+  DevGuard guard(out.device());
+  grace::sign_unpack(ct, seg_start.data_ptr<int64_t>(), word_off.data_ptr<int64_t>(), base.data_ptr<uint8_t>(),
+                     rank_stride, words_off, vals_off, n_seg, (int)n_ranks, vote, (float)scale, out.data_ptr<float>(),
+                     accumulate, cur_stream());
+}
+
+// ------------------------------------------------------------------------------ quantizers
+void qsgd_quantize(const Tensor& x, const Tensor& norms, double s, int64_t seed, const Tensor& codes,
+                   const c10::optional<Tensor>& resid, const Tensor& seg, const Tensor& cb, const Tensor& ce) {
+  CHECK_F32(x);
+  CHECK_F32(norms);
+  CHECK_DEV(codes);
+  CHECK_CONTIG(codes);
+  TORCH_CHECK(codes.numel() >= x.numel(), "codes too small");
+  const int cb_ = (int)codes.element_size();
+  TORCH_CHECK(cb_ == 1 || cb_ == 2 || cb_ == 4, "codes must be int8/int16/int32");
+  auto ct = make_ct(seg, cb, ce);
+  DevGuard guard(x.device());
+  grace::qsgd_quantize(ct, x.data_ptr<float>(), norms.data_ptr<float>(), (float)s, (uint64_t)seed, codes.data_ptr(),
+                       cb_, opt_f32_mut(resid), cur_stream());
+}
+
+void qsgd_aggregate(const Tensor& base, int64_t rank_stride, int64_t codes_off, int64_t norms_off, int64_t code_bytes,
+                    int64_t n_ranks, double s, double scale, const Tensor& out, bool accumulate, const Tensor& seg,
+                    const Tensor& cb, const Tensor& ce, int64_t n_seg) {
+  CHECK_F32(out);
+  check_rows(base, rank_stride, n_ranks, std::max(codes_off + out.numel() * code_bytes, norms_off + 4 * n_seg));
+  auto ct = make_ct(seg, cb, ce);
+  DevGuard guard(out.device());
+  grace::qsgd_aggregate(ct, base.data_ptr<uint8_t>(), rank_stride, codes_off, norms_off, (int)code_bytes,
+                        (int)n_ranks, (float)s, (float)scale, out.data_ptr<float>(), accumulate, cur_stream());
+}
+
+void tern_quantize(const Tensor& x, const Tensor& clips, const Tensor& scal, int64_t seed, const Tensor& words,
+                   const c10::optional<Tensor>& resid, const Tensor& seg, const Tensor& cb, const Tensor& ce,
+                   const Tensor& seg_start, const Tensor& word_off, int64_t n_words) {
+  CHECK_F32(x);
+  CHECK_F32(clips);
+  CHECK_F32(scal);
+  CHECK_DEV(words);
+  CHECK_DT(words, at::kLong);
+  CHECK_I64(seg_start);
+  CHECK_I64(word_off);
+  TORCH_CHECK(words.numel() >= 2 * n_words, "words too small");
+  auto ct = make_ct(seg, cb, ce);
+  DevGuard guard(x.device());
+  grace::tern_quantize(ct, seg_start.data_ptr<int64_t>(), word_off.data_ptr<int64_t>(), x.data_ptr<float>(),
+                       clips.data_ptr<float>(), scal.data_ptr<float>(), (uint64_t)seed,
+                       reinterpret_cast<uint64_t*>(words.data_ptr<int64_t>()), opt_f32_mut(resid), cur_stream());
+}
+
+void tern_aggregate(const Tensor& base, int64_t rank_stride, int64_t words_off, int64_t scal_off, int64_t n_ranks,
+                    double scale, const Tensor& out, bool accumulate, const Tensor& seg, const Tensor& cb,
+                    const Tensor& ce, const Tensor& seg_start, const Tensor& word_off, int64_t nw) {
+  CHECK_F32(out);
+  const int64_t n_seg = seg_start.numel() - 1;
+  check_rows(base, rank_stride, n_ranks, std::max(words_off + 16 * nw, scal_off + 4 * n_seg));
+  auto ct = make_ct(seg, cb, ce);
+  DevGuard guard(out.device());
+  grace::tern_aggregate(ct, seg_start.data_ptr<int64_t>(), word_off.data_ptr<int64_t>(), base.data_ptr<uint8_t>(),
+                        rank_stride, words_off, scal_off, (int)n_ranks, (float)scale, out.data_ptr<float>(), accumulate,
+                        cur_stream());
+}
+
+void natural_encode(const Tensor& x, int64_t seed, const Tensor& codes, const c10::optional<Tensor>& resid) {
+  CHECK_F32(x);
+  CHECK_DEV(codes);
+  CHECK_DT(codes, at::kByte);
+  TORCH_CHECK(codes.numel() >= x.numel(), "codes too small");
+  DevGuard guard(x.device());
+  grace::natural_encode(x.data_ptr<float>(), x.numel(), (uint64_t)seed, codes.data_ptr<uint8_t>(), opt_f32_mut(resid),
+                        cur_stream());
+}
+
+void natural_aggregate(const Tensor& base, int64_t rank_stride, int64_t n_ranks, double scale, const Tensor& out,
+                       bool accumulate) {
+  CHECK_F32(out);
+  check_rows(base, rank_stride, n_ranks, out.numel());
+  DevGuard guard(out.device());
+  grace::natural_aggregate(base.data_ptr<uint8_t>(), rank_stride, out.numel(), (int)n_ranks, (float)scale,
+                           out.data_ptr<float>(), accumulate, cur_stream());
+}
+
+void u8_encode(const Tensor& x, const Tensor& scales, const Tensor& codes, const c10::optional<Tensor>& resid,
+               const Tensor& seg, const Tensor& cb, const Tensor& ce) {
+  CHECK_F32(x);
+  CHECK_F32(scales);
+  CHECK_DEV(codes);
+  CHECK_DT(codes, at::kChar);
+  TORCH_CHECK(codes.numel() >= x.numel(), "codes too small");
+  auto ct = make_ct(seg, cb, ce);
+  DevGuard guard(x.device());
+  grace::u8_encode(ct, x.data_ptr<float>(), scales.data_ptr<float>(), codes.data_ptr<int8_t>(), opt_f32_mut(resid),
+                   cur_stream());
+}
+
+void u8_aggregate(const Tensor& base, int64_t rank_stride, int64_t codes_off, int64_t scal_off, int64_t n_ranks,
+                  double scale, const Tensor& out, bool accumulate, const Tensor& seg, const Tensor& cb,
+                  const Tensor& ce, int64_t n_seg) {
+  CHECK_F32(out);
+  check_rows(base, rank_stride, n_ranks, std::max(codes_off + out.numel(), scal_off + 4 * n_seg));
+  auto ct = make_ct(seg, cb, ce);
+  DevGuard guard(out.device());
+  grace::u8_aggregate(ct, base.data_ptr<uint8_t>(), rank_stride, codes_off, scal_off, (int)n_ranks, (float)scale,
+                      out.data_ptr<float>(), accumulate, cur_stream());
+}
+
+// ------------------------------------------------------------------------------ DGC
+void dgc_sample(const Tensor& x, const Tensor& seg_off, const Tensor& samp_off, int64_t seed, const Tensor& samples) {
+  CHECK_F32(x);
+  CHECK_I64(seg_off);
+  CHECK_I64(samp_off);
+  CHECK_F32(samples);
+  TORCH_CHECK(seg_off.numel() == samp_off.numel(), "offset tables");
+  DevGuard guard(x.device());
+  grace::dgc_sample(x.data_ptr<float>(), (int)seg_off.numel() - 1, seg_off.data_ptr<int64_t>(),
+                    samp_off.data_ptr<int64_t>(), samples.numel(), (uint64_t)seed, samples.data_ptr<float>(),
+                    cur_stream());
+}
+
+void dgc_refine(const Tensor& x, const Tensor& state, const Tensor& target, int64_t max_iters, const Tensor& thr,
+                const Tensor& count, const Tensor& done, const Tensor& seg, const Tensor& cb, const Tensor& ce) {
+  CHECK_F32(x);
+  CHECK_I32(state);
+  CHECK_F32(target);
+  CHECK_F32(thr);
+  CHECK_I32(count);
+  CHECK_I32(done);
+  const int n_seg = (int)target.numel();
+  TORCH_CHECK(thr.numel() == n_seg && count.numel() == n_seg && done.numel() == n_seg && state.numel() >= 2 * n_seg,
+              "per-segment tables");
+  auto ct = make_ct(seg, cb, ce);
+  DevGuard guard(x.device());
+  grace::dgc_refine(ct, n_seg, x.data_ptr<float>(), reinterpret_cast<const grace::TopkState*>(state.data_ptr<int32_t>()),
+                    target.data_ptr<float>(), (int)max_iters, thr.data_ptr<float>(), count.data_ptr<int32_t>(),
+                    done.data_ptr<int32_t>(), cur_stream());
+}
+
+void dgc_compact(const Tensor& x, const Tensor& thr, const Tensor& out_val, const Tensor& out_idx,
+                 const Tensor& counter, const Tensor& seg, const Tensor& cb, const Tensor& ce) {
+  CHECK_F32(x);
+  CHECK_F32(thr);
+  CHECK_F32(out_val);
+  CHECK_I32(out_idx);
+  CHECK_I32(counter);
+  TORCH_CHECK(out_val.numel() >= x.numel() && out_idx.numel() >= x.numel(), "capacity");
+  auto ct = make_ct(seg, cb, ce);
+  DevGuard guard(x.device());
+  grace::dgc_compact(ct, x.data_ptr<float>(), thr.data_ptr<float>(), out_val.data_ptr<float>(),
+                     out_idx.data_ptr<int32_t>(), counter.data_ptr<int32_t>(), cur_stream());
+}
+
+// ------------------------------------------------------------------------------ PowerSGD
+void powersgd_mq(const Tensor& x, const Tensor& small, const Tensor& out, const Tensor& mats, const Tensor& tiles,
+                 int64_t mode) {
+  CHECK_F32(x);
+  CHECK_F32(small);
+  CHECK_F32(out);
+  CHECK_I64(mats);
+  CHECK_I32(tiles);
+  DevGuard guard(x.device());
+  grace::powersgd_mq(x.data_ptr<float>(), small.data_ptr<float>(), out.data_ptr<float>(), out.numel(),
+                     mats.data_ptr<int64_t>(), tiles.data_ptr<int32_t>(), (int)(tiles.numel() / 3), (int)mode,
+                     cur_stream());
+}
+
+void gram_schmidt(const Tensor& buf, const Tensor& mats, int64_t which, int64_t n_mat) {
+  CHECK_F32(buf);
+  CHECK_I64(mats);
+  TORCH_CHECK(mats.numel() >= 6 * n_mat, "mats table");
+  DevGuard guard(buf.device());
+  grace::gram_schmidt(buf.data_ptr<float>(), mats.data_ptr<int64_t>(), (int)n_mat, (int)which, cur_stream());
+}
+
+void powersgd_pqt(const Tensor& P, const Tensor& Q, const Tensor& out, const Tensor& mats, const Tensor& tiles) {
+  CHECK_F32(P);
+  CHECK_F32(Q);
+  CHECK_F32(out);
+  CHECK_I64(mats);
+  CHECK_I32(tiles);
+  DevGuard guard(out.device());
+  grace::powersgd_pqt(P.data_ptr<float>(), Q.data_ptr<float>(), out.data_ptr<float>(), mats.data_ptr<int64_t>(),
+                      tiles.data_ptr<int32_t>(), (int)(tiles.numel() / 3), cur_stream());
+}
+
+void philox_normal(const Tensor& out, int64_t seed) {
+  CHECK_F32(out);
+  DevGuard guard(out.device());
+  grace::philox_normal(out.data_ptr<float>(), out.numel(), (uint64_t)seed, cur_stream());
+}
+
+// ------------------------------------------------------------------------------ segment stats
+void segment_stats(const Tensor& x, const c10::optional<Tensor>& r, int64_t mode, double beta, double gamma,
+                   const c10::optional<Tensor>& xout, const Tensor& seg, const Tensor& cb, const Tensor& ce,
+                   const Tensor& seg_chunk_begin, const Tensor& partials, const Tensor& stats) {
+  CHECK_F32(x);
+  const float* rp = nullptr;
+  if (mode == 1) {
+    TORCH_CHECK(r.has_value(), "mode 1 needs r");
+    CHECK_F32((*r));
+    TORCH_CHECK(r->numel() == x.numel(), "r size");
+    rp = r->data_ptr<float>();
+  }
+  float* xp = nullptr;
+  if (xout.has_value()) {
+    CHECK_F32((*xout));
+    TORCH_CHECK(xout->numel() == x.numel(), "xout size");
+    xp = xout->data_ptr<float>();
+  }
+  CHECK_I32(seg_chunk_begin);
+  CHECK_DEV(partials);
+  CHECK_DT(partials, at::kDouble);
+  CHECK_F32(stats);
+  const int n_seg = (int)seg_chunk_begin.numel() - 1;
+  TORCH_CHECK(stats.numel() >= (int64_t)n_seg * grace::kSegStats, "stats too small");
+  TORCH_CHECK(partials.numel() >= seg.numel() * grace::kSegStats, "partials too small");
+  auto ct = make_ct(seg, cb, ce);
+  DevGuard guard(x.device());
+  grace::segment_stats(ct, n_seg, seg_chunk_begin.data_ptr<int32_t>(), x.data_ptr<float>(), rp, (int)mode,
+                       (float)beta, (float)gamma, xp, partials.data_ptr<double>(), stats.data_ptr<float>(),
+                       cur_stream());
+}
+
 // ------------------------------------------------------------------------------ elementwise
 void axpby(const Tensor& x, const Tensor& y, const Tensor& out, double a, double b) {
   CHECK_F32(x);
@@ -144,6 +484,27 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("topk_select", &topk_select);
   m.def("topk_compact", &topk_compact);
   m.def("sparse_scatter_add", &sparse_scatter_add);
+  m.def("segment_stats", &segment_stats);
+  m.def("randk_gather", &randk_gather);
+  m.def("randk_scatter", &randk_scatter);
+  m.def("threshold_compact", &threshold_compact);
+  m.def("sign_pack", &sign_pack);
+  m.def("sign_unpack", &sign_unpack);
+  m.def("qsgd_quantize", &qsgd_quantize);
+  m.def("qsgd_aggregate", &qsgd_aggregate);
+  m.def("tern_quantize", &tern_quantize);
+  m.def("tern_aggregate", &tern_aggregate);
+  m.def("natural_encode", &natural_encode);
+  m.def("natural_aggregate", &natural_aggregate);
+  m.def("u8_encode", &u8_encode);
+  m.def("u8_aggregate", &u8_aggregate);
+  m.def("dgc_sample", &dgc_sample);
+  m.def("dgc_refine", &dgc_refine);
+  m.def("dgc_compact", &dgc_compact);
+  m.def("powersgd_mq", &powersgd_mq);
+  m.def("gram_schmidt", &gram_schmidt);
+  m.def("powersgd_pqt", &powersgd_pqt);
+  m.def("philox_normal", &philox_normal);
   m.def("axpby", &axpby);
   m.def("scale_", &scale_);
 }

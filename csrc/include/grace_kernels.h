@@ -25,6 +25,68 @@ void topk_compact_bucket(const ChunkTable& ct, int n_seg, const float* x, const 
 void sparse_scatter_add(const float* val, const int32_t* idx, int64_t K, float* out, float scale,
                         bool accumulate, hipStream_t stream);
 
+// ---------------------------------------------------------------- segstats.hip
+// per segment: [sum, sumsq, max|x|, sum|x|, sum(x<0), count(x<0)]
+constexpr int kSegStats = 6;
+// g, r, mode, beta, gamma, xout: optional fused error-feedback compensate (see ef.hip)
+void segment_stats(const ChunkTable& ct, int n_seg, const int32_t* seg_chunk_begin, const float* g,
+                   const float* r, int mode, float beta, float gamma, float* xout, double* partials, float* stats,
+                   hipStream_t stream);
+
+// ---------------------------------------------------------------- sparsify.hip
+void randk_gather(const float* x, int n_seg, const int64_t* seg_off, const int64_t* out_off,
+                  const int64_t* seeds, int64_t K, float* vals, float* resid, hipStream_t stream);
+void randk_scatter(const float* vals, int64_t rank_stride, int n_ranks, int n_seg, const int64_t* seg_off,
+                   const int64_t* out_off, const int64_t* seeds, int64_t K, float* out, float scale,
+                   bool accumulate, hipStream_t stream);
+void threshold_compact(const float* g, const float* r, int mode, float beta, float gamma, int64_t n, float thr,
+                       float* out_val, int32_t* out_idx, int32_t* counter, float* resid, hipStream_t stream);
+
+// ---------------------------------------------------------------- signbits.hip
+void sign_pack(const ChunkTable& ct, const int64_t* seg_start, const int64_t* word_off, const float* g,
+               const float* r, int ef_mode, float beta, float gamma, float* mom, float mom_beta, int mom_valid,
+               const float* vT, const float* vF, float* resid, bool neg, uint64_t* words, hipStream_t stream);
+void sign_unpack(const ChunkTable& ct, const int64_t* seg_start, const int64_t* word_off, const uint8_t* base,
+                 int64_t rank_stride, int64_t words_off_bytes, int64_t vals_off_bytes, int n_seg, int n_ranks,
+                 bool vote, float scale, float* out, bool accumulate, hipStream_t stream);
+
+// ---------------------------------------------------------------- quant.hip
+void qsgd_quantize(const ChunkTable& ct, const float* x, const float* norms, float s, uint64_t seed, void* codes,
+                   int code_bytes, float* resid, hipStream_t stream);
+void qsgd_aggregate(const ChunkTable& ct, const uint8_t* base, int64_t rank_stride, int64_t codes_off,
+                    int64_t norms_off, int code_bytes, int n_ranks, float s, float scale, float* out, bool accumulate,
+                    hipStream_t stream);
+void tern_quantize(const ChunkTable& ct, const int64_t* seg_start, const int64_t* word_off, const float* x,
+                   const float* clips, const float* scal, uint64_t seed, uint64_t* words, float* resid,
+                   hipStream_t stream);
+void tern_aggregate(const ChunkTable& ct, const int64_t* seg_start, const int64_t* word_off, const uint8_t* base,
+                    int64_t rank_stride, int64_t words_off, int64_t scal_off, int n_ranks, float scale, float* out,
+                    bool accumulate, hipStream_t stream);
+void natural_encode(const float* x, int64_t n, uint64_t seed, uint8_t* codes, float* resid, hipStream_t stream);
+void natural_aggregate(const uint8_t* base, int64_t rank_stride, int64_t n, int n_ranks, float scale, float* out,
+                       bool accumulate, hipStream_t stream);
+void u8_encode(const ChunkTable& ct, const float* x, const float* scales, int8_t* codes, float* resid,
+               hipStream_t stream);
+void u8_aggregate(const ChunkTable& ct, const uint8_t* base, int64_t rank_stride, int64_t codes_off, int64_t scal_off,
+                  int n_ranks, float scale, float* out, bool accumulate, hipStream_t stream);
+
+// ---------------------------------------------------------------- dgc.hip
+void dgc_sample(const float* x, int n_seg, const int64_t* seg_off, const int64_t* samp_off, int64_t n_samples,
+                uint64_t seed, float* samples, hipStream_t stream);
+void dgc_refine(const ChunkTable& ct, int n_seg, const float* x, const TopkState* st, const float* target,
+                int max_iters, float* thr, int32_t* count, int32_t* done, hipStream_t stream);
+void dgc_compact(const ChunkTable& ct, const float* x, const float* thr, float* out_val, int32_t* out_idx,
+                 int32_t* counter, hipStream_t stream);
+
+// ---------------------------------------------------------------- powersgd.hip
+// mats: int64 [n_mat][6] = (x_off, n, m, r, p_off, q_off); tiles: int32 [n_tiles][3]
+void powersgd_mq(const float* x, const float* small, float* out, int64_t out_len, const int64_t* mats,
+                 const int32_t* tiles, int n_tiles, int mode, hipStream_t stream);
+void gram_schmidt(float* buf, const int64_t* mats, int n_mat, int which, hipStream_t stream);
+void powersgd_pqt(const float* P, const float* Q, float* out, const int64_t* mats, const int32_t* tiles, int n_tiles,
+                  hipStream_t stream);
+void philox_normal(float* out, int64_t n, uint64_t seed, hipStream_t stream);
+
 // ---------------------------------------------------------------- ef.hip (elementwise)
 void axpby(const float* x, const float* y, float* out, int64_t n, float a, float b, hipStream_t stream);
 void scale_inplace(float* x, int64_t n, float s, hipStream_t stream);

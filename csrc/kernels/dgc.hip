@@ -1,0 +1,169 @@
+// Deep Gradient Compression threshold selection on the device (CDNA4).
+//
+// Reference per tensor (/root/reference/grace_dl/dist/compressor/dgc.py:12-43): uniform 1%
+// sample -> k'-th largest |sample| -> up to 10 host-side refinements (x1.3 / x0.7) each with a
+// full mask + sum -> torch.where.  That is ~30 launches and up to 10 host syncs per tensor.
+//
+// Here, for all segments of a bucket at once:
+//   dgc_sample   : Philox-uniform sample positions per segment, |x| gathered (1 thread/sample)
+//   (top-k of the samples reuses the segmented radix select of topk.hip -> exact k'-th key)
+//   dgc_count    : per-chunk count of |x| >= thr[seg] (segments already converged exit early),
+//                  workgroup-reduced, one atomic per workgroup
+//   dgc_adjust   : per segment, the reference's rule; marks converged segments done
+//   dgc_compact  : ballot compaction of |x| >= thr[seg] into (value, flat index)
+// The only host sync left is reading the final element count (payload size is data dependent).
+#include "grace_common.h"
+#include "grace_kernels.h"
+
+namespace grace {
+namespace {
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ int find_seg64(const int64_t* __restrict__ off, int n_seg, int64_t j) {
+  int lo = 0, hi = n_seg;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (off[mid] <= j)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(kBlock) void dgc_sample_kernel(const float* __restrict__ x, int n_seg,
+                                                            const int64_t* __restrict__ seg_off,
+                                                            const int64_t* __restrict__ samp_off, uint64_t seed,
+                                                            float* __restrict__ samples) {
+  const int64_t S = samp_off[n_seg];
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < S; j += stride) {
+    const int s = find_seg64(samp_off, n_seg, j);
+    const int64_t n = seg_off[s + 1] - seg_off[s];
+    const uint4 r = Philox::gen(seed, (uint64_t)j);
+    // 48 random bits -> uniform position in [0, n)
+    const uint64_t u = ((uint64_t)r.x << 16) ^ (uint64_t)(r.y >> 16);
+    const int64_t pos = (int64_t)__umul64hi(u << 16, (uint64_t)n);  // floor(u * n / 2^48)
+    samples[j] = fabsf(x[seg_off[s] + (pos < n ? pos : n - 1)]);
+  }
+}
+
+// thr[s] <- float(prefix of the k'-th largest sample key); count[s] = 0; done[s] = 0
+__global__ void dgc_init_kernel(int n_seg, const TopkState* __restrict__ st, float* __restrict__ thr,
+                                int32_t* __restrict__ count, int32_t* __restrict__ done) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_seg) return;
+  thr[s] = __uint_as_float(st[s].prefix);
+  count[s] = 0;
+  done[s] = 0;
+}
+
+__global__ __launch_bounds__(kBlock) void dgc_count_kernel(ChunkTable ct, const float* __restrict__ x,
+                                                           const float* __restrict__ thr,
+                                                           const int32_t* __restrict__ done,
+                                                           int32_t* __restrict__ count) {
+  const int c = blockIdx.x;
+  const int s = ct.seg[c];
+  if (done[s]) return;
+  const int64_t b = ct.begin[c], e = ct.end[c];
+  const float t = thr[s];
+  unsigned cnt = 0;
+  for (int64_t i = b + threadIdx.x; i < e; i += kBlock) cnt += fabsf(x[i]) >= t ? 1u : 0u;
+  cnt = wave_sum_u32(cnt);
+  __shared__ unsigned red[kBlock / kWave];
+  if (lane_id() == 0) red[wave_id()] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned tot = 0;
+    for (int w = 0; w < kBlock / kWave; ++w) tot += red[w];
+    if (tot) atomicAdd(&count[s], (int32_t)tot);
+  }
+}
+
+__global__ void dgc_adjust_kernel(int n_seg, const float* __restrict__ target, float* __restrict__ thr,
+                                  int32_t* __restrict__ count, int32_t* __restrict__ done) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_seg || done[s]) return;
+  const float sel = (float)count[s];
+  if (sel > 1.3f * target[s]) {
+    thr[s] *= 1.3f;
+  } else if (sel < 0.7f * target[s]) {
+    thr[s] *= 0.7f;
+  } else {
+    done[s] = 1;
+    return;
+  }
+  count[s] = 0;  // recounted by the next dgc_count
+}
+
+__device__ __forceinline__ unsigned long long lanemask_lt() {
+  const int l = lane_id();
+  return (l == 0) ? 0ull : (~0ull >> (64 - l));
+}
+
+__global__ __launch_bounds__(kBlock) void dgc_compact_kernel(ChunkTable ct, const float* __restrict__ x,
+                                                             const float* __restrict__ thr,
+                                                             float* __restrict__ out_val,
+                                                             int32_t* __restrict__ out_idx,
+                                                             int32_t* __restrict__ counter) {
+  const int c = blockIdx.x;
+  const int s = ct.seg[c];
+  const int64_t b = ct.begin[c], e = ct.end[c];
+  const float t = thr[s];
+  const int64_t steps = (e - b + kBlock - 1) / kBlock;
+  for (int64_t k = 0; k < steps; ++k) {
+    const int64_t i = b + k * kBlock + threadIdx.x;
+    const bool valid = i < e;
+    const float v = valid ? x[i] : 0.f;
+    const bool take = valid && fabsf(v) >= t;
+    const unsigned long long m = __ballot(take);
+    if (m) {
+      int32_t base = 0;
+      const int leader = __ffsll((long long)m) - 1;
+      if (lane_id() == leader) base = atomicAdd(counter, __popcll(m));
+      base = __shfl(base, leader, kWave);
+      if (take) {
+        const int32_t p = base + __popcll(m & lanemask_lt());
+        out_val[p] = v;
+        out_idx[p] = (int32_t)i;
+      }
+    }
+  }
+}
+
+inline int grid_for(int64_t n) {
+  int64_t b = (n + kBlock - 1) / kBlock;
+  if (b > 2048) b = 2048;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace
+
+void dgc_sample(const float* x, int n_seg, const int64_t* seg_off, const int64_t* samp_off, int64_t n_samples,
+                uint64_t seed, float* samples, hipStream_t stream) {
+  if (n_samples <= 0) return;
+  dgc_sample_kernel<<<grid_for(n_samples), kBlock, 0, stream>>>(x, n_seg, seg_off, samp_off, seed, samples);
+}
+
+void dgc_refine(const ChunkTable& ct, int n_seg, const float* x, const TopkState* st, const float* target,
+                int max_iters, float* thr, int32_t* count, int32_t* done, hipStream_t stream) {
+  const int g = (n_seg + 255) / 256;
+  dgc_init_kernel<<<g, 256, 0, stream>>>(n_seg, st, thr, count, done);
+  dgc_count_kernel<<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, thr, done, count);
+  for (int it = 0; it < max_iters; ++it) {
+    dgc_adjust_kernel<<<g, 256, 0, stream>>>(n_seg, target, thr, count, done);
+    // the count after the last adjustment would be unused (the reference computes and drops it)
+    if (it + 1 < max_iters) dgc_count_kernel<<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, thr, done, count);
+  }
+}
+
+void dgc_compact(const ChunkTable& ct, const float* x, const float* thr, float* out_val, int32_t* out_idx,
+                 int32_t* counter, hipStream_t stream) {
+  GRACE_HIP_CHECK(hipMemsetAsync(counter, 0, sizeof(int32_t), stream));
+  if (ct.n_chunks == 0) return;
+  dgc_compact_kernel<<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, thr, out_val, out_idx, counter);
+}
+
+}  // namespace grace

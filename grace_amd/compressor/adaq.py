@@ -1,0 +1,88 @@
+"""AdaComp-style two-sided quantization (Dryden et al., MLHPC 2016) -- the TF-only ``Adaq``.
+
+Reference: /root/reference/grace_dl/tensorflow/compressor/adaq.py:6-93 -- for the positive and
+the negative entries separately: estimate a threshold from a 1% sample so that about
+``ratio`` of that side's entries pass, refine it (x1.25 if > 1.25*target, else x0.9, while the
+count is outside [0.8, 1.25]*target, at most 20 times; if nothing passes lower it by 0.8),
+then send only the MEAN of the selected values and their indices:
+``[plus_mean, minus_mean, n_plus, plus_idx..., minus_idx...]`` as one int32 tensor.
+Decompress writes plus_mean / minus_mean at the indices.
+
+Here: the same algorithm per segment, implemented with PyTorch-ROCm ops (no dedicated HIP
+kernel yet -- it shares the threshold-refinement shape of DGC, csrc/kernels/dgc.hip, which is
+the planned port); payload [means fp32 (+,- per segment) | counts int32 (+,- per segment) |
+indices int32].  A side with no
+entries sends mean 0 and no index (the reference computes the mean of an empty set -> NaN).
+Variable-size payload (Allgather).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ..ops import topk as K
+from ._base import BucketCompressor
+
+
+def _side(vals_abs: torch.Tensor, ratio: float, gen) -> torch.Tensor:
+    """Boolean selection over one side's |values| (reference quan(), adaq.py:16-51)."""
+    n = vals_abs.numel()
+    if n == 0:
+        return torch.zeros(0, dtype=torch.bool, device=vals_abs.device)
+    ns = max(1, math.ceil(n * 0.01))
+    k = max(1, math.ceil(n * 0.01 * ratio))
+    pos = (torch.rand(ns, generator=gen, device=vals_abs.device) * n).long().clamp_max(n - 1)
+    thr = torch.topk(vals_abs[pos], min(k, ns)).values.min()
+    target = math.ceil(n * ratio)
+    mask = vals_abs > thr
+    sel = int(mask.sum())
+    it = 0
+    while (sel > 1.25 * target or sel < 0.8 * target) and it < 20:
+        thr = thr * 1.25 if sel > 1.25 * target else thr * 0.9
+        mask = vals_abs >= thr
+        sel = int(mask.sum())
+        it += 1
+    if sel < 1:
+        thr = thr * 0.8
+    return vals_abs > thr
+
+
+class AdaqCompressor(BucketCompressor):
+    def __init__(self, compress_ratio: float = 0.01):
+        super().__init__(tensors_size_are_same=False)
+        self.compress_ratio = compress_ratio
+
+    def compress(self, tensor, name):
+        ctx = self.ctx(tensor, name)
+        x = self.flat(tensor)
+        lay = ctx.layout
+        gen = torch.Generator(device=x.device)
+        gen.manual_seed(self.next_seed(name) & 0x7FFFFFFFFFFFFFFF)
+        means = torch.zeros(2 * lay.n_seg, dtype=torch.float32, device=x.device)
+        counts = torch.zeros(2 * lay.n_seg, dtype=torch.int32)
+        idx_all = []
+        for i, o, n in lay.segments():
+            seg = x[o:o + n]
+            for side in (0, 1):  # 0: positive entries, 1: negative entries
+                (sidx,) = torch.where(seg > 0 if side == 0 else seg < 0)
+                chosen = sidx[_side(seg[sidx].abs(), self.compress_ratio, gen)]
+                if chosen.numel():
+                    means[2 * i + side] = seg[chosen].mean()
+                counts[2 * i + side] = chosen.numel()
+                idx_all.append((chosen + o).to(torch.int32))
+        idx = torch.cat(idx_all) if idx_all else torch.empty(0, dtype=torch.int32, device=x.device)
+        m, cnt, ix = self.payload(x.device, [(torch.float32, (2 * lay.n_seg,)), (torch.int32, (2 * lay.n_seg,)),
+                                             (torch.int32, (idx.numel(),))])
+        m.copy_(means)
+        cnt.copy_(counts)
+        ix.copy_(idx)
+        return [m, cnt, ix], ctx
+
+    def decompress_aggregate_impl(self, per_rank, ctx, n_ranks, scale):
+        out = torch.zeros(ctx.layout.total, dtype=torch.float32, device=per_rank[0][0].device)
+        for means, counts, idx in per_rank:
+            reps = counts.to(device=means.device, dtype=torch.int64)
+            v = torch.repeat_interleave(means, reps)  # [plus_0.., minus_0.., plus_1.., ...]
+            K.scatter_add(v, idx, out, scale, accumulate=True)
+        return self.finish(out, ctx)

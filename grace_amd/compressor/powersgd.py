@@ -1,0 +1,113 @@
+"""PowerSGD -- rank-r power-iteration compression (Vogels et al., NeurIPS 2019).
+
+Reference: /root/reference/grace_dl/dist/compressor/powersgd.py:7-65 -- for every >=2-D tensor
+M (n x m): Q (m x r) ~ N(0,1) orthogonalised, P = M Q, all_reduce(P)/W, orthogonalise(P),
+Q = M^T P, all_reduce(Q)/W, decompress P Q^T; 1-D tensors are sent uncompressed; the payload of
+matrices is empty (all communication happens inside compress).
+
+Fixes / design (survey 2.14 #4, #5, #7): the real world size divides P and Q (the reference's
+default world_size=1 makes the result W x too large); Q is drawn from a seed shared by all
+ranks (name, step) so every rank multiplies by the SAME Q; warm start (reuse last Q, the
+paper's recipe) is available as ``warm_start=True``.  For a flat bucket all matrices' P live in
+ONE buffer and all Q in another, so a whole bucket costs exactly two all-reduces; the 1-D
+segments travel through the communicator (Allreduce).  PowerSGD is only meaningful with the
+Allreduce communicator (Allgather would silently zero matrices in the reference).
+
+MI355X kernels (csrc/kernels/powersgd.hip): P = M Q and Q = M^T P as batched tall-skinny
+fp32 MFMA GEMMs (v_mfma_f32_32x32x2_f32 / 16x16x4, all matrices of the bucket in ONE launch
+each), batched LDS-resident Gram-Schmidt (one workgroup per matrix), and decompress
+P Q^T fused with the residual update.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import List, Tuple
+
+import torch
+
+from ..ops import powersgd as PS
+from ..ops.randomk import fnv1a64
+from ._base import BucketCompressor, Ctx
+
+
+class PowerSGDCompressor(BucketCompressor):
+    allreduce_compatible = True
+    _state_attrs = ("steps", "q_memory")
+
+    def __init__(self, rank: int = 1, use_memory: bool = False, world_size: int | None = None,
+                 warm_start: bool | None = None):
+        super().__init__()
+        self.rank_r = int(rank)
+        self.warm_start = bool(use_memory if warm_start is None else warm_start)
+        self.world_size = world_size
+        self.q_memory = {}
+        self.comm = None
+
+    def bind_comm(self, comm):
+        super().bind_comm(comm)
+        if self.world_size is None:
+            self.world_size = comm.world_size
+
+    def _plan(self, ctx: Ctx) -> PS.Plan:
+        return PS.plan_for(ctx.layout, self.rank_r)
+
+    def compress(self, tensor, name):
+        ctx = self.ctx(tensor, name)
+        plan = self._plan(ctx)
+        if plan.n_mat == 0:  # no matrix: reference passes 1-D tensors through
+            ctx.extra["plan"] = plan
+            return [self.flat(tensor)], ctx
+        x = self.flat(tensor)
+        W = self.world_size or 1
+        step = self.steps.get(name, 0)
+        self.steps[name] = step + 1
+        q = self.q_memory.get(name) if self.warm_start else None
+        if q is None or q.numel() != plan.q_total:
+            seed = (fnv1a64(name.encode()) ^ (0x9E3779B97F4A7C15 * (step + 1))) & 0xFFFFFFFFFFFFFFFF
+            q = PS.randn_shared(plan.q_total, seed, x.device)
+            PS.orthogonalize(q, plan, which="q")
+        p = PS.mq(x, q, plan)  # P = M Q for every matrix (one launch)
+        if self.comm is not None and W > 1:
+            self.comm.all_reduce(p)
+        if W > 1:
+            p.div_(W)
+        PS.orthogonalize(p, plan, which="p")
+        q = PS.mtp(x, p, plan)  # Q = M^T P
+        if self.comm is not None and W > 1:
+            self.comm.all_reduce(q)
+        if W > 1:
+            q.div_(W)
+        if self.warm_start:
+            self.q_memory[name] = q
+        ctx.extra.update(plan=plan, p=p, q=q)
+        vec = PS.gather_vectors(x, plan)  # 1-D segments, sent through the communicator
+        return ([vec] if vec.numel() else []), ctx
+
+    def _decompress(self, tensors, ctx, vec_scale: float):
+        plan = ctx.extra["plan"]
+        dev = tensors[0].device if tensors else ctx.extra["p"].device
+        if plan.n_mat == 0:
+            (v,) = tensors
+            out = v * vec_scale if vec_scale != 1.0 else v
+            return self.finish(out.reshape(-1), ctx)
+        out = torch.empty(ctx.layout.total, dtype=torch.float32, device=dev)
+        PS.pqt(ctx.extra["p"], ctx.extra["q"], plan, out)
+        if tensors:
+            PS.scatter_vectors(tensors[0], plan, out, vec_scale)
+        return self.finish(out, ctx)
+
+    def decompress(self, tensors, ctx):
+        return self._decompress(tensors, ctx, 1.0)
+
+    def decompress_reduced(self, tensors, ctx, world_size):
+        return self._decompress(tensors, ctx, 1.0 / world_size if self.average else 1.0)
+
+    def decompress_aggregate(self, per_rank, ctx, world_size):
+        # Allgather/Broadcast: matrices are already averaged inside compress; sum the 1-D parts
+        if not per_rank[0]:
+            return self._decompress([], ctx, 1.0)
+        vec = per_rank[0][0].clone()
+        for p in per_rank[1:]:
+            vec.add_(p[0])
+        return self._decompress([vec], ctx, 1.0 / world_size if self.average else 1.0)

@@ -1,0 +1,103 @@
+"""QSGD -- stochastic uniform quantization to s levels (Alistarh et al., arXiv 1610.02132).
+
+Reference: /root/reference/grace_dl/dist/compressor/qsgd.py:6-38 -- norm = ||x||_2,
+l = s/norm*|x|, stochastic rounding, q = sign*level stored int8 (s < 128) else fp16; payload
+(q, norm); decompress norm/s*q.
+
+MI355X (csrc/kernels/quant.hip): norms of every segment of a bucket from one statistics pass
+(fused with the residual compensate when paired with ResidualMemory), then one Philox
+quantize pass that also writes the residual; int16 instead of the reference's lossy fp16 for
+s >= 128 (survey 2.14 #12).  Aggregation decodes all W ranks in one pass.
+
+Allreduce (BASELINE "QSGD 8-bit Allreduce"): *shared-scale* variant -- the per-segment norms
+are MAX-all-reduced first (one tiny collective for the whole bucket), every rank quantizes
+against the same norm, so integer levels are summable and RCCL sums them directly.  The code
+width is the smallest integer type holding s*W (int8 when s*W <= 127, e.g. s=15 at W=8).
+"""
+from __future__ import annotations
+
+import torch
+
+from ..memory.residual import ResidualMemory
+from ..ops import quant as Q
+from ..ops import segstats as S
+from ._base import BucketCompressor
+
+
+class QSGDCompressor(BucketCompressor):
+    def __init__(self, quantum_num: int = 127, shared_scale: bool = False):
+        super().__init__()
+        self.quantum_num = int(quantum_num)
+        self.shared_scale = shared_scale
+        self.comm = None
+
+    @property
+    def allreduce_compatible(self):
+        return True
+
+    def enable_allreduce_mode(self):
+        self.shared_scale = True
+
+    def code_dtype(self, world_size: int = 1):
+        levels = self.quantum_num * (world_size if self.shared_scale else 1)
+        if levels <= 127:
+            return torch.int8
+        if levels <= 32767:
+            return torch.int16
+        return torch.int32
+
+    def _encode(self, g, ctx, name, memory=None):
+        lay = ctx.layout
+        W = self.comm.world_size if (self.shared_scale and self.comm is not None) else 1
+        cdt = self.code_dtype(W)
+        codes, norms = self.payload(g.device, [(cdt, (lay.total,)), (torch.float32, (lay.n_seg,))])
+        r = None
+        if memory is None:
+            stats = S.segment_stats(g, lay)
+            x = g
+        else:
+            r, valid = memory.residual_buffer(name, g)
+            stats = S.segment_stats(g, lay, r=r, r_valid=valid, beta=memory.beta, gamma=memory.gamma, xout=r)
+            x = r
+        torch.sqrt(stats[:, S.SUMSQ], out=norms)
+        if self.shared_scale and W > 1:
+            self.comm.all_reduce(norms, op="max")
+        Q.qsgd_quantize(x, lay, norms, self.quantum_num, self.next_seed(name), codes, resid=r)
+        if self.shared_scale:
+            ctx.extra["norms"] = norms
+            return [codes]
+        return [codes, norms]
+
+    def compress(self, tensor, name):
+        ctx = self.ctx(tensor, name)
+        return self._encode(self.flat(tensor), ctx, name), ctx
+
+    def fused_compress(self, tensor, name, memory):
+        if not isinstance(memory, ResidualMemory):
+            return None
+        ctx = self.ctx(tensor, name)
+        return self._encode(self.flat(tensor), ctx, name, memory), ctx
+
+    def _agg(self, per_rank, ctx, n_ranks, scale, norms=None):
+        from ..parallel.comm import PayloadBuilder
+
+        if norms is not None:  # shared-scale payloads carry no norm: re-attach ours
+            rows = []
+            for p in per_rank:
+                pb = PayloadBuilder(p[0].device, [(p[0].dtype, tuple(p[0].shape)), (torch.float32, (ctx.layout.n_seg,))])
+                pb.tensors[0].copy_(p[0])
+                pb.tensors[1].copy_(norms)
+                rows.append(pb.tensors)
+            per_rank = rows
+        base, stride, offs = self.rows(per_rank)
+        out = torch.empty(ctx.layout.total, dtype=torch.float32, device=base.device)
+        Q.qsgd_aggregate(base, stride, offs[0], offs[1], per_rank[0][0].dtype, n_ranks, self.quantum_num, ctx.layout,
+                         out, scale)
+        return self.finish(out, ctx)
+
+    def decompress_aggregate_impl(self, per_rank, ctx, n_ranks, scale):
+        return self._agg(per_rank, ctx, n_ranks, scale, ctx.extra.get("norms"))
+
+    def decompress_reduced(self, tensors, ctx, world_size):
+        # integer levels were SUM-all-reduced with a shared norm
+        return self._agg([list(tensors)], ctx, 1, 1.0 / world_size if self.average else 1.0, ctx.extra.get("norms"))

@@ -59,6 +59,17 @@ class SegmentLayout:
         for i, n in enumerate(self.numels):
             yield i, self.offsets[i], n
 
+    def word_offsets(self) -> List[int]:
+        """Per-segment offsets of 64-element groups (1 uint64 bit-plane word per group)."""
+        w = [0]
+        for n in self.numels:
+            w.append(w[-1] + (n + 63) // 64)
+        return w
+
+    @property
+    def n_words(self) -> int:
+        return self.word_offsets()[-1]
+
     def views(self, flat: torch.Tensor) -> List[torch.Tensor]:
         return [flat[o:o + n].view(s) for (_, o, n), s in zip(self.segments(), self.shapes)]
 
@@ -83,12 +94,19 @@ class SegmentLayout:
         d = self._dev.get(key)
         if d is None:
             seg, beg, end = self._host_chunks(chunk)
+            scb = [0] * (self.n_seg + 1)
+            for s_ in seg:
+                scb[s_ + 1] += 1
+            for i in range(self.n_seg):
+                scb[i + 1] += scb[i]
             d = {
+                "seg_chunk_begin": torch.tensor(scb, dtype=torch.int32, device=device),
                 "seg": torch.tensor(seg, dtype=torch.int32, device=device),
                 "begin": torch.tensor(beg, dtype=torch.int64, device=device),
                 "end": torch.tensor(end, dtype=torch.int64, device=device),
                 "offsets": torch.tensor(self.offsets, dtype=torch.int64, device=device),
                 "n_chunks": len(seg),
+                "word_off": torch.tensor(self.word_offsets(), dtype=torch.int64, device=device),
             }
             self._dev[key] = d
         return d

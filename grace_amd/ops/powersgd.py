@@ -1,0 +1,178 @@
+"""PowerSGD building blocks over a flat bucket (native: csrc/kernels/powersgd.hip).
+
+A :class:`Plan` describes every matrix segment of a bucket (rows n, cols m, rank r and its
+offsets into the flat gradient, the flat P buffer [sum n*r] and the flat Q buffer [sum m*r]),
+plus the 1-D segments that bypass the low-rank path.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Tuple
+
+import torch
+
+from . import _native
+from .layout import SegmentLayout
+
+
+@dataclass
+class Plan:
+    rank: int
+    mats: List[Tuple[int, int, int, int, int, int]]  # (x_off, n, m, r, p_off, q_off)
+    vecs: List[Tuple[int, int, int]]  # (x_off, numel, vec_off)
+    p_total: int
+    q_total: int
+    v_total: int
+    _dev: Dict[str, dict] = field(default_factory=dict, repr=False)
+
+    @property
+    def n_mat(self) -> int:
+        return len(self.mats)
+
+    def tables(self, device):
+        key = str(device)
+        t = self._dev.get(key)
+        if t is None:
+            t0, t1, tp = [], [], []
+            for i, (xo, n, m, r, po, qo) in enumerate(self.mats):
+                for rb in range((n + 63) // 64):
+                    for sidx in range((m + 1023) // 1024):
+                        t0.append((i, rb, sidx))
+                for cb in range((m + 63) // 64):
+                    for sidx in range((n + 1023) // 1024):
+                        t1.append((i, cb, sidx))
+                for rb in range((n + 15) // 16):
+                    for cb in range((m + 63) // 64):
+                        tp.append((i, rb, cb))
+
+            def it(lst):
+                return torch.tensor(lst, dtype=torch.int32, device=device).view(-1) if lst else \
+                    torch.empty(0, dtype=torch.int32, device=device)
+
+            t = {
+                "mat": torch.tensor([list(m) for m in self.mats] or [[0] * 6], dtype=torch.int64,
+                                    device=device).contiguous(),
+                "tiles0": it(t0),
+                "tiles1": it(t1),
+                "tilesp": it(tp),
+            }
+            self._dev[key] = t
+        return t
+
+
+_PLANS: Dict[Tuple, Plan] = {}
+
+
+def plan_for(layout: SegmentLayout, rank: int) -> Plan:
+    if not 1 <= rank <= 16:
+        raise ValueError("PowerSGD rank must be in [1, 16] (MFMA N-tile / LDS Gram-Schmidt bound)")
+    key = (layout.shapes, rank)
+    p = _PLANS.get(key)
+    if p is not None:
+        return p
+    mats, vecs = [], []
+    po = qo = vo = 0
+    for (i, o, n), shape in zip(layout.segments(), layout.shapes):
+        if len(shape) >= 2 and n > 0:
+            rows = shape[0]
+            cols = n // rows
+            r = min(rows, cols, rank)
+            mats.append((o, rows, cols, r, po, qo))
+            po += rows * r
+            qo += cols * r
+        elif n > 0:
+            vecs.append((o, n, vo))
+            vo += n
+    p = Plan(rank, mats, vecs, po, qo, vo)
+    _PLANS[key] = p
+    return p
+
+
+def randn_shared(n: int, seed: int, device) -> torch.Tensor:
+    """N(0,1) vector identical on every rank for the same seed."""
+    if _native.use_native(torch.empty(0, device=device)):
+        out = torch.empty(n, dtype=torch.float32, device=device)
+        sd = seed & 0xFFFFFFFFFFFFFFFF
+        _native.lib().philox_normal(out, sd - (1 << 64) if sd >= (1 << 63) else sd)
+        return out
+    g = torch.Generator(device=device)
+    g.manual_seed(seed & 0x7FFFFFFFFFFFFFFF)
+    return torch.randn(n, generator=g, device=device)
+
+
+def _views(buf, plan, which):
+    out = []
+    for (xo, n, m, r, po, qo) in plan.mats:
+        if which == "p":
+            out.append(buf[po:po + n * r].view(n, r))
+        else:
+            out.append(buf[qo:qo + m * r].view(m, r))
+    return out
+
+
+def orthogonalize(buf: torch.Tensor, plan: Plan, which: str) -> None:
+    """In-place Gram-Schmidt of the columns of every P_i (or Q_i) -- reference
+    dist/compressor/powersgd.py:7-18 (zero columns stay zero instead of becoming NaN)."""
+    if _native.use_native(buf):
+        t = plan.tables(buf.device)
+        _native.lib().gram_schmidt(buf, t["mat"], 0 if which == "p" else 1, plan.n_mat)
+        return
+    for a in _views(buf, plan, which):
+        r = a.shape[1]
+        for i in range(r):
+            col = a[:, i:i + 1]
+            nrm = torch.sqrt(torch.sum(col * col))
+            col /= torch.clamp(nrm, min=1e-30)
+            if i + 1 < r:
+                rest = a[:, i + 1:]
+                rest -= torch.sum(col * rest, dim=0) * col
+
+
+def mq(x: torch.Tensor, q: torch.Tensor, plan: Plan) -> torch.Tensor:
+    """P_i = M_i Q_i for every matrix (flat P buffer)."""
+    p = torch.empty(plan.p_total, dtype=torch.float32, device=x.device)
+    if _native.use_native(x):
+        t = plan.tables(x.device)
+        _native.lib().powersgd_mq(x, q, p, t["mat"], t["tiles0"], 0)
+        return p
+    for (xo, n, m, r, po, qo) in plan.mats:
+        torch.mm(x[xo:xo + n * m].view(n, m), q[qo:qo + m * r].view(m, r), out=p[po:po + n * r].view(n, r))
+    return p
+
+
+def mtp(x: torch.Tensor, p: torch.Tensor, plan: Plan) -> torch.Tensor:
+    """Q_i = M_i^T P_i for every matrix (flat Q buffer)."""
+    q = torch.empty(plan.q_total, dtype=torch.float32, device=x.device)
+    if _native.use_native(x):
+        t = plan.tables(x.device)
+        _native.lib().powersgd_mq(x, p, q, t["mat"], t["tiles1"], 1)
+        return q
+    for (xo, n, m, r, po, qo) in plan.mats:
+        torch.mm(x[xo:xo + n * m].view(n, m).t(), p[po:po + n * r].view(n, r), out=q[qo:qo + m * r].view(m, r))
+    return q
+
+
+def pqt(p: torch.Tensor, q: torch.Tensor, plan: Plan, out: torch.Tensor) -> None:
+    """out[matrix i] = P_i Q_i^T (vector segments untouched)."""
+    if _native.use_native(out):
+        t = plan.tables(out.device)
+        _native.lib().powersgd_pqt(p, q, out, t["mat"], t["tilesp"])
+        return
+    for (xo, n, m, r, po, qo) in plan.mats:
+        torch.mm(p[po:po + n * r].view(n, r), q[qo:qo + m * r].view(m, r).t(), out=out[xo:xo + n * m].view(n, m))
+
+
+def gather_vectors(x: torch.Tensor, plan: Plan) -> torch.Tensor:
+    v = torch.empty(plan.v_total, dtype=torch.float32, device=x.device)
+    for (xo, n, vo) in plan.vecs:
+        v[vo:vo + n].copy_(x[xo:xo + n])
+    return v
+
+
+def scatter_vectors(v: torch.Tensor, plan: Plan, out: torch.Tensor, scale: float) -> None:
+    for (xo, n, vo) in plan.vecs:
+        if scale != 1.0:
+            torch.mul(v[vo:vo + n], scale, out=out[xo:xo + n])
+        else:
+            out[xo:xo + n].copy_(v[vo:vo + n])

@@ -4,8 +4,8 @@ Reference: /root/reference/grace_dl/dist/compressor/topk.py:6-36 (per-tensor
 ``torch.topk(|x|, k)`` + gather + scatter decompress) and
 /root/reference/grace_dl/dist/memory/residual.py:10-20 (compensate / update).
 
-Payload format (one collective per bucket instead of two per tensor):
-``packed`` int32 tensor of 2K words = [ fp32 values bit-cast (K) | int32 flat indices (K) ].
+Payload format (one collective per bucket instead of two per tensor): one 16-B aligned
+buffer holding [ fp32 values (K) | int32 flat indices (K) ].
 The TF backend's layout (fp32 values + int32 indices in one tensor,
 /root/reference/grace_dl/tensorflow/compressor/topk.py:32-35) - 8 bytes per element instead
 of the dist backend's 12.
@@ -43,11 +43,6 @@ def _workspace(layout: SegmentLayout, ks: Sequence[int], device):
     return layout.cached(device, f"topk_ws:{hash(tuple(ks))}", build)
 
 
-def split_packed(packed: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-    K = packed.numel() // 2
-    return packed[:K].view(torch.float32), packed[K:]
-
-
 def topk_ef(
     g: torch.Tensor,
     layout: SegmentLayout,
@@ -56,21 +51,25 @@ def topk_ef(
     resid_valid: bool = False,
     beta: float = 1.0,
     gamma: float = 1.0,
-    out: Optional[torch.Tensor] = None,
-) -> torch.Tensor:
+    out: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+) -> Tuple[torch.Tensor, torch.Tensor]:
     """Compensate + select + (residual update) over a flat bucket.
 
     ``g``      flat fp32 gradient bucket (read only)
     ``resid``  flat fp32 residual buffer or None (NoneMemory). If given it is read (when
                ``resid_valid``), overwritten with x = beta*r + gamma*g and finally left holding
                x - decompress(compress(x)), i.e. x with the selected entries zeroed.
-    returns the packed int32 payload [vals | idx] (2K words).
+    returns (vals fp32[K], idx int32[K]) -- views of ONE buffer laid out as the packed wire
+    format (grace_amd.parallel.comm.pack is then zero-copy).
     """
     assert g.dtype == torch.float32 and g.dim() == 1 and g.is_contiguous()
     K = sum(ks)
     if out is None:
-        out = torch.empty(2 * K, dtype=torch.int32, device=g.device)
-    vals, idx = split_packed(out)
+        from ..parallel.comm import PayloadBuilder
+
+        vals, idx = PayloadBuilder(g.device, [(torch.float32, (K,)), (torch.int32, (K,))]).tensors
+    else:
+        vals, idx = out
     if _native.use_native(g):
         C = _native.lib()
         ws = _workspace(layout, ks, g.device)
@@ -81,7 +80,7 @@ def topk_ef(
                       ws["kseg"], ws["state"], ws["hist"])
         C.topk_compact(x, t["seg"], t["begin"], t["end"], ws["state"], ws["out_off"], ws["counters"],
                        vals, idx, resid, 0)
-        return out
+        return vals, idx
     # ---- PyTorch reference path (CPU / oracle)
     if resid is not None:
         if resid_valid:
@@ -103,12 +102,12 @@ def topk_ef(
         if resid is not None:
             seg[li] = 0.0
         p += k
-    return out
+    return vals, idx
 
 
-def scatter_add(packed: torch.Tensor, out: torch.Tensor, scale: float = 1.0, accumulate: bool = True) -> None:
-    """out[idx] (+)= vals * scale for one rank's packed payload (indices unique)."""
-    vals, idx = split_packed(packed)
+def scatter_add(vals: torch.Tensor, idx: torch.Tensor, out: torch.Tensor, scale: float = 1.0,
+                accumulate: bool = True) -> None:
+    """out[idx] (+)= vals * scale for one rank's payload (indices unique within a payload)."""
     if _native.use_native(out):
         _native.lib().sparse_scatter_add(vals, idx, out, scale, accumulate)
         return

@@ -9,7 +9,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _check(x_ref, layout, ks, packed, resid=None):
-    vals, idx = T.split_packed(packed.cpu())
+    vals, idx = packed[0].cpu(), packed[1].cpu()
     p = 0
     for (i, o, n), k in zip(layout.segments(), ks):
         v = vals[p:p + k]
@@ -53,7 +53,7 @@ def test_topk_fused_residual_two_steps():
         packed = T.topk_ef(g, lay, ks, resid=r, resid_valid=step > 0, beta=0.9, gamma=1.1)
         torch.cuda.synchronize()
         # fused fma vs two-rounding reference: compare with tolerance, then use GPU x for set check
-        vals, idx = T.split_packed(packed.cpu())
+        vals, idx = packed[0].cpu(), packed[1].cpu()
         x_gpu = r.cpu().clone()
         x_gpu[idx.long()] = vals
         torch.testing.assert_close(x_gpu, x_ref, rtol=1e-6, atol=1e-6)
@@ -84,7 +84,7 @@ def test_scatter_add_matches_dense():
     for r in range(4):
         g = torch.randn(n, device="cuda")
         packed = T.topk_ef(g, lay, ks)
-        T.scatter_add(packed, out, scale=0.25)
-        v, i = T.split_packed(packed.cpu())
+        T.scatter_add(packed[0], packed[1], out, scale=0.25)
+        v, i = packed[0].cpu(), packed[1].cpu()
         ref.index_add_(0, i.long(), v * 0.25)
     torch.testing.assert_close(out.cpu(), ref, rtol=1e-6, atol=1e-7)
