@@ -1,0 +1,168 @@
+#!/usr/bin/env python3
+"""grace_amd benchmark: data-parallel training throughput with GRACE gradient compression.
+
+Headline (BASELINE.json): ResNet-50, ImageNet shape 3x224x224, batch 32 per GPU, Top-K 1% +
+ResidualMemory + Allgather, SGD(lr = 0.01 * W, momentum 0.5) -- the reference harness
+/root/reference/examples/torch/pytorch_synthetic_benchmark.py:46-55, 110-111, 151-154 with
+``Allgather(TopKCompressor(0.01), ResidualMemory())`` (line 119).  Synthetic data and
+random-init weights (no datasets / checkpoints offline).
+
+    python bench.py --gpus 1 --steps 20 --warmup 10
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+        --master-port 29500 bench.py --gpus 8 --steps 20 --warmup 10
+
+Weak scaling: the per-GPU batch is fixed, ``value`` is the WHOLE-JOB throughput (all ranks);
+the timed region is bracketed by a barrier + device synchronize on both sides and the
+maximum elapsed time over ranks is used.  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+HEADLINE_METRIC = "images/sec (whole node) ResNet-50 Top-K 1% @ 1/2/4/8 MI355X; comm wall-time"
+
+
+def parse():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workload", default="resnet50_topk")
+    ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (0 = workload default)")
+    ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16", help="autocast compute dtype")
+    ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--no-benchmark-mode", action="store_true", help="disable MIOpen find (cudnn.benchmark)")
+    ap.add_argument("--exposed-steps", type=int, default=3, help="untimed steps measuring exposed GRACE time")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    from grace_amd import grace_from_params
+    from grace_amd.parallel import DistributedOptimizer, broadcast_parameters
+    from grace_amd.utils.workloads import WORKLOADS, build_model
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a GPU")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
+    torch.backends.cudnn.benchmark = not args.no_benchmark_mode
+
+    w = WORKLOADS[args.workload]
+    batch = args.batch or w.batch
+    torch.manual_seed(0)
+    model = build_model(w, dev)
+    base_opt = torch.optim.SGD(model.parameters(), lr=0.01 * world, momentum=0.5)
+    grc = grace_from_params(dict(w.grace, world_size=world))
+    opt = DistributedOptimizer(base_opt, grc, named_parameters=model.named_parameters(),
+                               bucket_cap_mb=args.bucket_mb, overlap=not args.no_overlap)
+    broadcast_parameters(model.state_dict(), root_rank=0)
+    data = w.make_batch(batch, dev)
+    if w.channels_last and isinstance(data, tuple) and data[0].dim() == 4:
+        data = (data[0].contiguous(memory_format=torch.channels_last),) + tuple(data[1:])
+    amp = args.dtype == "bf16"
+
+    def step():
+        opt.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            loss = w.loss(model, data)
+        loss.backward()
+        opt.step()
+        return loss
+
+    def barrier():
+        if world > 1:
+            dist.barrier(device_ids=[local])
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+
+    # untimed: exposed GRACE time (compress tail + collective + decompress + optimizer after
+    # a fully synchronized backward) -- the "comm wall-time" split of the reference harness
+    # (pytorch_synthetic_benchmark.py:166-167)
+    exposed = []
+    for _ in range(args.exposed_steps):
+        opt.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            l2 = w.loss(model, data)
+        l2.backward()
+        torch.cuda.synchronize()
+        barrier()
+        t = time.perf_counter()
+        opt.step()
+        torch.cuda.synchronize()
+        exposed.append(time.perf_counter() - t)
+    ex = torch.tensor([sum(exposed) / max(1, len(exposed))], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(ex, op=dist.ReduceOp.MAX)
+
+    samples = w.samples_per_batch(batch) * world * args.steps
+    value = samples / elapsed
+    if rank == 0:
+        metric = HEADLINE_METRIC if w.name == "resnet50_topk" else f"{w.unit}/sec (whole node) {w.name}"
+        out = {
+            "metric": metric,
+            "value": round(value, 2),
+            "unit": f"{w.unit}/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic (random-init weights)",
+            "config": {
+                "model": w.model,
+                "global_batch": batch * world,
+                "per_gpu_batch": batch,
+                "seq_len": w.seq_len,
+                "parallelism": f"dp{world}",
+                "grace": w.grace,
+                "bucket_mb": args.bucket_mb,
+                "overlap": not args.no_overlap,
+            },
+            "comm_wall_ms": round(float(ex.item()) * 1e3, 3),
+            "final_loss": round(float(loss.float().item()), 4),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,118 @@
+"""Horovod-style ``DistributedOptimizer`` without the Horovod patch, plus broadcast helpers.
+
+Parity with the patched Horovod 0.18.2 torch integration
+(/root/reference/patch_files/horovod/torch/__init__.py:46-250: ``DistributedOptimizer(opt,
+grace, named_parameters, backward_passes_per_step)``, ``synchronize``, ``skip_synchronize``,
+the double-synchronize warning and the ``zero_grad`` race guard; broadcast_parameters /
+broadcast_optimizer_state at 253-403).  The gradient exchange is the bucketed, overlapped
+:class:`~grace_amd.parallel.engine.GraceEngine` on RCCL instead of per-parameter Horovod
+handles.
+"""
+from __future__ import annotations
+
+import contextlib
+import warnings
+from typing import Iterable, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+from .engine import GraceEngine
+
+
+class _DistributedOptimizer:
+    def __init__(self, optimizer, grace, named_parameters=None, backward_passes_per_step: int = 1,
+                 bucket_cap_mb: float = 64.0, overlap: bool = True):
+        self._opt = optimizer
+        if named_parameters is None:
+            params = [p for g in optimizer.param_groups for p in g["params"]]
+            named_parameters = [(f"param.{i}", p) for i, p in enumerate(params)]
+        named_parameters = list(named_parameters)
+        opt_ids = {id(p) for g in optimizer.param_groups for p in g["params"]}
+        missing = [n for n, p in named_parameters if id(p) not in opt_ids]
+        if missing:
+            raise ValueError(f"named_parameters not in the optimizer: {missing[:5]}")
+        self.engine = GraceEngine(named_parameters, grace, bucket_cap_mb=bucket_cap_mb,
+                                  backward_passes_per_step=backward_passes_per_step, overlap=overlap)
+        self._synchronized = False
+        self._should_sync = True
+
+    # attribute passthrough (param_groups, state, ...)
+    def __getattr__(self, item):
+        return getattr(self._opt, item)
+
+    def synchronize(self):
+        self.engine.synchronize()
+        self._synchronized = True
+
+    @contextlib.contextmanager
+    def skip_synchronize(self):
+        self._should_sync = False
+        try:
+            yield
+        finally:
+            self._should_sync = True
+
+    def step(self, closure=None):
+        if self._should_sync:
+            if self._synchronized:
+                warnings.warn("optimizer.step() called without a new backward after synchronize(); "
+                              "use skip_synchronize() to avoid a double exchange")
+            else:
+                self.synchronize()
+        self._synchronized = False
+        return self._opt.step(closure)
+
+    def zero_grad(self, set_to_none: bool = False):
+        # gradients live in bucket buffers: one memset per bucket, never None
+        self.engine.zero_grad()
+
+    def state_dict(self):
+        return {"optimizer": self._opt.state_dict(), "grace": self.engine.state_dict()}
+
+    def load_state_dict(self, sd):
+        self._opt.load_state_dict(sd["optimizer"])
+        self.engine.load_state_dict(sd["grace"])
+
+
+def DistributedOptimizer(optimizer, grace, named_parameters=None, backward_passes_per_step: int = 1, **kw):
+    """Wrap ``optimizer`` so that ``step()`` exchanges gradients through ``grace``."""
+    return _DistributedOptimizer(optimizer, grace, named_parameters, backward_passes_per_step, **kw)
+
+
+def broadcast_parameters(params, root_rank: int = 0, group=None):
+    """Bucketed broadcast of a ``state_dict()`` / named parameters (consistent init & resume)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return
+    items = list(params.items()) if isinstance(params, dict) else list(params)
+    tensors = [t for _, t in items if isinstance(t, torch.Tensor)]
+    by = {}
+    for t in tensors:
+        by.setdefault((t.device, t.dtype), []).append(t)
+    for ts in by.values():
+        flat = torch.cat([t.detach().reshape(-1) for t in ts])
+        dist.broadcast(flat, root_rank, group=group)
+        off = 0
+        for t in ts:
+            n = t.numel()
+            with torch.no_grad():
+                t.copy_(flat[off:off + n].view_as(t))
+            off += n
+
+
+def broadcast_optimizer_state(optimizer, root_rank: int = 0, group=None):
+    """Broadcast every tensor of the optimizer state from ``root_rank`` (creates missing state
+    by a zero-gradient no-op step first, as Horovod does)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return
+    opt = getattr(optimizer, "_opt", optimizer)
+    state = opt.state_dict()["state"]
+    if not state and dist.get_world_size(group) > 1:
+        return
+    tensors = []
+    for pid in sorted(state):
+        for k in sorted(state[pid]):
+            v = state[pid][k]
+            if isinstance(v, torch.Tensor):
+                tensors.append((f"{pid}.{k}", v))
+    broadcast_parameters(tensors, root_rank, group)

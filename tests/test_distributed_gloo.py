@@ -1,0 +1,101 @@
+"""Multi-process communicator semantics on CPU (gloo, W = 2 and 3).
+
+Every rank holds rank-specific data; results are checked against the oracle of the reference
+semantics computed from ALL ranks' data, and for bit-identity across ranks (the DP invariant).
+"""
+import os
+import sys
+
+import pytest
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(__file__))
+import oracles as O  # noqa: E402
+from dist_utils import run_distributed  # noqa: E402
+
+
+def _data(rank, shape=(31, 17), seed=0):
+    g = torch.Generator().manual_seed(1000 * seed + rank)
+    return torch.randn(*shape, generator=g)
+
+
+def _same_on_all_ranks(t):
+    W = dist.get_world_size()
+    out = [torch.empty_like(t) for _ in range(W)]
+    dist.all_gather(out, t.contiguous())
+    for o in out[1:]:
+        assert torch.equal(o, out[0]), "result differs across ranks"
+
+
+def _body(rank, world):
+    from grace_amd import grace_from_params
+
+    xs = [_data(r) for r in range(world)]
+    x = xs[rank]
+
+    def run(params, name="w"):
+        p = dict(params, world_size=world)
+        grc = grace_from_params(p)
+        out = grc.step(x.clone(), name)
+        _same_on_all_ranks(out)
+        return out
+
+    # None: allreduce / allgather / broadcast all give the mean
+    mean = sum(xs) / world
+    for comm in ("allreduce", "allgather", "broadcast"):
+        torch.testing.assert_close(run({"compressor": "none", "communicator": comm}), mean)
+    # FP16
+    torch.testing.assert_close(run({"compressor": "fp16", "communicator": "allreduce"}), mean, rtol=2e-3, atol=2e-3)
+    # Top-K via allgather and broadcast: mean of per-rank top-k
+    exp = sum(O.topk(t, 0.1) for t in xs) / world
+    for comm in ("allgather", "broadcast"):
+        torch.testing.assert_close(run({"compressor": "topk", "compress_ratio": 0.1, "communicator": comm}), exp)
+    # Threshold (variable size) via allgather
+    exp = sum(O.threshold(t, 0.8) for t in xs) / world
+    torch.testing.assert_close(run({"compressor": "threshold", "threshold": 0.8, "communicator": "allgather"}), exp)
+    # Random-K: identical indices on all ranks -> allreduce == allgather
+    a = run({"compressor": "randomk", "compress_ratio": 0.2, "communicator": "allreduce"}, "rk")
+    b = run({"compressor": "randomk", "compress_ratio": 0.2, "communicator": "allgather"}, "rk")
+    torch.testing.assert_close(a, b)
+    nz = a != 0
+    torch.testing.assert_close(a[nz], mean[nz])
+    # SignSGD majority vote (allgather and "bit-packed allreduce")
+    exp = O.signsgd_vote(xs)
+    torch.testing.assert_close(run({"compressor": "signsgd", "communicator": "allgather"}), exp)
+    torch.testing.assert_close(run({"compressor": "signsgd", "communicator": "allreduce"}), exp)
+    # EF-SignSGD: sum of mean*sign / lr
+    exp = sum(O.efsign(t) for t in xs) / 0.5
+    torch.testing.assert_close(run({"compressor": "efsignsgd", "lr": 0.5, "communicator": "allgather"}), exp,
+                               rtol=1e-5, atol=1e-5)
+    # OneBit: mean of per-rank decode
+    exp = sum(O.onebit(t) for t in xs) / world
+    torch.testing.assert_close(run({"compressor": "onebit", "communicator": "allgather"}), exp, rtol=1e-5, atol=1e-5)
+    # QSGD shared-scale allreduce and allgather: within one quantisation step of the mean
+    for comm in ("allreduce", "allgather"):
+        out = run({"compressor": "qsgd", "quantum_num": 15, "communicator": comm}, "q")
+        bound = max(t.norm() for t in xs) / 15
+        assert (out - mean).abs().max() <= bound * (1 + 1e-4)
+    # TernGrad / Natural / U8bit / Sketch run and agree across ranks
+    for comp in ("terngrad", "natural", "u8bit", "sketch", "inceptionn", "adaq", "dgc"):
+        comm = "allgather"
+        out = run({"compressor": comp, "communicator": comm, "compress_ratio": 0.05}, comp)
+        assert torch.isfinite(out).all()
+    # PowerSGD (W-averaged P and Q)
+    out = run({"compressor": "powersgd", "compress_rank": 2, "communicator": "allreduce"}, "ps")
+    assert torch.isfinite(out).all()
+    # DGC memory with clipping (batched scalar allreduce)
+    out = run({"compressor": "dgc", "memory": "dgc", "gradient_clipping": True, "communicator": "allgather",
+               "compress_ratio": 0.05}, "dg")
+    assert torch.isfinite(out).all()
+    # Residual memory + Top-K over 3 steps keeps ranks identical
+    grc = grace_from_params({"compressor": "topk", "compress_ratio": 0.05, "memory": "residual",
+                             "communicator": "allgather", "world_size": world})
+    for s in range(3):
+        out = grc.step(_data(rank, seed=s + 1), "w")
+        _same_on_all_ranks(out)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_communicators_gloo(world):
+    run_distributed(_body, world)

@@ -1,0 +1,155 @@
+"""Training-integration tests on CPU: DistributedOptimizer engine, DDP comm hook, broadcasts."""
+import os
+import sys
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(__file__))
+from dist_utils import run_distributed  # noqa: E402
+
+
+def _model(seed=0):
+    torch.manual_seed(seed)
+    return nn.Sequential(nn.Linear(20, 64), nn.ReLU(), nn.Linear(64, 32), nn.ReLU(), nn.Linear(32, 5))
+
+
+def _batch(rank, seed=0):
+    g = torch.Generator().manual_seed(100 * seed + rank)
+    return torch.randn(16, 20, generator=g), torch.randint(0, 5, (16,), generator=g)
+
+
+def test_engine_none_equals_plain_sgd_single_process():
+    from grace_amd import grace_from_params
+    from grace_amd.parallel import DistributedOptimizer
+
+    m1, m2 = _model(), _model()
+    o1 = torch.optim.SGD(m1.parameters(), lr=0.1, momentum=0.9)
+    grc = grace_from_params({"compressor": "none", "communicator": "allreduce"})
+    o2 = DistributedOptimizer(torch.optim.SGD(m2.parameters(), lr=0.1, momentum=0.9), grc,
+                              named_parameters=m2.named_parameters(), bucket_cap_mb=0.001)
+    assert len(o2.engine.buckets) > 1
+    for s in range(4):
+        x, y = _batch(0, s)
+        o1.zero_grad()
+        F.cross_entropy(m1(x), y).backward()
+        o1.step()
+        o2.zero_grad()
+        F.cross_entropy(m2(x), y).backward()
+        o2.step()
+    for a, b in zip(m1.parameters(), m2.parameters()):
+        torch.testing.assert_close(a, b)
+
+
+def test_backward_passes_per_step_accumulates():
+    from grace_amd import grace_from_params
+    from grace_amd.parallel import DistributedOptimizer
+
+    m1, m2 = _model(), _model()
+    o1 = torch.optim.SGD(m1.parameters(), lr=0.1)
+    o2 = DistributedOptimizer(torch.optim.SGD(m2.parameters(), lr=0.1), grace_from_params({}),
+                              named_parameters=m2.named_parameters(), backward_passes_per_step=2)
+    o1.zero_grad()
+    o2.zero_grad()
+    for s in range(2):
+        x, y = _batch(0, s)
+        F.cross_entropy(m1(x), y).backward()
+        F.cross_entropy(m2(x), y).backward()
+    o1.step()
+    o2.step()
+    for a, b in zip(m1.parameters(), m2.parameters()):
+        torch.testing.assert_close(a, b)
+
+
+def test_zero_grad_race_guard():
+    from grace_amd import grace_from_params
+    from grace_amd.parallel import DistributedOptimizer
+
+    m = _model()
+    o = DistributedOptimizer(torch.optim.SGD(m.parameters(), lr=0.1), grace_from_params({}),
+                             named_parameters=m.named_parameters())
+    x, y = _batch(0)
+    F.cross_entropy(m(x), y).backward()
+    with pytest.raises(AssertionError):
+        o.zero_grad()
+    o.step()
+    o.zero_grad()
+
+
+def _dp_body(rank, world, params):
+    from grace_amd import grace_from_params
+    from grace_amd.parallel import DistributedOptimizer, broadcast_parameters
+
+    m = _model(seed=rank)  # different init on purpose: broadcast must fix it
+    broadcast_parameters(m.state_dict(), root_rank=0)
+    ref = _model(seed=0)
+    for a, b in zip(m.parameters(), ref.parameters()):
+        torch.testing.assert_close(a, b)
+    grc = grace_from_params(dict(params, world_size=world))
+    opt = DistributedOptimizer(torch.optim.SGD(m.parameters(), lr=0.05), grc, named_parameters=m.named_parameters(),
+                               bucket_cap_mb=0.002)
+    ref_opt = torch.optim.SGD(ref.parameters(), lr=0.05)
+    for s in range(3):
+        x, y = _batch(rank, s)
+        opt.zero_grad()
+        F.cross_entropy(m(x), y).backward()
+        opt.step()
+        if params.get("compressor", "none") == "none":
+            # reference: average of all ranks' gradients
+            ref_opt.zero_grad()
+            for r in range(world):
+                xr, yr = _batch(r, s)
+                (F.cross_entropy(ref(xr), yr) / world).backward()
+            ref_opt.step()
+    # replicas identical on every rank
+    flat = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+    out = [torch.empty_like(flat) for _ in range(world)]
+    dist.all_gather(out, flat)
+    for o in out[1:]:
+        assert torch.equal(o, out[0])
+    if params.get("compressor", "none") == "none":
+        for a, b in zip(m.parameters(), ref.parameters()):
+            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("params", [
+    {"compressor": "none", "communicator": "allreduce"},
+    {"compressor": "topk", "compress_ratio": 0.1, "memory": "residual", "communicator": "allgather"},
+    {"compressor": "efsignsgd", "lr": 0.1, "memory": "efsignsgd", "communicator": "allreduce"},
+    {"compressor": "qsgd", "quantum_num": 15, "communicator": "allreduce"},
+    {"compressor": "powersgd", "compress_rank": 2, "memory": "powersgd", "communicator": "allreduce"},
+])
+def test_distributed_optimizer_gloo(params):
+    run_distributed(_dp_body, 2, params)
+
+
+def _ddp_body(rank, world):
+    from grace_amd import grace_from_params
+    from grace_amd.parallel import GraceHookState, grace_comm_hook
+
+    m = _model(seed=0)
+    ddp = nn.parallel.DistributedDataParallel(m, bucket_cap_mb=0.002)
+    ddp.register_comm_hook(GraceHookState(grace_from_params({"compressor": "none", "world_size": world})),
+                           grace_comm_hook)
+    ref = _model(seed=0)
+    opt = torch.optim.SGD(ddp.parameters(), lr=0.05)
+    ref_opt = torch.optim.SGD(ref.parameters(), lr=0.05)
+    for s in range(2):
+        x, y = _batch(rank, s)
+        opt.zero_grad()
+        F.cross_entropy(ddp(x), y).backward()
+        opt.step()
+        ref_opt.zero_grad()
+        for r in range(world):
+            xr, yr = _batch(r, s)
+            (F.cross_entropy(ref(xr), yr) / world).backward()
+        ref_opt.step()
+    for a, b in zip(m.parameters(), ref.parameters()):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+def test_ddp_comm_hook_gloo():
+    run_distributed(_ddp_body, 2)

@@ -1,0 +1,191 @@
+"""GPU numerics: every native compressor kernel vs the PyTorch fp32 reference path.
+
+Deterministic codecs must match the CPU/PyTorch path (bit-exact or to fp32 rounding);
+stochastic ones (QSGD, TernGrad, Natural) are checked for their error bounds and
+unbiasedness, on the GPU path that runs the HIP kernels.
+"""
+import os
+import sys
+
+import pytest
+import torch
+
+sys.path.insert(0, os.path.dirname(__file__))
+import oracles as O  # noqa: E402
+from grace_amd import compressor as Z  # noqa: E402
+from grace_amd import memory as M  # noqa: E402
+from grace_amd.communicator import Allgather, Allreduce  # noqa: E402
+from grace_amd.core import register_layout  # noqa: E402
+from grace_amd.ops import _native  # noqa: E402
+from grace_amd.ops.layout import SegmentLayout  # noqa: E402
+from grace_amd.parallel.comm import LocalComm  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [(10, 7), (64,), (3, 3, 3, 3), (1,), (129,), (257, 129), (4096,), (100003,)]
+
+
+def _bucket(seed=0):
+    g = torch.Generator().manual_seed(seed)
+    ts = [torch.randn(*s, generator=g) for s in SHAPES]
+    flat = torch.cat([t.flatten() for t in ts])
+    lay = SegmentLayout.from_tensors(ts)
+    register_layout("gpu_bucket", lay)
+    return flat, lay
+
+
+def _rt(comp, x, name="gpu_bucket"):
+    payload, ctx = comp.compress(x, name)
+    return comp.decompress(payload, ctx)
+
+
+def test_native_library_loaded():
+    assert _native.available(), "grace_amd/_C.so must load on the GPU box"
+    assert "gfx950" in _native.lib().build_info()
+
+
+@pytest.mark.parametrize("make", [
+    lambda: Z.TopKCompressor(0.05),
+    lambda: Z.SignSGDCompressor(),
+    lambda: Z.EFSignSGDCompressor(0.1),
+    lambda: Z.OneBitCompressor(),
+    lambda: Z.U8bitCompressor(),
+    lambda: Z.ThresholdCompressor(1.5),
+])
+def test_deterministic_codecs_match_torch(make):
+    flat, lay = _bucket()
+    cpu = _rt(make(), flat)
+    gpu = _rt(make(), flat.cuda())
+    torch.testing.assert_close(gpu.cpu(), cpu, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("make", [
+    lambda: Z.TopKCompressor(0.05),
+    lambda: Z.SignSGDCompressor(),
+    lambda: Z.SignumCompressor(0.9),
+    lambda: Z.EFSignSGDCompressor(0.1),
+    lambda: Z.OneBitCompressor(),
+    lambda: Z.U8bitCompressor(),
+    lambda: Z.RandomKCompressor(0.05),
+])
+def test_fused_residual_matches_torch(make):
+    """Fused error-feedback kernels == PyTorch path over 3 steps (residuals too)."""
+    outs = {}
+    for dev in ("cpu", "cuda"):
+        grc = Allgather(make(), M.ResidualMemory(beta=0.9, gamma=1.0), comm=LocalComm())
+        res = []
+        for s in range(3):
+            flat, _ = _bucket(seed=s)
+            res.append(grc.step(flat.to(dev), "gpu_bucket").cpu())
+        res.append(grc.memory.residuals["gpu_bucket"].cpu())
+        outs[dev] = res
+    for a, b in zip(outs["cpu"], outs["cuda"]):
+        torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-5)
+
+
+def test_randomk_same_indices_cpu_gpu():
+    flat, lay = _bucket()
+    a = _rt(Z.RandomKCompressor(0.1), flat)
+    b = _rt(Z.RandomKCompressor(0.1), flat.cuda()).cpu()
+    torch.testing.assert_close(a, b)
+
+
+def test_qsgd_gpu_bounds_unbiased():
+    flat, lay = _bucket()
+    x = flat.cuda()
+    c = Z.QSGDCompressor(64)
+    acc = torch.zeros_like(x)
+    n = 100
+    for _ in range(n):
+        d = _rt(c, x)
+        acc += d
+    # per-segment bound: |dec - x| <= ||seg||/s
+    for (i, o, k) in lay.segments():
+        seg = flat[o:o + k]
+        assert (d[o:o + k].cpu() - seg).abs().max() <= seg.norm() / 64 * (1 + 1e-4) + 1e-7
+    # unbiased: per-element error of the n-sample mean has std <= step/(2 sqrt(n)), so
+    # E|err| <= 0.4 step/sqrt(n); and the signed errors average out (no systematic bias)
+    big = slice(lay.offsets[-2], lay.offsets[-1])
+    step = flat[big].norm().item() / 64
+    err = (acc[big] / n - x[big]).cpu()
+    assert err.abs().mean() <= 0.45 * step / n ** 0.5
+    assert abs(err.mean().item()) <= 5 * 0.5 * step / (n * err.numel()) ** 0.5
+
+
+def test_terngrad_gpu():
+    flat, lay = _bucket()
+    x = flat.cuda()
+    c = Z.TernGradCompressor()
+    d = _rt(c, x).cpu()
+    for (i, o, k) in lay.segments():
+        seg = flat[o:o + k]
+        sc = O.terngrad_scalar(seg)
+        vals = set(torch.unique(d[o:o + k] / sc).round().tolist()) if sc > 0 else {0.0}
+        assert vals <= {-1.0, 0.0, 1.0}
+
+
+def test_natural_gpu_power_of_two():
+    flat, _ = _bucket()
+    d = _rt(Z.NaturalCompressor(), flat.cuda()).cpu()
+    lo, hi = O.natural_decode_range(flat)
+    a = d.abs()
+    assert torch.all(torch.isclose(a, lo) | torch.isclose(a, hi))
+
+
+def test_dgc_gpu_selects_about_ratio():
+    flat, lay = _bucket()
+    c = Z.DgcCompressor(0.01)
+    payload, ctx = c.compress(flat.cuda(), "gpu_bucket")
+    big = lay.numels[-1]
+    idx = payload[1].cpu().long()
+    n_big = ((idx >= lay.offsets[-2]) & (idx < lay.offsets[-1])).sum().item()
+    assert 0.5 * 0.01 * big <= n_big <= 1.5 * 0.01 * big
+    assert torch.equal(payload[0].cpu(), flat[idx])
+
+
+@pytest.mark.parametrize("rank", [1, 2, 4])
+def test_powersgd_mfma_matches_torch(rank):
+    from grace_amd.ops import powersgd as PS
+
+    g = torch.Generator().manual_seed(3)
+    shapes = [(300, 257), (64, 3, 3, 3), (1000,), (4096, 1100)]
+    ts = [torch.randn(*s, generator=g) for s in shapes]
+    flat = torch.cat([t.flatten() for t in ts])
+    lay = SegmentLayout.from_tensors(ts)
+    plan = PS.plan_for(lay, rank)
+    q = torch.randn(plan.q_total, generator=g)
+    xg, qg = flat.cuda(), q.cuda()
+    p_ref = PS.mq(flat, q, plan)
+    p_gpu = PS.mq(xg, qg, plan)
+    torch.testing.assert_close(p_gpu.cpu(), p_ref, rtol=1e-4, atol=1e-3)
+    q_ref = PS.mtp(flat, p_ref, plan)
+    q_gpu = PS.mtp(xg, p_ref.cuda(), plan)
+    torch.testing.assert_close(q_gpu.cpu(), q_ref, rtol=1e-4, atol=1e-3)
+    a = p_ref.clone()
+    PS.orthogonalize(a, plan, "p")
+    b = p_ref.cuda()
+    PS.orthogonalize(b, plan, "p")
+    torch.testing.assert_close(b.cpu(), a, rtol=1e-4, atol=1e-4)
+    out_ref = torch.zeros(lay.total)
+    PS.pqt(a, q_ref, plan, out_ref)
+    out_gpu = torch.zeros(lay.total, device="cuda")
+    PS.pqt(a.cuda(), q_ref.cuda(), plan, out_gpu)
+    torch.testing.assert_close(out_gpu.cpu(), out_ref, rtol=1e-4, atol=1e-4)
+
+
+def test_powersgd_allreduce_gpu_step():
+    x = torch.randn(512, 300, device="cuda")
+    grc = Allreduce(Z.PowerSGDCompressor(rank=4), M.PowerSGDMemory(compress_rank=4), comm=LocalComm())
+    out = grc.step(x, "w")
+    assert torch.isfinite(out).all()
+    # rank-4 approximation never exceeds the input energy
+    assert out.norm() <= x.norm() * 1.0001
+
+
+def test_segment_stats_gpu():
+    from grace_amd.ops import segstats as S
+
+    flat, lay = _bucket()
+    a = S.segment_stats(flat, lay)
+    b = S.segment_stats(flat.cuda(), lay).cpu()
+    torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-4)
