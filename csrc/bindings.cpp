@@ -478,7 +478,10 @@ std::string build_info() {
 
 }  // namespace
 
+void grace_bind_comm(py::module& m);  // csrc/comm/rccl_comm.cpp
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  grace_bind_comm(m);
   m.doc() = "grace_amd native CDNA4 kernels and RCCL runtime";
   m.def("build_info", &build_info);
   m.def("topk_select", &topk_select);

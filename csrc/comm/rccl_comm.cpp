@@ -1,0 +1,242 @@
+// Native RCCL communication runtime for grace_amd (one process per MI355X, RCCL over xGMI).
+//
+// The reference relies on Horovod's C++ core (background thread, handle table, poll /
+// synchronize -- /root/reference/patch_files/horovod/torch/mpi_ops.py:57-60, 407-439) for async
+// collectives.  Here the equivalent is small and stream-native:
+//
+//   * RcclComm owns its own ncclComm_t (bootstrapped from a unique id exchanged through the
+//     torch.distributed Store by the Python side) and a dedicated high-priority HIP stream;
+//   * every collective first makes the comm stream wait on the caller's current stream (an
+//     event, no host sync), is issued on the comm stream, and records a completion event;
+//   * Work::wait() makes the caller's current stream wait on that event (the host never
+//     blocks); Work::is_completed() polls it; Work::synchronize() blocks the host (debug);
+//   * group() batches several collectives into one ncclGroupStart/End (one launch for all
+//     payload tensors of many buckets);
+//   * a watchdog-friendly check_async_error() surfaces RCCL failures (peer death, timeouts)
+//     instead of hanging, and abort() tears the communicator down.
+//
+// Everything is graph-capturable: no allocation and no host synchronisation on the issue path.
+#include <torch/extension.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace grace_comm {
+
+using at::Tensor;
+
+#define RCCL_CHECK(expr)                                                                             \
+  do {                                                                                               \
+    ncclResult_t _r = (expr);                                                                        \
+    if (_r != ncclSuccess) throw std::runtime_error(std::string("RCCL error: ") + ncclGetErrorString(_r) + \
+                                                    " at " #expr);                                   \
+  } while (0)
+#define HIP_OK(expr)                                                                                 \
+  do {                                                                                               \
+    hipError_t _e = (expr);                                                                          \
+    if (_e != hipSuccess) throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(_e) + \
+                                                   " at " #expr);                                    \
+  } while (0)
+
+inline hipStream_t current_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+
+ncclDataType_t nccl_dtype(const Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return ncclFloat32;
+    case at::kHalf: return ncclFloat16;
+    case at::kBFloat16: return ncclBfloat16;
+    case at::kDouble: return ncclFloat64;
+    case at::kInt: return ncclInt32;
+    case at::kLong: return ncclInt64;
+    case at::kChar: return ncclInt8;
+    case at::kByte: return ncclUint8;
+    case at::kBool: return ncclUint8;
+    case at::kShort:
+    default: break;
+  }
+  throw std::runtime_error("unsupported dtype for RCCL");
+}
+
+ncclRedOp_t nccl_op(const std::string& op) {
+  if (op == "sum") return ncclSum;
+  if (op == "max") return ncclMax;
+  if (op == "min") return ncclMin;
+  if (op == "prod") return ncclProd;
+  if (op == "avg") return ncclAvg;
+  throw std::runtime_error("unsupported reduce op " + op);
+}
+
+class Work {
+ public:
+  explicit Work(int device) : device_(device) {
+    HIP_OK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
+  }
+  ~Work() { (void)hipEventDestroy(done_); }
+  hipEvent_t event() const { return done_; }
+  void wait() {  // stream-level: the caller's current stream waits, the host does not
+    HIP_OK(hipStreamWaitEvent(current_stream(), done_, 0));
+  }
+  bool is_completed() {
+    hipError_t e = hipEventQuery(done_);
+    if (e == hipSuccess) return true;
+    if (e == hipErrorNotReady) return false;
+    HIP_OK(e);
+    return false;
+  }
+  void synchronize() { HIP_OK(hipEventSynchronize(done_)); }
+
+ private:
+  int device_;
+  hipEvent_t done_;
+};
+
+py::bytes unique_id() {
+  ncclUniqueId id;
+  RCCL_CHECK(ncclGetUniqueId(&id));
+  return py::bytes(id.internal, NCCL_UNIQUE_ID_BYTES);
+}
+
+class RcclComm {
+ public:
+  RcclComm(int rank, int world, const std::string& id_bytes, int device, bool high_priority)
+      : rank_(rank), world_(world), device_(device) {
+    if ((int)id_bytes.size() != NCCL_UNIQUE_ID_BYTES) throw std::runtime_error("bad unique id size");
+    HIP_OK(hipSetDevice(device));
+    ncclUniqueId id;
+    std::memcpy(id.internal, id_bytes.data(), NCCL_UNIQUE_ID_BYTES);
+    RCCL_CHECK(ncclCommInitRank(&comm_, world, id, rank));
+    int lo = 0, hi = 0;
+    HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIP_OK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, high_priority ? hi : lo));
+    HIP_OK(hipEventCreateWithFlags(&fork_, hipEventDisableTiming));
+  }
+  ~RcclComm() {
+    if (comm_ != nullptr) (void)ncclCommDestroy(comm_);
+    if (stream_ != nullptr) (void)hipStreamDestroy(stream_);
+    (void)hipEventDestroy(fork_);
+  }
+
+  int rank() const { return rank_; }
+  int world_size() const { return world_; }
+  uintptr_t stream_ptr() const { return reinterpret_cast<uintptr_t>(stream_); }
+
+  std::shared_ptr<Work> all_gather(const Tensor& out, const Tensor& in) {
+    check(out);
+    check(in);
+    TORCH_CHECK(out.numel() == in.numel() * world_, "all_gather: out must be world_size x in");
+    TORCH_CHECK(out.scalar_type() == in.scalar_type(), "dtype mismatch");
+    begin();
+    RCCL_CHECK(ncclAllGather(in.data_ptr(), out.data_ptr(), in.numel(), nccl_dtype(in), comm_, stream_));
+    return end();
+  }
+
+  std::shared_ptr<Work> all_reduce(const Tensor& t, const std::string& op) {
+    check(t);
+    begin();
+    RCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t), nccl_op(op), comm_, stream_));
+    return end();
+  }
+
+  std::shared_ptr<Work> broadcast(const Tensor& t, int root) {
+    check(t);
+    begin();
+    RCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t), root, comm_, stream_));
+    return end();
+  }
+
+  std::shared_ptr<Work> reduce_scatter(const Tensor& out, const Tensor& in, const std::string& op) {
+    check(out);
+    check(in);
+    TORCH_CHECK(in.numel() == out.numel() * world_, "reduce_scatter: in must be world_size x out");
+    begin();
+    RCCL_CHECK(ncclReduceScatter(in.data_ptr(), out.data_ptr(), out.numel(), nccl_dtype(in), nccl_op(op), comm_,
+                                 stream_));
+    return end();
+  }
+
+  // Batched: all_gathers of (out_i, in_i) pairs and in-place sum all_reduces in ONE group.
+  std::shared_ptr<Work> group(const std::vector<std::pair<Tensor, Tensor>>& gathers,
+                              const std::vector<Tensor>& reduces) {
+    for (auto& g : gathers) {
+      check(g.first);
+      check(g.second);
+      TORCH_CHECK(g.first.numel() == g.second.numel() * world_, "group all_gather size");
+    }
+    for (auto& t : reduces) check(t);
+    begin();
+    RCCL_CHECK(ncclGroupStart());
+    for (auto& g : gathers)
+      RCCL_CHECK(ncclAllGather(g.second.data_ptr(), g.first.data_ptr(), g.second.numel(), nccl_dtype(g.second),
+                               comm_, stream_));
+    for (auto& t : reduces)
+      RCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t), ncclSum, comm_, stream_));
+    RCCL_CHECK(ncclGroupEnd());
+    return end();
+  }
+
+  std::string check_async_error() {
+    ncclResult_t r = ncclSuccess;
+    RCCL_CHECK(ncclCommGetAsyncError(comm_, &r));
+    return r == ncclSuccess ? std::string() : std::string(ncclGetErrorString(r));
+  }
+
+  void abort() {
+    if (comm_ != nullptr) {
+      (void)ncclCommAbort(comm_);
+      comm_ = nullptr;
+    }
+  }
+
+ private:
+  void check(const Tensor& t) {
+    TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "RCCL tensors must be contiguous GPU tensors");
+    TORCH_CHECK(t.get_device() == device_, "tensor on the wrong device");
+    TORCH_CHECK(comm_ != nullptr, "communicator aborted");
+  }
+  void begin() {
+    HIP_OK(hipEventRecord(fork_, current_stream()));
+    HIP_OK(hipStreamWaitEvent(stream_, fork_, 0));
+  }
+  std::shared_ptr<Work> end() {
+    auto w = std::make_shared<Work>(device_);
+    HIP_OK(hipEventRecord(w->event(), stream_));
+    return w;
+  }
+
+  int rank_, world_, device_;
+  ncclComm_t comm_ = nullptr;
+  hipStream_t stream_ = nullptr;
+  hipEvent_t fork_;
+};
+
+void bind(py::module& m) {
+  py::class_<Work, std::shared_ptr<Work>>(m, "RcclWork")
+      .def("wait", &Work::wait)
+      .def("is_completed", &Work::is_completed)
+      .def("synchronize", &Work::synchronize);
+  py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
+      .def(py::init<int, int, const std::string&, int, bool>(), py::arg("rank"), py::arg("world"),
+           py::arg("unique_id"), py::arg("device"), py::arg("high_priority") = true)
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def_property_readonly("world_size", &RcclComm::world_size)
+      .def_property_readonly("stream_ptr", &RcclComm::stream_ptr)
+      .def("all_gather", &RcclComm::all_gather)
+      .def("all_reduce", &RcclComm::all_reduce, py::arg("t"), py::arg("op") = "sum")
+      .def("broadcast", &RcclComm::broadcast)
+      .def("reduce_scatter", &RcclComm::reduce_scatter, py::arg("out"), py::arg("inp"), py::arg("op") = "sum")
+      .def("group", &RcclComm::group)
+      .def("check_async_error", &RcclComm::check_async_error)
+      .def("abort", &RcclComm::abort);
+  m.def("rccl_unique_id", &unique_id);
+}
+
+}  // namespace grace_comm
+
+// called from bindings.cpp's PYBIND11_MODULE
+void grace_bind_comm(py::module& m) { grace_comm::bind(m); }

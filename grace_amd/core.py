@@ -146,6 +146,7 @@ class Communicator(Stateful, ABC):
 
         self.compressor = compressor
         self.memory = memory
+        self.profiler = None  # grace_amd.utils.profiler.GraceProfiler (opt-in)
         self.comm = comm if comm is not None else default_comm()
         self.world_size = int(world_size) if world_size is not None else self.comm.world_size
         if self.world_size != self.comm.world_size:
@@ -165,21 +166,31 @@ class Communicator(Stateful, ABC):
         return self.wait_receive(self.async_send(tensors, name), ctx)
 
     # -------------------------------------------------------------- split-phase API
+    def _prof(self):
+        from .utils.profiler import NULL
+
+        return self.profiler if self.profiler is not None else NULL
+
     def compress_step(self, tensor: torch.Tensor, name: str):
-        fused = self.compressor.fused_compress(tensor, name, self.memory)
-        if fused is not None:
-            return fused
-        tensor = self.memory.compensate(tensor, name)
-        payload, ctx = self.compressor.compress(tensor, name)
-        self.memory.update(tensor, name, self.compressor, payload, ctx)
-        return payload, ctx
+        with self._prof().phase("compress", name):
+            fused = self.compressor.fused_compress(tensor, name, self.memory)
+            if fused is not None:
+                return fused
+            tensor = self.memory.compensate(tensor, name)
+            payload, ctx = self.compressor.compress(tensor, name)
+            self.memory.update(tensor, name, self.compressor, payload, ctx)
+            return payload, ctx
 
     def send_step(self, tensor: torch.Tensor, name: str):
         payload, ctx = self.compress_step(tensor, name)
-        return self.async_send(payload, name), ctx
+        prof = self._prof()
+        prof.add_bytes(sum(t.numel() * t.element_size() for t in payload))
+        with prof.phase("comm_issue", name):
+            return self.async_send(payload, name), ctx
 
     def receive_step(self, handles, ctx):
-        return self.wait_receive(handles, ctx)
+        with self._prof().phase("comm_wait_decompress", ""):
+            return self.wait_receive(handles, ctx)
 
     @abstractmethod
     def async_send(self, tensors: Sequence[torch.Tensor], name: str):

@@ -22,15 +22,14 @@ but more kernel launches.  288 GB of HBM per GPU makes the extra flat buffers ir
 """
 from __future__ import annotations
 
-import itertools
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 
 from ..core import Communicator, register_layout
 from ..ops.layout import SegmentLayout
+from ..ops.randomk import fnv1a64
 
-_ENGINE_IDS = itertools.count()
 
 
 def _record_stream(obj, stream, _depth=0):
@@ -60,7 +59,17 @@ class Bucket:
         self.layout = SegmentLayout.from_tensors(params)
         register_layout(name, self.layout)
         self.flat = torch.zeros(self.layout.total, dtype=dtype, device=device)
-        for p, v in zip(params, self.layout.views(self.flat)):
+        self.views = []
+        for (_, o, n), p in zip(self.layout.segments(), params):
+            seg = self.flat[o:o + n]
+            if (not p.is_contiguous() and p.dim() == 4 and p.is_contiguous(memory_format=torch.channels_last)):
+                # keep the parameter's memory format (channels_last convs): AccumulateGrad then
+                # adds in place with no layout-conversion copy; the segment is the gradient's
+                # memory image, per-tensor compression is order independent
+                v = seg.as_strided(p.shape, p.stride())
+            else:
+                v = seg.view(p.shape)
+            self.views.append(v)
             p.grad = v  # gradients accumulate straight into the bucket buffer
         self.pending = len(params)
         self.handles = None
@@ -87,22 +96,27 @@ class GraceEngine:
         if len(set(names)) != len(names):
             raise ValueError("parameter names must be unique")
         self.device = named[0][1].device
-        eid = next(_ENGINE_IDS)
         cap = int(bucket_cap_mb * 1024 * 1024 / 4)
-        self.buckets: List[Bucket] = []
-        cur: List[torch.nn.Parameter] = []
+        groups: List[List[Tuple[str, torch.nn.Parameter]]] = []
+        cur: List[Tuple[str, torch.nn.Parameter]] = []
         size = 0
         for n, p in reversed(named):  # backward order
             if cur and size + p.numel() > cap:
-                self.buckets.append(Bucket(f"grace{eid}.bucket{len(self.buckets)}", cur, self.device))
+                groups.append(cur)
                 cur, size = [], 0
-            cur.append(p)
+            cur.append((n, p))
             size += p.numel()
         if cur:
-            self.buckets.append(Bucket(f"grace{eid}.bucket{len(self.buckets)}", cur, self.device))
+            groups.append(cur)
+        # deterministic bucket names (same on every rank and across restarts, so GRACE state
+        # in checkpoints -- residuals, momenta, step counters -- maps back to its bucket)
+        self.buckets: List[Bucket] = []
+        for i, grp in enumerate(groups):
+            sig = ";".join(f"{n}:{tuple(p.shape)}" for n, p in grp).encode()
+            self.buckets.append(Bucket(f"grace.b{i}.{fnv1a64(sig):016x}", [p for _, p in grp], self.device))
         self._where: Dict[int, Tuple[Bucket, int, torch.Tensor]] = {}
         for b in self.buckets:
-            for i, (p, v) in enumerate(zip(b.params, b.layout.views(b.flat))):
+            for i, (p, v) in enumerate(zip(b.params, b.views)):
                 self._where[id(p)] = (b, i, v)
         self._passes: Dict[int, int] = {}
         self._hooks = []

@@ -1,0 +1,86 @@
+"""Python face of the native RCCL runtime (csrc/comm/rccl_comm.cpp).
+
+``RcclComm.from_process_group()`` bootstraps a dedicated RCCL communicator for GRACE traffic:
+rank 0 creates the unique id, it travels through the torch.distributed Store (no extra
+rendezvous), every rank calls ncclCommInitRank on its own GPU.  Collectives run on the
+runtime's own high-priority HIP stream, ordered after the caller's current stream by an event;
+``Work.wait()`` is stream-level (the host never blocks).  Select it for the default comm with
+``GRACE_AMD_COMM=native``.
+"""
+from __future__ import annotations
+
+import itertools
+
+import torch
+import torch.distributed as dist
+
+from . import comm as _comm
+from ..ops import _native
+
+_UID_COUNTER = itertools.count()
+
+
+class RcclComm(_comm.Comm):
+    def __init__(self, rank: int, world: int, unique_id: bytes, device: int, high_priority: bool = True):
+        C = _native.lib()
+        self._c = C.RcclComm(rank, world, unique_id, device, high_priority)
+        self.rank, self.world_size, self.device = rank, world, device
+        self._stream = torch.cuda.ExternalStream(self._c.stream_ptr, device=torch.device("cuda", device))
+
+    @classmethod
+    def from_process_group(cls, group=None, high_priority: bool = True) -> "RcclComm":
+        if not dist.is_initialized():
+            raise RuntimeError("torch.distributed must be initialised (it provides the Store)")
+        rank = dist.get_rank(group)
+        world = dist.get_world_size(group)
+        store = dist.distributed_c10d._get_default_store()
+        key = f"grace_amd/rccl_uid/{next(_UID_COUNTER)}"
+        if rank == 0:
+            uid = _native.lib().rccl_unique_id()
+            store.set(key, uid)
+        else:
+            uid = store.get(key)
+        return cls(rank, world, bytes(uid), torch.cuda.current_device(), high_priority)
+
+    @property
+    def stream(self) -> torch.cuda.Stream:
+        return self._stream
+
+    def _mark(self, *ts):
+        for t in ts:
+            t.record_stream(self._stream)
+
+    def _ret(self, w, async_op):
+        if not async_op:
+            w.wait()
+            return _comm.Work()
+        return _comm.Work([w])
+
+    def all_reduce(self, t, op="sum", async_op=False):
+        self._mark(t)
+        return self._ret(self._c.all_reduce(t, op), async_op)
+
+    def all_gather_into(self, out, inp, async_op=False):
+        self._mark(out, inp)
+        return self._ret(self._c.all_gather(out.view(-1), inp.view(-1)), async_op)
+
+    def broadcast(self, t, src, async_op=False):
+        self._mark(t)
+        return self._ret(self._c.broadcast(t, src), async_op)
+
+    def reduce_scatter(self, out, inp, op="sum", async_op=False):
+        self._mark(out, inp)
+        return self._ret(self._c.reduce_scatter(out, inp, op), async_op)
+
+    def barrier(self):
+        t = torch.zeros(1, device=torch.device("cuda", self.device))
+        self._c.all_reduce(t, "sum").synchronize()
+
+    def check(self):
+        """Raise if RCCL reported an asynchronous error (peer failure, timeout)."""
+        err = self._c.check_async_error()
+        if err:
+            raise RuntimeError(f"RCCL async error: {err}")
+
+    def abort(self):
+        self._c.abort()

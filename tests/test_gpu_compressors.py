@@ -157,10 +157,11 @@ def test_powersgd_mfma_matches_torch(rank):
     xg, qg = flat.cuda(), q.cuda()
     p_ref = PS.mq(flat, q, plan)
     p_gpu = PS.mq(xg, qg, plan)
-    torch.testing.assert_close(p_gpu.cpu(), p_ref, rtol=1e-4, atol=1e-3)
+    # fp32 sums of up to 4096 terms in a different order: compare against the output scale
+    torch.testing.assert_close(p_gpu.cpu(), p_ref, rtol=1e-4, atol=2e-6 * p_ref.abs().max().item())
     q_ref = PS.mtp(flat, p_ref, plan)
     q_gpu = PS.mtp(xg, p_ref.cuda(), plan)
-    torch.testing.assert_close(q_gpu.cpu(), q_ref, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(q_gpu.cpu(), q_ref, rtol=1e-4, atol=2e-6 * q_ref.abs().max().item())
     a = p_ref.clone()
     PS.orthogonalize(a, plan, "p")
     b = p_ref.cuda()
