@@ -14,6 +14,7 @@
 // The only host sync left is reading the final element count (payload size is data dependent).
 #include "grace_common.h"
 #include "grace_kernels.h"
+#include "grace_scan.h"
 
 namespace grace {
 namespace {
@@ -97,38 +98,49 @@ __global__ void dgc_adjust_kernel(int n_seg, const float* __restrict__ target, f
   count[s] = 0;  // recounted by the next dgc_count
 }
 
-__device__ __forceinline__ unsigned long long lanemask_lt() {
-  const int l = lane_id();
-  return (l == 0) ? 0ull : (~0ull >> (64 - l));
-}
+constexpr int kPer = 32;
+constexpr int kTile = kBlock * kPer;
 
+// |x| >= thr[seg] -> (value, flat index); one atomic per 256x32 tile (grace_scan.h)
 __global__ __launch_bounds__(kBlock) void dgc_compact_kernel(ChunkTable ct, const float* __restrict__ x,
                                                              const float* __restrict__ thr,
                                                              float* __restrict__ out_val,
                                                              int32_t* __restrict__ out_idx,
                                                              int32_t* __restrict__ counter) {
+  __shared__ int lds[kBlock / kWave];
+  __shared__ int bcast;
   const int c = blockIdx.x;
   const int s = ct.seg[c];
   const int64_t b = ct.begin[c], e = ct.end[c];
   const float t = thr[s];
-  const int64_t steps = (e - b + kBlock - 1) / kBlock;
-  for (int64_t k = 0; k < steps; ++k) {
-    const int64_t i = b + k * kBlock + threadIdx.x;
-    const bool valid = i < e;
-    const float v = valid ? x[i] : 0.f;
-    const bool take = valid && fabsf(v) >= t;
-    const unsigned long long m = __ballot(take);
-    if (m) {
-      int32_t base = 0;
-      const int leader = __ffsll((long long)m) - 1;
-      if (lane_id() == leader) base = atomicAdd(counter, __popcll(m));
-      base = __shfl(base, leader, kWave);
-      if (take) {
-        const int32_t p = base + __popcll(m & lanemask_lt());
-        out_val[p] = v;
-        out_idx[p] = (int32_t)i;
+  for (int64_t tb = b; tb < e; tb += kTile) {
+    float v[kPer];
+    uint32_t take = 0;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int64_t i = tb + (int64_t)j * kBlock + threadIdx.x;
+      v[j] = 0.f;
+      if (i < e) {
+        v[j] = x[i];
+        take |= (fabsf(v[j]) >= t ? 1u : 0u) << j;
       }
     }
+    int tot = 0;
+    const int pre = block_exclusive_scan<kBlock>(__popc(take), lds, &tot);
+    if (tot > 0) {
+      if (threadIdx.x == 0) bcast = atomicAdd(counter, tot);
+      __syncthreads();
+      int p = bcast + pre;
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        if ((take >> j) & 1u) {
+          out_val[p] = v[j];
+          out_idx[p] = (int32_t)(tb + (int64_t)j * kBlock + threadIdx.x);
+          ++p;
+        }
+      }
+    }
+    __syncthreads();
   }
 }
 

@@ -9,11 +9,12 @@
 //                      rank gets bit-identical results; serves Allgather AND Allreduce)
 //
 // Threshold (reference threshold.py:6-27): |x| > thr  -> (value, flat index), compacted with one
-//   64-lane ballot + one atomic per wave; fused error feedback (x = beta*r + gamma*g, residual =
+//   workgroup prefix sum + one atomic per 8192-element tile; fused error feedback (x = beta*r + gamma*g, residual =
 //   x with the sent entries zeroed) in the same pass.
 #include "grace_common.h"
 #include "grace_kernels.h"
 #include "grace_rand.h"
+#include "grace_scan.h"
 
 namespace grace {
 namespace {
@@ -70,42 +71,56 @@ __global__ __launch_bounds__(kBlock) void randk_scatter_kernel(const float* __re
   }
 }
 
-__device__ __forceinline__ unsigned long long lanemask_lt() {
-  const int l = lane_id();
-  return (l == 0) ? 0ull : (~0ull >> (64 - l));
-}
-
 // mode 0: x = g ; mode 1: x = beta*r + gamma*g (and residual written when resid != nullptr)
+// Tiles of 256 x 32 elements; ONE atomic per tile reserves the output (grace_scan.h).
+constexpr int kPer = 32;
+constexpr int kTile = kBlock * kPer;
+
 __global__ __launch_bounds__(kBlock) void threshold_compact_kernel(const float* g, const float* r, int mode,
                                                                    float beta, float gamma, int64_t n,
                                                                    float thr, float* __restrict__ out_val,
                                                                    int32_t* __restrict__ out_idx,
                                                                    int32_t* __restrict__ counter,
                                                                    float* resid) {
-  const int64_t stride = (int64_t)gridDim.x * kBlock;
-  const int64_t steps = (n + stride - 1) / stride;
-  for (int64_t s = 0; s < steps; ++s) {
-    const int64_t i = s * stride + (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    const bool valid = i < n;
-    float v = 0.f;
-    if (valid) {
-      v = g[i];
-      if (mode == 1) v = fmaf(beta, r[i], gamma * v);
-    }
-    const bool take = valid && fabsf(v) > thr;
-    const unsigned long long m = __ballot(take);
-    if (m) {
-      int32_t base = 0;
-      const int leader = __ffsll((long long)m) - 1;
-      if (lane_id() == leader) base = atomicAdd(counter, __popcll(m));
-      base = __shfl(base, leader, kWave);
-      if (take) {
-        const int32_t p = base + __popcll(m & lanemask_lt());
-        out_val[p] = v;
-        out_idx[p] = (int32_t)i;
+  __shared__ int lds[kBlock / kWave];
+  __shared__ int bcast;
+  for (int64_t tb = (int64_t)blockIdx.x * kTile; tb < n; tb += (int64_t)gridDim.x * kTile) {
+    float v[kPer];
+    uint32_t take = 0;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int64_t i = tb + (int64_t)j * kBlock + threadIdx.x;
+      v[j] = 0.f;
+      if (i < n) {
+        float x = g[i];
+        if (mode == 1) x = fmaf(beta, r[i], gamma * x);
+        v[j] = x;
+        take |= (fabsf(x) > thr ? 1u : 0u) << j;
       }
     }
-    if (resid != nullptr && valid) resid[i] = take ? 0.f : v;
+    int tot = 0;
+    const int pre = block_exclusive_scan<kBlock>(__popc(take), lds, &tot);
+    if (tot > 0) {
+      if (threadIdx.x == 0) bcast = atomicAdd(counter, tot);
+      __syncthreads();
+      int p = bcast + pre;
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        if ((take >> j) & 1u) {
+          out_val[p] = v[j];
+          out_idx[p] = (int32_t)(tb + (int64_t)j * kBlock + threadIdx.x);
+          ++p;
+        }
+      }
+    }
+    if (resid != nullptr) {
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        const int64_t i = tb + (int64_t)j * kBlock + threadIdx.x;
+        if (i < n) resid[i] = ((take >> j) & 1u) ? 0.f : v[j];
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -136,8 +151,10 @@ void threshold_compact(const float* g, const float* r, int mode, float beta, flo
                        float* out_val, int32_t* out_idx, int32_t* counter, float* resid, hipStream_t stream) {
   GRACE_HIP_CHECK(hipMemsetAsync(counter, 0, sizeof(int32_t), stream));
   if (n <= 0) return;
-  threshold_compact_kernel<<<grid_for(n), kBlock, 0, stream>>>(g, r, mode, beta, gamma, n, thr, out_val, out_idx,
-                                                               counter, resid);
+  int64_t tiles = (n + kTile - 1) / kTile;
+  if (tiles > 2048) tiles = 2048;
+  threshold_compact_kernel<<<(int)tiles, kBlock, 0, stream>>>(g, r, mode, beta, gamma, n, thr, out_val, out_idx,
+                                                              counter, resid);
 }
 
 }  // namespace grace

@@ -20,6 +20,7 @@
 // the choice among equal |x| at the threshold.
 #include "grace_common.h"
 #include "grace_kernels.h"
+#include "grace_scan.h"
 
 namespace grace {
 
@@ -136,18 +137,22 @@ __global__ __launch_bounds__(kBlock) void topk_select_kernel(int n_seg, const in
   }
 }
 
-__device__ __forceinline__ unsigned long long lanemask_lt() {
-  const int l = lane_id();
-  return (l == 0) ? 0ull : (~0ull >> (64 - l));
-}
-
-// Compaction + residual.  One chunk per workgroup.
+// Compaction + residual.  One chunk per workgroup, processed in tiles of 256 x 32 elements.
 //   take = key > T  or  (key == T and rank-among-ties < ties)
+// Each thread keeps its 32 values in registers; output slots are reserved with ONE atomic per
+// tile (workgroup prefix sums, grace_scan.h) instead of one per wave -- the per-segment counter
+// is shared by every workgroup of the segment, so per-wave atomics serialised at the memory
+// side (measured 0.5 ms per 25M-element bucket before this change).
+constexpr int kPer = 32;
+constexpr int kTile = kBlock * kPer;
+
 __global__ __launch_bounds__(kBlock) void topk_compact_kernel(
     ChunkTable ct, const float* x, const TopkState* __restrict__ st,
     const int64_t* __restrict__ out_off, int32_t* __restrict__ counters /* [2*n_seg] */, int n_seg,
     float* __restrict__ out_val, int32_t* __restrict__ out_idx, float* resid,
     int64_t idx_base) {
+  __shared__ int lds[kBlock / kWave];
+  __shared__ int bcast[2];
   const int c = blockIdx.x;
   const int seg = ct.seg[c];
   const int64_t b = ct.begin[c], e = ct.end[c];
@@ -156,42 +161,60 @@ __global__ __launch_bounds__(kBlock) void topk_compact_kernel(
   const int64_t base_off = out_off[seg];
   int32_t* out_ctr = counters + seg;
   int32_t* tie_ctr = counters + n_seg + seg;
-  // Iterate over the chunk in whole-wave steps so ballots are full-width (inactive tail lanes
-  // simply vote 0).
-  const int64_t len = e - b;
-  const int64_t steps = (len + kBlock - 1) / kBlock;
-  for (int64_t s = 0; s < steps; ++s) {
-    const int64_t i = b + s * kBlock + threadIdx.x;
-    const bool valid = i < e;
-    float v = 0.f;
-    uint32_t key = 0;
-    if (valid) {
-      v = x[i];
-      key = abs_key(v);
-    }
-    bool take = valid && key > T;
-    const bool tie = valid && key == T;
-    const unsigned long long tmask = __ballot(tie);
-    if (tmask) {
-      int32_t tbase = 0;
-      const int leader = __ffsll((long long)tmask) - 1;
-      if (lane_id() == leader) tbase = atomicAdd(tie_ctr, __popcll(tmask));
-      tbase = __shfl(tbase, leader, kWave);
-      if (tie) take = (tbase + __popcll(tmask & lanemask_lt())) < ties;
-    }
-    const unsigned long long m = __ballot(take);
-    if (m) {
-      int32_t obase = 0;
-      const int leader = __ffsll((long long)m) - 1;
-      if (lane_id() == leader) obase = atomicAdd(out_ctr, __popcll(m));
-      obase = __shfl(obase, leader, kWave);
-      if (take) {
-        const int64_t p = base_off + obase + __popcll(m & lanemask_lt());
-        out_val[p] = v;
-        out_idx[p] = (int32_t)(i + idx_base);
+  for (int64_t tb = b; tb < e; tb += kTile) {
+    float v[kPer];
+    uint32_t take = 0, tie = 0;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int64_t i = tb + (int64_t)j * kBlock + threadIdx.x;
+      v[j] = 0.f;
+      if (i < e) {
+        v[j] = x[i];
+        const uint32_t key = abs_key(v[j]);
+        take |= (key > T ? 1u : 0u) << j;
+        tie |= (key == T ? 1u : 0u) << j;
       }
     }
-    if (resid != nullptr && valid) resid[i] = take ? 0.f : v;
+    // ties: rank every tie of the tile, keep the first `ties` over the whole segment
+    int tot_tie = 0;
+    const int ntie = __popc(tie);
+    const int tie_pre = block_exclusive_scan<kBlock>(ntie, lds, &tot_tie);
+    if (tot_tie > 0) {
+      if (threadIdx.x == 0) bcast[0] = atomicAdd(tie_ctr, tot_tie);
+      __syncthreads();
+      int r = bcast[0] + tie_pre;
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {  // static indices keep v[] in registers
+        if ((tie >> j) & 1u) {
+          if (r < ties) take |= 1u << j;
+          ++r;
+        }
+      }
+    }
+    int tot_take = 0;
+    const int ntake = __popc(take);
+    const int pre = block_exclusive_scan<kBlock>(ntake, lds, &tot_take);
+    if (tot_take > 0) {
+      if (threadIdx.x == 0) bcast[1] = atomicAdd(out_ctr, tot_take);
+      __syncthreads();
+      int64_t p = base_off + bcast[1] + pre;
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        if ((take >> j) & 1u) {
+          out_val[p] = v[j];
+          out_idx[p] = (int32_t)(tb + (int64_t)j * kBlock + threadIdx.x + idx_base);
+          ++p;
+        }
+      }
+    }
+    if (resid != nullptr) {
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        const int64_t i = tb + (int64_t)j * kBlock + threadIdx.x;
+        if (i < e) resid[i] = ((take >> j) & 1u) ? 0.f : v[j];
+      }
+    }
+    __syncthreads();  // lds / bcast reuse by the next tile
   }
 }
 

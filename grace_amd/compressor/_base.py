@@ -23,6 +23,9 @@ class Ctx:
     shape: torch.Size
     dtype: torch.dtype
     extra: Dict[str, Any] = field(default_factory=dict)
+    #: optional destination for the aggregated result (the engine passes the bucket buffer so
+    #: decompress writes the averaged gradient in place: no extra allocation / copy pass)
+    out: Any = None
 
 
 class BucketCompressor(Compressor):
@@ -64,6 +67,15 @@ class BucketCompressor(Compressor):
     @staticmethod
     def rows(per_rank):
         return rank_rows(per_rank)
+
+    @staticmethod
+    def out_buffer(ctx, device, zero: bool = False) -> torch.Tensor:
+        o = getattr(ctx, "out", None)
+        if o is not None and o.device == device and o.dtype == torch.float32 and o.numel() == ctx.layout.total \
+                and o.is_contiguous():
+            ctx.out = None  # one use
+            return o.view(-1).zero_() if zero else o.view(-1)
+        return (torch.zeros if zero else torch.empty)(ctx.layout.total, dtype=torch.float32, device=device)
 
     def finish(self, out: torch.Tensor, ctx: Ctx) -> torch.Tensor:
         return out.view(ctx.shape).to(ctx.dtype) if ctx.dtype != torch.float32 else out.view(ctx.shape)

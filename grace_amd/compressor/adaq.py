@@ -80,7 +80,7 @@ class AdaqCompressor(BucketCompressor):
         return [m, cnt, ix], ctx
 
     def decompress_aggregate_impl(self, per_rank, ctx, n_ranks, scale):
-        out = torch.zeros(ctx.layout.total, dtype=torch.float32, device=per_rank[0][0].device)
+        out = self.out_buffer(ctx, per_rank[0][0].device, zero=True)
         for means, counts, idx in per_rank:
             reps = counts.to(device=means.device, dtype=torch.int64)
             v = torch.repeat_interleave(means, reps)  # [plus_0.., minus_0.., plus_1.., ...]

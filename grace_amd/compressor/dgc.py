@@ -39,7 +39,7 @@ class DgcCompressor(BucketCompressor):
         return [vals, idx], ctx
 
     def decompress_aggregate_impl(self, per_rank, ctx, n_ranks, scale):
-        out = torch.zeros(ctx.layout.total, dtype=torch.float32, device=per_rank[0][0].device)
+        out = self.out_buffer(ctx, per_rank[0][0].device, zero=True)
         for v, i in per_rank:
             K.scatter_add(v, i, out, scale, accumulate=True)
         return self.finish(out, ctx)

@@ -66,7 +66,7 @@ class EFSignSGDCompressor(BucketCompressor):
 
     def decompress_aggregate_impl(self, per_rank, ctx, n_ranks, scale):
         base, stride, offs = self.rows(per_rank)
-        out = torch.empty(ctx.layout.total, dtype=torch.float32, device=base.device)
+        out = self.out_buffer(ctx, base.device)
         SB.sign_unpack(base, stride, offs[1], offs[0], n_ranks, ctx.layout, out, vote=False, scale=scale)
         return self.finish(out, ctx)
 

@@ -101,7 +101,7 @@ class INCEPTIONNCompressor(BucketCompressor):
 
     def decompress_aggregate_impl(self, per_rank, ctx, n_ranks, scale):
         dev = per_rank[0][0].device
-        out = torch.zeros(ctx.layout.total, dtype=torch.float32, device=dev)
+        out = self.out_buffer(ctx, dev, zero=True)
         for v32, v16, v8, packed in per_rank:
             out += self._decode(v32, v16, v8, packed, ctx.layout.total, dev)
         if scale != 1.0:

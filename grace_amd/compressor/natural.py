@@ -46,6 +46,6 @@ class NaturalCompressor(BucketCompressor):
 
     def decompress_aggregate_impl(self, per_rank, ctx, n_ranks, scale):
         base, stride, offs = self.rows(per_rank)
-        out = torch.empty(ctx.layout.total, dtype=torch.float32, device=base.device)
+        out = self.out_buffer(ctx, base.device)
         Q.natural_aggregate(base[offs[0]:], stride, n_ranks, out, scale)
         return self.finish(out, ctx)

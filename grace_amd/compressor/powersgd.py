@@ -91,7 +91,7 @@ class PowerSGDCompressor(BucketCompressor):
             (v,) = tensors
             out = v * vec_scale if vec_scale != 1.0 else v
             return self.finish(out.reshape(-1), ctx)
-        out = torch.empty(ctx.layout.total, dtype=torch.float32, device=dev)
+        out = self.out_buffer(ctx, dev)
         PS.pqt(ctx.extra["p"], ctx.extra["q"], plan, out)
         if tensors:
             PS.scatter_vectors(tensors[0], plan, out, vec_scale)

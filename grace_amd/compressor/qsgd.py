@@ -90,7 +90,7 @@ class QSGDCompressor(BucketCompressor):
                 rows.append(pb.tensors)
             per_rank = rows
         base, stride, offs = self.rows(per_rank)
-        out = torch.empty(ctx.layout.total, dtype=torch.float32, device=base.device)
+        out = self.out_buffer(ctx, base.device)
         Q.qsgd_aggregate(base, stride, offs[0], offs[1], per_rank[0][0].dtype, n_ranks, self.quantum_num, ctx.layout,
                          out, scale)
         return self.finish(out, ctx)

@@ -57,7 +57,7 @@ class SignSGDCompressor(BucketCompressor):
     def decompress_aggregate_impl(self, per_rank, ctx, n_ranks, scale):
         # one rank: 2b-1 (reference decompress); W ranks: majority vote (reference aggregate)
         base, stride, offs = self.rows(per_rank)
-        out = torch.empty(ctx.layout.total, dtype=torch.float32, device=base.device)
+        out = self.out_buffer(ctx, base.device)
         SB.sign_unpack(base, stride, offs[0], 0, n_ranks, ctx.layout, out, vote=True)
         return self.finish(out, ctx)
 

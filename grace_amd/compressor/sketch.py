@@ -54,7 +54,7 @@ class SketchCompressor(BucketCompressor):
 
     def decompress_aggregate_impl(self, per_rank, ctx, n_ranks, scale):
         lay, q = ctx.layout, self.quantiles
-        out = torch.zeros(lay.total, dtype=torch.float32, device=per_rank[0][0].device)
+        out = self.out_buffer(ctx, per_rank[0][0].device, zero=True)
         seg_id = torch.repeat_interleave(torch.arange(lay.n_seg, device=out.device),
                                          torch.tensor(lay.numels, device=out.device))
         for bins, means in per_rank:

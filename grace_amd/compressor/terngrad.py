@@ -58,6 +58,6 @@ class TernGradCompressor(BucketCompressor):
 
     def decompress_aggregate_impl(self, per_rank, ctx, n_ranks, scale):
         base, stride, offs = self.rows(per_rank)
-        out = torch.empty(ctx.layout.total, dtype=torch.float32, device=base.device)
+        out = self.out_buffer(ctx, base.device)
         Q.tern_aggregate(base, stride, offs[0], offs[1], n_ranks, ctx.layout, out, scale)
         return self.finish(out, ctx)

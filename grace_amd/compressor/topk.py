@@ -36,6 +36,7 @@ class TopKCtx:
     shape: torch.Size
     device: torch.device
     dtype: torch.dtype
+    out: object = None  # optional destination (see compressor._base.Ctx.out)
 
 
 class TopKCompressor(Compressor):
@@ -75,7 +76,10 @@ class TopKCompressor(Compressor):
         return out.view(ctx.shape).to(ctx.dtype)
 
     def decompress_aggregate(self, per_rank, ctx, world_size):
-        out = torch.zeros(ctx.numel, dtype=torch.float32, device=per_rank[0][0].device)
+        from ._base import BucketCompressor
+
+        out = BucketCompressor.out_buffer(ctx, per_rank[0][0].device, zero=True) if ctx.dtype == torch.float32 \
+            else torch.zeros(ctx.numel, dtype=torch.float32, device=per_rank[0][0].device)
         scale = (1.0 / world_size) if self.average else 1.0
         for vals, idx in per_rank:  # fixed rank order -> identical result on every rank
             K.scatter_add(vals, idx, out, scale, accumulate=True)

@@ -21,8 +21,9 @@ from .layout import SegmentLayout
 
 
 def k_per_segment(layout: SegmentLayout, ratio: float) -> Tuple[int, ...]:
-    """k_i = max(1, int(n_i * ratio)) -- reference topk.py:7."""
-    return tuple(min(n, max(1, int(n * ratio))) if n > 0 else 0 for n in layout.numels)
+    """k_i = max(1, int(n_i * ratio)) -- reference topk.py:7 (cached per layout)."""
+    return layout.cached("host", f"k:{ratio!r}",
+                         lambda: tuple(min(n, max(1, int(n * ratio))) if n > 0 else 0 for n in layout.numels))
 
 
 def _workspace(layout: SegmentLayout, ks: Sequence[int], device):

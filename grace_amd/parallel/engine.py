@@ -167,6 +167,8 @@ class GraceEngine:
             for b in self.buckets:
                 _record_stream((b.handles, b.ctx), cur)
         for b in self.buckets:
+            if hasattr(b.ctx, "out"):
+                b.ctx.out = b.flat  # decompress straight into the gradient bucket
             out = self.grc.receive_step(b.handles, b.ctx)
             if out.data_ptr() != b.flat.data_ptr():
                 b.flat.copy_(out.view(-1))

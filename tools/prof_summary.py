@@ -1,0 +1,75 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 ``--kernel-trace`` CSV over the steady-state steps of a bench run.
+
+Steps are delimited by a marker kernel (default: the last GRACE kernel of a step,
+``topk_compact_kernel``); the summary covers the last ``--steps`` steps: wall time per step
+(first kernel start -> last kernel end), busy GPU time per step (union of kernel intervals),
+and the top kernels by time, with grace_amd kernels tagged.
+
+    python tools/prof_summary.py gpurun_out/prof/run_kernel_trace.csv --steps 10 --marker topk_compact
+"""
+import argparse
+import collections
+import csv
+import re
+import sys
+
+
+def short(name: str) -> str:
+    name = re.sub(r"\(.*", "", name)
+    name = re.sub(r"<.*", "", name)
+    return name[:90]
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--marker", default="topk_compact_kernel")
+    ap.add_argument("--per-step-markers", type=int, default=0, help="marker kernels per step (0 = auto)")
+    ap.add_argument("--top", type=int, default=30)
+    args = ap.parse_args(argv)
+    rows = list(csv.DictReader(open(args.trace)))
+    ks = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows))
+    marks = [i for i, k in enumerate(ks) if args.marker in k[2]]
+    if not marks:
+        sys.exit(f"marker {args.marker!r} not found")
+    per = args.per_step_markers
+    if per == 0:  # markers per step: guess from the last gaps
+        per = 1
+    # window: from the end of the marker that closes step (last - steps) to the last marker
+    last = marks[-1]
+    first_idx = len(marks) - 1 - args.steps * per
+    start_t = ks[marks[first_idx]][1] if first_idx >= 0 else ks[0][0]
+    end_t = ks[last][1]
+    win = [k for k in ks if k[0] >= start_t and k[1] <= end_t]
+    busy, cur_s, cur_e = 0, None, None
+    for s, e, _ in win:
+        if cur_e is None or s > cur_e:
+            if cur_e is not None:
+                busy += cur_e - cur_s
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    if cur_e is not None:
+        busy += cur_e - cur_s
+    wall = end_t - start_t
+    agg = collections.defaultdict(lambda: [0, 0])
+    for s, e, n in win:
+        a = agg[short(n)]
+        a[0] += e - s
+        a[1] += 1
+    total = sum(v[0] for v in agg.values())
+    steps = args.steps
+    print(f"window: {steps} steps, wall {wall / 1e6 / steps:.3f} ms/step, GPU busy {busy / 1e6 / steps:.3f} ms/step "
+          f"({100 * busy / max(1, wall):.1f}%), kernels {len(win) / steps:.0f}/step, sum of kernel time "
+          f"{total / 1e6 / steps:.3f} ms/step")
+    grace = sum(v[0] for k, v in agg.items() if k.startswith("grace::") or "grace" in k)
+    print(f"grace_amd kernels: {grace / 1e6 / steps:.3f} ms/step ({100 * grace / max(1, total):.1f}% of kernel time)")
+    print(f"{'ms/step':>8} {'calls/step':>10}  kernel")
+    for n, (t, c) in sorted(agg.items(), key=lambda kv: -kv[1][0])[: args.top]:
+        print(f"{t / 1e6 / steps:8.3f} {c / steps:10.1f}  {n}")
+
+
+if __name__ == "__main__":
+    main()
