@@ -45,6 +45,9 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--no-benchmark-mode", action="store_true", help="disable MIOpen find (cudnn.benchmark)")
     ap.add_argument("--exposed-steps", type=int, default=3, help="untimed steps measuring exposed GRACE time")
+    ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
+                    help="capture the whole step (fwd+bwd+GRACE+optimizer) in a HIP graph; auto = on for "
+                         "graph-safe GRACE pipelines on a single GPU")
     return ap.parse_args()
 
 
@@ -83,24 +86,38 @@ def main():
 
     def step():
         opt.zero_grad()
-        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp, cache_enabled=False):
             loss = w.loss(model, data)
         loss.backward()
         opt.step()
         return loss
+
+    from grace_amd.parallel.graph import GraphedStep, graph_safe
+
+    use_graph = args.graph == "on" or (args.graph == "auto" and world == 1 and graph_safe(grc) is None)
+    graph_note = "off"
+    run = step
+    if use_graph:
+        try:
+            run = GraphedStep(step, warmup=max(3, args.warmup // 2))
+            graph_note = "on"
+        except Exception as e:  # capture unsupported -> stay eager
+            graph_note = f"failed: {type(e).__name__}: {str(e)[:120]}"
+            torch.cuda.synchronize()
+            run = step
 
     def barrier():
         if world > 1:
             dist.barrier(device_ids=[local])
 
     for _ in range(args.warmup):
-        step()
+        run()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = step()
+        loss = run()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -155,6 +172,7 @@ def main():
                 "grace": w.grace,
                 "bucket_mb": args.bucket_mb,
                 "overlap": not args.no_overlap,
+                "hip_graph": graph_note,
             },
             "comm_wall_ms": round(float(ex.item()) * 1e3, 3),
             "final_loss": round(float(loss.float().item()), 4),

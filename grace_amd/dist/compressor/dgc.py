@@ -1,0 +1,1 @@
+from ...compressor import DgcCompressor  # noqa: F401

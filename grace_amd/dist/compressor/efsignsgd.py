@@ -1,0 +1,1 @@
+from ...compressor import EFSignSGDCompressor  # noqa: F401

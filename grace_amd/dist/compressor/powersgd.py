@@ -1,0 +1,1 @@
+from ...compressor import PowerSGDCompressor  # noqa: F401

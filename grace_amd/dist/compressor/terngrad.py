@@ -1,0 +1,1 @@
+from ...compressor import TernGradCompressor  # noqa: F401

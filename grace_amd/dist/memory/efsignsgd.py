@@ -1,0 +1,1 @@
+from ...memory import EFSignSGDMemory  # noqa: F401

@@ -1,0 +1,1 @@
+from ...memory import NoneMemory  # noqa: F401

@@ -1,0 +1,1 @@
+from ...memory import ResidualMemory  # noqa: F401

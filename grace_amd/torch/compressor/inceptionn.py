@@ -1,0 +1,1 @@
+from ...compressor import INCEPTIONNCompressor  # noqa: F401
