@@ -45,9 +45,12 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--no-benchmark-mode", action="store_true", help="disable MIOpen find (cudnn.benchmark)")
     ap.add_argument("--exposed-steps", type=int, default=3, help="untimed steps measuring exposed GRACE time")
-    ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
-                    help="capture the whole step (fwd+bwd+GRACE+optimizer) in a HIP graph; auto = on for "
-                         "graph-safe GRACE pipelines on a single GPU")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="initialise the RCCL process group even for one GPU (exercises the collective path)")
+    ap.add_argument("--graph", choices=["auto", "full", "compute", "off"], default="auto",
+                    help="HIP graphs: full = whole step (fwd+bwd+GRACE+optimizer) captured; compute = "
+                         "forward+backward graphed, GRACE + optimizer eager (any comm backend); "
+                         "auto = full for graph-safe pipelines on one GPU, compute otherwise")
     return ap.parse_args()
 
 
@@ -66,8 +69,10 @@ def main():
         raise SystemExit("bench.py needs a GPU")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
+    if world > 1 or args.force_dist:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)  # RCCL over xGMI
     torch.backends.cudnn.benchmark = not args.no_benchmark_mode
 
     w = WORKLOADS[args.workload]
@@ -84,27 +89,42 @@ def main():
         data = (data[0].contiguous(memory_format=torch.channels_last),) + tuple(data[1:])
     amp = args.dtype == "bf16"
 
+    fwd_model = model
+
     def step():
         opt.zero_grad()
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp, cache_enabled=False):
-            loss = w.loss(model, data)
+            loss = w.loss(fwd_model, data)
         loss.backward()
         opt.step()
         return loss
 
-    from grace_amd.parallel.graph import GraphedStep, graph_safe
+    from grace_amd.parallel.graph import GraphedStep, graph_compute, graph_safe
 
-    use_graph = args.graph == "on" or (args.graph == "auto" and world == 1 and graph_safe(grc) is None)
+    mode = args.graph
+    if mode == "auto":
+        mode = "full" if (world == 1 and not args.force_dist and graph_safe(grc) is None) else "compute"
+    if mode == "compute" and not (isinstance(data, tuple) and data[0].is_floating_point()):
+        mode = "off"  # token-input models: graph only with the full-step capture
     graph_note = "off"
     run = step
-    if use_graph:
-        try:
+    try:
+        if mode == "full":
             run = GraphedStep(step, warmup=max(3, args.warmup // 2))
-            graph_note = "on"
-        except Exception as e:  # capture unsupported -> stay eager
-            graph_note = f"failed: {type(e).__name__}: {str(e)[:120]}"
-            torch.cuda.synchronize()
-            run = step
+            graph_note = "full"
+        elif mode == "compute":
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp, cache_enabled=False):
+                fwd_model = graph_compute(model, data[0], engine=opt.engine)
+            graph_note = "compute"
+    except Exception as e:  # capture unsupported -> stay eager
+        graph_note = f"failed: {type(e).__name__}: {str(e)[:120]}"
+        torch.cuda.synchronize()
+        fwd_model, run = model, step
+    if dist.is_initialized():  # every rank must run the same mode (collective sequences must match)
+        ok = torch.tensor([0 if graph_note.startswith("failed") else 1], device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if ok.item() == 0 and not graph_note.startswith("failed"):
+            graph_note, fwd_model, run = "off (a peer failed to capture)", model, step
 
     def barrier():
         if world > 1:
@@ -133,8 +153,8 @@ def main():
     exposed = []
     for _ in range(args.exposed_steps):
         opt.zero_grad()
-        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
-            l2 = w.loss(model, data)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp, cache_enabled=False):
+            l2 = w.loss(fwd_model, data)
         l2.backward()
         torch.cuda.synchronize()
         barrier()
@@ -178,7 +198,7 @@ def main():
             "final_loss": round(float(loss.float().item()), 4),
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -125,9 +125,26 @@ class GraceEngine:
             for p in b.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._hook))
         self.in_flight = 0
+        self._paused = False
 
     # ------------------------------------------------------------------ backward hooks
+    def pause(self):
+        """Context manager: backward passes inside do not trigger the GRACE exchange (used while
+        warming up / capturing graphed forward-backward callables)."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def _ctx():
+            self._paused = True
+            try:
+                yield
+            finally:
+                self._paused = False
+        return _ctx()
+
     def _hook(self, p: torch.Tensor):
+        if self._paused:
+            return
         b, idx, view = self._where[id(p)]
         cnt = self._passes.get(id(p), 0) + 1
         if cnt < self.backward_passes_per_step:

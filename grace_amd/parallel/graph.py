@@ -65,3 +65,19 @@ class GraphedStep:
     def __call__(self) -> torch.Tensor:
         self.graph.replay()
         return self.loss
+
+
+def graph_compute(model: torch.nn.Module, sample_input: torch.Tensor, engine=None, warmup: int = 3):
+    """Capture only the model's forward and backward (``torch.cuda.make_graphed_callables``);
+    gradient accumulation, the GRACE exchange and the optimizer stay eager.  Works with any
+    communication backend (no collective inside the graph), so it is the multi-GPU-safe graph
+    mode; ~1000 eager launches per ResNet-50 step become 2 graph launches.
+    ``engine`` (a GraceEngine) is paused during the warm-up/capture backward passes."""
+    import contextlib
+
+    ctx = engine.pause() if engine is not None else contextlib.nullcontext()
+    with ctx:
+        g = torch.cuda.make_graphed_callables(model, (sample_input,), num_warmup_iters=warmup)
+    if engine is not None:
+        engine.zero_grad()
+    return g
