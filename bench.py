@@ -48,9 +48,9 @@ def parse():
     ap.add_argument("--force-dist", action="store_true",
                     help="initialise the RCCL process group even for one GPU (exercises the collective path)")
     ap.add_argument("--graph", choices=["auto", "full", "compute", "off"], default="auto",
-                    help="HIP graphs: full = whole step (fwd+bwd+GRACE+optimizer) captured; compute = "
-                         "forward+backward graphed, GRACE + optimizer eager (any comm backend); "
-                         "auto = full for graph-safe pipelines on one GPU, compute otherwise")
+                    help="HIP graphs: full = whole step (fwd+bwd+GRACE+RCCL+optimizer) captured; compute = "
+                         "forward+backward graphed, GRACE + optimizer eager; auto = full for graph-safe "
+                         "GRACE pipelines (any world size), eager otherwise")
     return ap.parse_args()
 
 
@@ -103,7 +103,9 @@ def main():
 
     mode = args.graph
     if mode == "auto":
-        mode = "full" if (world == 1 and not args.force_dist and graph_safe(grc) is None) else "compute"
+        # measured on MI355X (ResNet-50 Top-K 1%): full 3205 img/s, compute 2640, eager 2520-3240
+        # (eager is host-launch bound: ~1100 kernels per step)
+        mode = "full" if graph_safe(grc) is None else "off"
     if mode == "compute" and not (isinstance(data, tuple) and data[0].is_floating_point()):
         mode = "off"  # token-input models: graph only with the full-step capture
     graph_note = "off"

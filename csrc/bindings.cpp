@@ -422,6 +422,51 @@ void philox_normal(const Tensor& out, int64_t seed) {
   grace::philox_normal(out.data_ptr<float>(), out.numel(), (uint64_t)seed, cur_stream());
 }
 
+// ------------------------------------------------------------------------------ 16-bit cast, sketch
+void cast16(const Tensor& x, const Tensor& y, bool bf16) {
+  CHECK_F32(x);
+  CHECK_DEV(y);
+  CHECK_CONTIG(y);
+  TORCH_CHECK(y.element_size() == 2 && y.numel() >= x.numel(), "y must be a 16-bit tensor of numel >= x");
+  DevGuard guard(x.device());
+  grace::cast16(x.data_ptr<float>(), reinterpret_cast<uint16_t*>(y.data_ptr()), x.numel(), bf16, cur_stream());
+}
+
+void decode16_sum(const Tensor& base, int64_t rank_stride, int64_t n_ranks, bool bf16, double scale,
+                  const Tensor& out) {
+  CHECK_F32(out);
+  check_rows(base, rank_stride, n_ranks, 2 * out.numel());
+  DevGuard guard(out.device());
+  grace::decode16_sum(base.data_ptr<uint8_t>(), rank_stride, (int)n_ranks, out.numel(), bf16, (float)scale,
+                      out.data_ptr<float>(), cur_stream());
+}
+
+void sketch_encode(const Tensor& x, const Tensor& edges, int64_t q, const Tensor& bins, const Tensor& sums,
+                   const Tensor& counts, const Tensor& seg, const Tensor& cb, const Tensor& ce) {
+  CHECK_F32(x);
+  CHECK_F32(edges);
+  CHECK_F32(sums);
+  CHECK_F32(counts);
+  CHECK_DEV(bins);
+  TORCH_CHECK(q >= 1 && q <= 1024, "quantiles must be in [1, 1024]");
+  TORCH_CHECK(bins.numel() >= x.numel(), "bins too small");
+  auto ct = make_ct(seg, cb, ce);
+  DevGuard guard(x.device());
+  grace::sketch_encode(ct, x.data_ptr<float>(), edges.data_ptr<float>(), (int)q, bins.data_ptr(),
+                       (int)bins.element_size(), sums.data_ptr<float>(), counts.data_ptr<float>(), cur_stream());
+}
+
+void sketch_decode(const Tensor& base, int64_t rank_stride, int64_t bins_off, int64_t means_off, int64_t q,
+                   int64_t bin_bytes, int64_t n_ranks, double scale, const Tensor& out, const Tensor& seg,
+                   const Tensor& cb, const Tensor& ce, int64_t n_seg) {
+  CHECK_F32(out);
+  check_rows(base, rank_stride, n_ranks, std::max(bins_off + bin_bytes * out.numel(), means_off + 4 * q * n_seg));
+  auto ct = make_ct(seg, cb, ce);
+  DevGuard guard(out.device());
+  grace::sketch_decode(ct, base.data_ptr<uint8_t>(), rank_stride, bins_off, means_off, (int)q, (int)bin_bytes,
+                       (int)n_ranks, (float)scale, out.data_ptr<float>(), cur_stream());
+}
+
 // ------------------------------------------------------------------------------ segment stats
 void segment_stats(const Tensor& x, const c10::optional<Tensor>& r, int64_t mode, double beta, double gamma,
                    const c10::optional<Tensor>& xout, const Tensor& seg, const Tensor& cb, const Tensor& ce,
@@ -508,6 +553,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gram_schmidt", &gram_schmidt);
   m.def("powersgd_pqt", &powersgd_pqt);
   m.def("philox_normal", &philox_normal);
+  m.def("cast16", &cast16);
+  m.def("decode16_sum", &decode16_sum);
+  m.def("sketch_encode", &sketch_encode);
+  m.def("sketch_decode", &sketch_decode);
   m.def("axpby", &axpby);
   m.def("scale_", &scale_);
 }

@@ -21,6 +21,7 @@
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <cstring>
 #include <memory>
 #include <stdexcept>
@@ -43,6 +44,11 @@ using at::Tensor;
     if (_e != hipSuccess) throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(_e) + \
                                                    " at " #expr);                                    \
   } while (0)
+
+// Set from Python's atexit: once the interpreter is shutting down the HIP runtime / RCCL may
+// already be torn down, so destructors must not call into them (leaking at exit is harmless).
+static std::atomic<bool> g_exiting{false};
+void mark_exiting() { g_exiting.store(true); }
 
 inline hipStream_t current_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
 
@@ -77,7 +83,9 @@ class Work {
   explicit Work(int device) : device_(device) {
     HIP_OK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
   }
-  ~Work() { (void)hipEventDestroy(done_); }
+  ~Work() {
+    if (!g_exiting.load()) (void)hipEventDestroy(done_);
+  }
   hipEvent_t event() const { return done_; }
   void wait() {  // stream-level: the caller's current stream waits, the host does not
     HIP_OK(hipStreamWaitEvent(current_stream(), done_, 0));
@@ -117,8 +125,12 @@ class RcclComm {
     HIP_OK(hipEventCreateWithFlags(&fork_, hipEventDisableTiming));
   }
   ~RcclComm() {
+    if (g_exiting.load()) return;
     if (comm_ != nullptr) (void)ncclCommDestroy(comm_);
-    if (stream_ != nullptr) (void)hipStreamDestroy(stream_);
+    // The comm stream is deliberately NOT destroyed: tensors that crossed it were
+    // record_stream()-ed, and the caching allocator records events on that stream when those
+    // tensors are freed -- possibly after this communicator is gone (a destroyed stream there
+    // segfaults).  One leaked stream per communicator lifetime is the price.
     (void)hipEventDestroy(fork_);
   }
 
@@ -234,6 +246,7 @@ void bind(py::module& m) {
       .def("check_async_error", &RcclComm::check_async_error)
       .def("abort", &RcclComm::abort);
   m.def("rccl_unique_id", &unique_id);
+  m.def("rccl_mark_exiting", &mark_exiting);
 }
 
 }  // namespace grace_comm

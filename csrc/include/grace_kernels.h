@@ -87,6 +87,15 @@ void powersgd_pqt(const float* P, const float* Q, float* out, const int64_t* mat
                   hipStream_t stream);
 void philox_normal(float* out, int64_t n, uint64_t seed, hipStream_t stream);
 
+// ---------------------------------------------------------------- cast_sketch.hip
+void cast16(const float* x, uint16_t* y, int64_t n, bool bf16, hipStream_t stream);
+void decode16_sum(const uint8_t* base, int64_t rank_stride, int n_ranks, int64_t n, bool bf16, float scale, float* out,
+                  hipStream_t stream);
+void sketch_encode(const ChunkTable& ct, const float* x, const float* edges, int q, void* bins, int bin_bytes,
+                   float* sums, float* counts, hipStream_t stream);
+void sketch_decode(const ChunkTable& ct, const uint8_t* base, int64_t rank_stride, int64_t bins_off, int64_t means_off,
+                   int q, int bin_bytes, int n_ranks, float scale, float* out, hipStream_t stream);
+
 // ---------------------------------------------------------------- ef.hip (elementwise)
 void axpby(const float* x, const float* y, float* out, int64_t n, float a, float b, hipStream_t stream);
 void scale_inplace(float* x, int64_t n, float s, hipStream_t stream);

@@ -6,13 +6,15 @@ quantile edges of x (tfp.stats.quantiles), bin of every element (tfp find_bins),
 
 Here per segment: edges from torch.quantile (linear interpolation, as the reference), bins by
 searchsorted clamped to [0, q-1] (values equal to the last edge go to the last bin), bin means
-by index_add.  Payload [bins uint8/int16 | means fp32 (q per segment)].  PyTorch-ROCm ops (no
-dedicated HIP kernel yet).
+by index_add.  Payload [bins uint8/int16 | means fp32 (q per segment)].  On the GPU the edges of
+ALL segments come from one segmented sort, and bucketisation + per-bin sums/counts
+(csrc/kernels/cast_sketch.hip) and the W-rank decode are single passes.
 """
 from __future__ import annotations
 
 import torch
 
+from ..ops import _native
 from ._base import BucketCompressor
 
 
@@ -25,6 +27,27 @@ def _quantiles(seg: torch.Tensor, probs: torch.Tensor) -> torch.Tensor:
     hi = pos.ceil().long()
     w = pos - lo.float()
     return srt[lo] * (1 - w) + srt[hi] * w
+
+
+def segmented_quantile_edges(x: torch.Tensor, lay, q: int) -> torch.Tensor:
+    """[n_seg, q+1] linear-interpolation quantile edges of every segment from ONE sort of the
+    bucket (keys = segment id << 32 | order-preserving float bits)."""
+    dev = x.device
+    seg_id = lay.cached(dev, "seg_id", lambda: torch.repeat_interleave(
+        torch.arange(lay.n_seg, device=dev), torch.tensor(lay.numels, device=dev)))
+    u = x.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    ordered = torch.where(u >= 0x80000000, (~u) & 0xFFFFFFFF, u | 0x80000000)
+    order = torch.sort((seg_id << 32) | ordered).indices
+    sx = x[order]
+    offs = torch.tensor(lay.offsets[:-1], device=dev, dtype=torch.float64)
+    n = torch.tensor(lay.numels, device=dev, dtype=torch.float64)
+    probs = torch.linspace(0, 1, q + 1, device=dev, dtype=torch.float64)
+    pos = probs[None, :] * (n[:, None] - 1).clamp_min(0)
+    lo, hi = pos.floor(), pos.ceil()
+    w = (pos - lo).float()
+    a = sx[(offs[:, None] + lo).long()]
+    b = sx[(offs[:, None] + hi).long()]
+    return (a * (1 - w) + b * w).contiguous()
 
 
 class SketchCompressor(BucketCompressor):
@@ -41,6 +64,14 @@ class SketchCompressor(BucketCompressor):
         lay, q = ctx.layout, self.quantiles
         bdt = torch.uint8 if q < 256 else torch.int16
         bins, means = self.payload(x.device, [(bdt, (lay.total,)), (torch.float32, (q * lay.n_seg,))])
+        if _native.use_native(x) and q <= 1024:
+            edges = segmented_quantile_edges(x, lay, q)
+            sums = torch.zeros(lay.n_seg * q, device=x.device)
+            cnts = torch.zeros(lay.n_seg * q, device=x.device)
+            t = lay.device_tables(x.device)
+            _native.lib().sketch_encode(x, edges, q, bins, sums, cnts, t["seg"], t["begin"], t["end"])
+            torch.where(cnts > 0, sums / cnts.clamp_min(1), torch.zeros_like(sums), out=means)
+            return [bins, means], ctx
         probs = torch.linspace(0, 1, q + 1, device=x.device)
         for i, o, n in lay.segments():
             seg = x[o:o + n]
@@ -54,6 +85,13 @@ class SketchCompressor(BucketCompressor):
 
     def decompress_aggregate_impl(self, per_rank, ctx, n_ranks, scale):
         lay, q = ctx.layout, self.quantiles
+        if _native.use_native(per_rank[0][0]):
+            base, stride, offs = self.rows(per_rank)
+            out = self.out_buffer(ctx, base.device)
+            t = lay.device_tables(base.device)
+            _native.lib().sketch_decode(base, stride, offs[0], offs[1], q, per_rank[0][0].element_size(), n_ranks,
+                                        scale, out, t["seg"], t["begin"], t["end"], lay.n_seg)
+            return self.finish(out, ctx)
         out = self.out_buffer(ctx, per_rank[0][0].device, zero=True)
         seg_id = torch.repeat_interleave(torch.arange(lay.n_seg, device=out.device),
                                          torch.tensor(lay.numels, device=out.device))

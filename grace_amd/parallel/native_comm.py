@@ -18,11 +18,22 @@ from . import comm as _comm
 from ..ops import _native
 
 _UID_COUNTER = itertools.count()
+_EXIT_HOOKED = False
+
+
+def _hook_exit():
+    global _EXIT_HOOKED
+    if not _EXIT_HOOKED:
+        import atexit
+
+        atexit.register(_native.lib().rccl_mark_exiting)
+        _EXIT_HOOKED = True
 
 
 class RcclComm(_comm.Comm):
     def __init__(self, rank: int, world: int, unique_id: bytes, device: int, high_priority: bool = True):
         C = _native.lib()
+        _hook_exit()
         self._c = C.RcclComm(rank, world, unique_id, device, high_priority)
         self.rank, self.world_size, self.device = rank, world, device
         self._stream = torch.cuda.ExternalStream(self._c.stream_ptr, device=torch.device("cuda", device))
@@ -84,3 +95,7 @@ class RcclComm(_comm.Comm):
 
     def abort(self):
         self._c.abort()
+
+    def close(self):
+        """Destroy the communicator now (before torch.distributed is torn down)."""
+        self._c = None
