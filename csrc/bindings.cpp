@@ -34,6 +34,12 @@ using DevGuard = c10::hip::HIPGuardMasqueradingAsCUDA;
   CHECK_CONTIG(t);   \
   CHECK_DT(t, at::kLong)
 
+inline const int64_t* opt_i64(const c10::optional<Tensor>& t) {
+  if (!t.has_value()) return nullptr;
+  CHECK_I64((*t));
+  return t->data_ptr<int64_t>();
+}
+
 grace::ChunkTable make_ct(const Tensor& seg, const Tensor& cb, const Tensor& ce) {
   CHECK_I32(seg);
   CHECK_I64(cb);
@@ -116,7 +122,7 @@ void sparse_scatter_add(const Tensor& val, const Tensor& idx, const Tensor& out,
 
 // ------------------------------------------------------------------------------ random-k / threshold
 void randk_gather(const Tensor& x, const Tensor& seg_off, const Tensor& out_off, const Tensor& seeds,
-                  const Tensor& vals, const c10::optional<Tensor>& resid) {
+                  const c10::optional<Tensor>& step, const Tensor& vals, const c10::optional<Tensor>& resid) {
   CHECK_F32(x);
   CHECK_I64(seg_off);
   CHECK_I64(out_off);
@@ -132,12 +138,14 @@ void randk_gather(const Tensor& x, const Tensor& seg_off, const Tensor& out_off,
   }
   DevGuard guard(x.device());
   grace::randk_gather(x.data_ptr<float>(), n_seg, seg_off.data_ptr<int64_t>(), out_off.data_ptr<int64_t>(),
-                      seeds.data_ptr<int64_t>(), vals.numel(), vals.data_ptr<float>(), rp, cur_stream());
+                      seeds.data_ptr<int64_t>(), opt_i64(step), vals.numel(), vals.data_ptr<float>(), rp,
+                      cur_stream());
 }
 
 // vals: [n_ranks, rank_stride] fp32 view (row r = rank r payload, first K entries used)
 void randk_scatter(const Tensor& vals, int64_t rank_stride, int64_t n_ranks, int64_t K, const Tensor& seg_off,
-                   const Tensor& out_off, const Tensor& seeds, const Tensor& out, double scale, bool accumulate) {
+                   const Tensor& out_off, const Tensor& seeds, const c10::optional<Tensor>& step, const Tensor& out,
+                   double scale, bool accumulate) {
   CHECK_DEV(vals);
   CHECK_DT(vals, at::kFloat);
   CHECK_I64(seg_off);
@@ -148,8 +156,8 @@ void randk_scatter(const Tensor& vals, int64_t rank_stride, int64_t n_ranks, int
               "vals view too small");
   DevGuard guard(out.device());
   grace::randk_scatter(vals.data_ptr<float>(), rank_stride, (int)n_ranks, (int)seeds.numel(),
-                       seg_off.data_ptr<int64_t>(), out_off.data_ptr<int64_t>(), seeds.data_ptr<int64_t>(), K,
-                       out.data_ptr<float>(), (float)scale, accumulate, cur_stream());
+                       seg_off.data_ptr<int64_t>(), out_off.data_ptr<int64_t>(), seeds.data_ptr<int64_t>(),
+                       opt_i64(step), K, out.data_ptr<float>(), (float)scale, accumulate, cur_stream());
 }
 
 int64_t threshold_compact(const Tensor& g, const c10::optional<Tensor>& r, int64_t mode, double beta, double gamma,
@@ -192,6 +200,14 @@ inline const float* opt_f32(const c10::optional<Tensor>& t) {
   if (!t.has_value()) return nullptr;
   CHECK_F32((*t));
   return t->data_ptr<float>();
+}
+inline grace::SeedArg seed_arg(int64_t seed, const c10::optional<Tensor>& step) {
+  grace::SeedArg sa{(uint64_t)seed, nullptr};
+  if (step.has_value()) {
+    CHECK_I64((*step));
+    sa.step = step->data_ptr<int64_t>();
+  }
+  return sa;
 }
 inline float* opt_f32_mut(const c10::optional<Tensor>& t) {
   if (!t.has_value()) return nullptr;
@@ -238,7 +254,8 @@ void sign_unpack(const Tensor& base, int64_t rank_stride, int64_t words_off, int
 }
 
 // ------------------------------------------------------------------------------ quantizers
-void qsgd_quantize(const Tensor& x, const Tensor& norms, double s, int64_t seed, const Tensor& codes,
+void qsgd_quantize(const Tensor& x, const Tensor& norms, double s, int64_t seed, const c10::optional<Tensor>& step,
+                   const Tensor& codes,
                    const c10::optional<Tensor>& resid, const Tensor& seg, const Tensor& cb, const Tensor& ce) {
   CHECK_F32(x);
   CHECK_F32(norms);
@@ -249,7 +266,7 @@ void qsgd_quantize(const Tensor& x, const Tensor& norms, double s, int64_t seed,
   TORCH_CHECK(cb_ == 1 || cb_ == 2 || cb_ == 4, "codes must be int8/int16/int32");
   auto ct = make_ct(seg, cb, ce);
   DevGuard guard(x.device());
-  grace::qsgd_quantize(ct, x.data_ptr<float>(), norms.data_ptr<float>(), (float)s, (uint64_t)seed, codes.data_ptr(),
+  grace::qsgd_quantize(ct, x.data_ptr<float>(), norms.data_ptr<float>(), (float)s, seed_arg(seed, step), codes.data_ptr(),
                        cb_, opt_f32_mut(resid), cur_stream());
 }
 
@@ -264,7 +281,8 @@ void qsgd_aggregate(const Tensor& base, int64_t rank_stride, int64_t codes_off, 
                         (int)n_ranks, (float)s, (float)scale, out.data_ptr<float>(), accumulate, cur_stream());
 }
 
-void tern_quantize(const Tensor& x, const Tensor& clips, const Tensor& scal, int64_t seed, const Tensor& words,
+void tern_quantize(const Tensor& x, const Tensor& clips, const Tensor& scal, int64_t seed,
+                   const c10::optional<Tensor>& step, const Tensor& words,
                    const c10::optional<Tensor>& resid, const Tensor& seg, const Tensor& cb, const Tensor& ce,
                    const Tensor& seg_start, const Tensor& word_off, int64_t n_words) {
   CHECK_F32(x);
@@ -278,7 +296,7 @@ void tern_quantize(const Tensor& x, const Tensor& clips, const Tensor& scal, int
   auto ct = make_ct(seg, cb, ce);
   DevGuard guard(x.device());
   grace::tern_quantize(ct, seg_start.data_ptr<int64_t>(), word_off.data_ptr<int64_t>(), x.data_ptr<float>(),
-                       clips.data_ptr<float>(), scal.data_ptr<float>(), (uint64_t)seed,
+                       clips.data_ptr<float>(), scal.data_ptr<float>(), seed_arg(seed, step),
                        reinterpret_cast<uint64_t*>(words.data_ptr<int64_t>()), opt_f32_mut(resid), cur_stream());
 }
 
@@ -295,13 +313,14 @@ void tern_aggregate(const Tensor& base, int64_t rank_stride, int64_t words_off, 
                         cur_stream());
 }
 
-void natural_encode(const Tensor& x, int64_t seed, const Tensor& codes, const c10::optional<Tensor>& resid) {
+void natural_encode(const Tensor& x, int64_t seed, const c10::optional<Tensor>& step, const Tensor& codes,
+                    const c10::optional<Tensor>& resid) {
   CHECK_F32(x);
   CHECK_DEV(codes);
   CHECK_DT(codes, at::kByte);
   TORCH_CHECK(codes.numel() >= x.numel(), "codes too small");
   DevGuard guard(x.device());
-  grace::natural_encode(x.data_ptr<float>(), x.numel(), (uint64_t)seed, codes.data_ptr<uint8_t>(), opt_f32_mut(resid),
+  grace::natural_encode(x.data_ptr<float>(), x.numel(), seed_arg(seed, step), codes.data_ptr<uint8_t>(), opt_f32_mut(resid),
                         cur_stream());
 }
 
@@ -416,10 +435,10 @@ void powersgd_pqt(const Tensor& P, const Tensor& Q, const Tensor& out, const Ten
                       tiles.data_ptr<int32_t>(), (int)(tiles.numel() / 3), cur_stream());
 }
 
-void philox_normal(const Tensor& out, int64_t seed) {
+void philox_normal(const Tensor& out, int64_t seed, const c10::optional<Tensor>& step) {
   CHECK_F32(out);
   DevGuard guard(out.device());
-  grace::philox_normal(out.data_ptr<float>(), out.numel(), (uint64_t)seed, cur_stream());
+  grace::philox_normal(out.data_ptr<float>(), out.numel(), seed_arg(seed, step), cur_stream());
 }
 
 // ------------------------------------------------------------------------------ 16-bit cast, sketch

@@ -92,6 +92,17 @@ struct Philox {
   }
 };
 
+// RNG seed = host base seed, optionally mixed with a DEVICE step counter.  Reading the step
+// from device memory (bumped by a captured kernel every step) keeps stochastic codecs correct
+// under HIP-graph replay: a host-side seed would be frozen into the graph.
+struct SeedArg {
+  uint64_t base;
+  const int64_t* step;  // nullptr: use base as is
+  __device__ __forceinline__ uint64_t get() const {
+    return step ? (base ^ ((uint64_t)(*step) * 0x9E3779B97F4A7C15ull)) : base;
+  }
+};
+
 // uniform float in [0, 1) from 24 random bits
 __device__ __forceinline__ float u01(uint32_t r) { return (r >> 8) * (1.0f / 16777216.0f); }
 

@@ -35,10 +35,11 @@ void segment_stats(const ChunkTable& ct, int n_seg, const int32_t* seg_chunk_beg
 
 // ---------------------------------------------------------------- sparsify.hip
 void randk_gather(const float* x, int n_seg, const int64_t* seg_off, const int64_t* out_off,
-                  const int64_t* seeds, int64_t K, float* vals, float* resid, hipStream_t stream);
+                  const int64_t* seeds, const int64_t* step, int64_t K, float* vals, float* resid,
+                  hipStream_t stream);
 void randk_scatter(const float* vals, int64_t rank_stride, int n_ranks, int n_seg, const int64_t* seg_off,
-                   const int64_t* out_off, const int64_t* seeds, int64_t K, float* out, float scale,
-                   bool accumulate, hipStream_t stream);
+                   const int64_t* out_off, const int64_t* seeds, const int64_t* step, int64_t K, float* out,
+                   float scale, bool accumulate, hipStream_t stream);
 void threshold_compact(const float* g, const float* r, int mode, float beta, float gamma, int64_t n, float thr,
                        float* out_val, int32_t* out_idx, int32_t* counter, float* resid, hipStream_t stream);
 
@@ -51,18 +52,18 @@ void sign_unpack(const ChunkTable& ct, const int64_t* seg_start, const int64_t* 
                  bool vote, float scale, float* out, bool accumulate, hipStream_t stream);
 
 // ---------------------------------------------------------------- quant.hip
-void qsgd_quantize(const ChunkTable& ct, const float* x, const float* norms, float s, uint64_t seed, void* codes,
+void qsgd_quantize(const ChunkTable& ct, const float* x, const float* norms, float s, SeedArg seed, void* codes,
                    int code_bytes, float* resid, hipStream_t stream);
 void qsgd_aggregate(const ChunkTable& ct, const uint8_t* base, int64_t rank_stride, int64_t codes_off,
                     int64_t norms_off, int code_bytes, int n_ranks, float s, float scale, float* out, bool accumulate,
                     hipStream_t stream);
 void tern_quantize(const ChunkTable& ct, const int64_t* seg_start, const int64_t* word_off, const float* x,
-                   const float* clips, const float* scal, uint64_t seed, uint64_t* words, float* resid,
+                   const float* clips, const float* scal, SeedArg seed, uint64_t* words, float* resid,
                    hipStream_t stream);
 void tern_aggregate(const ChunkTable& ct, const int64_t* seg_start, const int64_t* word_off, const uint8_t* base,
                     int64_t rank_stride, int64_t words_off, int64_t scal_off, int n_ranks, float scale, float* out,
                     bool accumulate, hipStream_t stream);
-void natural_encode(const float* x, int64_t n, uint64_t seed, uint8_t* codes, float* resid, hipStream_t stream);
+void natural_encode(const float* x, int64_t n, SeedArg seed, uint8_t* codes, float* resid, hipStream_t stream);
 void natural_aggregate(const uint8_t* base, int64_t rank_stride, int64_t n, int n_ranks, float scale, float* out,
                        bool accumulate, hipStream_t stream);
 void u8_encode(const ChunkTable& ct, const float* x, const float* scales, int8_t* codes, float* resid,
@@ -85,7 +86,7 @@ void powersgd_mq(const float* x, const float* small, float* out, int64_t out_len
 void gram_schmidt(float* buf, const int64_t* mats, int n_mat, int which, hipStream_t stream);
 void powersgd_pqt(const float* P, const float* Q, float* out, const int64_t* mats, const int32_t* tiles, int n_tiles,
                   hipStream_t stream);
-void philox_normal(float* out, int64_t n, uint64_t seed, hipStream_t stream);
+void philox_normal(float* out, int64_t n, SeedArg seed, hipStream_t stream);
 
 // ---------------------------------------------------------------- cast_sketch.hip
 void cast16(const float* x, uint16_t* y, int64_t n, bool bf16, hipStream_t stream);

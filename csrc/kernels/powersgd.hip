@@ -190,7 +190,8 @@ __global__ __launch_bounds__(kBlock) void pqt_kernel(const float* __restrict__ P
   }
 }
 
-__global__ __launch_bounds__(kBlock) void philox_normal_kernel(float* __restrict__ out, int64_t n, uint64_t seed) {
+__global__ __launch_bounds__(kBlock) void philox_normal_kernel(float* __restrict__ out, int64_t n, SeedArg sa) {
+  const uint64_t seed = sa.get();
   const int64_t stride = (int64_t)gridDim.x * kBlock * 4;
   for (int64_t base = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 4; base < n; base += stride) {
     const uint4 r = Philox::gen(seed, (uint64_t)base >> 2, 0x6e6f726du);
@@ -232,7 +233,7 @@ void powersgd_pqt(const float* P, const float* Q, float* out, const int64_t* mat
   pqt_kernel<<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles);
 }
 
-void philox_normal(float* out, int64_t n, uint64_t seed, hipStream_t stream) {
+void philox_normal(float* out, int64_t n, SeedArg seed, hipStream_t stream) {
   if (n <= 0) return;
   int64_t b = (n + 4 * kBlock - 1) / (4 * kBlock);
   if (b > 2048) b = 2048;

@@ -35,8 +35,9 @@ __device__ __forceinline__ uint32_t pick(const uint4& r, int k) {
 template <typename CodeT, bool RESID>
 __global__ __launch_bounds__(kBlock) void qsgd_quant_kernel(ChunkTable ct, const float* x,
                                                             const float* __restrict__ norms, float s,
-                                                            uint64_t seed, CodeT* __restrict__ codes,
+                                                            SeedArg sa, CodeT* __restrict__ codes,
                                                             float* resid) {
+  const uint64_t seed = sa.get();
   const int c = blockIdx.x;
   const int sg = ct.seg[c];
   const int64_t b = ct.begin[c], e = ct.end[c];
@@ -87,8 +88,9 @@ template <bool RESID>
 __global__ __launch_bounds__(kBlock) void tern_quant_kernel(ChunkTable ct, const int64_t* __restrict__ seg_start,
                                                             const int64_t* __restrict__ word_off, const float* x,
                                                             const float* __restrict__ clips,
-                                                            const float* __restrict__ scal, uint64_t seed,
+                                                            const float* __restrict__ scal, SeedArg sa,
                                                             uint64_t* __restrict__ words, float* resid) {
+  const uint64_t seed = sa.get();
   const int c = blockIdx.x;
   const int sg = ct.seg[c];
   const int64_t b = ct.begin[c], e = ct.end[c];
@@ -167,8 +169,9 @@ __device__ __forceinline__ float natural_decode(uint8_t code) {
 }
 
 template <bool RESID>
-__global__ __launch_bounds__(kBlock) void natural_encode_kernel(const float* x, int64_t n, uint64_t seed,
+__global__ __launch_bounds__(kBlock) void natural_encode_kernel(const float* x, int64_t n, SeedArg sa,
                                                                 uint8_t* __restrict__ codes, float* resid) {
+  const uint64_t seed = sa.get();
   const int64_t stride = (int64_t)gridDim.x * kBlock * 4;
   for (int64_t base = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 4; base < n; base += stride) {
     const uint4 rnd = Philox::gen(seed, (uint64_t)base >> 2);
@@ -284,7 +287,7 @@ inline int grid_for(int64_t n) {
 
 }  // namespace
 
-void qsgd_quantize(const ChunkTable& ct, const float* x, const float* norms, float s, uint64_t seed, void* codes,
+void qsgd_quantize(const ChunkTable& ct, const float* x, const float* norms, float s, SeedArg seed, void* codes,
                    int code_bytes, float* resid, hipStream_t stream) {
   if (ct.n_chunks == 0) return;
   if (code_bytes == 1) {
@@ -322,7 +325,7 @@ void qsgd_aggregate(const ChunkTable& ct, const uint8_t* base, int64_t rank_stri
 }
 
 void tern_quantize(const ChunkTable& ct, const int64_t* seg_start, const int64_t* word_off, const float* x,
-                   const float* clips, const float* scal, uint64_t seed, uint64_t* words, float* resid,
+                   const float* clips, const float* scal, SeedArg seed, uint64_t* words, float* resid,
                    hipStream_t stream) {
   if (ct.n_chunks == 0) return;
   if (resid)
@@ -341,7 +344,7 @@ void tern_aggregate(const ChunkTable& ct, const int64_t* seg_start, const int64_
                                                             scal_off, n_ranks, scale, out, accumulate ? 1 : 0);
 }
 
-void natural_encode(const float* x, int64_t n, uint64_t seed, uint8_t* codes, float* resid, hipStream_t stream) {
+void natural_encode(const float* x, int64_t n, SeedArg seed, uint8_t* codes, float* resid, hipStream_t stream) {
   if (n <= 0) return;
   const int grid = grid_for((n + 3) / 4);
   if (resid)

@@ -37,13 +37,15 @@ __global__ __launch_bounds__(kBlock) void randk_gather_kernel(const float* x, in
                                                               const int64_t* __restrict__ seg_off,
                                                               const int64_t* __restrict__ out_off,
                                                               const int64_t* __restrict__ seeds,
+                                                              const int64_t* __restrict__ step,
                                                               float* __restrict__ vals, float* resid) {
   const int64_t K = out_off[n_seg];
+  const uint64_t mix = step ? (uint64_t)(*step) * 0x9E3779B97F4A7C15ull : 0ull;
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < K; j += stride) {
     const int s = find_seg(out_off, n_seg, j);
     const uint64_t n = (uint64_t)(seg_off[s + 1] - seg_off[s]);
-    const FeistelKey fk = feistel_key((uint64_t)seeds[s], n);
+    const FeistelKey fk = feistel_key((uint64_t)seeds[s] ^ mix, n);
     const int64_t i = seg_off[s] + (int64_t)feistel_perm((uint64_t)(j - out_off[s]), n, fk);
     vals[j] = x[i];
     if (resid) resid[i] = 0.f;
@@ -55,14 +57,16 @@ __global__ __launch_bounds__(kBlock) void randk_scatter_kernel(const float* __re
                                                                const int64_t* __restrict__ seg_off,
                                                                const int64_t* __restrict__ out_off,
                                                                const int64_t* __restrict__ seeds,
+                                                               const int64_t* __restrict__ step,
                                                                float* __restrict__ out, float scale,
                                                                int accumulate) {
   const int64_t K = out_off[n_seg];
+  const uint64_t mix = step ? (uint64_t)(*step) * 0x9E3779B97F4A7C15ull : 0ull;
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < K; j += stride) {
     const int s = find_seg(out_off, n_seg, j);
     const uint64_t n = (uint64_t)(seg_off[s + 1] - seg_off[s]);
-    const FeistelKey fk = feistel_key((uint64_t)seeds[s], n);
+    const FeistelKey fk = feistel_key((uint64_t)seeds[s] ^ mix, n);
     const int64_t i = seg_off[s] + (int64_t)feistel_perm((uint64_t)(j - out_off[s]), n, fk);
     float acc = 0.f;
     for (int r = 0; r < n_ranks; ++r) acc += vals[(int64_t)r * rank_stride + j];
@@ -134,17 +138,18 @@ inline int grid_for(int64_t n) {
 }  // namespace
 
 void randk_gather(const float* x, int n_seg, const int64_t* seg_off, const int64_t* out_off,
-                  const int64_t* seeds, int64_t K, float* vals, float* resid, hipStream_t stream) {
+                  const int64_t* seeds, const int64_t* step, int64_t K, float* vals, float* resid,
+                  hipStream_t stream) {
   if (K <= 0) return;
-  randk_gather_kernel<<<grid_for(K), kBlock, 0, stream>>>(x, n_seg, seg_off, out_off, seeds, vals, resid);
+  randk_gather_kernel<<<grid_for(K), kBlock, 0, stream>>>(x, n_seg, seg_off, out_off, seeds, step, vals, resid);
 }
 
 void randk_scatter(const float* vals, int64_t rank_stride, int n_ranks, int n_seg, const int64_t* seg_off,
-                   const int64_t* out_off, const int64_t* seeds, int64_t K, float* out, float scale,
-                   bool accumulate, hipStream_t stream) {
+                   const int64_t* out_off, const int64_t* seeds, const int64_t* step, int64_t K, float* out,
+                   float scale, bool accumulate, hipStream_t stream) {
   if (K <= 0) return;
   randk_scatter_kernel<<<grid_for(K), kBlock, 0, stream>>>(vals, rank_stride, n_ranks, n_seg, seg_off, out_off,
-                                                           seeds, out, scale, accumulate ? 1 : 0);
+                                                           seeds, step, out, scale, accumulate ? 1 : 0);
 }
 
 void threshold_compact(const float* g, const float* r, int mode, float beta, float gamma, int64_t n, float thr,

@@ -7,8 +7,9 @@ from typing import Any, Dict, Tuple
 import torch
 
 from ..core import Compressor, layout_of
+from ..ops import _native
 from ..ops.layout import SegmentLayout
-from ..ops.randomk import fnv1a64
+from ..ops.randomk import fnv1a64, mix_step
 from ..parallel.comm import PayloadBuilder, rank_rows
 
 MASK64 = 0xFFFFFFFFFFFFFFFF
@@ -28,14 +29,69 @@ class Ctx:
     out: Any = None
 
 
-class BucketCompressor(Compressor):
+class DeviceSteps:
+    """Per-name step counters mirrored in device memory.
+
+    A stochastic codec's kernel reads its step from a 1-element int64 device tensor and mixes it
+    into the Philox / Feistel seed (``csrc/include/grace_common.h`` SeedArg).  ``bump`` issues an
+    ``add_(1)`` on the current stream, so a HIP-graph replay of the step advances the counter
+    too: the randomness stays fresh on every replay instead of freezing the capture-time seed.
+    In eager mode the device value always equals the host counter ``steps[name]``.
+    """
+
+    def __init__(self):
+        self._t: Dict[str, torch.Tensor] = {}
+
+    def bump(self, name: str, device: torch.device, host_value: int) -> torch.Tensor:
+        t = self._t.get(name)
+        if t is None or t.device != device:
+            t = torch.full((1,), host_value, dtype=torch.int64, device=device)
+            self._t[name] = t
+        else:
+            t.add_(1)
+        return t
+
+    def sync_to(self, steps: Dict[str, int]) -> None:
+        """Copy the device counters (advanced by graph replays) back into the host dict."""
+        for name, t in self._t.items():
+            steps[name] = int(t.item())
+
+    def reset(self) -> None:
+        self._t.clear()
+
+
+class StepState:
+    """Mixin: host ``steps`` dict + device mirrors, kept consistent through state_dict."""
+
+    def _init_steps(self):
+        self.steps: Dict[str, int] = {}
+        self._dsteps = DeviceSteps()
+
+    def advance(self, name: str, device) -> Tuple[int, Any]:
+        """Advance ``name``'s step.  Returns (host step, device counter or None)."""
+        step = self.steps.get(name, 0) + 1
+        self.steps[name] = step
+        if _native.native_on(device):
+            return step, self._dsteps.bump(name, torch.device(device), step)
+        return step, None
+
+    def state_dict(self):
+        self._dsteps.sync_to(self.steps)
+        return super().state_dict()
+
+    def load_state_dict(self, state):
+        super().load_state_dict(state)
+        self._dsteps.reset()
+
+
+class BucketCompressor(StepState, Compressor):
     """Compressor whose kernels run over a whole flat bucket (per-segment semantics)."""
 
     _state_attrs: Tuple[str, ...] = ("steps",)
 
     def __init__(self, average=True, tensors_size_are_same=True):
         super().__init__(average, tensors_size_are_same)
-        self.steps: Dict[str, int] = {}
+        self._init_steps()
         self.rank = 0
 
     def bind_comm(self, comm):
@@ -53,12 +109,22 @@ class BucketCompressor(Compressor):
     def ctx(self, tensor, name) -> Ctx:
         return Ctx(layout_of(tensor, name), tensor.numel(), tensor.shape, tensor.dtype)
 
+    def base_seed(self, name: str) -> int:
+        """Per-(name, rank) seed: independent rounding noise on every rank."""
+        return (fnv1a64(name.encode("utf8")) ^ (0xD1B54A32D192ED03 * (self.rank + 1))) & MASK64
+
     def next_seed(self, name: str) -> int:
-        """Per-(name, step, rank) seed: independent rounding noise on every rank/step."""
-        step = self.steps.get(name, 0)
-        self.steps[name] = step + 1
-        h = fnv1a64(name.encode("utf8"))
-        return (h ^ (0x9E3779B97F4A7C15 * (step + 1)) ^ (0xD1B54A32D192ED03 * (self.rank + 1))) & MASK64
+        """Per-(name, step, rank) host seed (for codecs without a device step counter)."""
+        step, _ = self.advance(name, "cpu")
+        return mix_step(self.base_seed(name), step)
+
+    def next_rng(self, name: str, device):
+        """(seed, step_tensor) for a native kernel: the kernel mixes the DEVICE step into the
+        seed (graph-replay safe).  Off the native path: (host-mixed seed, None)."""
+        step, t = self.advance(name, device)
+        if t is None:
+            return mix_step(self.base_seed(name), step), None
+        return self.base_seed(name), t
 
     @staticmethod
     def payload(device, entries):

@@ -24,14 +24,16 @@ class NaturalCompressor(BucketCompressor):
     def _encode(self, g, ctx, name, memory=None):
         (codes,) = self.payload(g.device, [(torch.uint8, (ctx.layout.total,))])
         if memory is None:
-            Q.natural_encode(g, self.next_seed(name), codes)
+            seed, step = self.next_rng(name, g.device)
+            Q.natural_encode(g, seed, codes, step=step)
         else:
             r, valid = memory.residual_buffer(name, g)
             if valid:
                 axpby(r, g, memory.beta, memory.gamma, out=r)
             else:
                 r.copy_(g)
-            Q.natural_encode(r, self.next_seed(name), codes, resid=r)
+            seed, step = self.next_rng(name, r.device)
+            Q.natural_encode(r, seed, codes, resid=r, step=step)
         return [codes]
 
     def compress(self, tensor, name):

@@ -27,7 +27,7 @@ from typing import List, Tuple
 import torch
 
 from ..ops import powersgd as PS
-from ..ops.randomk import fnv1a64
+from ..ops.randomk import fnv1a64, mix_step
 from ._base import BucketCompressor, Ctx
 
 
@@ -60,12 +60,14 @@ class PowerSGDCompressor(BucketCompressor):
             return [self.flat(tensor)], ctx
         x = self.flat(tensor)
         W = self.world_size or 1
-        step = self.steps.get(name, 0)
-        self.steps[name] = step + 1
+        step, step_t = self.advance(name, x.device)
         q = self.q_memory.get(name) if self.warm_start else None
         if q is None or q.numel() != plan.q_total:
-            seed = (fnv1a64(name.encode()) ^ (0x9E3779B97F4A7C15 * (step + 1))) & 0xFFFFFFFFFFFFFFFF
-            q = PS.randn_shared(plan.q_total, seed, x.device)
+            # identical on every rank (no rank in the seed); the device step counter keeps a fresh
+            # Q per HIP-graph replay when warm_start is off
+            seed = fnv1a64(name.encode())
+            q = PS.randn_shared(plan.q_total, seed if step_t is not None else mix_step(seed, step), x.device,
+                                step=step_t)
             PS.orthogonalize(q, plan, which="q")
         p = PS.mq(x, q, plan)  # P = M Q for every matrix (one launch)
         if self.comm is not None and W > 1:

@@ -62,7 +62,8 @@ class QSGDCompressor(BucketCompressor):
         torch.sqrt(stats[:, S.SUMSQ], out=norms)
         if self.shared_scale and W > 1:
             self.comm.all_reduce(norms, op="max")
-        Q.qsgd_quantize(x, lay, norms, self.quantum_num, self.next_seed(name), codes, resid=r)
+        seed, step = self.next_rng(name, x.device)
+        Q.qsgd_quantize(x, lay, norms, self.quantum_num, seed, codes, resid=r, step=step)
         if self.shared_scale:
             ctx.extra["norms"] = norms
             return [codes]

@@ -15,11 +15,12 @@ Payload: [vals fp32 (K)].  Allreduce-compatible (identical indices on every rank
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Tuple
+from typing import Optional, Tuple
 
 import torch
 
 from ..core import Compressor, layout_of
+from ._base import StepState
 from ..memory.residual import ResidualMemory
 from ..ops import randomk as R
 from ..ops.elementwise import axpby
@@ -36,9 +37,11 @@ class RandomKCtx:
     numel: int
     shape: torch.Size
     dtype: torch.dtype
+    step: int = 0                      # host step (mixed into the seeds on the torch path)
+    step_t: Optional[torch.Tensor] = None  # device step counter (mixed in by the kernels)
 
 
-class RandomKCompressor(Compressor):
+class RandomKCompressor(StepState, Compressor):
     allreduce_compatible = True
     _state_attrs = ("steps",)
 
@@ -46,7 +49,7 @@ class RandomKCompressor(Compressor):
         super().__init__()
         self.compress_ratio = compress_ratio
         self.seed = seed
-        self.steps = {}
+        self._init_steps()
 
     @property
     def global_step(self) -> int:  # reference attribute name
@@ -55,17 +58,17 @@ class RandomKCompressor(Compressor):
     def _ctx(self, tensor, name) -> RandomKCtx:
         lay = layout_of(tensor, name)
         ks = k_per_segment(lay, self.compress_ratio)
-        step = self.steps.get(name, 0)
-        self.steps[name] = step + 1
+        step, step_t = self.advance(name, tensor.device)
+        # per-segment base seeds are step-independent; the step is mixed in by R.gather/scatter
+        # (on device when step_t is given, so graph replays draw new indices)
         base = R.fnv1a64(name.encode("utf8")) ^ (self.seed * 0x9E3779B97F4A7C15 & 0xFFFFFFFFFFFFFFFF)
-        seeds = tuple(((base + 0x9E3779B97F4A7C15 * step) ^ (0xBF58476D1CE4E5B9 * (i + 1))) & 0xFFFFFFFFFFFFFFFF
-                      for i in range(lay.n_seg))
-        return RandomKCtx(lay, ks, seeds, tensor.numel(), tensor.shape, tensor.dtype)
+        seeds = tuple((base ^ (0xBF58476D1CE4E5B9 * (i + 1))) & 0xFFFFFFFFFFFFFFFF for i in range(lay.n_seg))
+        return RandomKCtx(lay, ks, seeds, tensor.numel(), tensor.shape, tensor.dtype, step, step_t)
 
     def compress(self, tensor, name):
         ctx = self._ctx(tensor, name)
         x = tensor.reshape(-1).float().contiguous()
-        vals = R.gather(x, ctx.layout, ctx.ks, ctx.seeds)
+        vals = R.gather(x, ctx.layout, ctx.ks, ctx.seeds, step=ctx.step, step_t=ctx.step_t)
         return [vals], ctx
 
     def fused_compress(self, tensor, name, memory):
@@ -79,26 +82,31 @@ class RandomKCompressor(Compressor):
         else:
             r.copy_(g)
         # gather the sent values and zero them in the residual in the same kernel
-        vals = R.gather(r, ctx.layout, ctx.ks, ctx.seeds, zero_selected=True)
+        vals = R.gather(r, ctx.layout, ctx.ks, ctx.seeds, zero_selected=True, step=ctx.step, step_t=ctx.step_t)
         return [vals], ctx
 
+    def _scale(self, world_size: int) -> float:
+        return 1.0 / world_size if self.average else 1.0
+
     def indices(self, ctx: RandomKCtx, device="cpu") -> torch.Tensor:
-        return R.indices(ctx.layout, ctx.ks, ctx.seeds, device)
+        return R.indices(ctx.layout, ctx.ks, ctx.seeds, device, step=ctx.step)
 
     def decompress(self, tensors, ctx):
         (vals,) = tensors
         out = torch.zeros(ctx.numel, dtype=torch.float32, device=vals.device)
-        R.scatter(vals, ctx.layout, ctx.ks, ctx.seeds, out, 1.0)
+        R.scatter(vals, ctx.layout, ctx.ks, ctx.seeds, out, 1.0, step=ctx.step, step_t=ctx.step_t)
         return out.view(ctx.shape).to(ctx.dtype)
 
     def decompress_reduced(self, tensors, ctx, world_size):
         (vals,) = tensors
         out = torch.zeros(ctx.numel, dtype=torch.float32, device=vals.device)
-        R.scatter(vals, ctx.layout, ctx.ks, ctx.seeds, out, 1.0 / world_size if self.average else 1.0)
+        R.scatter(vals, ctx.layout, ctx.ks, ctx.seeds, out, self._scale(world_size),
+                  step=ctx.step, step_t=ctx.step_t)
         return out.view(ctx.shape).to(ctx.dtype)
 
     def decompress_aggregate(self, per_rank, ctx, world_size):
         rows = stack_rows([p[0] for p in per_rank])
         out = torch.zeros(ctx.numel, dtype=torch.float32, device=rows.device)
-        R.scatter(rows, ctx.layout, ctx.ks, ctx.seeds, out, 1.0 / world_size if self.average else 1.0)
+        R.scatter(rows, ctx.layout, ctx.ks, ctx.seeds, out, self._scale(world_size),
+                  step=ctx.step, step_t=ctx.step_t)
         return out.view(ctx.shape).to(ctx.dtype)

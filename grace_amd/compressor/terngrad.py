@@ -38,12 +38,14 @@ class TernGradCompressor(BucketCompressor):
             r, valid = memory.residual_buffer(name, g)
             stats = S.segment_stats(g, lay, r=r, r_valid=valid, beta=memory.beta, gamma=memory.gamma, xout=r)
             x = r
-        n = torch.tensor(lay.numels, dtype=torch.float32, device=g.device).clamp_min(1)
+        n = lay.cached(g.device, "numels_f32",
+                       lambda: torch.tensor(lay.numels, dtype=torch.float32, device=g.device).clamp_min(1))
         mean = stats[:, S.SUM] / n
         var = (stats[:, S.SUMSQ] / n - mean * mean).clamp_min(0)
         clip = self.clip_factor * torch.sqrt(var)
         torch.minimum(stats[:, S.ABSMAX], clip, out=scal)
-        Q.tern_quantize(x, lay, clip, scal, self.next_seed(name), words, resid=r)
+        seed, step = self.next_rng(name, x.device)
+        Q.tern_quantize(x, lay, clip, scal, seed, words, resid=r, step=step)
         return [words, scal]
 
     def compress(self, tensor, name):

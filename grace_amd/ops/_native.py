@@ -15,6 +15,8 @@ from __future__ import annotations
 import importlib
 import os
 
+import torch
+
 _lib = None
 _err: Exception | None = None
 
@@ -54,3 +56,10 @@ def use_native(t) -> bool:
     if os.environ.get("GRACE_AMD_FORCE_TORCH", "0") == "1":
         return False
     return True
+
+
+def native_on(device) -> bool:
+    """use_native() for a device instead of a tensor."""
+    if torch.device(device).type != "cuda":
+        return False
+    return os.environ.get("GRACE_AMD_FORCE_TORCH", "0") != "1"

@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import math
 from dataclasses import dataclass, field
-from typing import Dict, List, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import torch
 
@@ -89,12 +89,13 @@ def plan_for(layout: SegmentLayout, rank: int) -> Plan:
     return p
 
 
-def randn_shared(n: int, seed: int, device) -> torch.Tensor:
-    """N(0,1) vector identical on every rank for the same seed."""
+def randn_shared(n: int, seed: int, device, step: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """N(0,1) vector identical on every rank for the same seed (and device ``step`` counter,
+    mixed in by the kernel when given)."""
     if _native.use_native(torch.empty(0, device=device)):
         out = torch.empty(n, dtype=torch.float32, device=device)
         sd = seed & 0xFFFFFFFFFFFFFFFF
-        _native.lib().philox_normal(out, sd - (1 << 64) if sd >= (1 << 63) else sd)
+        _native.lib().philox_normal(out, sd - (1 << 64) if sd >= (1 << 63) else sd, step)
         return out
     g = torch.Generator(device=device)
     g.manual_seed(seed & 0x7FFFFFFFFFFFFFFF)

@@ -51,10 +51,12 @@ def _seed64(seed: int) -> int:
 
 # ------------------------------------------------------------------------------ QSGD
 def qsgd_quantize(x: torch.Tensor, layout: SegmentLayout, norms: torch.Tensor, s: int, seed: int,
-                  codes: torch.Tensor, resid: Optional[torch.Tensor] = None) -> None:
+                  codes: torch.Tensor, resid: Optional[torch.Tensor] = None,
+                  step: Optional[torch.Tensor] = None) -> None:
+    """``step``: optional device int64 counter mixed into ``seed`` by the kernel (graph replay)."""
     if _native.use_native(x):
         t = _tables(layout, x.device)
-        _native.lib().qsgd_quantize(x, norms, float(s), _seed64(seed), codes, resid, t["seg"], t["begin"], t["end"])
+        _native.lib().qsgd_quantize(x, norms, float(s), _seed64(seed), step, codes, resid, t["seg"], t["begin"], t["end"])
         return
     nrm = expand(norms, layout)
     inv = torch.where(nrm > 0, s / nrm, torch.zeros_like(nrm))
@@ -91,10 +93,10 @@ def qsgd_aggregate(base, rank_stride, codes_off, norms_off, code_dtype, n_ranks,
 
 
 # ------------------------------------------------------------------------------ TernGrad
-def tern_quantize(x, layout, clips, scal, seed, words, resid=None):
+def tern_quantize(x, layout, clips, scal, seed, words, resid=None, step=None):
     if _native.use_native(x):
         t = _tables(layout, x.device)
-        _native.lib().tern_quantize(x, clips, scal, _seed64(seed), words, resid, t["seg"], t["begin"], t["end"],
+        _native.lib().tern_quantize(x, clips, scal, _seed64(seed), step, words, resid, t["seg"], t["begin"], t["end"],
                                     t["offsets"], t["word_off"], layout.n_words)
         return
     from .signbits import pack_bits_torch
@@ -137,9 +139,9 @@ def tern_aggregate(base, rank_stride, words_off, scal_off, n_ranks, layout, out,
 
 
 # ------------------------------------------------------------------------------ Natural
-def natural_encode(x, seed, codes, resid=None):
+def natural_encode(x, seed, codes, resid=None, step=None):
     if _native.use_native(x):
-        _native.lib().natural_encode(x, _seed64(seed), codes, resid)
+        _native.lib().natural_encode(x, _seed64(seed), step, codes, resid)
         return
     bits = x.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
     sign = bits & 0x80000000

@@ -6,7 +6,7 @@ permutation of csrc/include/grace_rand.h.  The PyTorch implementation below uses
 """
 from __future__ import annotations
 
-from typing import Sequence, Tuple
+from typing import Optional, Sequence, Tuple
 
 import torch
 
@@ -78,15 +78,26 @@ def feistel_perm(j: torch.Tensor, n: int, seed: int) -> torch.Tensor:
     return y
 
 
-def indices(layout: SegmentLayout, ks: Sequence[int], seeds: Sequence[int], device="cpu") -> torch.Tensor:
+_GOLDEN = 0x9E3779B97F4A7C15
+
+
+def mix_step(seed: int, step: int) -> int:
+    """seed ^ step * golden (mod 2^64): host twin of the kernels' device-step mixing."""
+    return (seed ^ (step * _GOLDEN)) & 0xFFFFFFFFFFFFFFFF
+
+
+def indices(layout: SegmentLayout, ks: Sequence[int], seeds: Sequence[int], device="cpu",
+            step: int = 0) -> torch.Tensor:
     out = []
     for (i, o, n), k, sd in zip(layout.segments(), ks, seeds):
         if k:
-            out.append(feistel_perm(torch.arange(k, dtype=torch.int64, device=device), n, sd) + o)
+            out.append(feistel_perm(torch.arange(k, dtype=torch.int64, device=device), n, mix_step(sd, step)) + o)
     return torch.cat(out) if out else torch.empty(0, dtype=torch.int64, device=device)
 
 
-def _tables(layout: SegmentLayout, ks: Sequence[int], seeds: Sequence[int], device):
+def _tables(layout: SegmentLayout, ks: Sequence[int], seeds: Sequence[int], device, step: int, step_t):
+    """Device tables; with a device step counter the seed table is step-independent and
+    cached (no per-step host->device copy: capturable in a HIP graph)."""
     def build():
         off = [0]
         for k in ks:
@@ -96,20 +107,30 @@ def _tables(layout: SegmentLayout, ks: Sequence[int], seeds: Sequence[int], devi
             "out_off": torch.tensor(off, dtype=torch.int64, device=device),
         }
 
+    def seed_tensor(ss):
+        return torch.tensor([s - (1 << 64) if s >= (1 << 63) else s for s in ss], dtype=torch.int64)
+
     t = layout.cached(device, f"randk:{hash(tuple(ks))}", build)
-    sd = torch.tensor([s - (1 << 64) if s >= (1 << 63) else s for s in seeds], dtype=torch.int64)
+    if step_t is not None:
+        sd = layout.cached(device, f"randk_seeds:{hash(tuple(seeds))}", lambda: seed_tensor(seeds).to(device))
+        return t, sd
+    sd = seed_tensor([mix_step(s, step) for s in seeds])
     return t, sd.to(device, non_blocking=True)
 
 
-def gather(x: torch.Tensor, layout, ks, seeds, zero_selected: bool = False) -> torch.Tensor:
-    """vals[j] = x[idx_j]; optionally x[idx_j] = 0 afterwards (residual update)."""
+def gather(x: torch.Tensor, layout, ks, seeds, zero_selected: bool = False, step: int = 0,
+           step_t: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """vals[j] = x[idx_j]; optionally x[idx_j] = 0 afterwards (residual update).
+
+    Effective seed of segment s: ``seeds[s] ^ step * golden`` with the step taken from the
+    device counter ``step_t`` when given (native path), else from the host ``step``."""
     K = sum(ks)
     vals = torch.empty(K, dtype=torch.float32, device=x.device)
     if _native.use_native(x):
-        t, sd = _tables(layout, ks, seeds, x.device)
-        _native.lib().randk_gather(x, t["seg_off"], t["out_off"], sd, vals, x if zero_selected else None)
+        t, sd = _tables(layout, ks, seeds, x.device, step, step_t)
+        _native.lib().randk_gather(x, t["seg_off"], t["out_off"], sd, step_t, vals, x if zero_selected else None)
         return vals
-    idx = indices(layout, ks, seeds, x.device)
+    idx = indices(layout, ks, seeds, x.device, step)
     vals.copy_(x[idx])
     if zero_selected:
         x[idx] = 0.0
@@ -117,19 +138,19 @@ def gather(x: torch.Tensor, layout, ks, seeds, zero_selected: bool = False) -> t
 
 
 def scatter(vals_rows: torch.Tensor, layout, ks, seeds, out: torch.Tensor, scale: float,
-            accumulate: bool = False) -> None:
+            accumulate: bool = False, step: int = 0, step_t: Optional[torch.Tensor] = None) -> None:
     """out[idx_j] (+)= scale * sum_r vals_rows[r, j] (rank-ordered sum)."""
     K = sum(ks)
     if vals_rows.dim() == 1:
         vals_rows = vals_rows.view(1, -1)
     if _native.use_native(out):
-        t, sd = _tables(layout, ks, seeds, out.device)
+        t, sd = _tables(layout, ks, seeds, out.device, step, step_t)
         stride = vals_rows.stride(0) if vals_rows.size(0) > 1 else K
         assert vals_rows.stride(1) == 1
-        _native.lib().randk_scatter(vals_rows, stride, vals_rows.size(0), K, t["seg_off"], t["out_off"], sd, out,
-                                    scale, accumulate)
+        _native.lib().randk_scatter(vals_rows, stride, vals_rows.size(0), K, t["seg_off"], t["out_off"], sd, step_t,
+                                    out, scale, accumulate)
         return
-    idx = indices(layout, ks, seeds, out.device)
+    idx = indices(layout, ks, seeds, out.device, step)
     acc = vals_rows[0, :K].clone()
     for r in range(1, vals_rows.size(0)):
         acc += vals_rows[r, :K]

@@ -13,9 +13,11 @@ Requirements on the step (checked by construction in grace_amd):
   payload sizes read back to the host) do not and must run eagerly;
 * steady state before capture: the warm-up steps allocate residual / momentum state, so the
   captured kernels read and update it in place on every replay;
-* host-side step counters do not advance on replay: compressors that draw randomness per step
-  (Random-K indices, QSGD/TernGrad/Natural rounding, PowerSGD's Q) replay the captured seed --
-  ``GraphedStep`` therefore refuses them unless ``allow_static_seeds=True``.
+* per-step randomness must advance on replay: Random-K indices, QSGD/TernGrad/Natural rounding
+  and PowerSGD's Q mix a DEVICE step counter into their seeds (compressor/_base.py DeviceSteps,
+  bumped by a captured ``add_(1)``), so they are capturable on the native path.  Their torch
+  fallbacks seed a host generator, which a replay would freeze: refused unless
+  ``allow_static_seeds=True``.
 """
 from __future__ import annotations
 
@@ -23,8 +25,9 @@ from typing import Callable, Optional
 
 import torch
 
-_STOCHASTIC = ("RandomKCompressor", "QSGDCompressor", "TernGradCompressor", "NaturalCompressor",
-               "PowerSGDCompressor", "DgcCompressor", "AdaqCompressor")
+#: stochastic codecs whose native kernels read a device step counter
+_DEVICE_STEPPED = ("RandomKCompressor", "QSGDCompressor", "TernGradCompressor", "NaturalCompressor",
+                   "PowerSGDCompressor")
 _HOST_SYNC = ("ThresholdCompressor", "DgcCompressor", "AdaqCompressor", "INCEPTIONNCompressor",
               "SketchCompressor")
 
@@ -36,8 +39,11 @@ def graph_safe(grc, allow_static_seeds: bool = False) -> Optional[str]:
         return f"{name} reads payload sizes back to the host"
     if not grc.compressor.tensors_size_are_same:
         return f"{name} has variable-size payloads"
-    if name in _STOCHASTIC and not allow_static_seeds:
-        return f"{name} draws per-step randomness from host-side seeds"
+    if name in _DEVICE_STEPPED and not allow_static_seeds:
+        from ..ops import _native
+
+        if not _native.available() or not _native.native_on("cuda"):
+            return f"{name} without the native extension draws randomness from host-side seeds"
     return None
 
 

@@ -28,6 +28,8 @@ def main(argv=None):
     ap.add_argument("--marker", default="topk_compact_kernel")
     ap.add_argument("--per-step-markers", type=int, default=0, help="marker kernels per step (0 = auto)")
     ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--gaps", type=int, default=0, help="also list the N largest idle gaps (kernel pairs)")
+    ap.add_argument("--gap-min-us", type=float, default=5.0)
     args = ap.parse_args(argv)
     rows = list(csv.DictReader(open(args.trace)))
     ks = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows))
@@ -69,6 +71,22 @@ def main(argv=None):
     print(f"{'ms/step':>8} {'calls/step':>10}  kernel")
     for n, (t, c) in sorted(agg.items(), key=lambda kv: -kv[1][0])[: args.top]:
         print(f"{t / 1e6 / steps:8.3f} {c / steps:10.1f}  {n}")
+    if args.gaps:
+        # idle time between the end of everything launched so far and the next kernel start
+        pairs = collections.defaultdict(lambda: [0, 0])
+        hi, prev = None, None
+        for s, e, n in win:
+            if hi is not None and s - hi > args.gap_min_us * 1e3:
+                g = pairs[(short(prev)[:45], short(n)[:45])]
+                g[0] += s - hi
+                g[1] += 1
+            if hi is None or e > hi:
+                hi, prev = e, n
+        idle = sum(v[0] for v in pairs.values())
+        print(f"\nidle gaps > {args.gap_min_us} us: {idle / 1e6 / steps:.3f} ms/step")
+        print(f"{'ms/step':>8} {'n/step':>7}  after -> before")
+        for (a, b), (t, c) in sorted(pairs.items(), key=lambda kv: -kv[1][0])[: args.gaps]:
+            print(f"{t / 1e6 / steps:8.3f} {c / steps:7.1f}  {a} -> {b}")
 
 
 if __name__ == "__main__":
