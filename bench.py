@@ -42,7 +42,11 @@ def parse():
     ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (0 = workload default)")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16", help="autocast compute dtype")
-    ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--overlap", choices=["auto", "on", "off"], default="auto",
+                    help="compress+communicate on a side stream during backward; auto = off under a "
+                         "whole-step HIP graph (a forked capture costs ~0.9 ms/step on ROCm for ResNet-50, "
+                         "more than the overlap can hide), on otherwise")
+    ap.add_argument("--no-overlap", action="store_true", help="same as --overlap off")
     ap.add_argument("--no-benchmark-mode", action="store_true", help="disable MIOpen find (cudnn.benchmark)")
     ap.add_argument("--exposed-steps", type=int, default=3, help="untimed steps measuring exposed GRACE time")
     ap.add_argument("--force-dist", action="store_true",
@@ -81,8 +85,18 @@ def main():
     model = build_model(w, dev)
     base_opt = torch.optim.SGD(model.parameters(), lr=0.01 * world, momentum=0.5)
     grc = grace_from_params(dict(w.grace, world_size=world))
+    from grace_amd.parallel.graph import GraphedStep, graph_compute, graph_safe
+
+    mode = args.graph
+    if mode == "auto":
+        # measured on MI355X (ResNet-50 Top-K 1%): full 3205 img/s, compute 2640, eager 2520-3240
+        # (eager is host-launch bound: ~1100 kernels per step); full without overlap 3525
+        mode = "full" if graph_safe(grc) is None else "off"
+    if args.no_overlap:
+        args.overlap = "off"
+    overlap = args.overlap == "on" or (args.overlap == "auto" and mode != "full")
     opt = DistributedOptimizer(base_opt, grc, named_parameters=model.named_parameters(),
-                               bucket_cap_mb=args.bucket_mb, overlap=not args.no_overlap)
+                               bucket_cap_mb=args.bucket_mb, overlap=overlap)
     broadcast_parameters(model.state_dict(), root_rank=0)
     data = w.make_batch(batch, dev)
     if w.channels_last and isinstance(data, tuple) and data[0].dim() == 4:
@@ -99,13 +113,6 @@ def main():
         opt.step()
         return loss
 
-    from grace_amd.parallel.graph import GraphedStep, graph_compute, graph_safe
-
-    mode = args.graph
-    if mode == "auto":
-        # measured on MI355X (ResNet-50 Top-K 1%): full 3205 img/s, compute 2640, eager 2520-3240
-        # (eager is host-launch bound: ~1100 kernels per step)
-        mode = "full" if graph_safe(grc) is None else "off"
     if mode == "compute" and not (isinstance(data, tuple) and data[0].is_floating_point()):
         mode = "off"  # token-input models: graph only with the full-step capture
     graph_note = "off"
@@ -193,7 +200,7 @@ def main():
                 "parallelism": f"dp{world}",
                 "grace": w.grace,
                 "bucket_mb": args.bucket_mb,
-                "overlap": not args.no_overlap,
+                "overlap": overlap,
                 "hip_graph": graph_note,
             },
             "comm_wall_ms": round(float(ex.item()) * 1e3, 3),

@@ -113,6 +113,37 @@ class TorchComm(Comm):
         dist.barrier(group=self.group)
 
 
+def allgather_rows(comm: Comm, t: torch.Tensor, async_op: bool = False):
+    """All-gather ``t`` along dim 0 when the first dimension differs per rank.
+
+    Returns ``(work, finish)``; ``finish()`` (after ``work.wait()``) yields the rank-ordered
+    concatenation.  The per-rank row counts travel in one tiny all-gather first (one host
+    read: this is the path for data-dependent sizes -- sparse embedding gradients, Horovod's
+    ``allgather`` -- never for the bucketed compressed exchange, which is fixed-size)."""
+    W = comm.world_size
+    if t.dim() == 0:
+        t = t.view(1)
+    t = t.contiguous()
+    tail = tuple(t.shape[1:])
+    row = 1
+    for d in tail:
+        row *= d
+    cnt = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
+    cnts = torch.empty(W, dtype=torch.int64, device=t.device)
+    comm.all_gather_into(cnts, cnt)
+    sz = [int(v) for v in cnts.cpu().tolist()]
+    mx = max(sz)
+    send = torch.zeros(mx * row, dtype=t.dtype, device=t.device)
+    send[: t.numel()].copy_(t.reshape(-1))
+    out = torch.empty((W, mx * row), dtype=t.dtype, device=t.device)
+    work = comm.all_gather_into(out, send, async_op=async_op)
+
+    def finish():
+        return torch.cat([out[r, : sz[r] * row].view((sz[r],) + tail) for r in range(W)], 0)
+
+    return work, finish
+
+
 _DEFAULT: Optional[Comm] = None
 
 
@@ -125,7 +156,9 @@ def default_comm() -> Comm:
         if os.environ.get("GRACE_AMD_COMM", "torch") == "native":
             from .native_comm import RcclComm
 
-            return RcclComm.from_process_group()
+            # one communicator per process (cached: every caller shares its stream)
+            _DEFAULT = RcclComm.from_process_group()
+            return _DEFAULT
         return TorchComm()
     return LocalComm()
 

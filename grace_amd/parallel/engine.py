@@ -85,7 +85,8 @@ class GraceEngine:
     """Owns the buckets, hooks, streams and in-flight handles of one model."""
 
     def __init__(self, params: Sequence[Tuple[str, torch.nn.Parameter]], grc: Communicator,
-                 bucket_cap_mb: float = 64.0, backward_passes_per_step: int = 1, overlap: bool = True):
+                 bucket_cap_mb: float = 64.0, backward_passes_per_step: int = 1, overlap: bool = True,
+                 sparse_params: Sequence[str] = ()):
         self.grc = grc
         self.overlap = overlap
         self.backward_passes_per_step = backward_passes_per_step
@@ -95,6 +96,18 @@ class GraceEngine:
         names = [n for n, _ in named]
         if len(set(names)) != len(names):
             raise ValueError("parameter names must be unique")
+        unknown = set(sparse_params) - set(names)
+        if unknown:
+            raise ValueError(f"sparse_params not among the trainable parameters: {sorted(unknown)[:5]}")
+        # parameters with sparse gradients (nn.Embedding(sparse=True)) bypass the buckets: their
+        # (indices, values) are all-gathered uncompressed, as the reference does for TF
+        # IndexedSlices (patch_files/horovod/tensorflow/__init__.py:62-73)
+        self._sparse: Dict[int, Tuple[str, torch.nn.Parameter]] = {
+            id(p): (n, p) for n, p in named if n in set(sparse_params)}
+        self._sparse_pending: Dict[int, Tuple] = {}
+        named = [(n, p) for n, p in named if id(p) not in self._sparse]
+        if not named:
+            raise ValueError("no dense trainable parameters")
         self.device = named[0][1].device
         cap = int(bucket_cap_mb * 1024 * 1024 / 4)
         groups: List[List[Tuple[str, torch.nn.Parameter]]] = []
@@ -124,6 +137,8 @@ class GraceEngine:
         for b in self.buckets:
             for p in b.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._hook))
+        for _, p in self._sparse.values():
+            self._hooks.append(p.register_post_accumulate_grad_hook(self._sparse_hook))
         self.in_flight = 0
         self._paused = False
 
@@ -151,6 +166,9 @@ class GraceEngine:
             self._passes[id(p)] = cnt
             return
         self._passes[id(p)] = 0
+        if p.grad is not None and p.grad.is_sparse:
+            raise RuntimeError(f"parameter {self._name_of(p)} produced a sparse gradient: pass its name in "
+                               "sparse_params= (uncompressed sparse all-gather)")
         if p.grad is not None and p.grad.data_ptr() != view.data_ptr():
             # .grad was replaced (e.g. zero_grad(set_to_none=True)): move it back into the bucket
             view.copy_(p.grad)
@@ -158,6 +176,48 @@ class GraceEngine:
         b.pending -= 1
         if b.pending == 0:
             self._launch(b)
+
+    def _name_of(self, p) -> str:
+        b, i, _ = self._where[id(p)]
+        return f"{b.name}[{i}]"
+
+    def _sparse_hook(self, p: torch.Tensor):
+        if self._paused or p.grad is None:
+            return
+        cnt = self._passes.get(id(p), 0) + 1
+        if cnt < self.backward_passes_per_step:
+            self._passes[id(p)] = cnt
+            return
+        self._passes[id(p)] = 0
+        self._launch_sparse(p)
+
+    def _launch_sparse(self, p: torch.Tensor):
+        from .comm import allgather_rows
+
+        g = p.grad
+        if not g.is_sparse:  # a dense gradient for a sparse-declared param: exchange as rows
+            g = g.to_sparse(1)
+        g = g.coalesce()
+        comm = self.grc.comm
+        wi, fi = allgather_rows(comm, g.indices().t(), async_op=True)
+        wv, fv = allgather_rows(comm, g.values(), async_op=True)
+        self._sparse_pending[id(p)] = (p, (wi, fi), (wv, fv), g.shape)
+        self.in_flight += 1
+
+    def _finish_sparse(self):
+        W = self.grc.comm.world_size
+        for pid in [i for i in self._sparse if i not in self._sparse_pending]:
+            p = self._sparse[pid][1]
+            if p.grad is not None:  # gradient exists but backward hook did not fire (paused)
+                self._launch_sparse(p)
+        for p, (wi, fi), (wv, fv), shape in self._sparse_pending.values():
+            wi.wait()
+            wv.wait()
+            vals = fv()
+            if self.grc.compressor.average and W > 1:
+                vals = vals / W
+            p.grad = torch.sparse_coo_tensor(fi().t(), vals, shape).coalesce()
+        self._sparse_pending.clear()
 
     def _launch(self, b: Bucket):
         if b.handles is not None:
@@ -190,6 +250,8 @@ class GraceEngine:
             if out.data_ptr() != b.flat.data_ptr():
                 b.flat.copy_(out.view(-1))
             b.reset()
+        if self._sparse:
+            self._finish_sparse()
         self.in_flight = 0
 
     def zero_grad(self):
@@ -198,6 +260,8 @@ class GraceEngine:
                                  "call synchronize()/step() first")
         for b in self.buckets:
             b.flat.zero_()
+        for _, p in self._sparse.values():
+            p.grad = None
 
     def remove(self):
         for h in self._hooks:

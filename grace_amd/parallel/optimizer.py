@@ -22,7 +22,7 @@ from .engine import GraceEngine
 
 class _DistributedOptimizer:
     def __init__(self, optimizer, grace, named_parameters=None, backward_passes_per_step: int = 1,
-                 bucket_cap_mb: float = 64.0, overlap: bool = True):
+                 bucket_cap_mb: float = 64.0, overlap: bool = True, sparse_params=()):
         self._opt = optimizer
         if named_parameters is None:
             params = [p for g in optimizer.param_groups for p in g["params"]]
@@ -33,7 +33,8 @@ class _DistributedOptimizer:
         if missing:
             raise ValueError(f"named_parameters not in the optimizer: {missing[:5]}")
         self.engine = GraceEngine(named_parameters, grace, bucket_cap_mb=bucket_cap_mb,
-                                  backward_passes_per_step=backward_passes_per_step, overlap=overlap)
+                                  backward_passes_per_step=backward_passes_per_step, overlap=overlap,
+                                  sparse_params=sparse_params)
         self._synchronized = False
         self._should_sync = True
 
@@ -100,15 +101,36 @@ def broadcast_parameters(params, root_rank: int = 0, group=None):
             off += n
 
 
+def _materialize_state(opt) -> None:
+    """Create the optimizer's lazily-initialised state with one lr=0 step on zero gradients
+    (Horovod's approach, patch_files/horovod/torch/__init__.py:300-330), so every rank holds
+    the same state tensors before the broadcast."""
+    saved = [g.get("lr") for g in opt.param_groups]
+    created = []
+    for g in opt.param_groups:
+        if "lr" in g:
+            g["lr"] = 0.0
+        for p in g["params"]:
+            if p.requires_grad and p.grad is None:
+                p.grad = torch.zeros_like(p)
+                created.append(p)
+    opt.step()
+    for p in created:
+        p.grad = None
+    for g, lr in zip(opt.param_groups, saved):
+        if lr is not None:
+            g["lr"] = lr
+
+
 def broadcast_optimizer_state(optimizer, root_rank: int = 0, group=None):
-    """Broadcast every tensor of the optimizer state from ``root_rank`` (creates missing state
-    by a zero-gradient no-op step first, as Horovod does)."""
+    """Broadcast every tensor of the optimizer state from ``root_rank``; state that does not
+    exist yet is first created on every rank by a no-op step (lr = 0, zero gradients)."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
         return
     opt = getattr(optimizer, "_opt", optimizer)
+    if not opt.state_dict()["state"]:
+        _materialize_state(opt)
     state = opt.state_dict()["state"]
-    if not state and dist.get_world_size(group) > 1:
-        return
     tensors = []
     for pid in sorted(state):
         for k in sorted(state[pid]):

@@ -5,3 +5,7 @@ implementations; the abstract base classes are the same objects as ``grace_amd.c
 """
 from ..core import Communicator, Compressor, Memory  # noqa: F401
 from ..parallel.optimizer import DistributedOptimizer, broadcast_optimizer_state, broadcast_parameters  # noqa: F401,E402
+from .mpi_ops import (  # noqa: F401,E402
+    allgather, allgather_async, allreduce, allreduce_, allreduce_async, allreduce_async_, broadcast, broadcast_,
+    broadcast_async, broadcast_async_, init, is_initialized, local_rank, local_size, poll, rank, shutdown, size,
+    synchronize)

@@ -94,9 +94,10 @@ def test_graph_replay_draws_fresh_rounding(make):
         torch.cuda.synchronize()
         seen.append(out.clone())
     assert not torch.equal(seen[0], seen[1]) and not torch.equal(seen[1], seen[2])
-    host_before = comp.steps["rng_bucket"]
+    # the counter counts EXECUTED compress calls: 2 warm-up + 3 replays (the capture-time call
+    # only records the graph); state_dict() folds it back into the host dict
     comp.state_dict()
-    assert comp.steps["rng_bucket"] == host_before + 3
+    assert comp.steps["rng_bucket"] == 5
 
 
 def test_graph_replay_randomk_roundtrip_consistent():
