@@ -404,35 +404,50 @@ void dgc_compact(const Tensor& x, const Tensor& thr, const Tensor& out_val, cons
 
 // ------------------------------------------------------------------------------ PowerSGD
 void powersgd_mq(const Tensor& x, const Tensor& small, const Tensor& out, const Tensor& mats, const Tensor& tiles,
-                 int64_t mode) {
+                 int64_t mode, const c10::optional<Tensor>& comp_r, double beta, double gamma,
+                 const c10::optional<Tensor>& xout) {
   CHECK_F32(x);
   CHECK_F32(small);
   CHECK_F32(out);
   CHECK_I64(mats);
   CHECK_I32(tiles);
+  TORCH_CHECK(mode == 0 || !(comp_r.has_value() || xout.has_value()), "compensation is fused into mode 0 only");
+  if (comp_r.has_value()) TORCH_CHECK(xout.has_value(), "comp_r needs xout");
+  if (xout.has_value()) TORCH_CHECK(xout->numel() == x.numel(), "xout size");
+  if (comp_r.has_value()) TORCH_CHECK(comp_r->numel() == x.numel(), "comp_r size");
   DevGuard guard(x.device());
   grace::powersgd_mq(x.data_ptr<float>(), small.data_ptr<float>(), out.data_ptr<float>(), out.numel(),
                      mats.data_ptr<int64_t>(), tiles.data_ptr<int32_t>(), (int)(tiles.numel() / 3), (int)mode,
-                     cur_stream());
+                     opt_f32(comp_r), (float)beta, (float)gamma, opt_f32_mut(xout), cur_stream());
 }
 
-void gram_schmidt(const Tensor& buf, const Tensor& mats, int64_t which, int64_t n_mat) {
+void gram_orthonormalize(const Tensor& buf, const Tensor& mats, int64_t which, int64_t n_mat, const Tensor& gtiles,
+                         const Tensor& gtile_begin, int64_t passes) {
   CHECK_F32(buf);
   CHECK_I64(mats);
-  TORCH_CHECK(mats.numel() >= 6 * n_mat, "mats table");
+  CHECK_I32(gtiles);
+  CHECK_I32(gtile_begin);
+  TORCH_CHECK(mats.numel() >= 6 * n_mat && gtile_begin.numel() == n_mat + 1, "gram tables");
   DevGuard guard(buf.device());
-  grace::gram_schmidt(buf.data_ptr<float>(), mats.data_ptr<int64_t>(), (int)n_mat, (int)which, cur_stream());
+  const int64_t nt = gtiles.numel() / 2;
+  auto part = at::empty({std::max<int64_t>(nt, 1) * 256}, buf.options().dtype(at::kDouble));
+  auto T = at::empty({std::max<int64_t>(n_mat, 1) * 256}, buf.options());
+  grace::gram_orthonormalize(buf.data_ptr<float>(), mats.data_ptr<int64_t>(), (int)n_mat, (int)which,
+                             gtiles.data_ptr<int32_t>(), (int)nt, gtile_begin.data_ptr<int32_t>(),
+                             part.data_ptr<double>(), T.data_ptr<float>(), (int)passes, cur_stream());
 }
 
-void powersgd_pqt(const Tensor& P, const Tensor& Q, const Tensor& out, const Tensor& mats, const Tensor& tiles) {
+void powersgd_pqt(const Tensor& P, const Tensor& Q, const Tensor& out, const Tensor& mats, const Tensor& tiles,
+                  const c10::optional<Tensor>& resid) {
   CHECK_F32(P);
   CHECK_F32(Q);
   CHECK_F32(out);
   CHECK_I64(mats);
   CHECK_I32(tiles);
+  if (resid.has_value()) TORCH_CHECK(resid->numel() == out.numel(), "resid size");
   DevGuard guard(out.device());
   grace::powersgd_pqt(P.data_ptr<float>(), Q.data_ptr<float>(), out.data_ptr<float>(), mats.data_ptr<int64_t>(),
-                      tiles.data_ptr<int32_t>(), (int)(tiles.numel() / 3), cur_stream());
+                      tiles.data_ptr<int32_t>(), (int)(tiles.numel() / 3), opt_f32_mut(resid), cur_stream());
 }
 
 void philox_normal(const Tensor& out, int64_t seed, const c10::optional<Tensor>& step) {
@@ -569,7 +584,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dgc_refine", &dgc_refine);
   m.def("dgc_compact", &dgc_compact);
   m.def("powersgd_mq", &powersgd_mq);
-  m.def("gram_schmidt", &gram_schmidt);
+  m.def("gram_orthonormalize", &gram_orthonormalize);
   m.def("powersgd_pqt", &powersgd_pqt);
   m.def("philox_normal", &philox_normal);
   m.def("cast16", &cast16);

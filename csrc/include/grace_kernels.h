@@ -82,10 +82,13 @@ void dgc_compact(const ChunkTable& ct, const float* x, const float* thr, float* 
 // ---------------------------------------------------------------- powersgd.hip
 // mats: int64 [n_mat][6] = (x_off, n, m, r, p_off, q_off); tiles: int32 [n_tiles][3]
 void powersgd_mq(const float* x, const float* small, float* out, int64_t out_len, const int64_t* mats,
-                 const int32_t* tiles, int n_tiles, int mode, hipStream_t stream);
-void gram_schmidt(float* buf, const int64_t* mats, int n_mat, int which, hipStream_t stream);
+                 const int32_t* tiles, int n_tiles, int mode, const float* comp_r, float beta, float gamma,
+                 float* xout, hipStream_t stream);
+void gram_orthonormalize(float* buf, const int64_t* mats, int n_mat, int which, const int32_t* gtiles,
+                         int n_gtiles, const int32_t* gtile_begin, double* partials, float* T, int passes,
+                         hipStream_t stream);
 void powersgd_pqt(const float* P, const float* Q, float* out, const int64_t* mats, const int32_t* tiles, int n_tiles,
-                  hipStream_t stream);
+                  float* resid, hipStream_t stream);
 void philox_normal(float* out, int64_t n, SeedArg seed, hipStream_t stream);
 
 // ---------------------------------------------------------------- cast_sketch.hip

@@ -12,9 +12,10 @@
 //      from a second LDS tile.  Strip partial sums are combined with fp32 atomics (the output
 //      is only n*r or m*r floats).  Tall-skinny with r=4 is bandwidth bound (2 FLOP/byte):
 //      the MFMA work is ~25% utilised by construction but still ~3x faster than HBM needs.
-//  gram_schmidt       one workgroup per matrix, modified Gram-Schmidt over its r columns with
-//                     workgroup reductions (columns normalised, later columns projected out)
-//  powersgd_pqt       out = P Q^T: exactly one 16x16x4 MFMA per 16x16 output tile when r <= 4
+//  gram_orthonormalize  Gram matrices on MFMA (all tiles of all matrices in one launch), MGS in
+//                     the Gram metric per matrix, A <- A T; twice (CholQR2) -- see below
+//  powersgd_pqt       out = P Q^T: exactly one 16x16x4 MFMA per 16x16 output tile when r <= 4,
+//                     optionally fused with the residual update  r = x - P Q^T
 //  philox_normal      N(0,1) via Philox4x32 + Box-Muller (Q identical on every rank)
 #include "grace_common.h"
 #include "grace_kernels.h"
@@ -40,16 +41,20 @@ __device__ __forceinline__ Mat load_mat(const int64_t* __restrict__ mats, int i)
 }
 
 // tiles: int32 [n_tiles][3] = (matrix, block index along the output dim, strip index)
-template <int MODE>
+// COMP (MODE 0 only; every element of M is staged by exactly one workgroup there):
+//   0: M = x      1: M = x, stored to xout      2: M = beta*r + gamma*x, stored to xout
+// i.e. the PowerSGD error-feedback compensate (memory/powersgd.py) fused into the first
+// product instead of a separate read-read-write pass over the bucket.
+template <int MODE, int COMP>
 __global__ __launch_bounds__(kBlock) void mq_kernel(const float* __restrict__ x, const float* __restrict__ small,
                                                     float* __restrict__ out, const int64_t* __restrict__ mats,
-                                                    const int32_t* __restrict__ tiles) {
+                                                    const int32_t* __restrict__ tiles, const float* cr, float beta,
+                                                    float gamma, float* xout) {
   __shared__ float ms[kT * kLd];
   __shared__ float ss[kT * kRPad];
   const int* tl = tiles + 3 * blockIdx.x;
   const Mat mt = load_mat(mats, tl[0]);
   const int64_t n = mt.n, m = mt.m, r = mt.r;
-  const float* M = x + mt.x_off;
   const int lane = lane_id(), w = wave_id();
   // MODE 0: output rows [ob, ob+64), reduce over cols [s0, s1)
   // MODE 1: output cols [ob, ob+64), reduce over rows [s0, s1)
@@ -68,7 +73,14 @@ __global__ __launch_bounds__(kBlock) void mq_kernel(const float* __restrict__ x,
       const int idx = it * kBlock + threadIdx.x;
       const int rr = idx >> 6, cc = idx & 63;
       const int64_t gr = r0 + rr, gc = c0 + cc;
-      ms[rr * kLd + cc] = (gr < n && gc < m) ? M[gr * m + gc] : 0.f;
+      float v = 0.f;
+      if (gr < n && gc < m) {
+        const int64_t gi = mt.x_off + gr * m + gc;
+        v = x[gi];
+        if (COMP == 2) v = fmaf(beta, cr[gi], gamma * v);
+        if (COMP != 0) xout[gi] = v;
+      }
+      ms[rr * kLd + cc] = v;
     }
     // small operand rows [sb, sb+64) of S, r padded to 16 with zeros
     for (int it = 0; it < kT * kRPad / kBlock; ++it) {
@@ -103,67 +115,124 @@ __global__ __launch_bounds__(kBlock) void mq_kernel(const float* __restrict__ x,
   }
 }
 
-// Modified Gram-Schmidt on the r columns of a (len x r) row-major block; one workgroup/matrix.
-__global__ __launch_bounds__(kBlock) void gram_schmidt_kernel(float* __restrict__ buf, const int64_t* __restrict__ mats,
-                                                              int which) {
-  const Mat mt = load_mat(mats, blockIdx.x);
-  const int64_t len = which == 0 ? mt.n : mt.m;
+// ---- Orthonormalisation of the r columns of every (len x r) block: Gram-matrix MGS.
+// The reference runs modified Gram-Schmidt column by column (dist/compressor/powersgd.py:7-18);
+// a one-workgroup-per-matrix MGS leaves the chip idle (VGG-16's 25088 x 4 Q took 77 us).  Here:
+//   gram_partial  G_tile = A_tile^T A_tile with one v_mfma_f32_16x16x4_f32 per 4 rows (A is both
+//                 MFMA operands), all tiles of all matrices in one launch -> fp64 partials;
+//   gram_fix      per matrix: fold the partials in tile order (fp64, deterministic), then MGS
+//                 expressed in the Gram metric on the r x r coefficient matrix T (columns of
+//                 A*T stay orthonormal; zero columns stay zero, as in the MGS kernel it replaces);
+//   gram_apply    A <- A T row by row.
+// Run twice (CholQR2): the second pass restores fp32-level orthogonality for ill-conditioned P.
+constexpr int kGRows = 1024;  // rows per Gram tile
+
+__device__ __forceinline__ int64_t blk_len(const Mat& mt, int which) { return which == 0 ? mt.n : mt.m; }
+__device__ __forceinline__ int64_t blk_off(const Mat& mt, int which) { return which == 0 ? mt.p_off : mt.q_off; }
+
+// gtiles: int32 [n][2] = (matrix, tile); part: fp64 [n][16*16]
+__global__ __launch_bounds__(kBlock) void gram_partial_kernel(const float* __restrict__ buf,
+                                                              const int64_t* __restrict__ mats,
+                                                              const int32_t* __restrict__ gtiles, int which,
+                                                              double* __restrict__ part) {
+  const int* tl = gtiles + 2 * blockIdx.x;
+  const Mat mt = load_mat(mats, tl[0]);
+  const int64_t len = blk_len(mt, which);
   const int r = (int)mt.r;
-  float* A = buf + (which == 0 ? mt.p_off : mt.q_off);
-  __shared__ float red[kRPad][kBlock / kWave];
-  __shared__ float coef[kRPad];
-  for (int i = 0; i < r; ++i) {
-    // norm of column i
-    float s = 0.f;
-    for (int64_t k = threadIdx.x; k < len; k += kBlock) {
-      const float v = A[k * r + i];
-      s += v * v;
-    }
-    s = wave_sum(s);
-    if (lane_id() == 0) red[0][wave_id()] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      float t = 0.f;
-      for (int q = 0; q < kBlock / kWave; ++q) t += red[0][q];
-      const float nrm = sqrtf(t);
-      coef[0] = nrm > 1e-30f ? 1.f / nrm : 1e30f;  // zero column stays zero (reference: NaN)
-    }
-    __syncthreads();
-    const float inv = coef[0];
-    for (int64_t k = threadIdx.x; k < len; k += kBlock) A[k * r + i] *= inv;
-    __syncthreads();
-    if (i + 1 >= r) break;
-    // projections of the normalised column on every later column
-    float d[kRPad];
+  const float* A = buf + blk_off(mt, which);
+  const int lane = lane_id(), w = wave_id();
+  const int64_t r0 = (int64_t)tl[1] * kGRows + (int64_t)w * (kGRows / 4);
+  int64_t r1 = r0 + kGRows / 4;
+  if (r1 > len) r1 = len;
+  const int col = lane & 15;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t k0 = r0; k0 < r1; k0 += 4) {
+    const int64_t row = k0 + (lane >> 4);
+    const float a = (row < r1 && col < r) ? A[row * r + col] : 0.f;
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, a, acc, 0, 0, 0);  // C[i][j] += A[k][i] A[k][j]
+  }
+  __shared__ double red[kBlock / kWave][256];
 #pragma unroll
-    for (int j = 0; j < kRPad; ++j) d[j] = 0.f;
-    for (int64_t k = threadIdx.x; k < len; k += kBlock) {
-      const float ci = A[k * r + i];
-      for (int j = i + 1; j < r; ++j) d[j] += ci * A[k * r + j];
+  for (int q = 0; q < 4; ++q) red[w][((lane >> 4) * 4 + q) * 16 + col] = (double)acc[q];
+  __syncthreads();
+  double* o = part + (int64_t)blockIdx.x * 256;
+  for (int e = threadIdx.x; e < 256; e += kBlock) o[e] = red[0][e] + red[1][e] + red[2][e] + red[3][e];
+}
+
+// one 64-thread workgroup per matrix; T: fp32 [n_mat][16*16] (row i, col j: A_new[:, j] = sum_i A[:, i] T[i][j])
+__global__ __launch_bounds__(kWave) void gram_fix_kernel(const int64_t* __restrict__ mats,
+                                                         const int32_t* __restrict__ gtile_begin,
+                                                         const double* __restrict__ part, float* __restrict__ T) {
+  const int mi = blockIdx.x;
+  const Mat mt = load_mat(mats, mi);
+  const int r = (int)mt.r;
+  __shared__ double G[16][16];
+  __shared__ double Tm[16][16];
+  const int t0 = gtile_begin[mi], t1 = gtile_begin[mi + 1];
+  for (int e = threadIdx.x; e < 256; e += kWave) {
+    double v = 0.0;
+    for (int t = t0; t < t1; ++t) v += part[(int64_t)t * 256 + e];
+    G[e >> 4][e & 15] = v;
+    Tm[e >> 4][e & 15] = (e >> 4) == (e & 15) ? 1.0 : 0.0;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 0; i < r; ++i) {
+      // ||A t_i||^2 = t_i^T G t_i
+      double nn = 0.0;
+      for (int a = 0; a <= i; ++a)
+        for (int b = 0; b <= i; ++b) nn += Tm[a][i] * G[a][b] * Tm[b][i];
+      const double nrm = nn > 0.0 ? sqrt(nn) : 0.0;
+      const double inv = nrm > 1e-30 ? 1.0 / nrm : 0.0;  // zero column stays zero
+      for (int a = 0; a <= i; ++a) Tm[a][i] *= inv;
+      for (int j = i + 1; j < r; ++j) {
+        double pr = 0.0;  // <A t_i, A t_j> = t_i^T G t_j
+        for (int a = 0; a <= i; ++a)
+          for (int b = 0; b <= j; ++b) pr += Tm[a][i] * G[a][b] * Tm[b][j];
+        for (int a = 0; a <= i; ++a) Tm[a][j] -= pr * Tm[a][i];
+      }
     }
-    for (int j = i + 1; j < r; ++j) {
-      const float v = wave_sum(d[j]);
-      if (lane_id() == 0) red[j][wave_id()] = v;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 256; e += kWave) T[(int64_t)mi * 256 + e] = (float)Tm[e >> 4][e & 15];
+}
+
+__global__ __launch_bounds__(kBlock) void gram_apply_kernel(float* __restrict__ buf, const int64_t* __restrict__ mats,
+                                                            const int32_t* __restrict__ gtiles, int which,
+                                                            const float* __restrict__ T) {
+  const int* tl = gtiles + 2 * blockIdx.x;
+  const int mi = tl[0];
+  const Mat mt = load_mat(mats, mi);
+  const int64_t len = blk_len(mt, which);
+  const int r = (int)mt.r;
+  float* A = buf + blk_off(mt, which);
+  __shared__ float Ts[256];
+  Ts[threadIdx.x] = T[(int64_t)mi * 256 + threadIdx.x];
+  __syncthreads();
+  const int64_t rb = (int64_t)tl[1] * kGRows;
+  int64_t re = rb + kGRows;
+  if (re > len) re = len;
+  for (int64_t row = rb + threadIdx.x; row < re; row += kBlock) {
+    float a[16], o[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) a[i] = i < r ? A[row * r + i] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      float v = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v = fmaf(a[i], Ts[i * 16 + j], v);
+      o[j] = v;
     }
-    __syncthreads();
-    if (threadIdx.x < kRPad && (int)threadIdx.x > i && (int)threadIdx.x < r) {
-      float t = 0.f;
-      for (int q = 0; q < kBlock / kWave; ++q) t += red[threadIdx.x][q];
-      coef[threadIdx.x] = t;
-    }
-    __syncthreads();
-    for (int64_t k = threadIdx.x; k < len; k += kBlock) {
-      const float ci = A[k * r + i];
-      for (int j = i + 1; j < r; ++j) A[k * r + j] -= coef[j] * ci;
-    }
-    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (j < r) A[row * r + j] = o[j];
   }
 }
 
 // out[x_off + row*m + col] = sum_j P[row][j] Q[col][j]; tiles: (matrix, row block of 16, col block of 64)
 __global__ __launch_bounds__(kBlock) void pqt_kernel(const float* __restrict__ P, const float* __restrict__ Q,
                                                      float* __restrict__ out, const int64_t* __restrict__ mats,
-                                                     const int32_t* __restrict__ tiles) {
+                                                     const int32_t* __restrict__ tiles, float* resid) {
   const int* tl = tiles + 3 * blockIdx.x;
   const Mat mt = load_mat(mats, tl[0]);
   const int64_t n = mt.n, m = mt.m, r = mt.r;
@@ -185,7 +254,11 @@ __global__ __launch_bounds__(kBlock) void pqt_kernel(const float* __restrict__ P
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int64_t row = row0 + (lane >> 4) * 4 + q;
-      if (row < n) out[mt.x_off + row * m + col] = acc[q];
+      if (row < n) {
+        const int64_t gi = mt.x_off + row * m + col;
+        out[gi] = acc[q];
+        if (resid != nullptr) resid[gi] -= acc[q];  // resid holds x: residual = x - P Q^T
+      }
     }
   }
 }
@@ -213,24 +286,35 @@ __global__ __launch_bounds__(kBlock) void philox_normal_kernel(float* __restrict
 }  // namespace
 
 void powersgd_mq(const float* x, const float* small, float* out, int64_t out_len, const int64_t* mats,
-                 const int32_t* tiles, int n_tiles, int mode, hipStream_t stream) {
+                 const int32_t* tiles, int n_tiles, int mode, const float* comp_r, float beta, float gamma,
+                 float* xout, hipStream_t stream) {
   GRACE_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(float) * out_len, stream));
   if (n_tiles <= 0) return;
-  if (mode == 0)
-    mq_kernel<0><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles);
+  if (mode == 1)
+    mq_kernel<1, 0><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles, nullptr, 0.f, 0.f, nullptr);
+  else if (xout == nullptr)
+    mq_kernel<0, 0><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles, nullptr, 0.f, 0.f, nullptr);
+  else if (comp_r == nullptr)
+    mq_kernel<0, 1><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles, nullptr, 0.f, 0.f, xout);
   else
-    mq_kernel<1><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles);
+    mq_kernel<0, 2><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles, comp_r, beta, gamma, xout);
 }
 
-void gram_schmidt(float* buf, const int64_t* mats, int n_mat, int which, hipStream_t stream) {
-  if (n_mat <= 0) return;
-  gram_schmidt_kernel<<<n_mat, kBlock, 0, stream>>>(buf, mats, which);
+void gram_orthonormalize(float* buf, const int64_t* mats, int n_mat, int which, const int32_t* gtiles,
+                         int n_gtiles, const int32_t* gtile_begin, double* partials, float* T, int passes,
+                         hipStream_t stream) {
+  if (n_mat <= 0 || n_gtiles <= 0) return;
+  for (int p = 0; p < passes; ++p) {
+    gram_partial_kernel<<<n_gtiles, kBlock, 0, stream>>>(buf, mats, gtiles, which, partials);
+    gram_fix_kernel<<<n_mat, kWave, 0, stream>>>(mats, gtile_begin, partials, T);
+    gram_apply_kernel<<<n_gtiles, kBlock, 0, stream>>>(buf, mats, gtiles, which, T);
+  }
 }
 
 void powersgd_pqt(const float* P, const float* Q, float* out, const int64_t* mats, const int32_t* tiles, int n_tiles,
-                  hipStream_t stream) {
+                  float* resid, hipStream_t stream) {
   if (n_tiles <= 0) return;
-  pqt_kernel<<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles);
+  pqt_kernel<<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid);
 }
 
 void philox_normal(float* out, int64_t n, SeedArg seed, hipStream_t stream) {

@@ -27,7 +27,7 @@ class EFSignSGDCompressor(BucketCompressor):
         self.learning_rate = lr
 
     def _vals(self, stats, lay):
-        n = torch.tensor(lay.numels, dtype=torch.float32, device=stats.device).clamp_min(1)
+        n = lay.numels_t(stats.device).clamp_min(1)
         mean = stats[:, S.ABSSUM] / n
         return mean, -mean
 

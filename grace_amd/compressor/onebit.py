@@ -25,7 +25,7 @@ class OneBitCompressor(BucketCompressor):
     allreduce_compatible = True
 
     def _means(self, stats, lay):
-        n = torch.tensor(lay.numels, dtype=torch.float32, device=stats.device)
+        n = lay.numels_t(stats.device)
         negsum, negcnt = stats[:, S.NEGSUM], stats[:, S.NEGCNT]
         possum, poscnt = stats[:, S.SUM] - negsum, n - negcnt
         mean0 = torch.where(negcnt > 0, negsum / negcnt.clamp_min(1), negsum)

@@ -59,6 +59,40 @@ class PowerSGDCompressor(BucketCompressor):
             ctx.extra["plan"] = plan
             return [self.flat(tensor)], ctx
         x = self.flat(tensor)
+        return self._power(x, x, name, ctx, plan), ctx
+
+    def fused_compress(self, tensor, name, memory):
+        """PowerSGDMemory fused into the kernels: the compensate x = r + g is computed while
+        staging M for P = M Q (and stored into the residual buffer), and the residual update
+        r = x - P Q^T happens in the decompress pass that writes P Q^T anyway -- 7 passes
+        over the bucket instead of 10 (axpby, MQ, M^T P, P Q^T twice, x - dec)."""
+        from ..memory.powersgd import PowerSGDMemory
+
+        if type(memory) is not PowerSGDMemory:
+            return None
+        ctx = self.ctx(tensor, name)
+        plan = self._plan(ctx)
+        if plan.n_mat == 0:
+            return None
+        g = self.flat(tensor)
+        if not memory.warm_start:
+            self.q_memory.pop(name, None)
+        rs = memory.residuals.get(name)
+        valid = rs is not None and rs.numel() == g.numel() and rs.dtype == torch.float32 and rs.is_contiguous()
+        if not valid:
+            # 1-D segments keep a zero residual (reference: no error feedback for them)
+            rs = torch.zeros(tensor.shape, dtype=torch.float32, device=g.device)
+            memory.residuals[name] = rs
+        r = rs.view(-1)
+        # x (matrix segments) lands in r; 1-D segments of x equal g (their residual is zero)
+        vec = self._power(g, r, name, ctx, plan, comp_r=r if valid else None, xout=r)
+        ctx.extra["resid"] = r
+        return vec, ctx
+
+    def _power(self, x, x_after, name, ctx, plan, comp_r=None, xout=None):
+        """One power iteration for every matrix of the bucket.  ``x`` feeds the first product
+        (compensated on the fly when ``xout`` is given, which then holds x); ``x_after`` is
+        what the second product reads."""
         W = self.world_size or 1
         step, step_t = self.advance(name, x.device)
         q = self.q_memory.get(name) if self.warm_start else None
@@ -69,13 +103,13 @@ class PowerSGDCompressor(BucketCompressor):
             q = PS.randn_shared(plan.q_total, seed if step_t is not None else mix_step(seed, step), x.device,
                                 step=step_t)
             PS.orthogonalize(q, plan, which="q")
-        p = PS.mq(x, q, plan)  # P = M Q for every matrix (one launch)
+        p = PS.mq(x, q, plan, comp_r=comp_r, xout=xout)  # P = M Q for every matrix (one launch)
         if self.comm is not None and W > 1:
             self.comm.all_reduce(p)
         if W > 1:
             p.div_(W)
         PS.orthogonalize(p, plan, which="p")
-        q = PS.mtp(x, p, plan)  # Q = M^T P
+        q = PS.mtp(x_after, p, plan)  # Q = M^T P
         if self.comm is not None and W > 1:
             self.comm.all_reduce(q)
         if W > 1:
@@ -84,7 +118,7 @@ class PowerSGDCompressor(BucketCompressor):
             self.q_memory[name] = q
         ctx.extra.update(plan=plan, p=p, q=q)
         vec = PS.gather_vectors(x, plan)  # 1-D segments, sent through the communicator
-        return ([vec] if vec.numel() else []), ctx
+        return [vec] if vec.numel() else []
 
     def _decompress(self, tensors, ctx, vec_scale: float):
         plan = ctx.extra["plan"]
@@ -94,7 +128,8 @@ class PowerSGDCompressor(BucketCompressor):
             out = v * vec_scale if vec_scale != 1.0 else v
             return self.finish(out.reshape(-1), ctx)
         out = self.out_buffer(ctx, dev)
-        PS.pqt(ctx.extra["p"], ctx.extra["q"], plan, out)
+        # fused path: the residual buffer holds x; this pass also leaves r = x - P Q^T there
+        PS.pqt(ctx.extra["p"], ctx.extra["q"], plan, out, resid=ctx.extra.pop("resid", None))
         if tensors:
             PS.scatter_vectors(tensors[0], plan, out, vec_scale)
         return self.finish(out, ctx)

@@ -34,13 +34,13 @@ def segmented_quantile_edges(x: torch.Tensor, lay, q: int) -> torch.Tensor:
     bucket (keys = segment id << 32 | order-preserving float bits)."""
     dev = x.device
     seg_id = lay.cached(dev, "seg_id", lambda: torch.repeat_interleave(
-        torch.arange(lay.n_seg, device=dev), torch.tensor(lay.numels, device=dev)))
+        torch.arange(lay.n_seg, device=dev), lay.numels_t(dev, torch.int64)))
     u = x.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
     ordered = torch.where(u >= 0x80000000, (~u) & 0xFFFFFFFF, u | 0x80000000)
     order = torch.sort((seg_id << 32) | ordered).indices
     sx = x[order]
-    offs = torch.tensor(lay.offsets[:-1], device=dev, dtype=torch.float64)
-    n = torch.tensor(lay.numels, device=dev, dtype=torch.float64)
+    offs = lay.offsets_t(dev, torch.float64)[:-1]
+    n = lay.numels_t(dev, torch.float64)
     probs = torch.linspace(0, 1, q + 1, device=dev, dtype=torch.float64)
     pos = probs[None, :] * (n[:, None] - 1).clamp_min(0)
     lo, hi = pos.floor(), pos.ceil()
@@ -94,7 +94,7 @@ class SketchCompressor(BucketCompressor):
             return self.finish(out, ctx)
         out = self.out_buffer(ctx, per_rank[0][0].device, zero=True)
         seg_id = torch.repeat_interleave(torch.arange(lay.n_seg, device=out.device),
-                                         torch.tensor(lay.numels, device=out.device))
+                                         lay.numels_t(out.device, torch.int64))
         for bins, means in per_rank:
             b = bins.long()
             if bins.dtype == torch.int16:

@@ -38,8 +38,7 @@ class TernGradCompressor(BucketCompressor):
             r, valid = memory.residual_buffer(name, g)
             stats = S.segment_stats(g, lay, r=r, r_valid=valid, beta=memory.beta, gamma=memory.gamma, xout=r)
             x = r
-        n = lay.cached(g.device, "numels_f32",
-                       lambda: torch.tensor(lay.numels, dtype=torch.float32, device=g.device).clamp_min(1))
+        n = lay.numels_t(g.device).clamp_min(1)
         mean = stats[:, S.SUM] / n
         var = (stats[:, S.SUMSQ] / n - mean * mean).clamp_min(0)
         clip = self.clip_factor * torch.sqrt(var)

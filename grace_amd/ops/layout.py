@@ -120,6 +120,14 @@ class SegmentLayout:
             self._dev[key] = v
         return v
 
+    def numels_t(self, device, dtype=torch.float32) -> torch.Tensor:
+        """Segment sizes as a cached device tensor (no per-step host->device copy, so code
+        using it can run inside a HIP-graph capture)."""
+        return self.cached(device, f"numels:{dtype}", lambda: torch.tensor(self.numels, dtype=dtype, device=device))
+
+    def offsets_t(self, device, dtype=torch.int64) -> torch.Tensor:
+        return self.cached(device, f"offsets:{dtype}", lambda: torch.tensor(self.offsets, dtype=dtype, device=device))
+
 
 _LAYOUT_CACHE: Dict[Tuple, SegmentLayout] = {}
 

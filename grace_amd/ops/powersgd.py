@@ -50,12 +50,24 @@ class Plan:
                 return torch.tensor(lst, dtype=torch.int32, device=device).view(-1) if lst else \
                     torch.empty(0, dtype=torch.int32, device=device)
 
+            # Gram tiles of 1024 rows over each P_i (n rows) and Q_i (m rows)
+            gt = {"p": [], "q": []}
+            gtb = {"p": [0], "q": [0]}
+            for (xo, n, m, r, po, qo) in self.mats:
+                for which, ln in (("p", n), ("q", m)):
+                    for tix in range((ln + 1023) // 1024):
+                        gt[which].append((len(gtb[which]) - 1, tix))
+                    gtb[which].append(len(gt[which]))
+            vec_idx = [i for (xo, n, vo) in self.vecs for i in range(xo, xo + n)]
             t = {
                 "mat": torch.tensor([list(m) for m in self.mats] or [[0] * 6], dtype=torch.int64,
                                     device=device).contiguous(),
                 "tiles0": it(t0),
                 "tiles1": it(t1),
                 "tilesp": it(tp),
+                "gt_p": it(gt["p"]), "gtb_p": it(gtb["p"]),
+                "gt_q": it(gt["q"]), "gtb_q": it(gtb["q"]),
+                "vec_idx": torch.tensor(vec_idx, dtype=torch.int64, device=device),
             }
             self._dev[key] = t
         return t
@@ -116,8 +128,10 @@ def orthogonalize(buf: torch.Tensor, plan: Plan, which: str) -> None:
     """In-place Gram-Schmidt of the columns of every P_i (or Q_i) -- reference
     dist/compressor/powersgd.py:7-18 (zero columns stay zero instead of becoming NaN)."""
     if _native.use_native(buf):
+        # Gram-matrix MGS on MFMA, two passes (CholQR2): csrc/kernels/powersgd.hip
         t = plan.tables(buf.device)
-        _native.lib().gram_schmidt(buf, t["mat"], 0 if which == "p" else 1, plan.n_mat)
+        _native.lib().gram_orthonormalize(buf, t["mat"], 0 if which == "p" else 1, plan.n_mat, t["gt_" + which],
+                                          t["gtb_" + which], 2)
         return
     for a in _views(buf, plan, which):
         r = a.shape[1]
@@ -130,15 +144,24 @@ def orthogonalize(buf: torch.Tensor, plan: Plan, which: str) -> None:
                 rest -= torch.sum(col * rest, dim=0) * col
 
 
-def mq(x: torch.Tensor, q: torch.Tensor, plan: Plan) -> torch.Tensor:
-    """P_i = M_i Q_i for every matrix (flat P buffer)."""
+def mq(x: torch.Tensor, q: torch.Tensor, plan: Plan, comp_r: Optional[torch.Tensor] = None, beta: float = 1.0,
+       gamma: float = 1.0, xout: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """P_i = M_i Q_i for every matrix (flat P buffer).
+
+    With ``xout``: M = beta*comp_r + gamma*x (or M = x without ``comp_r``) is also stored into
+    ``xout`` for the matrix segments -- the error-feedback compensate fused into this pass."""
     p = torch.empty(plan.p_total, dtype=torch.float32, device=x.device)
     if _native.use_native(x):
         t = plan.tables(x.device)
-        _native.lib().powersgd_mq(x, q, p, t["mat"], t["tiles0"], 0)
+        _native.lib().powersgd_mq(x, q, p, t["mat"], t["tiles0"], 0, comp_r, beta, gamma, xout)
         return p
     for (xo, n, m, r, po, qo) in plan.mats:
-        torch.mm(x[xo:xo + n * m].view(n, m), q[qo:qo + m * r].view(m, r), out=p[po:po + n * r].view(n, r))
+        mx = x[xo:xo + n * m]
+        if xout is not None:
+            v = beta * comp_r[xo:xo + n * m] + gamma * mx if comp_r is not None else mx
+            xout[xo:xo + n * m].copy_(v)
+            mx = xout[xo:xo + n * m]
+        torch.mm(mx.view(n, m), q[qo:qo + m * r].view(m, r), out=p[po:po + n * r].view(n, r))
     return p
 
 
@@ -147,24 +170,31 @@ def mtp(x: torch.Tensor, p: torch.Tensor, plan: Plan) -> torch.Tensor:
     q = torch.empty(plan.q_total, dtype=torch.float32, device=x.device)
     if _native.use_native(x):
         t = plan.tables(x.device)
-        _native.lib().powersgd_mq(x, p, q, t["mat"], t["tiles1"], 1)
+        _native.lib().powersgd_mq(x, p, q, t["mat"], t["tiles1"], 1, None, 1.0, 1.0, None)
         return q
     for (xo, n, m, r, po, qo) in plan.mats:
         torch.mm(x[xo:xo + n * m].view(n, m).t(), p[po:po + n * r].view(n, r), out=q[qo:qo + m * r].view(m, r))
     return q
 
 
-def pqt(p: torch.Tensor, q: torch.Tensor, plan: Plan, out: torch.Tensor) -> None:
-    """out[matrix i] = P_i Q_i^T (vector segments untouched)."""
+def pqt(p: torch.Tensor, q: torch.Tensor, plan: Plan, out: torch.Tensor, resid: Optional[torch.Tensor] = None) -> None:
+    """out[matrix i] = P_i Q_i^T (vector segments untouched); with ``resid`` (holding x) also
+    resid[matrix i] -= P_i Q_i^T in the same pass (PowerSGD residual update)."""
     if _native.use_native(out):
         t = plan.tables(out.device)
-        _native.lib().powersgd_pqt(p, q, out, t["mat"], t["tilesp"])
+        _native.lib().powersgd_pqt(p, q, out, t["mat"], t["tilesp"], resid)
         return
     for (xo, n, m, r, po, qo) in plan.mats:
-        torch.mm(p[po:po + n * r].view(n, r), q[qo:qo + m * r].view(m, r).t(), out=out[xo:xo + n * m].view(n, m))
+        o = out[xo:xo + n * m].view(n, m)
+        torch.mm(p[po:po + n * r].view(n, r), q[qo:qo + m * r].view(m, r).t(), out=o)
+        if resid is not None:
+            resid[xo:xo + n * m].view(n, m).sub_(o)
 
 
 def gather_vectors(x: torch.Tensor, plan: Plan) -> torch.Tensor:
+    """The 1-D segments of the bucket, packed (one gather kernel on the GPU)."""
+    if x.is_cuda:
+        return x.index_select(0, plan.tables(x.device)["vec_idx"])
     v = torch.empty(plan.v_total, dtype=torch.float32, device=x.device)
     for (xo, n, vo) in plan.vecs:
         v[vo:vo + n].copy_(x[xo:xo + n])
@@ -172,6 +202,9 @@ def gather_vectors(x: torch.Tensor, plan: Plan) -> torch.Tensor:
 
 
 def scatter_vectors(v: torch.Tensor, plan: Plan, out: torch.Tensor, scale: float) -> None:
+    if out.is_cuda and plan.v_total:
+        out.index_copy_(0, plan.tables(out.device)["vec_idx"], v * scale if scale != 1.0 else v)
+        return
     for (xo, n, vo) in plan.vecs:
         if scale != 1.0:
             torch.mul(v[vo:vo + n], scale, out=out[xo:xo + n])

@@ -24,7 +24,7 @@ def segment_stats(x: torch.Tensor, layout: SegmentLayout, r: torch.Tensor | None
         t = layout.device_tables(x.device)
         part = layout.cached(x.device, "segstats_part",
                              lambda: torch.empty(max(1, t["n_chunks"]) * NSTAT, dtype=torch.float64, device=x.device))
-        stats = torch.zeros(layout.n_seg, NSTAT, dtype=torch.float32, device=x.device)
+        stats = torch.empty(layout.n_seg, NSTAT, dtype=torch.float32, device=x.device)  # fold writes all
         _native.lib().segment_stats(x, r if mode else None, mode, beta, gamma, xout, t["seg"], t["begin"], t["end"],
                                     t["seg_chunk_begin"], part, stats)
         return stats
@@ -51,5 +51,5 @@ def segment_stats(x: torch.Tensor, layout: SegmentLayout, r: torch.Tensor | None
 
 def expand(per_seg: torch.Tensor, layout: SegmentLayout) -> torch.Tensor:
     """Broadcast a per-segment value to every element (torch path helper)."""
-    reps = torch.tensor(layout.numels, device=per_seg.device)
+    reps = layout.numels_t(per_seg.device, torch.int64)
     return torch.repeat_interleave(per_seg, reps)

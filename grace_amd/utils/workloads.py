@@ -103,6 +103,15 @@ WORKLOADS: Dict[str, Workload] = {
         _mlm_batch(128, 30522), _mlm_loss, seq_len=128),
 }
 
+# uncompressed reference point (None + Allreduce) for every BASELINE model
+for _k in ("vgg16_powersgd", "lstm_efsignsgd", "bert_qsgd"):
+    _w = WORKLOADS[_k]
+    _n = _k.split("_")[0] + "_none"
+    WORKLOADS[_n] = Workload(_n, _w.model, _w.batch, _w.unit,
+                             {"compressor": "none", "memory": "none", "communicator": "allreduce"},
+                             _w.make_batch, _w.loss, _w.samples_per_batch, dict(_w.model_kw), _w.channels_last,
+                             _w.seq_len)
+
 
 def build_model(w: Workload, device) -> torch.nn.Module:
     m = MODELS[w.model](**w.model_kw).to(device)

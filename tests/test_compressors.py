@@ -263,3 +263,28 @@ def test_broadcast_single_rank():
 def test_allreduce_rejects_nonlinear():
     with pytest.raises(ValueError):
         Allreduce(Z.TopKCompressor(0.1), M.NoneMemory(), comm=LocalComm())
+
+
+def test_powersgd_fused_memory_matches_unfused():
+    """fused_compress (compensate inside M Q, residual inside P Q^T) == the generic
+    compensate -> compress -> update sequence, over 3 steps of a bucket with 1-D segments."""
+    from grace_amd.core import register_layout
+    from grace_amd.ops.layout import SegmentLayout
+
+    class Unfused(M.PowerSGDMemory):
+        pass
+
+    shapes = [(20, 10), (7,), (6, 3, 2, 2), (5,)]
+    register_layout("psgd_bucket", SegmentLayout.from_tensors([torch.empty(s) for s in shapes]))
+    outs = {}
+    for mem_cls in (M.PowerSGDMemory, Unfused):
+        mem = mem_cls(compress_rank=2)
+        grc = Allreduce(Z.PowerSGDCompressor(rank=2), mem, comm=LocalComm())
+        res = []
+        for s in range(3):
+            g = torch.cat([_x(*sh, seed=10 * s + i).flatten() for i, sh in enumerate(shapes)])
+            res.append(grc.step(g, "psgd_bucket").clone())
+        res.append(mem.residuals["psgd_bucket"].clone())
+        outs[mem_cls] = res
+    for a, b in zip(outs[M.PowerSGDMemory], outs[Unfused]):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)

@@ -190,3 +190,83 @@ def test_segment_stats_gpu():
     a = S.segment_stats(flat, lay)
     b = S.segment_stats(flat.cuda(), lay).cpu()
     torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-4)
+
+
+def test_gram_orthonormalize_orthogonal_and_rank_deficient():
+    from grace_amd.ops import powersgd as PS
+
+    g = torch.Generator().manual_seed(5)
+    shapes = [(25088, 64), (300, 40), (7, 5)]
+    lay = SegmentLayout.from_tensors([torch.empty(s) for s in shapes])
+    plan = PS.plan_for(lay, 4)
+    p = torch.randn(plan.p_total, generator=g)
+    # ill-conditioned first matrix (column scales 1 .. 1e-3) and an exactly dependent column
+    (xo, n, m, r, po, qo) = plan.mats[0]
+    p[po:po + n * r].view(n, r).mul_(torch.tensor([1.0, 1e-1, 1e-2, 1e-3]))
+    (xo, n, m, r, po, qo) = plan.mats[1]
+    v = p[po:po + n * r].view(n, r)
+    v[:, 2] = 2.0 * v[:, 0]
+    b = p.cuda()
+    PS.orthogonalize(b, plan, "p")
+    b = b.cpu()
+    for i, (xo, n, m, r, po, qo) in enumerate(plan.mats):
+        a = b[po:po + n * r].view(n, r).double()
+        gram = a.t() @ a
+        if i == 1:  # dependent column -> (near) zero, the others orthonormal
+            keep = [0, 1, 3]
+            assert a[:, 2].norm() < 1e-3 or abs(a[:, 2].norm() - 1) < 1e-3
+            gram = gram[keep][:, keep]
+        assert (gram - torch.eye(gram.shape[0], dtype=torch.float64)).abs().max() < 1e-5
+    # same span / signs as the reference MGS on a well-conditioned matrix
+    ref = p.clone()
+    PS.orthogonalize(ref, plan, "p")
+    (xo, n, m, r, po, qo) = plan.mats[2]
+    torch.testing.assert_close(b[po:po + n * r], ref[po:po + n * r], rtol=1e-4, atol=1e-5)
+
+
+def test_powersgd_fused_memory_gpu_matches_cpu_unfused():
+    from grace_amd.core import register_layout
+
+    class Unfused(M.PowerSGDMemory):
+        pass
+
+    shapes = [(512, 300), (64,), (32, 16, 3, 3), (10,)]
+    register_layout("psgd_gpu", SegmentLayout.from_tensors([torch.empty(s) for s in shapes]))
+    outs = {}
+    for dev, mem_cls in (("cuda", M.PowerSGDMemory), ("cpu", Unfused)):
+        mem = mem_cls(compress_rank=4)
+        grc = Allreduce(Z.PowerSGDCompressor(rank=4), mem, comm=LocalComm())
+        res = []
+        for s in range(3):
+            gen = torch.Generator().manual_seed(s)
+            x = torch.cat([torch.randn(*sh, generator=gen).flatten() for sh in shapes])
+            res.append(grc.step(x.to(dev), "psgd_gpu").cpu())
+        res.append(mem.residuals["psgd_gpu"].reshape(-1).cpu())
+        outs[dev] = res
+    # different RNG streams for Q (Philox vs torch): compare energy and the EF invariant instead
+    for o in outs["cuda"]:
+        assert torch.isfinite(o).all()
+    gen = torch.Generator().manual_seed(2)
+    x_last = torch.cat([torch.randn(*sh, generator=gen).flatten() for sh in shapes])
+    assert outs["cuda"][2].norm() <= (x_last.norm() + outs["cuda"][3].norm()) * 1.01
+
+
+def test_segment_stats_large_unaligned_segment():
+    from grace_amd.ops import segstats as S
+
+    g = torch.Generator().manual_seed(9)
+    ts = [torch.randn(3, generator=g), torch.randn(5_000_011, generator=g), torch.randn(77, generator=g)]
+    lay = SegmentLayout.from_tensors(ts)
+    flat = torch.cat(ts)
+    r = torch.randn(flat.numel(), generator=g)
+    ref = torch.stack([torch.stack([t.double().sum(), (t.double() ** 2).sum(), t.abs().max().double(),
+                                    t.double().abs().sum(), t.double().clamp(max=0).sum(),
+                                    (t < 0).sum().double()]) for t in ts]).float()
+    b = S.segment_stats(flat.cuda(), lay).cpu()  # 16-B aligned base: float4 body
+    torch.testing.assert_close(b, ref, rtol=1e-5, atol=1e-3)
+    shifted = torch.cat([torch.zeros(1), flat]).cuda()[1:]  # 4-B offset base: scalar path
+    torch.testing.assert_close(S.segment_stats(shifted, lay).cpu(), ref, rtol=1e-5, atol=1e-3)
+    # fused compensate (x = 0.5 r + 2 g stored to xout) through the misaligned-view path
+    xg = torch.empty_like(flat).cuda()
+    S.segment_stats(flat.cuda(), lay, r=r.cuda(), r_valid=True, beta=0.5, gamma=2.0, xout=xg)
+    torch.testing.assert_close(xg.cpu(), 0.5 * r + 2.0 * flat, rtol=1e-6, atol=1e-6)
