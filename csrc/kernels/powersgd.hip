@@ -63,24 +63,39 @@ __global__ __launch_bounds__(kBlock) void mq_kernel(const float* __restrict__ x,
   const int64_t s0 = (int64_t)tl[2] * kStrip;
   const int64_t s1 = s0 + kStrip < red_len ? s0 + kStrip : red_len;
   const float* S = small + (MODE == 0 ? mt.q_off : mt.p_off);  // [red_len][r]
+  // Software pipeline: the global loads of sub-tile k+1 are issued into registers before the
+  // MFMAs of sub-tile k run, so HBM latency overlaps the matrix-core work.
+  constexpr int kPer = kT * kT / kBlock;  // 16 elements of M per thread per sub-tile
+  float pg[kPer], pr[kPer];
+  auto elem = [&](int64_t sb, int it, int64_t& gi) -> bool {
+    const int idx = it * kBlock + threadIdx.x;
+    const int64_t gr = (MODE == 0 ? ob : sb) + (idx >> 6), gc = (MODE == 0 ? sb : ob) + (idx & 63);
+    gi = mt.x_off + gr * m + gc;
+    return gr < n && gc < m;
+  };
+  auto fetch = [&](int64_t sb) {
+#pragma unroll
+    for (int it = 0; it < kPer; ++it) {
+      int64_t gi;
+      const bool ok = elem(sb, it, gi);
+      pg[it] = ok ? x[gi] : 0.f;
+      if (COMP == 2) pr[it] = ok ? cr[gi] : 0.f;
+    }
+  };
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  fetch(s0);
   for (int64_t sb = s0; sb < s1; sb += kT) {
     __syncthreads();
-    // stage the 64x64 sub-tile: rows/cols of M depend on MODE
-    const int64_t r0 = MODE == 0 ? ob : sb;
-    const int64_t c0 = MODE == 0 ? sb : ob;
-    for (int it = 0; it < kT * kT / kBlock; ++it) {
+#pragma unroll
+    for (int it = 0; it < kPer; ++it) {
       const int idx = it * kBlock + threadIdx.x;
-      const int rr = idx >> 6, cc = idx & 63;
-      const int64_t gr = r0 + rr, gc = c0 + cc;
-      float v = 0.f;
-      if (gr < n && gc < m) {
-        const int64_t gi = mt.x_off + gr * m + gc;
-        v = x[gi];
-        if (COMP == 2) v = fmaf(beta, cr[gi], gamma * v);
-        if (COMP != 0) xout[gi] = v;
+      float v = pg[it];
+      if (COMP == 2) v = fmaf(beta, pr[it], gamma * v);
+      if (COMP != 0) {
+        int64_t gi;
+        if (elem(sb, it, gi)) xout[gi] = v;
       }
-      ms[rr * kLd + cc] = v;
+      ms[(idx >> 6) * kLd + (idx & 63)] = v;
     }
     // small operand rows [sb, sb+64) of S, r padded to 16 with zeros
     for (int it = 0; it < kT * kRPad / kBlock; ++it) {
@@ -90,6 +105,7 @@ __global__ __launch_bounds__(kBlock) void mq_kernel(const float* __restrict__ x,
       ss[idx] = (j < r && gk < s1) ? S[gk * r + j] : 0.f;
     }
     __syncthreads();
+    if (sb + kT < s1) fetch(sb + kT);
 #pragma unroll 4
     for (int kk = 0; kk < kT; kk += 4) {
       const int ka = kk + (lane >> 4);

@@ -130,8 +130,10 @@ def orthogonalize(buf: torch.Tensor, plan: Plan, which: str) -> None:
     if _native.use_native(buf):
         # Gram-matrix MGS on MFMA, two passes (CholQR2): csrc/kernels/powersgd.hip
         t = plan.tables(buf.device)
+        # P = M Q can be ill-conditioned (near-low-rank gradients): CholQR2; the Gaussian Q
+        # (condition number ~1) needs one pass
         _native.lib().gram_orthonormalize(buf, t["mat"], 0 if which == "p" else 1, plan.n_mat, t["gt_" + which],
-                                          t["gtb_" + which], 2)
+                                          t["gtb_" + which], 2 if which == "p" else 1)
         return
     for a in _views(buf, plan, which):
         r = a.shape[1]

@@ -72,11 +72,13 @@ class Bucket:
             self.views.append(v)
             p.grad = v  # gradients accumulate straight into the bucket buffer
         self.pending = len(params)
+        self.fired = [False] * len(params)
         self.handles = None
         self.ctx = None
 
     def reset(self):
         self.pending = len(self.params)
+        self.fired = [False] * len(self.params)
         self.handles = None
         self.ctx = None
 
@@ -141,6 +143,7 @@ class GraceEngine:
             self._hooks.append(p.register_post_accumulate_grad_hook(self._sparse_hook))
         self.in_flight = 0
         self._paused = False
+        self._grads_none = False
 
     # ------------------------------------------------------------------ backward hooks
     def pause(self):
@@ -170,9 +173,14 @@ class GraceEngine:
             raise RuntimeError(f"parameter {self._name_of(p)} produced a sparse gradient: pass its name in "
                                "sparse_params= (uncompressed sparse all-gather)")
         if p.grad is not None and p.grad.data_ptr() != view.data_ptr():
-            # .grad was replaced (e.g. zero_grad(set_to_none=True)): move it back into the bucket
+            # .grad was None before backward (zero_grad(set_to_none=True)): AccumulateGrad stole
+            # the fresh gradient, one copy moves it into the bucket (cheaper than memset + add)
             view.copy_(p.grad)
             p.grad = view
+        if b.fired[idx]:
+            raise RuntimeError(f"{b.name}: gradient of parameter {idx} produced twice before synchronize() -- "
+                               "increase backward_passes_per_step or call synchronize()")
+        b.fired[idx] = True
         b.pending -= 1
         if b.pending == 0:
             self._launch(b)
@@ -237,6 +245,13 @@ class GraceEngine:
         parameters), wait for the collectives, decompress into the bucket buffers."""
         for b in self.buckets:
             if b.handles is None:
+                for i, p in enumerate(b.params):  # no gradient this step (unused parameter)
+                    if not b.fired[i]:
+                        if self._grads_none:
+                            b.views[i].zero_()
+                        elif p.grad is not None and p.grad.data_ptr() != b.views[i].data_ptr():
+                            b.views[i].copy_(p.grad)
+                        p.grad = b.views[i]
                 self._launch(b)
         cur = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
         if self.stream is not None:
@@ -254,12 +269,23 @@ class GraceEngine:
             self._finish_sparse()
         self.in_flight = 0
 
-    def zero_grad(self):
+    def zero_grad(self, set_to_none: bool = True):
+        """``set_to_none`` (torch's default): .grad becomes None and backward's AccumulateGrad
+        hands its fresh gradient to the hook, which copies it into the bucket -- one
+        read+write instead of a bucket memset plus an accumulate (read, read, write)."""
         if self.in_flight:
             raise AssertionError("zero_grad() called with gradients still being communicated -- "
                                  "call synchronize()/step() first")
-        for b in self.buckets:
-            b.flat.zero_()
+        self._grads_none = set_to_none
+        if set_to_none:
+            for b in self.buckets:
+                for p in b.params:
+                    p.grad = None
+        else:
+            for b in self.buckets:
+                b.flat.zero_()
+                for p, v in zip(b.params, b.views):
+                    p.grad = v
         for _, p in self._sparse.values():
             p.grad = None
 

@@ -64,9 +64,10 @@ class _DistributedOptimizer:
         self._synchronized = False
         return self._opt.step(closure)
 
-    def zero_grad(self, set_to_none: bool = False):
-        # gradients live in bucket buffers: one memset per bucket, never None
-        self.engine.zero_grad()
+    def zero_grad(self, set_to_none: bool = True):
+        # set_to_none: fresh gradients are copied into the buckets by the hooks; False: one
+        # memset per bucket and backward accumulates into the bucket views
+        self.engine.zero_grad(set_to_none)
 
     def state_dict(self):
         return {"optimizer": self._opt.state_dict(), "grace": self.engine.state_dict()}
