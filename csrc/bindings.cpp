@@ -559,6 +559,129 @@ std::string build_info() {
 
 void grace_bind_comm(py::module& m);  // csrc/comm/rccl_comm.cpp
 
+// ------------------------------------------------------------------------------ Adaq
+void adaq_sample(const Tensor& x, const Tensor& seg_off, const Tensor& samp_off, int64_t seed,
+                 const c10::optional<Tensor>& step, const Tensor& samples) {
+  CHECK_F32(x);
+  CHECK_I64(seg_off);
+  CHECK_I64(samp_off);
+  CHECK_F32(samples);
+  TORCH_CHECK(seg_off.numel() == samp_off.numel(), "offset tables");
+  DevGuard guard(x.device());
+  const int n_seg = (int)seg_off.numel() - 1;
+  grace::adaq_sample(x.data_ptr<float>(), n_seg, seg_off.data_ptr<int64_t>(), samp_off.data_ptr<int64_t>(),
+                     samples.numel() / 2, seed_arg(seed, step), samples.data_ptr<float>(), cur_stream());
+}
+
+void adaq_prepare(const Tensor& x, const Tensor& seg_off, const Tensor& samp_off, const Tensor& stats, double ratio,
+                  const Tensor& count, const Tensor& target, const Tensor& kseg, const Tensor& fallback,
+                  const Tensor& thr, const Tensor& done, const Tensor& seg, const Tensor& cb, const Tensor& ce) {
+  CHECK_F32(x);
+  CHECK_F32(stats);
+  CHECK_I32(count);
+  CHECK_F32(target);
+  CHECK_I32(kseg);
+  CHECK_F32(fallback);
+  CHECK_F32(thr);
+  CHECK_I32(done);
+  const int n_seg = (int)seg_off.numel() - 1;
+  TORCH_CHECK(count.numel() == 2 * n_seg && kseg.numel() == 2 * n_seg && thr.numel() == 2 * n_seg, "group arrays");
+  auto ct = make_ct(seg, cb, ce);
+  DevGuard guard(x.device());
+  grace::adaq_prepare(ct, n_seg, x.data_ptr<float>(), seg_off.data_ptr<int64_t>(), samp_off.data_ptr<int64_t>(),
+                      stats.data_ptr<float>(), (float)ratio, count.data_ptr<int32_t>(), target.data_ptr<float>(),
+                      kseg.data_ptr<int32_t>(), fallback.data_ptr<float>(), thr.data_ptr<float>(),
+                      done.data_ptr<int32_t>(), cur_stream());
+}
+
+void adaq_refine(const Tensor& x, const Tensor& state, const Tensor& fallback, const Tensor& target, int64_t max_iters,
+                 const Tensor& thr, const Tensor& count, const Tensor& done, const Tensor& seg, const Tensor& cb,
+                 const Tensor& ce) {
+  CHECK_F32(x);
+  CHECK_I32(state);
+  const int n_seg = (int)(thr.numel() / 2);
+  TORCH_CHECK(state.numel() >= 2 * 2 * n_seg, "state");
+  auto ct = make_ct(seg, cb, ce);
+  DevGuard guard(x.device());
+  grace::adaq_refine(ct, n_seg, x.data_ptr<float>(), reinterpret_cast<const grace::TopkState*>(state.data_ptr<int32_t>()),
+                     fallback.data_ptr<float>(), target.data_ptr<float>(), (int)max_iters, thr.data_ptr<float>(),
+                     count.data_ptr<int32_t>(), done.data_ptr<int32_t>(), cur_stream());
+}
+
+void adaq_offsets(const Tensor& count, const Tensor& goff, const Tensor& cursor) {
+  CHECK_I32(count);
+  CHECK_I32(goff);
+  CHECK_I32(cursor);
+  TORCH_CHECK(goff.numel() == count.numel() + 1 && cursor.numel() == count.numel(), "offset arrays");
+  DevGuard guard(count.device());
+  grace::adaq_offsets((int)(count.numel() / 2), count.data_ptr<int32_t>(), goff.data_ptr<int32_t>(),
+                      cursor.data_ptr<int32_t>(), cur_stream());
+}
+
+void adaq_compact(const Tensor& x, const Tensor& thr, const Tensor& goff, const Tensor& cursor, const Tensor& idx,
+                  const Tensor& psum, const Tensor& means, const Tensor& counts, const Tensor& seg, const Tensor& cb,
+                  const Tensor& ce, const Tensor& seg_chunk_begin) {
+  CHECK_F32(x);
+  CHECK_F32(thr);
+  CHECK_I32(idx);
+  CHECK_DT(psum, at::kDouble);
+  CHECK_F32(means);
+  CHECK_I32(counts);
+  CHECK_I32(seg_chunk_begin);
+  const int n_seg = (int)(thr.numel() / 2);
+  auto ct = make_ct(seg, cb, ce);
+  TORCH_CHECK(psum.numel() >= 2 * (int64_t)ct.n_chunks, "psum");
+  TORCH_CHECK(means.numel() == 2 * n_seg && counts.numel() == 2 * n_seg, "means/counts");
+  DevGuard guard(x.device());
+  grace::adaq_compact(ct, n_seg, seg_chunk_begin.data_ptr<int32_t>(), x.data_ptr<float>(), thr.data_ptr<float>(),
+                      goff.data_ptr<int32_t>(), cursor.data_ptr<int32_t>(), idx.data_ptr<int32_t>(),
+                      psum.data_ptr<double>(), means.data_ptr<float>(), counts.data_ptr<int32_t>(), cur_stream());
+}
+
+// ------------------------------------------------------------------------------ INCEPTIONN
+int64_t inceptionn_tiles(int64_t n) { return grace::inceptionn_tiles(n); }
+
+void inceptionn_count(const Tensor& x, int64_t e_b, int64_t mid, const Tensor& cnt, const Tensor& totals) {
+  CHECK_F32(x);
+  CHECK_I32(cnt);
+  CHECK_I32(totals);
+  TORCH_CHECK(cnt.numel() >= 4 * grace::inceptionn_tiles(x.numel()) && totals.numel() >= 4, "workspace");
+  DevGuard guard(x.device());
+  grace::inceptionn_count(x.data_ptr<float>(), x.numel(), (int)e_b, (int)mid, cnt.data_ptr<int32_t>(),
+                          totals.data_ptr<int32_t>(), cur_stream());
+}
+
+void inceptionn_encode(const Tensor& x, int64_t e_b, int64_t mid, const Tensor& off, const Tensor& v32,
+                       const Tensor& v16, const Tensor& v8, const Tensor& codes) {
+  CHECK_F32(x);
+  CHECK_I32(off);
+  CHECK_F32(v32);
+  CHECK_DT(v16, at::kShort);
+  CHECK_DT(v8, at::kByte);
+  CHECK_DT(codes, at::kByte);
+  TORCH_CHECK(codes.numel() >= (x.numel() + 3) / 4, "codes size");
+  DevGuard guard(x.device());
+  grace::inceptionn_encode(x.data_ptr<float>(), x.numel(), (int)e_b, (int)mid, off.data_ptr<int32_t>(),
+                           v32.data_ptr<float>(), reinterpret_cast<uint16_t*>(v16.data_ptr<int16_t>()),
+                           v8.data_ptr<uint8_t>(), codes.data_ptr<uint8_t>(), cur_stream());
+}
+
+void inceptionn_decode(const Tensor& ptrs, const Tensor& code_ptrs, int64_t n_ranks, const Tensor& cnt,
+                       const Tensor& totals, double scale, const Tensor& out, bool accumulate) {
+  CHECK_I64(ptrs);
+  CHECK_I64(code_ptrs);
+  CHECK_I32(cnt);
+  CHECK_I32(totals);
+  CHECK_F32(out);
+  const int64_t n = out.numel();
+  TORCH_CHECK(ptrs.numel() == 4 * n_ranks && code_ptrs.numel() == n_ranks, "pointer tables");
+  TORCH_CHECK(cnt.numel() >= 4 * n_ranks * grace::inceptionn_tiles(n) && totals.numel() >= 4 * n_ranks, "workspace");
+  DevGuard guard(out.device());
+  grace::inceptionn_decode(ptrs.data_ptr<int64_t>(), code_ptrs.data_ptr<int64_t>(), (int)n_ranks, n,
+                           cnt.data_ptr<int32_t>(), totals.data_ptr<int32_t>(), (float)scale, out.data_ptr<float>(),
+                           accumulate, cur_stream());
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   grace_bind_comm(m);
   m.doc() = "grace_amd native CDNA4 kernels and RCCL runtime";
@@ -585,6 +708,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dgc_compact", &dgc_compact);
   m.def("powersgd_mq", &powersgd_mq);
   m.def("gram_orthonormalize", &gram_orthonormalize);
+  m.def("adaq_sample", &adaq_sample);
+  m.def("adaq_prepare", &adaq_prepare);
+  m.def("adaq_refine", &adaq_refine);
+  m.def("adaq_offsets", &adaq_offsets);
+  m.def("adaq_compact", &adaq_compact);
+  m.def("inceptionn_tiles", &inceptionn_tiles);
+  m.def("inceptionn_count", &inceptionn_count);
+  m.def("inceptionn_encode", &inceptionn_encode);
+  m.def("inceptionn_decode", &inceptionn_decode);
   m.def("powersgd_pqt", &powersgd_pqt);
   m.def("philox_normal", &philox_normal);
   m.def("cast16", &cast16);

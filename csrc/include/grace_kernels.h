@@ -104,4 +104,25 @@ void sketch_decode(const ChunkTable& ct, const uint8_t* base, int64_t rank_strid
 void axpby(const float* x, const float* y, float* out, int64_t n, float a, float b, hipStream_t stream);
 void scale_inplace(float* x, int64_t n, float s, hipStream_t stream);
 
+// ---------------------------------------------------------------- inceptionn.hip
+int64_t inceptionn_tiles(int64_t n);
+void inceptionn_count(const float* x, int64_t n, int e_b, int mid, int32_t* cnt, int32_t* totals, hipStream_t stream);
+void inceptionn_encode(const float* x, int64_t n, int e_b, int mid, const int32_t* off, float* v32, uint16_t* v16,
+                       uint8_t* v8, uint8_t* codes, hipStream_t stream);
+void inceptionn_decode(const int64_t* ptrs, const int64_t* code_ptrs, int n_ranks, int64_t n, int32_t* cnt,
+                       int32_t* totals, float scale, float* out, bool accumulate, hipStream_t stream);
+
+// ---------------------------------------------------------------- adaq.hip
+void adaq_sample(const float* x, int n_seg, const int64_t* seg_off, const int64_t* samp_off, int64_t n_samples,
+                 SeedArg seed, float* samples, hipStream_t stream);
+void adaq_prepare(const ChunkTable& ct, int n_seg, const float* x, const int64_t* seg_off, const int64_t* samp_off,
+                  const float* stats, float ratio, int32_t* count, float* target, int32_t* kseg, float* fallback,
+                  float* thr, int32_t* done, hipStream_t stream);
+void adaq_refine(const ChunkTable& ct, int n_seg, const float* x, const TopkState* st, const float* fallback,
+                 const float* target, int max_iters, float* thr, int32_t* count, int32_t* done, hipStream_t stream);
+void adaq_offsets(int n_seg, const int32_t* count, int32_t* goff, int32_t* cursor, hipStream_t stream);
+void adaq_compact(const ChunkTable& ct, int n_seg, const int32_t* seg_chunk_begin, const float* x, const float* thr,
+                  const int32_t* goff, int32_t* cursor, int32_t* idx, double* psum, float* means, int32_t* counts,
+                  hipStream_t stream);
+
 }  // namespace grace

@@ -141,7 +141,7 @@ __global__ __launch_bounds__(kBlock) void mq_kernel(const float* __restrict__ x,
 //                 A*T stay orthonormal; zero columns stay zero, as in the MGS kernel it replaces);
 //   gram_apply    A <- A T row by row.
 // Run twice (CholQR2): the second pass restores fp32-level orthogonality for ill-conditioned P.
-constexpr int kGRows = 1024;  // rows per Gram tile
+constexpr int kGRows = 256;  // rows per Gram tile (64 per wave: short dependent MFMA chains)
 
 __device__ __forceinline__ int64_t blk_len(const Mat& mt, int which) { return which == 0 ? mt.n : mt.m; }
 __device__ __forceinline__ int64_t blk_off(const Mat& mt, int which) { return which == 0 ? mt.p_off : mt.q_off; }
@@ -162,6 +162,7 @@ __global__ __launch_bounds__(kBlock) void gram_partial_kernel(const float* __res
   if (r1 > len) r1 = len;
   const int col = lane & 15;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
   for (int64_t k0 = r0; k0 < r1; k0 += 4) {
     const int64_t row = k0 + (lane >> 4);
     const float a = (row < r1 && col < r) ? A[row * r + col] : 0.f;
@@ -187,6 +188,7 @@ __global__ __launch_bounds__(kWave) void gram_fix_kernel(const int64_t* __restri
   const int t0 = gtile_begin[mi], t1 = gtile_begin[mi + 1];
   for (int e = threadIdx.x; e < 256; e += kWave) {
     double v = 0.0;
+#pragma unroll 4
     for (int t = t0; t < t1; ++t) v += part[(int64_t)t * 256 + e];
     G[e >> 4][e & 15] = v;
     Tm[e >> 4][e & 15] = (e >> 4) == (e & 15) ? 1.0 : 0.0;
@@ -245,10 +247,15 @@ __global__ __launch_bounds__(kBlock) void gram_apply_kernel(float* __restrict__ 
   }
 }
 
-// out[x_off + row*m + col] = sum_j P[row][j] Q[col][j]; tiles: (matrix, row block of 16, col block of 64)
+// out[x_off + row*m + col] = sum_j P[row][j] Q[col][j]; tiles: (matrix, row block of 16, col block of 256).
+// Each wave computes four 16x16 MFMA tiles (64 columns); the 16 x 256 workgroup tile is staged in
+// LDS so every store instruction writes 64 consecutive floats of one row (256 B) instead of four
+// 64-B row pieces.  With ``resid`` (holding x) the residual r = x - P Q^T is updated in the same pass.
+constexpr int kPqtCols = 256;
 __global__ __launch_bounds__(kBlock) void pqt_kernel(const float* __restrict__ P, const float* __restrict__ Q,
                                                      float* __restrict__ out, const int64_t* __restrict__ mats,
                                                      const int32_t* __restrict__ tiles, float* resid) {
+  __shared__ float tile[16][kPqtCols + 1];
   const int* tl = tiles + 3 * blockIdx.x;
   const Mat mt = load_mat(mats, tl[0]);
   const int64_t n = mt.n, m = mt.m, r = mt.r;
@@ -256,24 +263,32 @@ __global__ __launch_bounds__(kBlock) void pqt_kernel(const float* __restrict__ P
   const float* Qm = Q + mt.q_off;
   const int lane = lane_id(), w = wave_id();
   const int64_t row0 = (int64_t)tl[1] * 16;
-  const int64_t col0 = (int64_t)tl[2] * 64 + 16 * w;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int k0 = 0; k0 < r; k0 += 4) {
-    const int k = k0 + (lane >> 4);
-    const int64_t ar = row0 + (lane & 15), bc = col0 + (lane & 15);
-    const float a = (ar < n && k < r) ? Pm[ar * r + k] : 0.f;   // A[i][k] = P[row i][k]
-    const float b = (bc < m && k < r) ? Qm[bc * r + k] : 0.f;   // B[k][j] = Q[col j][k]
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
-  }
-  const int64_t col = col0 + (lane & 15);
-  if (col < m) {
+  const int64_t cbase = (int64_t)tl[2] * kPqtCols;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int64_t row = row0 + (lane >> 4) * 4 + q;
+  for (int cb = 0; cb < 4; ++cb) {
+    const int lc0 = 64 * w + 16 * cb;  // local column of this 16x16 tile
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < r; k0 += 4) {
+      const int k = k0 + (lane >> 4);
+      const int64_t ar = row0 + (lane & 15), bc = cbase + lc0 + (lane & 15);
+      const float a = (ar < n && k < r) ? Pm[ar * r + k] : 0.f;  // A[i][k] = P[row i][k]
+      const float b = (bc < m && k < r) ? Qm[bc * r + k] : 0.f;  // B[k][j] = Q[col j][k]
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) tile[(lane >> 4) * 4 + q][lc0 + (lane & 15)] = acc[q];
+  }
+  __syncthreads();
+  const int64_t col = cbase + threadIdx.x;
+  if (col < m) {
+#pragma unroll 4
+    for (int rr = 0; rr < 16; ++rr) {
+      const int64_t row = row0 + rr;
       if (row < n) {
         const int64_t gi = mt.x_off + row * m + col;
-        out[gi] = acc[q];
-        if (resid != nullptr) resid[gi] -= acc[q];  // resid holds x: residual = x - P Q^T
+        const float v = tile[rr][threadIdx.x];
+        out[gi] = v;
+        if (resid != nullptr) resid[gi] -= v;
       }
     }
   }

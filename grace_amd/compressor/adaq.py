@@ -8,12 +8,14 @@ then send only the MEAN of the selected values and their indices:
 ``[plus_mean, minus_mean, n_plus, plus_idx..., minus_idx...]`` as one int32 tensor.
 Decompress writes plus_mean / minus_mean at the indices.
 
-Here: the same algorithm per segment, implemented with PyTorch-ROCm ops (no dedicated HIP
-kernel yet -- it shares the threshold-refinement shape of DGC, csrc/kernels/dgc.hip, which is
-the planned port); payload [means fp32 (+,- per segment) | counts int32 (+,- per segment) |
-indices int32].  A side with no
-entries sends mean 0 and no index (the reference computes the mean of an empty set -> NaN).
-Variable-size payload (Allgather).
+MI355X (csrc/kernels/adaq.hip): every segment of a bucket and both sides at once, on the
+device -- Philox 1% sample, the segmented radix select of topk.hip for the initial thresholds,
+the refinement loop with both sides counted per pass over the bucket, ordered compaction of the
+indices and deterministic per-group means; one host read sizes the payload.  The PyTorch path
+(per segment, torch RNG, sampling among the side's entries exactly as the reference) is the
+CPU oracle.  Payload [means fp32 (+,- per segment) | counts int32 (+,- per segment) | indices
+int32].  A side with no entries sends mean 0 and no index (the reference computes the mean of
+an empty set -> NaN).  Variable-size payload (Allgather).
 """
 from __future__ import annotations
 
@@ -21,7 +23,10 @@ import math
 
 import torch
 
+from ..ops import _native
+from ..ops import segstats as S
 from ..ops import topk as K
+from ..ops.layout import SegmentLayout
 from ._base import BucketCompressor
 
 
@@ -53,10 +58,60 @@ class AdaqCompressor(BucketCompressor):
         super().__init__(tensors_size_are_same=False)
         self.compress_ratio = compress_ratio
 
+    max_iters = 20
+
+    def _native_compress(self, x, lay, name):
+        C = _native.lib()
+        dev = x.device
+
+        def build():
+            ns = [max(1, math.ceil(n * 0.01)) if n > 0 else 0 for n in lay.numels]
+            off = [0]
+            for v in ns:
+                off.append(off[-1] + v)
+            gl = SegmentLayout(tuple(v for v in ns for _ in (0, 1)), tuple((v,) for v in ns for _ in (0, 1)))
+            ng = 2 * lay.n_seg
+            i32 = dict(dtype=torch.int32, device=dev)
+            f32 = dict(dtype=torch.float32, device=dev)
+            return {
+                "samp_off": torch.tensor(off, dtype=torch.int64, device=dev),
+                "glay": gl, "gt": gl.device_tables(dev),
+                "samples": torch.empty(max(1, gl.total), **f32),
+                "count": torch.empty(ng, **i32), "target": torch.empty(ng, **f32), "kseg": torch.empty(ng, **i32),
+                "fallback": torch.empty(ng, **f32), "thr": torch.empty(ng, **f32), "done": torch.empty(ng, **i32),
+                "state": torch.zeros(2 * ng, **i32), "hist": torch.zeros(ng * 2048, **i32),
+                "goff": torch.empty(ng + 1, **i32), "cursor": torch.empty(ng, **i32),
+            }
+
+        ws = lay.cached(dev, f"adaq_ws:{self.compress_ratio}", build)
+        t = lay.device_tables(dev)
+        seed, step = self.next_rng(name, dev)
+        sd = seed - (1 << 64) if seed >= (1 << 63) else seed
+        stats = S.segment_stats(x, lay)
+        C.adaq_sample(x, t["offsets"], ws["samp_off"], sd, step, ws["samples"][: ws["glay"].total])
+        C.adaq_prepare(x, t["offsets"], ws["samp_off"], stats, self.compress_ratio, ws["count"], ws["target"],
+                       ws["kseg"], ws["fallback"], ws["thr"], ws["done"], t["seg"], t["begin"], t["end"])
+        gt = ws["gt"]
+        smp = ws["samples"][: ws["glay"].total]
+        C.topk_select(smp, None, smp, 1.0, 1.0, 0, gt["seg"], gt["begin"], gt["end"], ws["kseg"], ws["state"],
+                      ws["hist"])
+        C.adaq_refine(x, ws["state"], ws["fallback"], ws["target"], self.max_iters, ws["thr"], ws["count"],
+                      ws["done"], t["seg"], t["begin"], t["end"])
+        C.adaq_offsets(ws["count"], ws["goff"], ws["cursor"])
+        total = int(ws["goff"][-1].item())  # payload size (data dependent): the one host read
+        m, cnt, ix = self.payload(dev, [(torch.float32, (2 * lay.n_seg,)), (torch.int32, (2 * lay.n_seg,)),
+                                        (torch.int32, (total,))])
+        psum = torch.empty(max(1, 2 * t["n_chunks"]), dtype=torch.float64, device=dev)
+        C.adaq_compact(x, ws["thr"], ws["goff"], ws["cursor"], ix, psum, m, cnt, t["seg"], t["begin"], t["end"],
+                       t["seg_chunk_begin"])
+        return [m, cnt, ix]
+
     def compress(self, tensor, name):
         ctx = self.ctx(tensor, name)
         x = self.flat(tensor)
         lay = ctx.layout
+        if _native.use_native(x):
+            return self._native_compress(x, lay, name), ctx
         gen = torch.Generator(device=x.device)
         gen.manual_seed(self.next_seed(name) & 0x7FFFFFFFFFFFFFFF)
         means = torch.zeros(2 * lay.n_seg, dtype=torch.float32, device=x.device)

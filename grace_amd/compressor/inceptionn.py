@@ -10,9 +10,13 @@ mid = e_b + ceil((127 - e_b) / 2):
 plus a 2-bit class code per element packed 4 per byte.  Decoding recovers the exponent from
 the position of the leading one (tfp find_bins over powers of two in the reference).
 
-Here: the same bit-level codec on int64 PyTorch-ROCm ops (no dedicated HIP kernel yet); the
-class codes are packed little-endian 4 per byte (element 4j+t at bits 2t of byte j) instead of
-the reference's quarter-split layout (wire-format detail, same information).
+MI355X: csrc/kernels/inceptionn.hip -- a per-tile class count + device scan, then ONE encode
+pass writes the 2-bit codes and the three order-preserving compacted streams; the decoder
+recounts classes from every rank's codes and decodes + sums all W ranks in one pass (rank
+order, deterministic).  One host read of the three class totals sizes the payload (the size is
+data dependent, as in the reference).  The PyTorch path below is the CPU oracle (bit-identical).
+The class codes are packed little-endian 4 per byte (element 4j+t at bits 2t of byte j) instead
+of the reference's quarter-split layout (wire-format detail, same information).
 Payload [fp32 v32 | int16 v16 | uint8 v8 | uint8 classes].  Variable size.
 """
 from __future__ import annotations
@@ -21,6 +25,7 @@ import math
 
 import torch
 
+from ..ops import _native
 from ._base import BucketCompressor
 
 
@@ -44,9 +49,26 @@ class INCEPTIONNCompressor(BucketCompressor):
         self.e_b = 127 + int(math.log(error_bound / 2, 10))
         self.mid = self.e_b + math.ceil((127 - self.e_b) / 2)
 
+    def _native_compress(self, x, ctx):
+        C = _native.lib()
+        n = x.numel()
+        nt = C.inceptionn_tiles(n)
+        lay = ctx.layout
+        ws = lay.cached(x.device, "inceptionn_enc", lambda: {
+            "cnt": torch.empty(max(1, 4 * nt), dtype=torch.int32, device=x.device),
+            "tot": torch.empty(4, dtype=torch.int32, device=x.device)})
+        C.inceptionn_count(x, self.e_b, self.mid, ws["cnt"], ws["tot"])
+        _, n8, n16, n32 = (int(v) for v in ws["tot"].tolist())  # payload size: one host read
+        a, b, c, d = self.payload(x.device, [(torch.float32, (n32,)), (torch.int16, (n16,)), (torch.uint8, (n8,)),
+                                             (torch.uint8, ((n + 3) // 4,))])
+        C.inceptionn_encode(x, self.e_b, self.mid, ws["cnt"], a, b, c, d)
+        return [a, b, c, d]
+
     def compress(self, tensor, name):
         ctx = self.ctx(tensor, name)
         x = self.flat(tensor)
+        if _native.use_native(x):
+            return self._native_compress(x, ctx), ctx
         u = x.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
         sign = u & 0x80000000
         expo = (u >> 23) & 0xFF
@@ -101,6 +123,16 @@ class INCEPTIONNCompressor(BucketCompressor):
 
     def decompress_aggregate_impl(self, per_rank, ctx, n_ranks, scale):
         dev = per_rank[0][0].device
+        if _native.use_native(per_rank[0][3]):
+            C = _native.lib()
+            n = ctx.layout.total
+            out = self.out_buffer(ctx, dev)
+            ptrs = torch.tensor([t.data_ptr() for p in per_rank for t in p], dtype=torch.int64).to(dev)
+            cptr = torch.tensor([p[3].data_ptr() for p in per_rank], dtype=torch.int64).to(dev)
+            cnt = torch.empty(max(1, 4 * n_ranks * C.inceptionn_tiles(n)), dtype=torch.int32, device=dev)
+            tot = torch.empty(4 * n_ranks, dtype=torch.int32, device=dev)
+            C.inceptionn_decode(ptrs, cptr, n_ranks, cnt, tot, scale, out, False)
+            return self.finish(out, ctx)
         out = self.out_buffer(ctx, dev, zero=True)
         for v32, v16, v8, packed in per_rank:
             out += self._decode(v32, v16, v8, packed, ctx.layout.total, dev)

@@ -43,19 +43,19 @@ class Plan:
                     for sidx in range((n + 1023) // 1024):
                         t1.append((i, cb, sidx))
                 for rb in range((n + 15) // 16):
-                    for cb in range((m + 63) // 64):
+                    for cb in range((m + 255) // 256):
                         tp.append((i, rb, cb))
 
             def it(lst):
                 return torch.tensor(lst, dtype=torch.int32, device=device).view(-1) if lst else \
                     torch.empty(0, dtype=torch.int32, device=device)
 
-            # Gram tiles of 1024 rows over each P_i (n rows) and Q_i (m rows)
+            # Gram tiles of 256 rows over each P_i (n rows) and Q_i (m rows)
             gt = {"p": [], "q": []}
             gtb = {"p": [0], "q": [0]}
             for (xo, n, m, r, po, qo) in self.mats:
                 for which, ln in (("p", n), ("q", m)):
-                    for tix in range((ln + 1023) // 1024):
+                    for tix in range((ln + 255) // 256):
                         gt[which].append((len(gtb[which]) - 1, tix))
                     gtb[which].append(len(gt[which]))
             vec_idx = [i for (xo, n, vo) in self.vecs for i in range(xo, xo + n)]

@@ -270,3 +270,67 @@ def test_segment_stats_large_unaligned_segment():
     xg = torch.empty_like(flat).cuda()
     S.segment_stats(flat.cuda(), lay, r=r.cuda(), r_valid=True, beta=0.5, gamma=2.0, xout=xg)
     torch.testing.assert_close(xg.cpu(), 0.5 * r + 2.0 * flat, rtol=1e-6, atol=1e-6)
+
+
+def test_inceptionn_native_bit_exact():
+    """HIP INCEPTIONN encode/decode == the PyTorch codec bit for bit (payload and result),
+    including W=3 rank-ordered aggregation."""
+    g = torch.Generator().manual_seed(11)
+    n = 300_001  # several tiles plus a ragged tail
+    x = torch.randn(n, generator=g) * torch.logspace(-12, 1, n)[torch.randperm(n, generator=g)]
+    x[::97] = 0.0
+    register_layout("inc_bucket", SegmentLayout.from_tensors([x]))
+    comp = Z.INCEPTIONNCompressor(2e-10)
+    pc, ctx_c = comp.compress(x, "inc_bucket")
+    pg, ctx_g = comp.compress(x.cuda(), "inc_bucket")
+    for a, b in zip(pc, pg):
+        assert a.dtype == b.dtype and a.numel() == b.numel()
+        assert torch.equal(a, b.cpu())
+    others = [comp.compress(x * s, "inc_bucket")[0] for s in (0.5, -3.0)]
+    ref = comp.decompress_aggregate([pc] + others, ctx_c, 3)
+    got = comp.decompress_aggregate([pg] + [[t.cuda() for t in o] for o in others], ctx_g, 3)
+    assert torch.equal(got.cpu(), ref)
+
+
+def test_adaq_native_properties():
+    """HIP Adaq: per (segment, side) group the indices lie in the segment with the right sign,
+    the sent mean is the mean of the selected values, the count is near ratio * side size,
+    and decompress scatters the means (stochastic sampling: checked by properties)."""
+    import math
+
+    g = torch.Generator().manual_seed(21)
+    shapes = [(1000, 50), (7,), (200_003,), (64, 3, 3, 3)]
+    ts = [torch.randn(*s, generator=g) for s in shapes]
+    ts[1] = ts[1].abs()  # a segment with no negative side
+    lay = SegmentLayout.from_tensors(ts)
+    register_layout("adaq_bucket", lay)
+    x = torch.cat([t.flatten() for t in ts])
+    comp = Z.AdaqCompressor(0.05)
+    payload, ctx = comp.compress(x.cuda(), "adaq_bucket")
+    m, cnt, ix = (t.cpu() for t in payload)
+    assert ix.numel() == int(cnt.sum())
+    pos = 0
+    for s, o, n in lay.segments():
+        seg = x[o:o + n]
+        for side in (0, 1):
+            c = int(cnt[2 * s + side])
+            idx = ix[pos:pos + c].long()
+            pos += c
+            assert ((idx >= o) & (idx < o + n)).all()
+            v = x[idx]
+            assert (v > 0).all() if side == 0 else (v < 0).all()
+            n_side = int((seg > 0).sum() if side == 0 else (seg < 0).sum())
+            if c:
+                torch.testing.assert_close(m[2 * s + side], v.mean(), rtol=1e-5, atol=1e-6)
+                assert len(set(idx.tolist())) == c
+            else:
+                assert m[2 * s + side] == 0
+            target = math.ceil(0.05 * n_side)
+            if n_side >= 1000:
+                assert 0.7 * target <= c <= 1.3 * target, (s, side, c, target)
+            if n_side == 0:
+                assert c == 0
+    dec = comp.decompress([t.cuda() for t in payload], ctx).cpu()
+    ref = torch.zeros_like(x)
+    ref[ix.long()] = torch.repeat_interleave(m, cnt.long())
+    torch.testing.assert_close(dec, ref)
