@@ -88,8 +88,12 @@ class GraceEngine:
 
     def __init__(self, params: Sequence[Tuple[str, torch.nn.Parameter]], grc: Communicator,
                  bucket_cap_mb: float = 64.0, backward_passes_per_step: int = 1, overlap: bool = True,
-                 sparse_params: Sequence[str] = ()):
+                 sparse_params: Sequence[str] = (), debug: Optional[bool] = None):
+        from ..utils import debug as _dbg
+
         self.grc = grc
+        self.debug = _dbg.ExchangeChecker(getattr(grc, "comm", None)) if (
+            debug if debug is not None else _dbg.enabled_from_env()) else None
         self.overlap = overlap
         self.backward_passes_per_step = backward_passes_per_step
         named = [(n, p) for n, p in params if p.requires_grad]
@@ -264,6 +268,8 @@ class GraceEngine:
             out = self.grc.receive_step(b.handles, b.ctx)
             if out.data_ptr() != b.flat.data_ptr():
                 b.flat.copy_(out.view(-1))
+            if self.debug is not None:
+                self.debug.check_bucket(b.name, b.flat)
             b.reset()
         if self._sparse:
             self._finish_sparse()
