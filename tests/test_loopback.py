@@ -57,8 +57,10 @@ def test_loopback_optimizer_keeps_replicas_identical():
     from grace_amd.parallel.optimizer import DistributedOptimizer
 
     def fn(rank, comm):
-        torch.manual_seed(0)
         net = torch.nn.Sequential(torch.nn.Linear(12, 24), torch.nn.Tanh(), torch.nn.Linear(24, 3))
+        with torch.no_grad():  # consistent init (the global RNG is shared by the rank threads)
+            for p in net.parameters():
+                comm.broadcast(p.data, 0)
         grc = grace_from_params({"compressor": "topk", "compress_ratio": 0.2, "memory": "residual",
                                  "communicator": "allgather", "world_size": W}, comm=comm)
         opt = DistributedOptimizer(torch.optim.SGD(net.parameters(), lr=0.05, momentum=0.9), grc,
