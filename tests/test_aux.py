@@ -121,3 +121,15 @@ def test_fault_injection_peer_death(tmp_path):
     except AssertionError:
         pass
     assert os.path.exists(marker), "surviving rank did not observe the failure"
+
+
+def test_packing_helpers_roundtrip_and_reference_format():
+    from grace_amd.ops import packing as P
+
+    for n in (1, 3, 4, 5, 8, 1001):
+        a = torch.randint(0, 4, (n,), generator=torch.Generator().manual_seed(n))
+        assert torch.equal(P.decode_byte(P.encode_byte(a), n), a.to(torch.int32))
+        assert torch.equal(P.unpack2(P.pack2(a), n), a.to(torch.int32))
+    # reference layout: quarters (n=4 pads 4 more entries 0..3 -> 2 bytes)
+    enc = P.encode_byte(torch.tensor([1, 2, 3, 0]))
+    assert enc.tolist() == [1 + 4 * 3 + 16 * 0 + 64 * 2, 2 + 4 * 0 + 16 * 1 + 64 * 3]
