@@ -275,10 +275,10 @@ class GraceEngine:
             self._finish_sparse()
         self.in_flight = 0
 
-    def zero_grad(self, set_to_none: bool = True):
-        """``set_to_none`` (torch's default): .grad becomes None and backward's AccumulateGrad
-        hands its fresh gradient to the hook, which copies it into the bucket -- one
-        read+write instead of a bucket memset plus an accumulate (read, read, write)."""
+    def zero_grad(self, set_to_none: bool = False):
+        """Default: memset the buckets; AccumulateGrad adds into the bucket views.
+        ``set_to_none``: .grad becomes None, AccumulateGrad hands its fresh gradient to the hook,
+        which copies it into the bucket (fewer bytes, one copy launch per parameter)."""
         if self.in_flight:
             raise AssertionError("zero_grad() called with gradients still being communicated -- "
                                  "call synchronize()/step() first")

@@ -64,9 +64,11 @@ class _DistributedOptimizer:
         self._synchronized = False
         return self._opt.step(closure)
 
-    def zero_grad(self, set_to_none: bool = True):
-        # set_to_none: fresh gradients are copied into the buckets by the hooks; False: one
-        # memset per bucket and backward accumulates into the bucket views
+    def zero_grad(self, set_to_none: bool = False):
+        # default: one memset per bucket, backward's AccumulateGrad adds straight into the bucket
+        # views.  set_to_none=True makes the hooks copy each fresh gradient instead: fewer bytes,
+        # but one blit per parameter (~5 us each on MI355X: 181 per BERT step = 0.9 ms), so it
+        # only pays for models with few, large parameters.
         self.engine.zero_grad(set_to_none)
 
     def state_dict(self):
