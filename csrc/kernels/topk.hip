@@ -12,10 +12,10 @@
 //                            fixes 11 bits of the k-th largest key; zeroes the histogram
 //   pass 1  topk_hist<1>   : histogram bits 19..9 of keys that match the prefix
 //   pass 2  topk_hist<2>   : histogram bits 8..0
-//   compact topk_compact   : emits exactly k (value, flat index) pairs per segment with
-//                            wave-aggregated atomics (one atomic per wave, not per element),
-//                            resolves ties deterministically in count, and writes the new
-//                            residual (x with the emitted entries zeroed) in the same pass.
+//   compact topk_compact   : emits exactly k (value, flat index) pairs per segment with one
+//                            atomic per 8K-element tile, resolves ties deterministically in
+//                            count, and zeroes the emitted entries of the residual (which
+//                            already holds x) in the same pass.
 // The radix select is exact (no sampling), so the selected set equals torch.topk's up to
 // the choice among equal |x| at the threshold.
 #include "grace_common.h"
@@ -146,6 +146,9 @@ __global__ __launch_bounds__(kBlock) void topk_select_kernel(int n_seg, const in
 constexpr int kPer = 32;
 constexpr int kTile = kBlock * kPer;
 
+// INPLACE (resid == x, the fused error-feedback path: x already holds the compensated values in
+// the residual buffer): only the k emitted entries are zeroed -- no full rewrite of the bucket.
+template <bool INPLACE>
 __global__ __launch_bounds__(kBlock) void topk_compact_kernel(
     ChunkTable ct, const float* x, const TopkState* __restrict__ st,
     const int64_t* __restrict__ out_off, int32_t* __restrict__ counters /* [2*n_seg] */, int n_seg,
@@ -207,7 +210,11 @@ __global__ __launch_bounds__(kBlock) void topk_compact_kernel(
         }
       }
     }
-    if (resid != nullptr) {
+    if (INPLACE) {
+#pragma unroll
+      for (int j = 0; j < kPer; ++j)
+        if ((take >> j) & 1u) resid[tb + (int64_t)j * kBlock + threadIdx.x] = 0.f;
+    } else if (resid != nullptr) {
 #pragma unroll
       for (int j = 0; j < kPer; ++j) {
         const int64_t i = tb + (int64_t)j * kBlock + threadIdx.x;
@@ -249,8 +256,12 @@ void topk_compact_bucket(const ChunkTable& ct, int n_seg, const float* x, const 
                          const int64_t* out_off, int32_t* counters, float* out_val,
                          int32_t* out_idx, float* resid, int64_t idx_base, hipStream_t stream) {
   GRACE_HIP_CHECK(hipMemsetAsync(counters, 0, sizeof(int32_t) * 2 * n_seg, stream));
-  topk_compact_kernel<<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, st, out_off, counters, n_seg, out_val,
-                                                          out_idx, resid, idx_base);
+  if (resid != nullptr && resid == x)
+    topk_compact_kernel<true><<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, st, out_off, counters, n_seg, out_val,
+                                                                  out_idx, resid, idx_base);
+  else
+    topk_compact_kernel<false><<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, st, out_off, counters, n_seg, out_val,
+                                                                   out_idx, resid, idx_base);
 }
 
 void sparse_scatter_add(const float* val, const int32_t* idx, int64_t K, float* out, float scale,
