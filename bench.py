@@ -47,6 +47,9 @@ def parse():
                          "whole-step HIP graph (a forked capture costs ~0.9 ms/step on ROCm for ResNet-50, "
                          "more than the overlap can hide), on otherwise")
     ap.add_argument("--no-overlap", action="store_true", help="same as --overlap off")
+    ap.add_argument("--grad-mode", choices=["gather", "accumulate"], default="gather",
+                    help="gather: zero_grad(set_to_none) + one native gather launch per bucket; "
+                         "accumulate: bucket memset + AccumulateGrad adds into bucket views")
     ap.add_argument("--no-benchmark-mode", action="store_true", help="disable MIOpen find (cudnn.benchmark)")
     ap.add_argument("--exposed-steps", type=int, default=3, help="untimed steps measuring exposed GRACE time")
     ap.add_argument("--force-dist", action="store_true",
@@ -105,8 +108,10 @@ def main():
 
     fwd_model = model
 
+    set_to_none = args.grad_mode == "gather"
+
     def step():
-        opt.zero_grad()
+        opt.zero_grad(set_to_none=set_to_none)
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp, cache_enabled=False):
             loss = w.loss(fwd_model, data)
         loss.backward()
@@ -161,7 +166,7 @@ def main():
     # (pytorch_synthetic_benchmark.py:166-167)
     exposed = []
     for _ in range(args.exposed_steps):
-        opt.zero_grad()
+        opt.zero_grad(set_to_none=set_to_none)
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp, cache_enabled=False):
             l2 = w.loss(fwd_model, data)
         l2.backward()
@@ -202,6 +207,7 @@ def main():
                 "bucket_mb": args.bucket_mb,
                 "overlap": overlap,
                 "hip_graph": graph_note,
+                "grad_mode": args.grad_mode,
             },
             "comm_wall_ms": round(float(ex.item()) * 1e3, 3),
             "final_loss": round(float(loss.float().item()), 4),

@@ -544,6 +544,27 @@ void axpby(const Tensor& x, const Tensor& y, const Tensor& out, double a, double
                (float)b, cur_stream());
 }
 
+// Copy the memory image of srcs[i] (dense fp32 GPU tensors) to dst[dst_off[i] : dst_off[i] + numel].
+void gather_segments(const std::vector<Tensor>& srcs, const std::vector<int64_t>& dst_off, const Tensor& dst) {
+  CHECK_F32(dst);
+  TORCH_CHECK(dst_off.size() == srcs.size(), "one destination offset per source");
+  std::vector<const float*> ptrs(srcs.size());
+  std::vector<int64_t> len(srcs.size());
+  for (size_t i = 0; i < srcs.size(); ++i) {
+    const Tensor& t = srcs[i];
+    CHECK_DEV(t);
+    CHECK_DT(t, at::kFloat);
+    TORCH_CHECK(t.is_non_overlapping_and_dense(), "gather source must be dense");
+    TORCH_CHECK(t.device() == dst.device(), "device mismatch");
+    TORCH_CHECK(dst_off[i] >= 0 && dst_off[i] + t.numel() <= dst.numel(), "segment ", i, " exceeds the destination");
+    ptrs[i] = t.data_ptr<float>();
+    len[i] = t.numel();
+  }
+  DevGuard guard(dst.device());
+  grace::gather_segments(ptrs.data(), dst_off.data(), len.data(), (int)srcs.size(), dst.data_ptr<float>(),
+                         cur_stream());
+}
+
 void scale_(const Tensor& x, double s) {
   CHECK_F32(x);
   DevGuard guard(x.device());
@@ -725,4 +746,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sketch_decode", &sketch_decode);
   m.def("axpby", &axpby);
   m.def("scale_", &scale_);
+  m.def("gather_segments", &gather_segments);
 }

@@ -125,4 +125,9 @@ void adaq_compact(const ChunkTable& ct, int n_seg, const int32_t* seg_chunk_begi
                   const int32_t* goff, int32_t* cursor, int32_t* idx, double* psum, float* means, int32_t* counts,
                   hipStream_t stream);
 
+// ---------------------------------------------------------------- ef.hip (bucket gather)
+constexpr int kGatherSegs = 120;
+void gather_segments(const float* const* src, const int64_t* dst_off, const int64_t* len, int n_seg, float* dst,
+                     hipStream_t stream);
+
 }  // namespace grace

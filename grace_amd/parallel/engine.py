@@ -27,6 +27,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 
 from ..core import Communicator, register_layout
+from ..ops import _native
 from ..ops.layout import SegmentLayout
 from ..ops.randomk import fnv1a64
 
@@ -73,12 +74,14 @@ class Bucket:
             p.grad = v  # gradients accumulate straight into the bucket buffer
         self.pending = len(params)
         self.fired = [False] * len(params)
+        self.stolen: List[Optional[torch.Tensor]] = [None] * len(params)  # fresh grads awaiting the gather
         self.handles = None
         self.ctx = None
 
     def reset(self):
         self.pending = len(self.params)
         self.fired = [False] * len(self.params)
+        self.stolen = [None] * len(self.params)
         self.handles = None
         self.ctx = None
 
@@ -177,10 +180,14 @@ class GraceEngine:
             raise RuntimeError(f"parameter {self._name_of(p)} produced a sparse gradient: pass its name in "
                                "sparse_params= (uncompressed sparse all-gather)")
         if p.grad is not None and p.grad.data_ptr() != view.data_ptr():
-            # .grad was None before backward (zero_grad(set_to_none=True)): AccumulateGrad stole
-            # the fresh gradient, one copy moves it into the bucket (cheaper than memset + add)
-            view.copy_(p.grad)
-            p.grad = view
+            # .grad was None before backward (zero_grad(set_to_none=True)): AccumulateGrad handed
+            # over its fresh gradient.  It is kept alive and copied into the bucket by ONE gather
+            # launch when the bucket is complete (native); else copied right here.
+            if self._gatherable(p.grad, view):
+                b.stolen[idx] = p.grad
+            else:
+                view.copy_(p.grad)
+                p.grad = view
         if b.fired[idx]:
             raise RuntimeError(f"{b.name}: gradient of parameter {idx} produced twice before synchronize() -- "
                                "increase backward_passes_per_step or call synchronize()")
@@ -188,6 +195,26 @@ class GraceEngine:
         b.pending -= 1
         if b.pending == 0:
             self._launch(b)
+
+    @staticmethod
+    def _gatherable(g: torch.Tensor, view: torch.Tensor) -> bool:
+        return (g.is_cuda and g.dtype == torch.float32 and g.stride() == view.stride()
+                and g.is_non_overlapping_and_dense() and _native.native_on(g.device))
+
+    def _gather(self, b: Bucket) -> None:
+        """Copy the handed-over gradients into the bucket (one kernel per <= 120 tensors), then
+        point .grad at the bucket views and release them (stream-ordered: safe to reuse)."""
+        idx = [i for i, g in enumerate(b.stolen) if g is not None]
+        if not idx:
+            return
+        srcs = [b.stolen[i] for i in idx]
+        _native.lib().gather_segments(srcs, [b.layout.offsets[i] for i in idx], b.flat)
+        if self.stream is not None:
+            for g in srcs:
+                g.record_stream(self.stream)
+        for i in idx:
+            b.params[i].grad = b.views[i]
+            b.stolen[i] = None
 
     def _name_of(self, p) -> str:
         b, i, _ = self._where[id(p)]
@@ -238,8 +265,10 @@ class GraceEngine:
         if self.stream is not None:
             self.stream.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(self.stream):
+                self._gather(b)
                 b.handles, b.ctx = self.grc.send_step(b.flat, b.name)
         else:
+            self._gather(b)
             b.handles, b.ctx = self.grc.send_step(b.flat, b.name)
         self.in_flight += 1
 
