@@ -198,8 +198,9 @@ class GraceEngine:
 
     @staticmethod
     def _gatherable(g: torch.Tensor, view: torch.Tensor) -> bool:
+        # same shape and strides as the (dense) bucket view -> same dense memory image
         return (g.is_cuda and g.dtype == torch.float32 and g.stride() == view.stride()
-                and g.is_non_overlapping_and_dense() and _native.native_on(g.device))
+                and _native.native_on(g.device))
 
     def _gather(self, b: Bucket) -> None:
         """Copy the handed-over gradients into the bucket (one kernel per <= 120 tensors), then
