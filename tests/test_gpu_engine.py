@@ -112,4 +112,5 @@ def test_gather_mode_equals_accumulate_mode(overlap):
             g()
         torch.cuda.synchronize()
         res.append(torch.cat([q.detach().reshape(-1) for q in m.parameters()]))
-    torch.testing.assert_close(res[1], res[0], rtol=0, atol=0)
+    # MIOpen's backward-weight kernels may reduce with atomics: equal up to fp32 rounding
+    torch.testing.assert_close(res[1], res[0], rtol=1e-5, atol=1e-6)
