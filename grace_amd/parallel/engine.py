@@ -305,10 +305,11 @@ class GraceEngine:
             self._finish_sparse()
         self.in_flight = 0
 
-    def zero_grad(self, set_to_none: bool = False):
-        """Default: memset the buckets; AccumulateGrad adds into the bucket views.
-        ``set_to_none``: .grad becomes None, AccumulateGrad hands its fresh gradient to the hook,
-        which copies it into the bucket (fewer bytes, one copy launch per parameter)."""
+    def zero_grad(self, set_to_none: bool = True):
+        """``set_to_none`` (default): .grad becomes None, AccumulateGrad hands its fresh gradient
+        to the hook and one native gather launch per bucket copies them in when the bucket is
+        complete.  ``False``: memset the buckets, AccumulateGrad adds into the bucket views
+        (one add kernel per parameter)."""
         if self.in_flight:
             raise AssertionError("zero_grad() called with gradients still being communicated -- "
                                  "call synchronize()/step() first")
