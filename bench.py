@@ -47,6 +47,9 @@ def parse():
                          "whole-step HIP graph (a forked capture costs ~0.9 ms/step on ROCm for ResNet-50, "
                          "more than the overlap can hide), on otherwise")
     ap.add_argument("--no-overlap", action="store_true", help="same as --overlap off")
+    ap.add_argument("--bf16-weights", choices=["on", "off"], default="on",
+                    help="fp32 master weights + bf16 working copies of conv/linear weights (autocast "
+                         "numerics without the per-layer cast kernels; parallel/precision.py)")
     ap.add_argument("--grad-mode", choices=["gather", "accumulate"], default="gather",
                     help="gather: zero_grad(set_to_none) + one native gather launch per bucket; "
                          "accumulate: bucket memset + AccumulateGrad adds into bucket views")
@@ -86,7 +89,15 @@ def main():
     batch = args.batch or w.batch
     torch.manual_seed(0)
     model = build_model(w, dev)
-    base_opt = torch.optim.SGD(model.parameters(), lr=0.01 * world, momentum=0.5)
+    broadcast_parameters(model.state_dict(), root_rank=0)
+    weights = None
+    named = list(model.named_parameters())
+    if args.bf16_weights == "on" and args.dtype == "bf16":
+        from grace_amd.parallel.precision import BF16Weights
+
+        weights = BF16Weights(model)
+        named = list(weights.named_master_parameters(model))
+    base_opt = torch.optim.SGD([p for _, p in named], lr=0.01 * world, momentum=0.5)
     grc = grace_from_params(dict(w.grace, world_size=world))
     from grace_amd.parallel.graph import GraphedStep, graph_compute, graph_safe
 
@@ -98,9 +109,8 @@ def main():
     if args.no_overlap:
         args.overlap = "off"
     overlap = args.overlap == "on" or (args.overlap == "auto" and mode != "full")
-    opt = DistributedOptimizer(base_opt, grc, named_parameters=model.named_parameters(),
-                               bucket_cap_mb=args.bucket_mb, overlap=overlap)
-    broadcast_parameters(model.state_dict(), root_rank=0)
+    opt = DistributedOptimizer(base_opt, grc, named_parameters=named,
+                               bucket_cap_mb=args.bucket_mb, overlap=overlap, weights=weights)
     data = w.make_batch(batch, dev)
     if w.channels_last and isinstance(data, tuple) and data[0].dim() == 4:
         data = (data[0].contiguous(memory_format=torch.channels_last),) + tuple(data[1:])
@@ -208,6 +218,7 @@ def main():
                 "overlap": overlap,
                 "hip_graph": graph_note,
                 "grad_mode": args.grad_mode,
+                "bf16_weights": weights is not None,
             },
             "comm_wall_ms": round(float(ex.item()) * 1e3, 3),
             "final_loss": round(float(loss.float().item()), 4),

@@ -544,25 +544,50 @@ void axpby(const Tensor& x, const Tensor& y, const Tensor& out, double a, double
                (float)b, cur_stream());
 }
 
-// Copy the memory image of srcs[i] (dense fp32 GPU tensors) to dst[dst_off[i] : dst_off[i] + numel].
+// Copy the memory image of srcs[i] (dense fp32 or bf16 GPU tensors, one dtype per call) to
+// dst[dst_off[i] : dst_off[i] + numel] (fp32, bf16 widened).
 void gather_segments(const std::vector<Tensor>& srcs, const std::vector<int64_t>& dst_off, const Tensor& dst) {
   CHECK_F32(dst);
   TORCH_CHECK(dst_off.size() == srcs.size(), "one destination offset per source");
-  std::vector<const float*> ptrs(srcs.size());
+  if (srcs.empty()) return;
+  const auto dt = srcs[0].scalar_type();
+  TORCH_CHECK(dt == at::kFloat || dt == at::kBFloat16, "gather sources must be fp32 or bf16");
+  std::vector<const void*> ptrs(srcs.size());
   std::vector<int64_t> len(srcs.size());
   for (size_t i = 0; i < srcs.size(); ++i) {
     const Tensor& t = srcs[i];
     CHECK_DEV(t);
-    CHECK_DT(t, at::kFloat);
+    TORCH_CHECK(t.scalar_type() == dt, "gather sources must share one dtype");
     TORCH_CHECK(t.is_non_overlapping_and_dense(), "gather source must be dense");
     TORCH_CHECK(t.device() == dst.device(), "device mismatch");
     TORCH_CHECK(dst_off[i] >= 0 && dst_off[i] + t.numel() <= dst.numel(), "segment ", i, " exceeds the destination");
-    ptrs[i] = t.data_ptr<float>();
+    ptrs[i] = t.data_ptr();
     len[i] = t.numel();
   }
   DevGuard guard(dst.device());
-  grace::gather_segments(ptrs.data(), dst_off.data(), len.data(), (int)srcs.size(), dst.data_ptr<float>(),
-                         cur_stream());
+  grace::gather_segments(ptrs.data(), dt == at::kBFloat16, dst_off.data(), len.data(), (int)srcs.size(),
+                         dst.data_ptr<float>(), cur_stream());
+}
+
+// dsts[i] <- bf16(srcs[i]) (round to nearest even), memory images, one launch per 120 tensors.
+void cast_segments_bf16(const std::vector<Tensor>& srcs, const std::vector<Tensor>& dsts) {
+  TORCH_CHECK(srcs.size() == dsts.size(), "srcs/dsts length");
+  if (srcs.empty()) return;
+  std::vector<const float*> sp(srcs.size());
+  std::vector<uint16_t*> dp(srcs.size());
+  std::vector<int64_t> len(srcs.size());
+  for (size_t i = 0; i < srcs.size(); ++i) {
+    CHECK_F32(srcs[i]);
+    CHECK_DEV(dsts[i]);
+    CHECK_DT(dsts[i], at::kBFloat16);
+    TORCH_CHECK(srcs[i].numel() == dsts[i].numel() && srcs[i].strides() == dsts[i].strides(), "shape/stride mismatch");
+    TORCH_CHECK(srcs[i].is_non_overlapping_and_dense(), "cast source must be dense");
+    sp[i] = srcs[i].data_ptr<float>();
+    dp[i] = reinterpret_cast<uint16_t*>(dsts[i].data_ptr());
+    len[i] = srcs[i].numel();
+  }
+  DevGuard guard(srcs[0].device());
+  grace::cast_segments_bf16(sp.data(), dp.data(), len.data(), (int)srcs.size(), cur_stream());
 }
 
 void scale_(const Tensor& x, double s) {
@@ -747,4 +772,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("axpby", &axpby);
   m.def("scale_", &scale_);
   m.def("gather_segments", &gather_segments);
+  m.def("cast_segments_bf16", &cast_segments_bf16);
 }

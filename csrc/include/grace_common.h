@@ -103,6 +103,15 @@ struct SeedArg {
   }
 };
 
+// fp32 -> bf16 bits, round-to-nearest-even; NaN -> canonical 0x7FC0 (c10::BFloat16's rule, so
+// kernels produce exactly what tensor.to(torch.bfloat16) produces)
+__device__ __forceinline__ uint16_t f32_to_bf16_rne(float f) {
+  const uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7FC0u;
+  return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+
 // uniform float in [0, 1) from 24 random bits
 __device__ __forceinline__ float u01(uint32_t r) { return (r >> 8) * (1.0f / 16777216.0f); }
 

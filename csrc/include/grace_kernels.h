@@ -127,7 +127,9 @@ void adaq_compact(const ChunkTable& ct, int n_seg, const int32_t* seg_chunk_begi
 
 // ---------------------------------------------------------------- ef.hip (bucket gather)
 constexpr int kGatherSegs = 120;
-void gather_segments(const float* const* src, const int64_t* dst_off, const int64_t* len, int n_seg, float* dst,
-                     hipStream_t stream);
+void gather_segments(const void* const* src, bool bf16, const int64_t* dst_off, const int64_t* len, int n_seg,
+                     float* dst, hipStream_t stream);
+void cast_segments_bf16(const float* const* src, uint16_t* const* dst, const int64_t* len, int n_seg,
+                        hipStream_t stream);
 
 }  // namespace grace

@@ -56,37 +56,89 @@ __global__ __launch_bounds__(kBlock) void scale_kernel(float* x, int64_t n, floa
 }
 
 // Bucket gather: copy the memory image of up to kGatherSegs parameter gradients into their
-// segments of the flat bucket in ONE launch (pointer table passed by value in the kernel
+// segments of the flat fp32 bucket in ONE launch (pointer table passed by value in the kernel
 // arguments, so a captured HIP graph replays it with no host work).  Replaces a bucket memset +
 // one AccumulateGrad add kernel per parameter (~4.5 us of device time each for the many small
-// tensors of a CNN/transformer).  blockIdx.y = segment, blockIdx.x strides its elements.
+// tensors of a CNN/transformer).  BF16 sources (gradients of bf16 working weights) are widened
+// on the fly.  blockIdx.y = segment, blockIdx.x strides its elements.
 struct GatherTable {
-  const float* src[kGatherSegs];
+  const void* src[kGatherSegs];
   int64_t dst_off[kGatherSegs];  // segment start in the destination
   int64_t len[kGatherSegs];
 };
 
+template <bool BF16>
 __global__ __launch_bounds__(kBlock) void gather_segments_kernel(GatherTable t, float* __restrict__ dst) {
   const int s = blockIdx.y;
-  const int64_t b = t.dst_off[s], n = t.len[s];
-  const float* __restrict__ src = t.src[s];
-  float* __restrict__ d = dst + b;
+  const int64_t n = t.len[s];
+  float* __restrict__ d = dst + t.dst_off[s];
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   int64_t tail = 0;
-  if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(d)) & 15) == 0) {
+  if constexpr (BF16) {
+    const uint16_t* __restrict__ src = static_cast<const uint16_t*>(t.src[s]);
+    if (((reinterpret_cast<uintptr_t>(src) & 7) | (reinterpret_cast<uintptr_t>(d) & 15)) == 0) {
+      const int64_t nv = n >> 2;
+      const ushort4* s4 = reinterpret_cast<const ushort4*>(src);
+      float4* d4 = reinterpret_cast<float4*>(d);
+      for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nv; i += stride) {
+        const ushort4 h = s4[i];
+        d4[i] = make_float4(bf16_to_f32(h.x), bf16_to_f32(h.y), bf16_to_f32(h.z), bf16_to_f32(h.w));
+      }
+      tail = nv << 2;
+    }
+    for (int64_t i = tail + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) d[i] = bf16_to_f32(src[i]);
+  } else {
+    const float* __restrict__ src = static_cast<const float*>(t.src[s]);
+    if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(d)) & 15) == 0) {
+      const int64_t nv = n >> 2;
+      const float4* s4 = reinterpret_cast<const float4*>(src);
+      float4* d4 = reinterpret_cast<float4*>(d);
+      for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nv; i += stride) d4[i] = s4[i];
+      tail = nv << 2;
+    }
+    for (int64_t i = tail + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) d[i] = src[i];
+  }
+}
+
+// Working-weight refresh: bf16 copies of up to kGatherSegs fp32 master tensors in one launch
+// (instead of one cast kernel per weight per forward under autocast).
+struct CastTable {
+  const float* src[kGatherSegs];
+  uint16_t* dst[kGatherSegs];
+  int64_t len[kGatherSegs];
+};
+
+__global__ __launch_bounds__(kBlock) void cast_segments_kernel(CastTable t) {
+  const int s = blockIdx.y;
+  const int64_t n = t.len[s];
+  const float* __restrict__ src = t.src[s];
+  uint16_t* __restrict__ d = t.dst[s];
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  int64_t tail = 0;
+  if (((reinterpret_cast<uintptr_t>(src) & 15) | (reinterpret_cast<uintptr_t>(d) & 7)) == 0) {
     const int64_t nv = n >> 2;
     const float4* s4 = reinterpret_cast<const float4*>(src);
-    float4* d4 = reinterpret_cast<float4*>(d);
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nv; i += stride) d4[i] = s4[i];
+    ushort4* d4 = reinterpret_cast<ushort4*>(d);
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nv; i += stride) {
+      const float4 v = s4[i];
+      d4[i] = make_ushort4(f32_to_bf16_rne(v.x), f32_to_bf16_rne(v.y), f32_to_bf16_rne(v.z), f32_to_bf16_rne(v.w));
+    }
     tail = nv << 2;
   }
-  for (int64_t i = tail + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) d[i] = src[i];
+  for (int64_t i = tail + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) d[i] = f32_to_bf16_rne(src[i]);
+}
+
+inline unsigned seg_grid(int64_t maxn) {
+  int64_t gx = (maxn / 4 + kBlock - 1) / kBlock;
+  if (gx > 512) gx = 512;
+  if (gx < 1) gx = 1;
+  return (unsigned)gx;
 }
 
 }  // namespace
 
-void gather_segments(const float* const* src, const int64_t* dst_off, const int64_t* len, int n_seg, float* dst,
-                     hipStream_t stream) {
+void gather_segments(const void* const* src, bool bf16, const int64_t* dst_off, const int64_t* len, int n_seg,
+                     float* dst, hipStream_t stream) {
   for (int g0 = 0; g0 < n_seg; g0 += kGatherSegs) {
     const int ng = n_seg - g0 < kGatherSegs ? n_seg - g0 : kGatherSegs;
     GatherTable t;
@@ -98,10 +150,27 @@ void gather_segments(const float* const* src, const int64_t* dst_off, const int6
       if (len[g0 + i] > maxn) maxn = len[g0 + i];
     }
     if (maxn == 0) continue;
-    int64_t gx = (maxn / 4 + kBlock - 1) / kBlock;
-    if (gx > 512) gx = 512;
-    if (gx < 1) gx = 1;
-    gather_segments_kernel<<<dim3((unsigned)gx, (unsigned)ng), kBlock, 0, stream>>>(t, dst);
+    if (bf16)
+      gather_segments_kernel<true><<<dim3(seg_grid(maxn), (unsigned)ng), kBlock, 0, stream>>>(t, dst);
+    else
+      gather_segments_kernel<false><<<dim3(seg_grid(maxn), (unsigned)ng), kBlock, 0, stream>>>(t, dst);
+  }
+}
+
+void cast_segments_bf16(const float* const* src, uint16_t* const* dst, const int64_t* len, int n_seg,
+                        hipStream_t stream) {
+  for (int g0 = 0; g0 < n_seg; g0 += kGatherSegs) {
+    const int ng = n_seg - g0 < kGatherSegs ? n_seg - g0 : kGatherSegs;
+    CastTable t;
+    int64_t maxn = 0;
+    for (int i = 0; i < ng; ++i) {
+      t.src[i] = src[g0 + i];
+      t.dst[i] = dst[g0 + i];
+      t.len[i] = len[g0 + i];
+      if (len[g0 + i] > maxn) maxn = len[g0 + i];
+    }
+    if (maxn == 0) continue;
+    cast_segments_kernel<<<dim3(seg_grid(maxn), (unsigned)ng), kBlock, 0, stream>>>(t);
   }
 }
 

@@ -72,6 +72,9 @@ class Bucket:
                 v = seg.view(p.shape)
             self.views.append(v)
             p.grad = v  # gradients accumulate straight into the bucket buffer
+        # the tensor whose backward gradient feeds segment i: the parameter itself, or its bf16
+        # working copy (parallel/precision.py) when the parameter is an fp32 master
+        self.srcs: List[torch.Tensor] = list(params)
         self.pending = len(params)
         self.fired = [False] * len(params)
         self.stolen: List[Optional[torch.Tensor]] = [None] * len(params)  # fresh grads awaiting the gather
@@ -91,7 +94,8 @@ class GraceEngine:
 
     def __init__(self, params: Sequence[Tuple[str, torch.nn.Parameter]], grc: Communicator,
                  bucket_cap_mb: float = 64.0, backward_passes_per_step: int = 1, overlap: bool = True,
-                 sparse_params: Sequence[str] = (), debug: Optional[bool] = None):
+                 sparse_params: Sequence[str] = (), debug: Optional[bool] = None,
+                 grad_sources: Optional[Dict[int, torch.Tensor]] = None):
         from ..utils import debug as _dbg
 
         self.grc = grc
@@ -136,16 +140,22 @@ class GraceEngine:
         for i, grp in enumerate(groups):
             sig = ";".join(f"{n}:{tuple(p.shape)}" for n, p in grp).encode()
             self.buckets.append(Bucket(f"grace.b{i}.{fnv1a64(sig):016x}", [p for _, p in grp], self.device))
+        # gradients of fp32 masters may arrive on bf16 working copies (grad_sources: id(master) ->
+        # working parameter, parallel/precision.py): hooks go on the tensor that gets the gradient
         self._where: Dict[int, Tuple[Bucket, int, torch.Tensor]] = {}
         for b in self.buckets:
             for i, (p, v) in enumerate(zip(b.params, b.views)):
-                self._where[id(p)] = (b, i, v)
+                src = (grad_sources or {}).get(id(p), p)
+                b.srcs[i] = src
+                if src is not p:
+                    src.grad = None
+                self._where[id(src)] = (b, i, v)
         self._passes: Dict[int, int] = {}
         self._hooks = []
         self.stream = torch.cuda.Stream(self.device) if (self.device.type == "cuda" and overlap) else None
         for b in self.buckets:
-            for p in b.params:
-                self._hooks.append(p.register_post_accumulate_grad_hook(self._hook))
+            for src in b.srcs:
+                self._hooks.append(src.register_post_accumulate_grad_hook(self._hook))
         for _, p in self._sparse.values():
             self._hooks.append(p.register_post_accumulate_grad_hook(self._sparse_hook))
         self.in_flight = 0
@@ -180,14 +190,16 @@ class GraceEngine:
             raise RuntimeError(f"parameter {self._name_of(p)} produced a sparse gradient: pass its name in "
                                "sparse_params= (uncompressed sparse all-gather)")
         if p.grad is not None and p.grad.data_ptr() != view.data_ptr():
-            # .grad was None before backward (zero_grad(set_to_none=True)): AccumulateGrad handed
-            # over its fresh gradient.  It is kept alive and copied into the bucket by ONE gather
-            # launch when the bucket is complete (native); else copied right here.
+            # .grad was None before backward (zero_grad(set_to_none=True), or a bf16 working copy):
+            # AccumulateGrad handed over its fresh gradient.  It is kept alive and copied into the
+            # bucket by ONE gather launch when the bucket is complete (native); else copied here.
             if self._gatherable(p.grad, view):
                 b.stolen[idx] = p.grad
             else:
                 view.copy_(p.grad)
-                p.grad = view
+                if p is not b.params[idx]:
+                    p.grad = None
+                b.params[idx].grad = view
         if b.fired[idx]:
             raise RuntimeError(f"{b.name}: gradient of parameter {idx} produced twice before synchronize() -- "
                                "increase backward_passes_per_step or call synchronize()")
@@ -199,21 +211,25 @@ class GraceEngine:
     @staticmethod
     def _gatherable(g: torch.Tensor, view: torch.Tensor) -> bool:
         # same shape and strides as the (dense) bucket view -> same dense memory image
-        return (g.is_cuda and g.dtype == torch.float32 and g.stride() == view.stride()
+        return (g.is_cuda and g.dtype in (torch.float32, torch.bfloat16) and g.stride() == view.stride()
                 and _native.native_on(g.device))
 
     def _gather(self, b: Bucket) -> None:
-        """Copy the handed-over gradients into the bucket (one kernel per <= 120 tensors), then
-        point .grad at the bucket views and release them (stream-ordered: safe to reuse)."""
+        """Copy the handed-over gradients into the bucket (one kernel per dtype and <= 120
+        tensors; bf16 gradients of working copies are widened), then point the masters' .grad at
+        the bucket views and release the fresh gradients (stream-ordered: safe to reuse)."""
         idx = [i for i, g in enumerate(b.stolen) if g is not None]
         if not idx:
             return
-        srcs = [b.stolen[i] for i in idx]
-        _native.lib().gather_segments(srcs, [b.layout.offsets[i] for i in idx], b.flat)
-        if self.stream is not None:
-            for g in srcs:
-                g.record_stream(self.stream)
+        for dt in (torch.float32, torch.bfloat16):
+            sel = [i for i in idx if b.stolen[i].dtype == dt]
+            if sel:
+                _native.lib().gather_segments([b.stolen[i] for i in sel], [b.layout.offsets[i] for i in sel], b.flat)
         for i in idx:
+            if self.stream is not None:
+                b.stolen[i].record_stream(self.stream)
+            if b.srcs[i] is not b.params[i]:
+                b.srcs[i].grad = None
             b.params[i].grad = b.views[i]
             b.stolen[i] = None
 
@@ -314,6 +330,10 @@ class GraceEngine:
             raise AssertionError("zero_grad() called with gradients still being communicated -- "
                                  "call synchronize()/step() first")
         self._grads_none = set_to_none
+        for b in self.buckets:
+            for p, src in zip(b.params, b.srcs):
+                if src is not p:
+                    src.grad = None  # working copies always hand over a fresh gradient
         if set_to_none:
             for b in self.buckets:
                 for p in b.params:

@@ -22,7 +22,7 @@ from .engine import GraceEngine
 
 class _DistributedOptimizer:
     def __init__(self, optimizer, grace, named_parameters=None, backward_passes_per_step: int = 1,
-                 bucket_cap_mb: float = 64.0, overlap: bool = True, sparse_params=()):
+                 bucket_cap_mb: float = 64.0, overlap: bool = True, sparse_params=(), weights=None):
         self._opt = optimizer
         if named_parameters is None:
             params = [p for g in optimizer.param_groups for p in g["params"]]
@@ -34,7 +34,9 @@ class _DistributedOptimizer:
             raise ValueError(f"named_parameters not in the optimizer: {missing[:5]}")
         self.engine = GraceEngine(named_parameters, grace, bucket_cap_mb=bucket_cap_mb,
                                   backward_passes_per_step=backward_passes_per_step, overlap=overlap,
-                                  sparse_params=sparse_params)
+                                  sparse_params=sparse_params,
+                                  grad_sources=weights.grad_sources() if weights is not None else None)
+        self.weights = weights  # parallel/precision.BF16Weights: refreshed after every step
         self._synchronized = False
         self._should_sync = True
 
@@ -62,7 +64,10 @@ class _DistributedOptimizer:
             else:
                 self.synchronize()
         self._synchronized = False
-        return self._opt.step(closure)
+        out = self._opt.step(closure)
+        if self.weights is not None:
+            self.weights.refresh()
+        return out
 
     def zero_grad(self, set_to_none: bool = True):
         # default (torch's): .grad = None; backward hands every fresh gradient over and ONE native

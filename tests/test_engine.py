@@ -153,3 +153,40 @@ def _ddp_body(rank, world):
 
 def test_ddp_comm_hook_gloo():
     run_distributed(_ddp_body, 2)
+
+
+def _mp_net():
+    torch.manual_seed(3)
+    return torch.nn.Sequential(torch.nn.Conv2d(3, 8, 3, padding=1), torch.nn.BatchNorm2d(8), torch.nn.ReLU(),
+                               torch.nn.AdaptiveAvgPool2d(1), torch.nn.Flatten(), torch.nn.Linear(8, 5))
+
+
+def _mp_train(dev, use_weights, steps=3):
+    from grace_amd import grace_from_params
+    from grace_amd.parallel import DistributedOptimizer
+    from grace_amd.parallel.comm import LocalComm
+    from grace_amd.parallel.precision import BF16Weights
+
+    net = _mp_net().to(dev)
+    w = BF16Weights(net) if use_weights else None
+    named = list(w.named_master_parameters(net)) if w else list(net.named_parameters())
+    grc = grace_from_params({"compressor": "topk", "compress_ratio": 0.3, "memory": "residual",
+                             "communicator": "allgather"}, comm=LocalComm())
+    opt = DistributedOptimizer(torch.optim.SGD([p for _, p in named], lr=0.05, momentum=0.9), grc,
+                               named_parameters=named, bucket_cap_mb=0.001, weights=w)
+    g = torch.Generator().manual_seed(5)
+    x, y = torch.randn(6, 3, 8, 8, generator=g).to(dev), torch.randint(0, 5, (6,), generator=g).to(dev)
+    for _ in range(steps):
+        opt.zero_grad()
+        with torch.autocast(torch.device(dev).type, dtype=torch.bfloat16):
+            loss = torch.nn.functional.cross_entropy(net(x), y)
+        loss.backward()
+        opt.step()
+    return torch.cat([p.detach().float().reshape(-1) for _, p in named])
+
+
+def test_bf16_working_weights_match_autocast_cpu():
+    """fp32 masters + bf16 working copies == plain autocast (same roundings, fewer kernels)."""
+    a = _mp_train("cpu", False)
+    b = _mp_train("cpu", True)
+    torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-6)

@@ -114,3 +114,14 @@ def test_gather_mode_equals_accumulate_mode(overlap):
         res.append(torch.cat([q.detach().reshape(-1) for q in m.parameters()]))
     # MIOpen's backward-weight kernels may reduce with atomics: equal up to fp32 rounding
     torch.testing.assert_close(res[1], res[0], rtol=1e-5, atol=1e-6)
+
+
+def test_bf16_working_weights_match_autocast_gpu():
+    """Native path: batched bf16 refresh kernel + bf16-widening gather == plain autocast."""
+    import sys, os
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_engine import _mp_train
+
+    a = _mp_train("cuda", False)
+    b = _mp_train("cuda", True)
+    torch.testing.assert_close(b.cpu(), a.cpu(), rtol=1e-4, atol=1e-5)

@@ -16,6 +16,13 @@ import sys
 
 
 def short(name: str) -> str:
+    name = name.replace("(anonymous namespace)::", "")
+    if "elementwise_kernel" in name or "reduce_kernel" in name:
+        # keep the functor: "vectorized_elementwise_kernel[bfloat16_copy_kernel_cuda]"
+        fn = re.findall(r"([A-Za-z0-9_]+(?:_kernel_cuda|_kernel_impl|Functor[A-Za-z0-9_]*|_kernel))", name)
+        base = re.sub(r"<.*", "", re.sub(r"\(.*", "", name))
+        tags = [f for f in dict.fromkeys(fn) if f not in base]
+        return (base + ("[" + ",".join(tags[:2]) + "]" if tags else ""))[:110]
     name = re.sub(r"\(.*", "", name)
     name = re.sub(r"<.*", "", name)
     return name[:90]
