@@ -577,7 +577,8 @@ void cast_segments_bf16(const std::vector<Tensor>& srcs, const std::vector<Tenso
   std::vector<uint16_t*> dp(srcs.size());
   std::vector<int64_t> len(srcs.size());
   for (size_t i = 0; i < srcs.size(); ++i) {
-    CHECK_F32(srcs[i]);
+    CHECK_DEV(srcs[i]);
+    CHECK_DT(srcs[i], at::kFloat);  // channels_last masters are dense, not contiguous
     CHECK_DEV(dsts[i]);
     CHECK_DT(dsts[i], at::kBFloat16);
     TORCH_CHECK(srcs[i].numel() == dsts[i].numel() && srcs[i].strides() == dsts[i].strides(), "shape/stride mismatch");

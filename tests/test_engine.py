@@ -161,13 +161,15 @@ def _mp_net():
                                torch.nn.AdaptiveAvgPool2d(1), torch.nn.Flatten(), torch.nn.Linear(8, 5))
 
 
-def _mp_train(dev, use_weights, steps=3):
+def _mp_train(dev, use_weights, steps=3, channels_last=False):
     from grace_amd import grace_from_params
     from grace_amd.parallel import DistributedOptimizer
     from grace_amd.parallel.comm import LocalComm
     from grace_amd.parallel.precision import BF16Weights
 
     net = _mp_net().to(dev)
+    if channels_last:  # conv masters become dense-but-not-contiguous (the bench's layout)
+        net = net.to(memory_format=torch.channels_last)
     w = BF16Weights(net) if use_weights else None
     named = list(w.named_master_parameters(net)) if w else list(net.named_parameters())
     grc = grace_from_params({"compressor": "topk", "compress_ratio": 0.3, "memory": "residual",
@@ -176,6 +178,8 @@ def _mp_train(dev, use_weights, steps=3):
                                named_parameters=named, bucket_cap_mb=0.001, weights=w)
     g = torch.Generator().manual_seed(5)
     x, y = torch.randn(6, 3, 8, 8, generator=g).to(dev), torch.randint(0, 5, (6,), generator=g).to(dev)
+    if channels_last:
+        x = x.contiguous(memory_format=torch.channels_last)
     for _ in range(steps):
         opt.zero_grad()
         with torch.autocast(torch.device(dev).type, dtype=torch.bfloat16):
@@ -189,4 +193,10 @@ def test_bf16_working_weights_match_autocast_cpu():
     """fp32 masters + bf16 working copies == plain autocast (same roundings, fewer kernels)."""
     a = _mp_train("cpu", False)
     b = _mp_train("cpu", True)
+    torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-6)
+
+
+def test_bf16_working_weights_channels_last_cpu():
+    a = _mp_train("cpu", False, channels_last=True)
+    b = _mp_train("cpu", True, channels_last=True)
     torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-6)

@@ -116,12 +116,14 @@ def test_gather_mode_equals_accumulate_mode(overlap):
     torch.testing.assert_close(res[1], res[0], rtol=1e-5, atol=1e-6)
 
 
-def test_bf16_working_weights_match_autocast_gpu():
-    """Native path: batched bf16 refresh kernel + bf16-widening gather == plain autocast."""
+@pytest.mark.parametrize("channels_last", [False, True])
+def test_bf16_working_weights_match_autocast_gpu(channels_last):
+    """Native path: batched bf16 refresh kernel + bf16-widening gather == plain autocast
+    (channels_last: dense, non-contiguous conv masters as in bench.py)."""
     import sys, os
     sys.path.insert(0, os.path.dirname(__file__))
     from test_engine import _mp_train
 
-    a = _mp_train("cuda", False)
-    b = _mp_train("cuda", True)
+    a = _mp_train("cuda", False, channels_last=channels_last)
+    b = _mp_train("cuda", True, channels_last=channels_last)
     torch.testing.assert_close(b.cpu(), a.cpu(), rtol=1e-4, atol=1e-5)
