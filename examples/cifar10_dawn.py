@@ -22,44 +22,14 @@ import time
 
 import numpy as np
 import torch
-import torch.nn as nn
 import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from grace_amd import grace_from_params  # noqa: E402
+from grace_amd.models.resnet9 import ResNet9  # noqa: E402
 from grace_amd.parallel import DistributedOptimizer, broadcast_parameters  # noqa: E402
 from grace_amd.parallel.launch import init_distributed  # noqa: E402
-
-
-def conv_bn(cin, cout):
-    return nn.Sequential(nn.Conv2d(cin, cout, 3, padding=1, bias=False), nn.BatchNorm2d(cout), nn.ReLU(inplace=True))
-
-
-class Residual(nn.Module):
-    def __init__(self, c):
-        super().__init__()
-        self.res = nn.Sequential(conv_bn(c, c), conv_bn(c, c))
-
-    def forward(self, x):
-        return x + self.res(x)
-
-
-class ResNet9(nn.Module):
-    """cifar10-fast / DAWNBench network (reference dawn.py:26-63)."""
-
-    def __init__(self, classes=10, weight=0.125):
-        super().__init__()
-        self.net = nn.Sequential(
-            conv_bn(3, 64),
-            conv_bn(64, 128), nn.MaxPool2d(2), Residual(128),
-            conv_bn(128, 256), nn.MaxPool2d(2),
-            conv_bn(256, 512), nn.MaxPool2d(2), Residual(512),
-            nn.AdaptiveMaxPool2d(1), nn.Flatten(), nn.Linear(512, classes, bias=False))
-        self.weight = weight
-
-    def forward(self, x):
-        return self.net(x) * self.weight
 
 
 def piecewise_linear(knots, vals):
@@ -133,7 +103,9 @@ def main():
         logf.write("epoch\thours\ttrain_loss\ttrain_acc\n")
         for epoch in range(args.epochs):
             perm = torch.randperm(x.shape[0], device=dev)
-            tot_loss = tot_acc = 0.0
+            # device-side accumulation, one host read per epoch (reference StatsLogger, core.py:180-192)
+            tot_loss = torch.zeros((), device=dev)
+            tot_acc = torch.zeros((), device=dev)
             model.train()
             for s in range(steps_per_epoch):
                 lr = lr_sched(epoch + s / steps_per_epoch) / args.batch_size
@@ -153,9 +125,10 @@ def main():
                     for n, p in zip(names, model.parameters()):
                         p.grad.copy_(grc.step(p.grad, n))
                 opt.step()
-                tot_loss += loss.item()
-                tot_acc += (out.argmax(1) == y[idx]).sum().item()
+                tot_loss += loss.detach().float()
+                tot_acc += (out.argmax(1) == y[idx]).sum()
             n_seen = steps_per_epoch * bs
+            tot_loss, tot_acc = float(tot_loss), float(tot_acc)
             hours = (time.time() - t_start) / 3600
             if rank == 0:
                 print(f"epoch {epoch + 1:3d}  loss {tot_loss / n_seen:.4f}  acc {tot_acc / n_seen:.4f}  "

@@ -89,6 +89,12 @@ WORKLOADS: Dict[str, Workload] = {
         "resnet18_cifar_none", "resnet18_cifar", 128, "images",
         {"compressor": "none", "memory": "none", "communicator": "allreduce"},
         _img_batch(32, 10), _img_loss, channels_last=True),
+    # the reference's only published number: cifar10-fast ResNet-9, batch 512, 24 epochs
+    # (examples/dist/CIFAR10-dawndist/README.md:17, 24-26) -- uncompressed like dawn.py:124-127
+    "resnet9_dawn": Workload(
+        "resnet9_dawn", "resnet9", 512, "images",
+        {"compressor": "none", "memory": "none", "communicator": "allreduce"},
+        _img_batch(32, 10), _img_loss, channels_last=True),
     "vgg16_powersgd": Workload(
         "vgg16_powersgd", "vgg16", 32, "images",
         {"compressor": "powersgd", "compress_rank": 4, "memory": "powersgd", "communicator": "allreduce"},
