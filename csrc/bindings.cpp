@@ -605,6 +605,7 @@ std::string build_info() {
 }  // namespace
 
 void grace_bind_comm(py::module& m);  // csrc/comm/rccl_comm.cpp
+void grace_bind_nn(py::module& m);    // csrc/nn_bindings.cpp
 
 // ------------------------------------------------------------------------------ Adaq
 void adaq_sample(const Tensor& x, const Tensor& seg_off, const Tensor& samp_off, int64_t seed,
@@ -731,6 +732,7 @@ void inceptionn_decode(const Tensor& ptrs, const Tensor& code_ptrs, int64_t n_ra
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   grace_bind_comm(m);
+  grace_bind_nn(m);
   m.doc() = "grace_amd native CDNA4 kernels and RCCL runtime";
   m.def("build_info", &build_info);
   m.def("topk_select", &topk_select);

@@ -1,0 +1,108 @@
+// Python bindings for the fused network-layer kernels (csrc/kernels/bnact.hip).  Kept out of
+// bindings.cpp so the codec bindings do not recompile when these change.
+#include <torch/extension.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+
+#include "grace_kernels.h"
+
+namespace {
+
+using at::Tensor;
+inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+using DevGuard = c10::hip::HIPGuardMasqueradingAsCUDA;
+
+// [M, C] row-major view of an NHWC (channels_last) or 2-D activation
+void check_rows(const Tensor& t, const char* what, int64_t* M, int64_t* C) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16, what, " must be a bf16 GPU tensor");
+  if (t.dim() == 4) {
+    TORCH_CHECK(t.is_contiguous(at::MemoryFormat::ChannelsLast), what, " must be channels_last");
+    *C = t.size(1);
+  } else {
+    TORCH_CHECK(t.dim() == 2 && t.is_contiguous(), what, " must be [M, C] contiguous or NHWC");
+    *C = t.size(1);
+  }
+  *M = t.numel() / std::max<int64_t>(*C, 1);
+  TORCH_CHECK(*C % 8 == 0 && *C <= 2048 && *C > 0, what, ": channels must be a multiple of 8 and <= 2048");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0, what, " must be 16-byte aligned");
+}
+
+void same_layout(const Tensor& a, const Tensor& b, const char* what) {
+  TORCH_CHECK(a.sizes() == b.sizes() && a.strides() == b.strides() && b.scalar_type() == at::kBFloat16 &&
+                  (reinterpret_cast<uintptr_t>(b.data_ptr()) & 15) == 0,
+              what, " must match the input's shape, strides and dtype");
+}
+
+const float* opt_f32(const c10::optional<Tensor>& t, int64_t C, const char* what) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == C, what,
+              " must be a contiguous fp32 [C] GPU tensor");
+  return t->data_ptr<float>();
+}
+
+// returns (y, save[4C] = mean, invstd, scale, shift)
+std::vector<Tensor> bn_act_fwd(const Tensor& x, const c10::optional<Tensor>& res, const c10::optional<Tensor>& weight,
+                               const c10::optional<Tensor>& bias, const c10::optional<Tensor>& running_mean,
+                               const c10::optional<Tensor>& running_var, const c10::optional<Tensor>& nbt,
+                               double momentum, double eps, bool relu) {
+  int64_t M, C;
+  check_rows(x, "x", &M, &C);
+  const bool has_res = res.has_value() && res->defined();
+  if (has_res) same_layout(x, *res, "residual");
+  float* rm = const_cast<float*>(opt_f32(running_mean, C, "running_mean"));
+  float* rv = const_cast<float*>(opt_f32(running_var, C, "running_var"));
+  TORCH_CHECK((rm == nullptr) == (rv == nullptr), "running_mean / running_var: both or neither");
+  int64_t* nb = nullptr;
+  if (nbt.has_value() && nbt->defined()) {
+    TORCH_CHECK(nbt->is_cuda() && nbt->scalar_type() == at::kLong && nbt->numel() == 1, "num_batches_tracked");
+    nb = nbt->data_ptr<int64_t>();
+  }
+  DevGuard guard(x.device());
+  Tensor y = at::empty_like(x);
+  auto f32 = x.options().dtype(at::kFloat);
+  Tensor save = at::empty({4 * C}, f32);
+  Tensor part = at::empty({grace::bn_workspace_floats(M, (int)C)}, f32);
+  grace::bn_act_forward(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                        has_res ? reinterpret_cast<const uint16_t*>(res->data_ptr()) : nullptr, M, (int)C,
+                        opt_f32(weight, C, "weight"), opt_f32(bias, C, "bias"), rm, rv, nb, (float)momentum,
+                        (float)eps, relu, save.data_ptr<float>(), part.data_ptr<float>(),
+                        reinterpret_cast<uint16_t*>(y.data_ptr()), cur_stream());
+  return {y, save};
+}
+
+// returns (dx, dres (undefined unless want_dres), dweight, dbias)
+std::vector<Tensor> bn_act_bwd(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& y,
+                               const c10::optional<Tensor>& weight, const Tensor& save, bool relu, bool want_dres,
+                               bool want_dweight) {
+  int64_t M, C;
+  check_rows(x, "x", &M, &C);
+  same_layout(x, dy, "grad_output");
+  if (relu) {
+    TORCH_CHECK(y.has_value() && y->defined(), "relu backward needs the forward output");
+    same_layout(x, *y, "output");
+  }
+  TORCH_CHECK(save.is_cuda() && save.scalar_type() == at::kFloat && save.numel() == 4 * C, "save");
+  DevGuard guard(x.device());
+  auto f32 = x.options().dtype(at::kFloat);
+  Tensor dx = at::empty_like(x);
+  Tensor dres = want_dres ? at::empty_like(x) : Tensor();
+  Tensor dg = want_dweight ? at::empty({C}, f32) : Tensor();
+  Tensor db = want_dweight ? at::empty({C}, f32) : Tensor();
+  Tensor coef = at::empty({3 * C}, f32);
+  Tensor part = at::empty({grace::bn_workspace_floats(M, (int)C)}, f32);
+  grace::bn_act_backward(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
+                         reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                         relu ? reinterpret_cast<const uint16_t*>(y->data_ptr()) : nullptr, M, (int)C,
+                         opt_f32(weight, C, "weight"), save.data_ptr<float>(), relu,
+                         want_dweight ? dg.data_ptr<float>() : nullptr, want_dweight ? db.data_ptr<float>() : nullptr,
+                         coef.data_ptr<float>(), part.data_ptr<float>(), reinterpret_cast<uint16_t*>(dx.data_ptr()),
+                         want_dres ? reinterpret_cast<uint16_t*>(dres.data_ptr()) : nullptr, cur_stream());
+  return {dx, dres, dg, db};
+}
+
+}  // namespace
+
+void grace_bind_nn(py::module& m) {
+  m.def("bn_act_fwd", &bn_act_fwd);
+  m.def("bn_act_bwd", &bn_act_bwd);
+}

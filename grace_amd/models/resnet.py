@@ -14,6 +14,8 @@ from typing import List, Type, Union
 import torch
 import torch.nn as nn
 
+from ..ops.bnact import BatchNormAct2d
+
 
 def _conv3x3(cin, cout, stride=1):
     return nn.Conv2d(cin, cout, 3, stride=stride, padding=1, bias=False)
@@ -29,17 +31,15 @@ class BasicBlock(nn.Module):
     def __init__(self, cin, planes, stride=1, down=None):
         super().__init__()
         self.conv1 = _conv3x3(cin, planes, stride)
-        self.bn1 = nn.BatchNorm2d(planes)
+        self.bn1 = BatchNormAct2d(planes, relu=True)
         self.conv2 = _conv3x3(planes, planes)
-        self.bn2 = nn.BatchNorm2d(planes)
-        self.relu = nn.ReLU(inplace=True)
+        self.bn2 = BatchNormAct2d(planes, relu=True)  # relu(bn2(.) + identity), one fused op
         self.downsample = down
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
-        y = self.relu(self.bn1(self.conv1(x)))
-        y = self.bn2(self.conv2(y))
-        return self.relu(y + idt)
+        y = self.bn1(self.conv1(x))
+        return self.bn2(self.conv2(y), idt)
 
 
 class Bottleneck(nn.Module):
@@ -49,20 +49,18 @@ class Bottleneck(nn.Module):
         super().__init__()
         width = planes
         self.conv1 = _conv1x1(cin, width)
-        self.bn1 = nn.BatchNorm2d(width)
+        self.bn1 = BatchNormAct2d(width, relu=True)
         self.conv2 = _conv3x3(width, width, stride)  # stride on the 3x3 (v1.5, as torchvision)
-        self.bn2 = nn.BatchNorm2d(width)
+        self.bn2 = BatchNormAct2d(width, relu=True)
         self.conv3 = _conv1x1(width, planes * 4)
-        self.bn3 = nn.BatchNorm2d(planes * 4)
-        self.relu = nn.ReLU(inplace=True)
+        self.bn3 = BatchNormAct2d(planes * 4, relu=True)  # relu(bn3(.) + identity), one fused op
         self.downsample = down
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
-        y = self.relu(self.bn1(self.conv1(x)))
-        y = self.relu(self.bn2(self.conv2(y)))
-        y = self.bn3(self.conv3(y))
-        return self.relu(y + idt)
+        y = self.bn1(self.conv1(x))
+        y = self.bn2(self.conv2(y))
+        return self.bn3(self.conv3(y), idt)
 
 
 class ResNet(nn.Module):
@@ -76,8 +74,7 @@ class ResNet(nn.Module):
         else:
             self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
             self.maxpool = nn.MaxPool2d(3, 2, 1)
-        self.bn1 = nn.BatchNorm2d(64)
-        self.relu = nn.ReLU(inplace=True)
+        self.bn1 = BatchNormAct2d(64, relu=True)
         self.layer1 = self._make(block, 64, layers[0])
         self.layer2 = self._make(block, 128, layers[1], 2)
         self.layer3 = self._make(block, 256, layers[2], 2)
@@ -95,14 +92,14 @@ class ResNet(nn.Module):
         down = None
         if stride != 1 or self.inplanes != planes * block.expansion:
             down = nn.Sequential(_conv1x1(self.inplanes, planes * block.expansion, stride),
-                                 nn.BatchNorm2d(planes * block.expansion))
+                                 BatchNormAct2d(planes * block.expansion))
         blocks = [block(self.inplanes, planes, stride, down)]
         self.inplanes = planes * block.expansion
         blocks += [block(self.inplanes, planes) for _ in range(1, n)]
         return nn.Sequential(*blocks)
 
     def forward(self, x):
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.maxpool(self.bn1(self.conv1(x)))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         return self.fc(torch.flatten(self.avgpool(x), 1))
 

@@ -8,9 +8,12 @@ examples/dist/CIFAR10-dawndist/README.md:17, 24-26).
 """
 import torch.nn as nn
 
+from ..ops.bnact import BatchNormAct2d
+
 
 def conv_bn(cin, cout):
-    return nn.Sequential(nn.Conv2d(cin, cout, 3, padding=1, bias=False), nn.BatchNorm2d(cout), nn.ReLU(inplace=True))
+    # conv -> BN -> ReLU; BN+ReLU is one fused op (grace_amd/ops/bnact.py)
+    return nn.Sequential(nn.Conv2d(cin, cout, 3, padding=1, bias=False), BatchNormAct2d(cout, relu=True))
 
 
 class Residual(nn.Module):

@@ -1,0 +1,94 @@
+"""Fused training-mode BatchNorm (+ residual add) (+ ReLU) -- ``BatchNormAct2d``.
+
+A drop-in ``nn.BatchNorm2d`` subclass (same parameters, buffers and state_dict keys) whose
+``forward(x, residual=None)`` computes ``act(bn(x) + residual)``.  On a GPU with bf16
+channels_last activations (the autocast + channels_last training setup of bench.py) it runs the
+four CDNA4 kernels of ``csrc/kernels/bnact.hip`` per layer (statistics with the running-stat /
+``num_batches_tracked`` update folded in, apply, backward reduce, backward dx) instead of
+~11 MIOpen + elementwise launches; everywhere else (CPU, fp32, eval mode, odd channel counts)
+it is exactly ``relu(F.batch_norm(x) + residual)``.
+
+Numerics: statistics and the affine are fp32 (fp64 fold of the per-block partial sums), the
+output is rounded to bf16 once (the unfused bf16 path rounds after BN, after the add and after
+the ReLU); the ReLU mask is taken from the bf16 output, as ``threshold_backward`` does.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _native
+
+
+def _fusable(x: torch.Tensor, bn: nn.BatchNorm2d, residual: Optional[torch.Tensor]) -> bool:
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and _native.native_on(x.device)):
+        return False
+    if x.dim() != 4 or not x.is_contiguous(memory_format=torch.channels_last):
+        return False
+    c = x.shape[1]
+    if c % 8 or c > 2048 or x.numel() == 0 or x.data_ptr() % 16:
+        return False
+    if residual is not None and (residual.shape != x.shape or residual.stride() != x.stride()
+                                 or residual.dtype != x.dtype or residual.data_ptr() % 16):
+        return False
+    # running statistics: momentum=None (cumulative average) needs the host-side count
+    if bn.track_running_stats and bn.momentum is None:
+        return False
+    return True
+
+
+class _BNActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, residual, weight, bias, running_mean, running_var, nbt, momentum, eps, relu):
+        y, save = _native.lib().bn_act_fwd(x, residual, weight, bias, running_mean, running_var, nbt,
+                                           float(momentum), float(eps), bool(relu))
+        ctx.relu = bool(relu)
+        ctx.has_res = residual is not None
+        ctx.save_for_backward(x, y if relu else None, weight, save)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, weight, save = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        if dy.data_ptr() % 16:
+            dy = dy.clone(memory_format=torch.channels_last)
+        want_w = weight is not None and ctx.needs_input_grad[2]
+        dx, dres, dw, db = _native.lib().bn_act_bwd(dy, x, y, weight, save, ctx.relu,
+                                                    ctx.has_res and ctx.needs_input_grad[1], want_w)
+        return (dx, dres if ctx.has_res and ctx.needs_input_grad[1] else None,
+                dw if want_w else None, db if want_w and ctx.needs_input_grad[3] else None,
+                None, None, None, None, None, None)
+
+
+def bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, residual: Optional[torch.Tensor] = None,
+           relu: bool = False) -> torch.Tensor:
+    """``act(bn(x) + residual)`` with the module's parameters and running statistics."""
+    training = bn.training or not bn.track_running_stats
+    if training and _fusable(x, bn, residual):
+        track = bn.training and bn.track_running_stats
+        return _BNActFn.apply(x, residual, bn.weight, bn.bias,
+                              bn.running_mean if track else None, bn.running_var if track else None,
+                              bn.num_batches_tracked if track else None,
+                              bn.momentum if bn.momentum is not None else 0.0, bn.eps, relu)
+    y = nn.BatchNorm2d.forward(bn, x)
+    if residual is not None:
+        y = y + residual
+    return F.relu(y) if relu else y
+
+
+class BatchNormAct2d(nn.BatchNorm2d):
+    """``nn.BatchNorm2d`` with an optional fused residual add and ReLU: ``forward(x, residual=None)``."""
+
+    def __init__(self, num_features: int, relu: bool = False, **kw):
+        super().__init__(num_features, **kw)
+        self.relu = relu
+
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+        return bn_act(x, self, residual, self.relu)
+
+    def extra_repr(self) -> str:
+        return super().extra_repr() + (", relu=True" if self.relu else "")

@@ -1,0 +1,129 @@
+"""Fused BN(+residual)(+ReLU) HIP kernels (csrc/kernels/bnact.hip) vs a plain PyTorch fp32
+reference of the same op."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from grace_amd.ops import _native
+from grace_amd.ops.bnact import BatchNormAct2d, _fusable
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _case(n, c, h, w, relu, with_res, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    x = (torch.randn(n, c, h, w, generator=g) * 2 + 0.5).to(DEV, torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last)
+    res = None
+    if with_res:
+        res = torch.randn(n, c, h, w, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(n, c, h, w, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    m = BatchNormAct2d(c, relu=relu).to(DEV)
+    with torch.no_grad():
+        m.weight.copy_(torch.rand(c, generator=g) + 0.5)
+        m.bias.copy_(torch.randn(c, generator=g) * 0.1)
+    return m, x, res, dy
+
+
+def _reference(m, x, res, dy, relu):
+    xf = x.detach().float().requires_grad_(True)
+    rf = res.detach().float().requires_grad_(True) if res is not None else None
+    w = m.weight.detach().clone().requires_grad_(True)
+    b = m.bias.detach().clone().requires_grad_(True)
+    rm = torch.zeros_like(m.running_mean)
+    rv = torch.ones_like(m.running_var)
+    y = F.batch_norm(xf, rm, rv, w, b, True, m.momentum, m.eps)
+    if rf is not None:
+        y = y + rf
+    if relu:
+        y = F.relu(y)
+    y.backward(dy.float())
+    return y.detach(), xf.grad, (rf.grad if rf is not None else None), w.grad, b.grad, rm, rv
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 9, 9), (2, 256, 7, 5), (3, 2048, 3, 3), (1, 8, 2, 3), (8, 96, 4, 4),
+                                   (32, 128, 28, 28)])
+@pytest.mark.parametrize("relu,with_res", [(False, False), (True, False), (True, True), (False, True)])
+def test_bnact_matches_fp32_reference(shape, relu, with_res):
+    assert _native.available()
+    m, x, res, dy = _case(*shape, relu, with_res)
+    assert _fusable(x, m, res)
+    xx = x.clone().requires_grad_(True)
+    rr = res.clone().requires_grad_(True) if res is not None else None
+    y = m(xx, rr)
+    y.backward(dy)
+    torch.cuda.synchronize()
+    y0, dx0, dr0, dw0, db0, rm0, rv0 = _reference(m, x, res, dy, relu)
+    assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=torch.channels_last)
+    # one bf16 rounding of the output
+    torch.testing.assert_close(y.float(), y0, rtol=1e-2, atol=2e-2)
+    torch.testing.assert_close(m.running_mean, rm0, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(m.running_var, rv0, rtol=1e-4, atol=1e-5)
+    assert int(m.num_batches_tracked) == 1
+    M = x.numel() // x.shape[1]
+    # parameter grads are fp32 sums over M rows of bf16 data; the ReLU mask comes from the bf16
+    # output, so an element whose fp32 pre-activation sits within bf16 rounding of 0 may differ
+    scale = dy.float().abs().mean().item() * M ** 0.5
+    torch.testing.assert_close(m.bias.grad, db0, rtol=2e-3, atol=2e-2 * scale)
+    torch.testing.assert_close(m.weight.grad, dw0, rtol=2e-3, atol=2e-2 * scale)
+    torch.testing.assert_close(xx.grad.float(), dx0, rtol=2e-2, atol=3e-2 * dx0.abs().max().item() + 1e-3)
+    if res is not None:
+        torch.testing.assert_close(rr.grad.float(), dr0, rtol=1e-2, atol=1e-2)
+
+
+def test_bnact_graph_replay():
+    """Arrival counters re-arm in-kernel: repeated graph replays give the eager result."""
+    m, x, res, dy = _case(8, 256, 14, 14, True, True, seed=3)
+    xs = x.clone().requires_grad_(True)
+    out = {}
+
+    def step():
+        xs.grad = None
+        y = m(xs, res)
+        y.backward(dy)
+        return y
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            y_e = step()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    dx_e = xs.grad.clone()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out["y"] = step()
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out["y"], y_e, rtol=0, atol=0)
+    torch.testing.assert_close(xs.grad, dx_e, rtol=0, atol=0)
+    assert int(m.num_batches_tracked) == 2 + 3  # warmup + replays (the capture itself runs nothing)
+
+
+def test_resnet50_fused_step_matches_unfused():
+    """One ResNet-50 (batch 4) forward/backward with the fused BN path vs the unfused one."""
+    import os
+    from grace_amd.models import resnet50
+
+    torch.manual_seed(0)
+    model = resnet50().to(DEV).to(memory_format=torch.channels_last)
+    x = torch.randn(4, 3, 64, 64, device=DEV).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (4,), device=DEV)
+    res = []
+    for force in ("0", "1"):
+        os.environ["GRACE_AMD_FORCE_TORCH"] = force
+        try:
+            model.zero_grad(set_to_none=True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = F.cross_entropy(model(x), y)
+            loss.backward()
+        finally:
+            os.environ["GRACE_AMD_FORCE_TORCH"] = "0"
+        res.append((loss.detach().float(), torch.cat([p.grad.float().reshape(-1) for p in model.parameters()])))
+    (l0, g0), (l1, g1) = res
+    torch.testing.assert_close(l0, l1, rtol=2e-2, atol=2e-2)
+    cos = F.cosine_similarity(g0, g1, dim=0).item()
+    assert cos > 0.99, cos
