@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""Per-shape timing of the fused BN(+add)(+ReLU) kernels vs the stock MIOpen + elementwise path,
+on every BatchNorm shape of ResNet-50 at batch 32 (bf16, channels_last).
+
+    python benchmarks/bnact_bench.py [--batch 32] [--iters 50]
+
+Columns: shape, forward / backward microseconds for fused and stock, and the fused kernels'
+effective HBM rate (bytes the fused path must move / time).
+"""
+import argparse
+import os
+import sys
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from grace_amd.ops.bnact import BatchNormAct2d  # noqa: E402
+
+# (C, H, W, relu, residual, count) of ResNet-50's BatchNorm layers at 224x224 input
+R50 = [(64, 112, 112, True, False, 1)]
+for (c, hw, n) in ((64, 56, 3), (128, 28, 4), (256, 14, 6), (512, 7, 3)):
+    R50 += [(c, hw, hw, True, False, 2 * n - 1), (c, hw * (2 if c > 64 else 1), hw * (2 if c > 64 else 1), True, False, 1),
+            (4 * c, hw, hw, True, True, n), (4 * c, hw, hw, False, False, 1)]
+
+
+def timed(fn, iters):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--iters", type=int, default=50)
+    a = ap.parse_args()
+    dev = "cuda"
+    tot = {"ff": 0.0, "fb": 0.0, "uf": 0.0, "ub": 0.0}
+    print(f"{'C':>5} {'H':>4} {'W':>4} relu res  cnt | fused fwd  bwd (us) | stock fwd  bwd (us) | fused GB/s fwd bwd")
+    for (c, h, w, relu, res, cnt) in R50:
+        m = BatchNormAct2d(c, relu=relu).to(dev)
+        x = torch.randn(a.batch, c, h, w, device=dev, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        r = torch.randn_like(x) if res else None
+        dy = torch.randn_like(x)
+        xg = x.clone().requires_grad_(True)
+        out = {}
+        res_t = {}
+        for force in ("0", "1"):
+            os.environ["GRACE_AMD_FORCE_TORCH"] = force
+
+            def fwd():
+                with torch.no_grad():
+                    return m(x, r)
+
+            def fb():
+                xg.grad = None
+                y = m(xg, r)
+                y.backward(dy)
+
+            tf = timed(fwd, a.iters)
+            tfb = timed(fb, a.iters)
+            res_t[force] = (tf, tfb - tf)
+        os.environ["GRACE_AMD_FORCE_TORCH"] = "0"
+        nbytes = x.numel() * 2
+        fwd_bytes = nbytes * (3 + (1 if res else 0))           # stats read, apply read+write (+res)
+        bwd_bytes = nbytes * ((3 if relu else 2) * 2 + 1 + (1 if res else 0))  # reduce + dx reads, dx (+dres) write
+        (ff, fbk), (uf, ub) = res_t["0"], res_t["1"]
+        for k, v in (("ff", ff), ("fb", fbk), ("uf", uf), ("ub", ub)):
+            tot[k] += v * cnt
+        print(f"{c:5d} {h:4d} {w:4d} {str(relu)[0]:>4} {str(res)[0]:>3} {cnt:4d} | {ff:9.1f} {fbk:5.1f} | {uf:9.1f} {ub:5.1f} | "
+              f"{fwd_bytes / ff / 1e3:8.0f} {bwd_bytes / fbk / 1e3:5.0f}")
+    print(f"ResNet-50 total per step (us): fused fwd {tot['ff']:.0f} bwd {tot['fb']:.0f} | stock fwd {tot['uf']:.0f} bwd {tot['ub']:.0f}")
+
+
+if __name__ == "__main__":
+    main()

@@ -133,13 +133,14 @@ void cast_segments_bf16(const float* const* src, uint16_t* const* dst, const int
                         hipStream_t stream);
 
 // ---------------------------------------------------------------- bnact.hip
-// fused training-mode BatchNorm (+ residual) (+ ReLU), channels_last bf16, C % 8 == 0, C <= 2048
-int64_t bn_workspace_floats(int64_t M, int C);
+// fused training-mode BatchNorm (+ residual) (+ ReLU), channels_last bf16
+bool bn_supported(int C);  // C % 8 == 0, C <= 2048, C % 256 == 0 above 256
+int64_t bn_workspace_floats(int64_t M, int C);  // `ws` size (fp32 words, 8-B aligned base)
 void bn_act_forward(const uint16_t* x, const uint16_t* res, int64_t M, int C, const float* gamma, const float* beta,
                     float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps, bool relu,
-                    float* save, float* part, uint16_t* y, hipStream_t stream);
+                    float* save, float* ws, uint16_t* y, hipStream_t stream);
 void bn_act_backward(const uint16_t* dy, const uint16_t* x, const uint16_t* y, int64_t M, int C, const float* gamma,
-                     const float* save, bool relu, float* dgamma, float* dbeta, float* coef, float* part,
+                     const float* save, bool relu, float* dgamma, float* dbeta, float* coef, float* ws,
                      uint16_t* dx, uint16_t* dres, hipStream_t stream);
 
 }  // namespace grace

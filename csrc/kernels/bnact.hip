@@ -6,18 +6,33 @@
 // dscale/dbias + final + dx, plus memsets (≈11 launches per layer, ~4.7 ms of a 9.4 ms step in
 // profiles/r1_resnet50_topk_graph_bf16w_kernels.txt).  Here a layer is 4 kernels:
 //
-//   fwd  bn_stats   : per-channel Σx, Σx² over the NHWC rows (16-B bf16 loads, fp32 sums),
-//                     per-block partials, the LAST block (agent-scope arrival counter) folds
-//                     them in fp64 and writes mean/invstd, the folded affine (scale, shift),
-//                     the running statistics and num_batches_tracked
+//   fwd  bn_stats   : per-channel Σx, Σx² (fp32 per thread, 16-B bf16 loads), one partial row
+//                     per block, folded by an in-kernel ARRIVAL TREE; the final block writes
+//                     mean/invstd, the folded affine (scale, shift), the running statistics
+//                     and num_batches_tracked
 //        bn_apply   : y = relu(x*scale + shift [+ residual]) -> bf16
-//   bwd  bn_reduce  : Σdz, Σdz·(x-mean) with dz = dy·[y>0]; last block writes dgamma, dbeta
-//                     and the 3 per-channel coefficients of dx = a·dz + b·x + c
+//   bwd  bn_reduce  : Σdz, Σdz·(x-mean) with dz = dy·[y>0]; the final block writes dgamma,
+//                     dbeta and the 3 per-channel coefficients of dx = a·dz + b·x + c
 //        bn_dx      : dx (bf16) and, for the fused residual, d(residual) = dz (bf16)
 //
-// Activations are [M = N·H·W rows, C channels] row-major (channels_last).  A thread owns 8
-// consecutive channels (one 16-B load per row); TPR = C/8 threads cover a row.  C % 8 == 0 and
-// C <= 2048 (checked on the host; other shapes use the PyTorch path).
+// Layout: activations are [M = N·H·W rows, C channels] row-major (channels_last).  The two
+// reduction kernels use a 2-D grid: blockIdx.x = chunk of rows, blockIdx.y = TILE of CT =
+// min(C, 256) channels (a thread owns 8 consecutive channels = one 16-B load per row).  Each
+// tile has its own two-level arrival tree (group finishers fold ~sqrt(#chunks) partial rows in
+// fp64, the last group finisher folds the group totals), so the serial tails stay short and
+// the large-C layers still get hundreds of blocks.  Fold order is fixed: deterministic.
+//
+// In-launch hand-offs follow the gfx950 publish/consume recipe (cdna_hip_programming.md
+// Guideline 16): partial rows are stored WRITE-THROUGH (`sc1`, relaxed agent-scope atomic
+// stores: no L2-writeback release fence), every storing wave drains (`s_waitcnt vmcnt(0)`),
+// workgroup barrier, ONE lane adds to the arrival counter; only the finishing block pays ONE
+// agent-scope acquire before its plain loads.  (Measured on MI355X: a `__threadfence()` in
+// every thread of every block made these kernels 5-10x slower than their streaming bound; a
+// flat one-block fold of 1024 partial rows, or fp64 atomics from 1024 blocks onto the same
+// 2C addresses, cost 25-130 us per launch.)
+//
+// Constraints (host-checked, other shapes use the PyTorch path): C % 8 == 0, C <= 2048, and
+// C % 256 == 0 when C > 256.
 #include "grace_common.h"
 #include "grace_kernels.h"
 
@@ -25,8 +40,11 @@ namespace grace {
 namespace {
 
 constexpr int kB = 256;           // threads per block
-constexpr int kMaxC = 2048;       // TPR <= 256
-constexpr int kPartFloats = 131072;  // cap on nblk * C (fold cost of the last block)
+constexpr int kMaxC = 2048;
+constexpr int kTileC = 256;       // channels per reduction tile (32 threads x 8 channels per row)
+constexpr int kMaxTiles = kMaxC / kTileC;
+constexpr int kMaxGroups = 64;
+constexpr int kSlotWords = kMaxTiles * (kMaxGroups + 1);
 
 struct Bf8 {
   float v[8];
@@ -55,92 +73,148 @@ __device__ __forceinline__ void store_bf8(uint16_t* p, const float* v) {
   *reinterpret_cast<uint4*>(p) = u;
 }
 
-struct Geo {
-  int C, tpr, tprp, rpi;  // channels, threads per row, pow2 >= tpr, rows per block iteration
+template <typename T>
+__device__ __forceinline__ void store_sc1(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Reduction-kernel geometry, computed on the host.
+struct Red {
+  int64_t M;           // rows
+  int C;               // channels (row stride)
+  int CT;              // channels per tile (= min(C, 256))
+  int tprp;            // pow2 >= CT/8: thread slots per row
+  int rpi;             // rows per block iteration = kB / tprp
+  int64_t rows_per_blk;
+  int nchunks;         // gridDim.x
+  int gsize, ngroups;  // arrival tree: chunks per group, groups
+  float* part;         // [tiles][nchunks][2*CT]
+  double* gpart;       // [tiles][ngroups][2*CT]
+  double* total;       // [tiles][2*CT]
+  unsigned* cnt;       // [tiles][kMaxGroups + 1]: group counters, top counter last
 };
 
-__device__ __forceinline__ Geo geo(int C) {
-  Geo g;
-  g.C = C;
-  g.tpr = C >> 3;
-  g.tprp = 1;
-  while (g.tprp < g.tpr) g.tprp <<= 1;
-  g.rpi = kB / g.tprp;
-  return g;
+// Column fold of `rows` rows (stride C2 elements) for the columns this thread owns, fp64,
+// fixed order.  Thread t owns column t % C2 and rows r ≡ t / C2 (mod P) when C2 <= kB
+// (P = kB / C2 row phases, combined through LDS by the caller), else columns t and t + kB.
+template <typename T>
+__device__ __forceinline__ void fold_cols(const T* src, int rows, int C2, double (&acc)[2]) {
+  acc[0] = acc[1] = 0.0;
+  if (C2 <= kB) {
+    const int P = kB / C2, p = threadIdx.x / C2, c = threadIdx.x % C2;
+    if (p >= P) return;
+    int r = p;
+    for (; r + 7 * P < rows; r += 8 * P) {  // 8 independent loads in flight
+      T v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = src[(size_t)(r + u * P) * C2 + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc[0] += (double)v[u];
+    }
+    for (; r < rows; r += P) acc[0] += (double)src[(size_t)r * C2 + c];
+  } else {  // C2 == 2 * kB (CT = 256)
+    const int c = threadIdx.x;
+    int r = 0;
+    for (; r + 3 < rows; r += 4) {
+      T v[4][2];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        v[u][0] = src[(size_t)(r + u) * C2 + c];
+        v[u][1] = src[(size_t)(r + u) * C2 + c + kB];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        acc[0] += (double)v[u][0];
+        acc[1] += (double)v[u][1];
+      }
+    }
+    for (; r < rows; ++r) {
+      acc[0] += (double)src[(size_t)r * C2 + c];
+      acc[1] += (double)src[(size_t)r * C2 + c + kB];
+    }
+  }
 }
 
-// Block-level column reduction of two 8-wide per-thread accumulators into part[blk][2C]
-// (first C: quantity A, next C: quantity B), then the arrival counter.  Returns true in every
-// thread of the last-arriving block.
-__device__ bool block_partials_and_arrive(const Geo& g, const float* a, const float* b, float* part,
-                                          unsigned* counter) {
-  __shared__ float sa[kB * 8];
-  __shared__ float sb[kB * 8];
-  __shared__ int last;
-  const int cg = threadIdx.x % g.tprp, rs = threadIdx.x / g.tprp;
-  if (cg < g.tpr) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      sa[rs * g.C + cg * 8 + j] = a[j];
-      sb[rs * g.C + cg * 8 + j] = b[j];
+// Fold + combine the row phases; calls put(col, value) once per column (all threads enter).
+template <typename T, typename Put>
+__device__ __forceinline__ void fold_block(const T* src, int rows, int C2, double* lds, Put put) {
+  double acc[2];
+  fold_cols(src, rows, C2, acc);
+  if (C2 <= kB) {
+    const int P = kB / C2;
+    lds[threadIdx.x] = acc[0];
+    __syncthreads();
+    if (threadIdx.x < C2) {
+      double v = lds[threadIdx.x];
+      for (int i = 1; i < P; ++i) v += lds[i * C2 + threadIdx.x];
+      put(threadIdx.x, v);
     }
+    __syncthreads();
+  } else {
+    put(threadIdx.x, acc[0]);
+    put(threadIdx.x + kB, acc[1]);
   }
-  __syncthreads();
-  float* pb = part + (size_t)blockIdx.x * 2 * g.C;
-  for (int c = threadIdx.x; c < g.C; c += kB) {
-    float x = 0.f, y = 0.f;
-    for (int i = 0; i < g.rpi; ++i) {
-      x += sa[i * g.C + c];
-      y += sb[i * g.C + c];
-    }
-    pb[c] = x;
-    pb[g.C + c] = y;
-  }
-  __threadfence();  // partials visible at agent scope before this block's arrival
+}
+
+// Every wave has drained its sc1 stores -> barrier -> one relaxed agent add.  True in every
+// thread of the block whose add completed the count; that block is acquired (one lane's agent
+// acquire + drain, then the barrier) before its plain loads.
+__device__ __forceinline__ bool arrive(unsigned* counter, unsigned expected_last) {
+  __shared__ int flag;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    last = (prev == gridDim.x - 1);
+    const unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag = (prev == expected_last);
+    if (flag) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   }
   __syncthreads();
-  if (last) __threadfence();  // acquire side for the other threads of the last block
-  return last != 0;
+  return flag != 0;
 }
 
-// Last block: fold part[nblk][2C] into fp64 totals.  Calls fn(c, A, B) once per channel.
-template <typename Fn>
-__device__ void fold_partials(int C, int nblk, const float* part, Fn fn) {
-  __shared__ double fa[kB];
-  __shared__ double fb[kB];
-  if (C >= kB) {
-    for (int c = threadIdx.x; c < C; c += kB) {
-      double x = 0.0, y = 0.0;
-      for (int b = 0; b < nblk; ++b) {
-        x += part[(size_t)b * 2 * C + c];
-        y += part[(size_t)b * 2 * C + C + c];
-      }
-      fn(c, x, y);
-    }
-  } else {
-    const int R = kB / C;  // threads per channel
-    const int c = threadIdx.x % C, r = threadIdx.x / C;
-    double x = 0.0, y = 0.0;
-    if (r < R)
-      for (int b = r; b < nblk; b += R) {
-        x += part[(size_t)b * 2 * C + c];
-        y += part[(size_t)b * 2 * C + C + c];
-      }
-    fa[threadIdx.x] = x;
-    fb[threadIdx.x] = y;
-    __syncthreads();
-    if (threadIdx.x < C) {
-      for (int i = 1; i < R; ++i) {
-        x += fa[i * C + c];
-        y += fb[i * C + c];
-      }
-      fn(c, x, y);
+// Per-thread 8-channel accumulators -> this block's partial row -> the tile's arrival tree.
+// True in every thread of the tile's final block; totals then in total[tile][0..2CT).
+__device__ bool block_reduce_tree(const Red& R, const float* a, const float* b) {
+  __shared__ float sa[kB * 8];
+  __shared__ float sb[kB * 8];
+  __shared__ double lds[kB];
+  const int CT = R.CT, C2 = 2 * CT, tile = blockIdx.y;
+  const int cg = threadIdx.x % R.tprp, rs = threadIdx.x / R.tprp;
+  if (cg < CT / 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sa[rs * CT + cg * 8 + j] = a[j];
+      sb[rs * CT + cg * 8 + j] = b[j];
     }
   }
+  __syncthreads();
+  float* part = R.part + (size_t)tile * R.nchunks * C2;
+  float* pb = part + (size_t)blockIdx.x * C2;
+  for (int c = threadIdx.x; c < CT; c += kB) {
+    float x = 0.f, y = 0.f;
+    for (int i = 0; i < R.rpi; ++i) {
+      x += sa[i * CT + c];
+      y += sb[i * CT + c];
+    }
+    store_sc1(pb + c, x);
+    store_sc1(pb + CT + c, y);
+  }
+  unsigned* cnt = R.cnt + tile * (kMaxGroups + 1);
+  const int grp = blockIdx.x / R.gsize, g0 = grp * R.gsize;
+  const int grows = min(R.nchunks - g0, R.gsize);
+  if (!arrive(cnt + grp, (unsigned)grows - 1)) return false;
+  double* gpart = R.gpart + (size_t)tile * R.ngroups * C2;
+  fold_block(part + (size_t)g0 * C2, grows, C2, lds,
+             [&](int c, double v) { store_sc1(gpart + (size_t)grp * C2 + c, v); });
+  if (!arrive(cnt + kMaxGroups, (unsigned)R.ngroups - 1)) return false;
+  double* total = R.total + (size_t)tile * C2;
+  fold_block(gpart, R.ngroups, C2, lds, [&](int c, double v) { total[c] = v; });
+  __syncthreads();
+  for (int i = threadIdx.x; i <= kMaxGroups; i += kB) cnt[i] = 0;  // re-arm (visible at kernel end)
+  return true;
 }
 
 struct StatsOut {
@@ -153,23 +227,29 @@ struct StatsOut {
   float* save;          // [4C]: mean, invstd, scale, shift
 };
 
-__global__ __launch_bounds__(kB) void bn_stats_kernel(const uint16_t* __restrict__ x, int64_t M, int C,
-                                                      int64_t rows_per_blk, float* __restrict__ part,
-                                                      unsigned* counter, StatsOut o) {
-  const Geo g = geo(C);
-  const int cg = threadIdx.x % g.tprp, rs = threadIdx.x / g.tprp;
+// Row loop shared by the two reduction kernels: body(element_offset, row_step, n) for this
+// thread's rows of the block's chunk, 4 rows per call (independent loads in flight), then 1.
+template <typename Body>
+__device__ __forceinline__ void for_rows(const Red& R, Body body) {
+  const int cg = threadIdx.x % R.tprp, rs = threadIdx.x / R.tprp;
+  if (cg >= R.CT / 8) return;
+  const int64_t r0 = (int64_t)blockIdx.x * R.rows_per_blk;
+  const int64_t r1 = min(R.M, r0 + R.rows_per_blk);
+  const int64_t col = (int64_t)blockIdx.y * R.CT + cg * 8;
+  int64_t r = r0 + rs;
+  for (; r + 3 * R.rpi < r1; r += 4 * R.rpi) body(r * R.C + col, R.rpi * (int64_t)R.C, 4);
+  for (; r < r1; r += R.rpi) body(r * R.C + col, (int64_t)0, 1);
+}
+
+__global__ __launch_bounds__(kB) void bn_stats_kernel(const uint16_t* __restrict__ x, Red R, StatsOut o) {
   float s[8], q[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
-  const int64_t r0 = (int64_t)blockIdx.x * rows_per_blk;
-  const int64_t r1 = min(M, r0 + rows_per_blk);
-  if (cg < g.tpr) {
-    const uint16_t* base = x + cg * 8;
-    int64_t r = r0 + rs;
-    for (; r + 3 * g.rpi < r1; r += 4 * g.rpi) {  // 4 independent 16-B loads in flight
+  for_rows(R, [&](int64_t e, int64_t step, int n) {
+    if (n == 4) {
       Bf8 v[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = load_bf8(base + (r + u * g.rpi) * C);
+      for (int u = 0; u < 4; ++u) v[u] = load_bf8(x + e + u * step);
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
@@ -177,22 +257,24 @@ __global__ __launch_bounds__(kB) void bn_stats_kernel(const uint16_t* __restrict
           s[j] += v[u].v[j];
           q[j] = fmaf(v[u].v[j], v[u].v[j], q[j]);
         }
-    }
-    for (; r < r1; r += g.rpi) {
-      const Bf8 v = load_bf8(base + r * C);
+    } else {
+      const Bf8 v = load_bf8(x + e);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         s[j] += v.v[j];
         q[j] = fmaf(v.v[j], v.v[j], q[j]);
       }
     }
-  }
-  if (!block_partials_and_arrive(g, s, q, part, counter)) return;
-  const double inv_m = 1.0 / (double)M;
-  const double unbias = M > 1 ? (double)M / (double)(M - 1) : 1.0;
-  fold_partials(C, gridDim.x, part, [&](int c, double S, double Q) {
-    const double mean = S * inv_m;
-    const double var = fmax(Q * inv_m - mean * mean, 0.0);
+  });
+  if (!block_reduce_tree(R, s, q)) return;
+  const int CT = R.CT, C = R.C;
+  const double* total = R.total + (size_t)blockIdx.y * 2 * CT;
+  const double inv_m = 1.0 / (double)R.M;
+  const double unbias = R.M > 1 ? (double)R.M / (double)(R.M - 1) : 1.0;
+  for (int cl = threadIdx.x; cl < CT; cl += kB) {
+    const int c = blockIdx.y * CT + cl;
+    const double mean = total[cl] * inv_m;
+    const double var = fmax(total[CT + cl] * inv_m - mean * mean, 0.0);
     const float invstd = (float)(1.0 / sqrt(var + (double)o.eps));
     const float ga = o.gamma ? o.gamma[c] : 1.f;
     const float be = o.beta ? o.beta[c] : 0.f;
@@ -205,11 +287,8 @@ __global__ __launch_bounds__(kB) void bn_stats_kernel(const uint16_t* __restrict
       o.running_mean[c] = (1.f - o.momentum) * o.running_mean[c] + o.momentum * (float)mean;
       o.running_var[c] = (1.f - o.momentum) * o.running_var[c] + o.momentum * (float)(var * unbias);
     }
-  });
-  if (threadIdx.x == 0) {
-    if (o.nbt) *o.nbt += 1;
-    *counter = 0;  // re-arm for the next launch (graph replays reuse the slot)
   }
+  if (threadIdx.x == 0 && blockIdx.y == 0 && o.nbt) *o.nbt += 1;
 }
 
 // y = act(x*scale + shift [+ res]); scale/shift = save[2C..4C)
@@ -256,58 +335,51 @@ struct GradOut {
 
 template <bool RELU>
 __global__ __launch_bounds__(kB) void bn_reduce_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
-                                                       const uint16_t* __restrict__ y, int64_t M, int C,
-                                                       int64_t rows_per_blk, float* __restrict__ part,
-                                                       unsigned* counter, GradOut o) {
-  const Geo g = geo(C);
-  const int cg = threadIdx.x % g.tprp, rs = threadIdx.x / g.tprp;
+                                                       const uint16_t* __restrict__ y, Red R, GradOut o) {
   float s1[8], s2[8], mu[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
-  const int64_t r0 = (int64_t)blockIdx.x * rows_per_blk;
-  const int64_t r1 = min(M, r0 + rows_per_blk);
-  if (cg < g.tpr) {
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = mu[j] = 0.f;
+  {
+    const int cg = threadIdx.x % R.tprp;
+    if (cg < R.CT / 8) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) mu[j] = o.save[cg * 8 + j];
-    const int64_t off = cg * 8;
-    int64_t r = r0 + rs;
-    for (; r + g.rpi < r1; r += 2 * g.rpi) {
-      Bf8 d[2], v[2], w[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int64_t e = (r + u * g.rpi) * C + off;
-        d[u] = load_bf8(dy + e);
-        v[u] = load_bf8(x + e);
-        if constexpr (RELU) w[u] = load_bf8(y + e);
-      }
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float dz = d[u].v[j];
-          if constexpr (RELU) dz = w[u].v[j] > 0.f ? dz : 0.f;
-          s1[j] += dz;
-          s2[j] = fmaf(dz, v[u].v[j] - mu[j], s2[j]);
-        }
-    }
-    for (; r < r1; r += g.rpi) {
-      const int64_t e = r * C + off;
-      const Bf8 d = load_bf8(dy + e);
-      const Bf8 v = load_bf8(x + e);
-      Bf8 w;
-      if constexpr (RELU) w = load_bf8(y + e);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float dz = d.v[j];
-        if constexpr (RELU) dz = w.v[j] > 0.f ? dz : 0.f;
-        s1[j] += dz;
-        s2[j] = fmaf(dz, v.v[j] - mu[j], s2[j]);
-      }
+      for (int j = 0; j < 8; ++j) mu[j] = o.save[blockIdx.y * R.CT + cg * 8 + j];
     }
   }
-  if (!block_partials_and_arrive(g, s1, s2, part, counter)) return;
-  const double inv_m = 1.0 / (double)M;
-  fold_partials(C, gridDim.x, part, [&](int c, double S1, double S2) {
+  auto acc = [&](const Bf8& d, const Bf8& v, const Bf8& w) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float dz = d.v[j];
+      if constexpr (RELU) dz = w.v[j] > 0.f ? dz : 0.f;
+      s1[j] += dz;
+      s2[j] = fmaf(dz, v.v[j] - mu[j], s2[j]);
+    }
+  };
+  for_rows(R, [&](int64_t e, int64_t step, int n) {
+    if (n == 4) {
+      Bf8 d[4], v[4], w[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        d[u] = load_bf8(dy + e + u * step);
+        v[u] = load_bf8(x + e + u * step);
+        if constexpr (RELU) w[u] = load_bf8(y + e + u * step);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc(d[u], v[u], w[u]);
+    } else {
+      const Bf8 d = load_bf8(dy + e), v = load_bf8(x + e);
+      Bf8 w;
+      if constexpr (RELU) w = load_bf8(y + e);
+      acc(d, v, w);
+    }
+  });
+  if (!block_reduce_tree(R, s1, s2)) return;
+  const int CT = R.CT, C = R.C;
+  const double* total = R.total + (size_t)blockIdx.y * 2 * CT;
+  const double inv_m = 1.0 / (double)R.M;
+  for (int cl = threadIdx.x; cl < CT; cl += kB) {
+    const int c = blockIdx.y * CT + cl;
+    const double S1 = total[cl], S2 = total[CT + cl];
     const float mean = o.save[c], invstd = o.save[C + c];
     const float ga = o.gamma ? o.gamma[c] : 1.f;
     const double dg = S2 * (double)invstd;  // dgamma = Σ dz·x̂
@@ -318,8 +390,7 @@ __global__ __launch_bounds__(kB) void bn_reduce_kernel(const uint16_t* __restric
     o.coef[c] = (float)a;
     o.coef[C + c] = (float)b;
     o.coef[2 * C + c] = (float)(-a * S1 * inv_m - b * mean);
-  });
-  if (threadIdx.x == 0) *counter = 0;
+  }
 }
 
 template <bool RELU, bool RES>
@@ -357,46 +428,79 @@ __global__ __launch_bounds__(kB) void bn_dx_kernel(const uint16_t* __restrict__ 
   }
 }
 
-// ---------------------------------------------------------------- launch geometry
-// Arrival counters: a small device pool, each launch takes the next slot round-robin (the
-// last block re-arms it), so concurrently running BN kernels never share a counter.
-constexpr int kSlots = 1024;
-unsigned* g_counters[64] = {};
-int g_next[64] = {};
+// ---------------------------------------------------------------- host-side geometry
+// Arrival counters: a device pool of per-launch slots (kSlotWords counters each) taken
+// round-robin; the final blocks re-arm their tile's counters, so graph replays reuse a slot and
+// BN kernels running concurrently never share one.  Zeroed once at allocation.
+constexpr int kSlots = 256;
+struct Slots {
+  unsigned* counters = nullptr;
+  int next = 0;
+};
+Slots g_slots[64];
 
-unsigned* next_counter(hipStream_t stream) {
+unsigned* next_slot(hipStream_t stream) {
   int dev = 0;
   GRACE_HIP_CHECK(hipGetDevice(&dev));
-  if (!g_counters[dev]) {
-    GRACE_HIP_CHECK(hipMalloc(&g_counters[dev], kSlots * sizeof(unsigned)));
-    GRACE_HIP_CHECK(hipMemsetAsync(g_counters[dev], 0, kSlots * sizeof(unsigned), stream));
+  Slots& p = g_slots[dev];
+  if (!p.counters) {  // first use happens eagerly (warm-up), never inside a graph capture
+    GRACE_HIP_CHECK(hipMalloc(&p.counters, (size_t)kSlots * kSlotWords * sizeof(unsigned)));
+    GRACE_HIP_CHECK(hipMemsetAsync(p.counters, 0, (size_t)kSlots * kSlotWords * sizeof(unsigned), stream));
     GRACE_HIP_CHECK(hipStreamSynchronize(stream));
   }
-  const int s = g_next[dev];
-  g_next[dev] = (s + 1) % kSlots;
-  return g_counters[dev] + s;
+  const int s = p.next;
+  p.next = (s + 1) % kSlots;
+  return p.counters + (size_t)s * kSlotWords;
 }
 
-int64_t tprp_of(int C) {
-  int64_t t = 1;
-  while (t < C / 8) t <<= 1;
-  return t;
+// Grid and tree shape.  Target >= ~512 blocks (2 per CU) with 4..16 16-B vectors per thread.
+Red plan(int64_t M, int C) {
+  Red R{};
+  R.M = M;
+  R.C = C;
+  R.CT = C < kTileC ? C : kTileC;
+  const int tiles = C / R.CT;
+  R.tprp = 1;
+  while (R.tprp < R.CT / 8) R.tprp <<= 1;
+  R.rpi = kB / R.tprp;
+  const int64_t n_vec = M * C / 8;
+  int64_t vpt = n_vec / ((int64_t)kB * 512);
+  if (vpt < 4) vpt = 4;
+  if (vpt > 16) vpt = 16;
+  const int64_t per_blk = R.rpi * vpt;
+  int64_t nc = (M + per_blk - 1) / per_blk;
+  if (nc * tiles > 2048) nc = (2048 + tiles - 1) / tiles;
+  if (nc < 1) nc = 1;
+  int64_t rpb = (M + nc - 1) / nc;
+  rpb = (rpb + R.rpi - 1) / R.rpi * R.rpi;
+  nc = (M + rpb - 1) / rpb;
+  R.rows_per_blk = rpb;
+  R.nchunks = (int)(nc < 1 ? 1 : nc);
+  int gs = 1;
+  while (gs * gs < R.nchunks) ++gs;
+  int ng = (R.nchunks + gs - 1) / gs;
+  while (ng > kMaxGroups) {
+    ++gs;
+    ng = (R.nchunks + gs - 1) / gs;
+  }
+  R.gsize = gs;
+  R.ngroups = ng;
+  return R;
 }
 
-// (#blocks, rows per block) for the two reduction kernels
-void reduce_grid(int64_t M, int C, int* nblk, int64_t* rows_per_blk) {
-  const int64_t rpi = kB / tprp_of(C);
-  int64_t cap = kPartFloats / C;                  // bounded fold work for the last block
-  if (cap > 2048) cap = 2048;
-  int64_t want = (M + 4 * rpi - 1) / (4 * rpi);  // >= 4 row iterations per block when possible
-  int64_t nb = want < cap ? want : cap;
-  if (nb < 1) nb = 1;
-  int64_t rpb = (M + nb - 1) / nb;
-  rpb = (rpb + rpi - 1) / rpi * rpi;
-  nb = (M + rpb - 1) / rpb;
-  if (nb < 1) nb = 1;
-  *nblk = (int)nb;
-  *rows_per_blk = rpb;
+int64_t even(int64_t n) { return (n + 1) & ~(int64_t)1; }
+
+int64_t ws_floats(const Red& R) {
+  const int tiles = R.C / R.CT, C2 = 2 * R.CT;
+  return even((int64_t)tiles * R.nchunks * C2) + 2 * (int64_t)tiles * (R.ngroups + 1) * C2;
+}
+
+void bind_ws(Red& R, float* ws, hipStream_t stream) {
+  const int tiles = R.C / R.CT, C2 = 2 * R.CT;
+  R.part = ws;
+  R.gpart = reinterpret_cast<double*>(ws + even((int64_t)tiles * R.nchunks * C2));  // 8-B aligned
+  R.total = R.gpart + (size_t)tiles * R.ngroups * C2;
+  R.cnt = next_slot(stream);
 }
 
 int apply_grid(int64_t n_vec, int C) {
@@ -404,32 +508,30 @@ int apply_grid(int64_t n_vec, int C) {
   int64_t b = (n_vec + kB - 1) / kB;
   if (b > 4096) b = 4096;
   if (b < 1) b = 1;
-  // stride must be a multiple of tpr: kB*b % tpr == 0 always holds for tpr | kB; otherwise
-  // round the grid up to a multiple of tpr / gcd(tpr, kB)
+  // the grid stride must be a multiple of tpr: round the grid to a multiple of tpr / gcd(tpr, kB)
   int64_t g = tpr, h = kB;
-  while (h) { const int64_t t = g % h; g = h; h = t; }
+  while (h) {
+    const int64_t t = g % h;
+    g = h;
+    h = t;
+  }
   const int64_t m = tpr / g;
-  b = (b + m - 1) / m * m;
-  return (int)b;
+  return (int)((b + m - 1) / m * m);
 }
 
 }  // namespace
 
-int64_t bn_workspace_floats(int64_t M, int C) {
-  int nblk;
-  int64_t rpb;
-  reduce_grid(M, C, &nblk, &rpb);
-  return (int64_t)nblk * 2 * C;
-}
+bool bn_supported(int C) { return C > 0 && C % 8 == 0 && C <= kMaxC && (C <= kTileC || C % kTileC == 0); }
+
+int64_t bn_workspace_floats(int64_t M, int C) { return ws_floats(plan(M, C)); }
 
 void bn_act_forward(const uint16_t* x, const uint16_t* res, int64_t M, int C, const float* gamma, const float* beta,
                     float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps, bool relu,
-                    float* save, float* part, uint16_t* y, hipStream_t stream) {
-  int nblk;
-  int64_t rpb;
-  reduce_grid(M, C, &nblk, &rpb);
+                    float* save, float* ws, uint16_t* y, hipStream_t stream) {
+  Red R = plan(M, C);
+  bind_ws(R, ws, stream);
   StatsOut o{gamma, beta, running_mean, running_var, nbt, momentum, eps, save};
-  hipLaunchKernelGGL(bn_stats_kernel, dim3(nblk), dim3(kB), 0, stream, x, M, C, rpb, part, next_counter(stream), o);
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(R.nchunks, C / R.CT), dim3(kB), 0, stream, x, R, o);
   const int64_t n_vec = M * C / 8;
   const int gb = apply_grid(n_vec, C);
   if (relu && res)
@@ -443,17 +545,16 @@ void bn_act_forward(const uint16_t* x, const uint16_t* res, int64_t M, int C, co
 }
 
 void bn_act_backward(const uint16_t* dy, const uint16_t* x, const uint16_t* y, int64_t M, int C, const float* gamma,
-                     const float* save, bool relu, float* dgamma, float* dbeta, float* coef, float* part,
+                     const float* save, bool relu, float* dgamma, float* dbeta, float* coef, float* ws,
                      uint16_t* dx, uint16_t* dres, hipStream_t stream) {
-  int nblk;
-  int64_t rpb;
-  reduce_grid(M, C, &nblk, &rpb);
+  Red R = plan(M, C);
+  bind_ws(R, ws, stream);
   GradOut o{gamma, save, dgamma, dbeta, coef};
-  unsigned* cnt = next_counter(stream);
+  const dim3 grid(R.nchunks, C / R.CT);
   if (relu)
-    hipLaunchKernelGGL(bn_reduce_kernel<true>, dim3(nblk), dim3(kB), 0, stream, dy, x, y, M, C, rpb, part, cnt, o);
+    hipLaunchKernelGGL(bn_reduce_kernel<true>, grid, dim3(kB), 0, stream, dy, x, y, R, o);
   else
-    hipLaunchKernelGGL(bn_reduce_kernel<false>, dim3(nblk), dim3(kB), 0, stream, dy, x, y, M, C, rpb, part, cnt, o);
+    hipLaunchKernelGGL(bn_reduce_kernel<false>, grid, dim3(kB), 0, stream, dy, x, y, R, o);
   const int64_t n_vec = M * C / 8;
   const int gb = apply_grid(n_vec, C);
   if (relu && dres)

@@ -23,7 +23,7 @@ void check_rows(const Tensor& t, const char* what, int64_t* M, int64_t* C) {
     *C = t.size(1);
   }
   *M = t.numel() / std::max<int64_t>(*C, 1);
-  TORCH_CHECK(*C % 8 == 0 && *C <= 2048 && *C > 0, what, ": channels must be a multiple of 8 and <= 2048");
+  TORCH_CHECK(grace::bn_supported((int)*C), what, ": channels must be a multiple of 8, <= 2048, and a multiple of 256 above 256");
   TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0, what, " must be 16-byte aligned");
 }
 
@@ -41,6 +41,8 @@ const float* opt_f32(const c10::optional<Tensor>& t, int64_t C, const char* what
 }
 
 // returns (y, save[4C] = mean, invstd, scale, shift)
+bool bn_supported(int64_t C) { return grace::bn_supported((int)C); }
+
 std::vector<Tensor> bn_act_fwd(const Tensor& x, const c10::optional<Tensor>& res, const c10::optional<Tensor>& weight,
                                const c10::optional<Tensor>& bias, const c10::optional<Tensor>& running_mean,
                                const c10::optional<Tensor>& running_var, const c10::optional<Tensor>& nbt,
@@ -61,11 +63,11 @@ std::vector<Tensor> bn_act_fwd(const Tensor& x, const c10::optional<Tensor>& res
   Tensor y = at::empty_like(x);
   auto f32 = x.options().dtype(at::kFloat);
   Tensor save = at::empty({4 * C}, f32);
-  Tensor part = at::empty({grace::bn_workspace_floats(M, (int)C)}, f32);
+  Tensor ws = at::empty({grace::bn_workspace_floats(M, (int)C)}, f32);
   grace::bn_act_forward(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                         has_res ? reinterpret_cast<const uint16_t*>(res->data_ptr()) : nullptr, M, (int)C,
                         opt_f32(weight, C, "weight"), opt_f32(bias, C, "bias"), rm, rv, nb, (float)momentum,
-                        (float)eps, relu, save.data_ptr<float>(), part.data_ptr<float>(),
+                        (float)eps, relu, save.data_ptr<float>(), ws.data_ptr<float>(),
                         reinterpret_cast<uint16_t*>(y.data_ptr()), cur_stream());
   return {y, save};
 }
@@ -89,13 +91,13 @@ std::vector<Tensor> bn_act_bwd(const Tensor& dy, const Tensor& x, const c10::opt
   Tensor dg = want_dweight ? at::empty({C}, f32) : Tensor();
   Tensor db = want_dweight ? at::empty({C}, f32) : Tensor();
   Tensor coef = at::empty({3 * C}, f32);
-  Tensor part = at::empty({grace::bn_workspace_floats(M, (int)C)}, f32);
+  Tensor ws = at::empty({grace::bn_workspace_floats(M, (int)C)}, f32);
   grace::bn_act_backward(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
                          reinterpret_cast<const uint16_t*>(x.data_ptr()),
                          relu ? reinterpret_cast<const uint16_t*>(y->data_ptr()) : nullptr, M, (int)C,
                          opt_f32(weight, C, "weight"), save.data_ptr<float>(), relu,
                          want_dweight ? dg.data_ptr<float>() : nullptr, want_dweight ? db.data_ptr<float>() : nullptr,
-                         coef.data_ptr<float>(), part.data_ptr<float>(), reinterpret_cast<uint16_t*>(dx.data_ptr()),
+                         coef.data_ptr<float>(), ws.data_ptr<float>(), reinterpret_cast<uint16_t*>(dx.data_ptr()),
                          want_dres ? reinterpret_cast<uint16_t*>(dres.data_ptr()) : nullptr, cur_stream());
   return {dx, dres, dg, db};
 }
@@ -103,6 +105,7 @@ std::vector<Tensor> bn_act_bwd(const Tensor& dy, const Tensor& x, const c10::opt
 }  // namespace
 
 void grace_bind_nn(py::module& m) {
+  m.def("bn_supported", &bn_supported);
   m.def("bn_act_fwd", &bn_act_fwd);
   m.def("bn_act_bwd", &bn_act_bwd);
 }

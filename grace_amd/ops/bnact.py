@@ -29,7 +29,7 @@ def _fusable(x: torch.Tensor, bn: nn.BatchNorm2d, residual: Optional[torch.Tenso
     if x.dim() != 4 or not x.is_contiguous(memory_format=torch.channels_last):
         return False
     c = x.shape[1]
-    if c % 8 or c > 2048 or x.numel() == 0 or x.data_ptr() % 16:
+    if c % 8 or c > 2048 or (c > 256 and c % 256) or x.numel() == 0 or x.data_ptr() % 16:
         return False
     if residual is not None and (residual.shape != x.shape or residual.stride() != x.stride()
                                  or residual.dtype != x.dtype or residual.data_ptr() % 16):

