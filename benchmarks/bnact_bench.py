@@ -25,23 +25,42 @@ for (c, hw, n) in ((64, 56, 3), (128, 28, 4), (256, 14, 6), (512, 7, 3)):
             (4 * c, hw, hw, True, True, n), (4 * c, hw, hw, False, False, 1)]
 
 
-def timed(fn, iters):
-    for _ in range(3):
-        fn()
+def timed(fn, iters, graph=True):
+    """us per call; with graph=True, `iters` calls are captured in one HIP graph and replayed
+    (no host launch overhead: the number the whole-step-graph training loop sees)."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    run = fn
+    if graph:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(iters):
+                fn()
+        run = g.replay
+        reps = 3
+    else:
+        reps = iters
+    run()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    for _ in range(iters):
-        fn()
+    for _ in range(reps if graph else iters):
+        run()
     e1.record()
     torch.cuda.synchronize()
-    return e0.elapsed_time(e1) / iters * 1e3
+    return e0.elapsed_time(e1) / (reps * iters if graph else iters) * 1e3
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32)
-    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--eager", action="store_true", help="time eager launches instead of graph replays")
     a = ap.parse_args()
     dev = "cuda"
     tot = {"ff": 0.0, "fb": 0.0, "uf": 0.0, "ub": 0.0}
@@ -66,8 +85,8 @@ def main():
                 y = m(xg, r)
                 y.backward(dy)
 
-            tf = timed(fwd, a.iters)
-            tfb = timed(fb, a.iters)
+            tf = timed(fwd, a.iters, not a.eager)
+            tfb = timed(fb, a.iters, not a.eager)
             res_t[force] = (tf, tfb - tf)
         os.environ["GRACE_AMD_FORCE_TORCH"] = "0"
         nbytes = x.numel() * 2
