@@ -32,6 +32,11 @@ if ROOT not in sys.path:
 
 HEADLINE_METRIC = "images/sec (whole node) ResNet-50 Top-K 1% @ 1/2/4/8 MI355X; comm wall-time"
 
+# Published reference numbers in the metric's unit.  The reference publishes none for its GRACE
+# harness; its only number is cifar10-fast ResNet-9: 24 epochs x 50 000 images in
+# 74 s of DAWNBench train time on one V100 (examples/dist/CIFAR10-dawndist/README.md:17, 24-26).
+REFERENCE_VALUE = {"resnet9_dawn": 24 * 50000 / 74.0}
+
 
 def parse():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
@@ -50,6 +55,9 @@ def parse():
     ap.add_argument("--bf16-weights", choices=["on", "off"], default="on",
                     help="fp32 master weights + bf16 working copies of conv/linear weights (autocast "
                          "numerics without the per-layer cast kernels; parallel/precision.py)")
+    ap.add_argument("--optimizer", choices=["fused", "torch"], default="fused",
+                    help="fused: grace_amd FusedSGD (one native multi-tensor kernel that also writes the bf16 "
+                         "working copies); torch: torch.optim.SGD (foreach)")
     ap.add_argument("--grad-mode", choices=["gather", "accumulate"], default="gather",
                     help="gather: zero_grad(set_to_none) + one native gather launch per bucket; "
                          "accumulate: bucket memset + AccumulateGrad adds into bucket views")
@@ -97,7 +105,12 @@ def main():
 
         weights = BF16Weights(model)
         named = list(weights.named_master_parameters(model))
-    base_opt = torch.optim.SGD([p for _, p in named], lr=0.01 * world, momentum=0.5)
+    if args.optimizer == "fused":
+        from grace_amd.parallel import FusedSGD
+
+        base_opt = FusedSGD([p for _, p in named], lr=0.01 * world, momentum=0.5)
+    else:
+        base_opt = torch.optim.SGD([p for _, p in named], lr=0.01 * world, momentum=0.5)
     grc = grace_from_params(dict(w.grace, world_size=world))
     from grace_amd.parallel.graph import GraphedStep, graph_compute, graph_safe
 
@@ -204,7 +217,7 @@ def main():
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": None,
+            "vs_baseline": round(value / REFERENCE_VALUE[w.name], 3) if w.name in REFERENCE_VALUE else None,
             "dtype": args.dtype,
             "data": "synthetic (random-init weights)",
             "config": {
@@ -219,6 +232,7 @@ def main():
                 "hip_graph": graph_note,
                 "grad_mode": args.grad_mode,
                 "bf16_weights": weights is not None,
+                "optimizer": f"{'FusedSGD' if args.optimizer == 'fused' else 'torch.optim.SGD'}(lr={0.01 * world:g}, momentum=0.5)",
             },
             "comm_wall_ms": round(float(ex.item()) * 1e3, 3),
             "final_loss": round(float(loss.float().item()), 4),

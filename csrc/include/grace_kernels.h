@@ -143,4 +143,11 @@ void bn_act_backward(const uint16_t* dy, const uint16_t* x, const uint16_t* y, i
                      const float* save, bool relu, float* dgamma, float* dbeta, float* coef, float* ws,
                      uint16_t* dx, uint16_t* dres, hipStream_t stream);
 
+// ---------------------------------------------------------------- optim.hip
+constexpr int kSgdSegs = 64;
+// buf[i] / w16[i] may be nullptr (no momentum / no bf16 working copy)
+void sgd_step(float* const* p, const float* const* g, float* const* buf, uint16_t* const* w16, const int64_t* len,
+              int n_seg, float lr, float momentum, float dampening, float wd, bool nesterov, bool maximize,
+              bool first, hipStream_t stream);
+
 }  // namespace grace

@@ -1,0 +1,124 @@
+// Fused multi-tensor SGD (torch.optim.SGD semantics) with optional bf16 working-copy refresh.
+//
+// One launch updates up to kSgdSegs parameters (pointer table in the kernel arguments, so a
+// captured HIP graph replays it with no host work).  Work is a flat list of 4096-element tiles:
+// tensor i owns blocks [start[i], start[i+1]) and a block finds its tensor by binary search, so
+// small tensors cost one block, not a strided grid row.  float4 accesses.  Per element
+// (maximize flips g first):
+//     g   = g + wd * p
+//     buf = first ? g : momentum * buf + (1 - dampening) * g         (momentum != 0)
+//     g   = nesterov ? g + momentum * buf : buf
+//     p   = p - lr * g ;   w16 = bf16_rne(p)                          (w16 optional)
+// which is torch.optim.SGD's update (torch/optim/sgd.py, _single_tensor_sgd) element for
+// element in fp32, followed by BF16Weights.refresh()'s cast -- one pass over p/g/buf instead of
+// the foreach kernels (two multi_tensor_apply passes) plus the separate cast pass.
+#include "grace_common.h"
+#include "grace_kernels.h"
+
+namespace grace {
+namespace {
+
+constexpr int kBlock = 256;
+
+struct SgdTable {
+  float* p[kSgdSegs];
+  const float* g[kSgdSegs];
+  float* buf[kSgdSegs];       // nullptr when momentum == 0
+  uint16_t* w16[kSgdSegs];    // nullptr: no working copy
+  int64_t len[kSgdSegs];
+  int32_t start[kSgdSegs + 1];  // first block of each tensor; start[n] = grid size
+  int32_t n;
+};
+constexpr int kTile = kBlock * 4 * 4;  // elements per block (4 float4 per thread)
+
+struct SgdHyper {
+  float lr, momentum, dampening, wd;
+  int nesterov, maximize, first;
+};
+
+__device__ __forceinline__ float sgd_elem(float& p, float g, float* bufp, const SgdHyper& h) {
+  if (h.maximize) g = -g;
+  if (h.wd != 0.f) g = fmaf(h.wd, p, g);
+  if (bufp) {
+    const float b = h.first ? g : fmaf(h.momentum, *bufp, (1.f - h.dampening) * g);
+    *bufp = b;
+    g = h.nesterov ? fmaf(h.momentum, b, g) : b;
+  }
+  p = fmaf(-h.lr, g, p);
+  return p;
+}
+
+__global__ __launch_bounds__(kBlock) void sgd_kernel(SgdTable t, SgdHyper h) {
+  int lo = 0, hi = t.n - 1;  // last tensor with start <= blockIdx.x
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (t.start[mid] <= (int)blockIdx.x) lo = mid; else hi = mid - 1;
+  }
+  const int s = lo;
+  const int64_t e0 = (int64_t)(blockIdx.x - t.start[s]) * kTile;
+  const int64_t n = min(t.len[s] - e0, (int64_t)kTile);  // this block's elements
+  float* __restrict__ p = t.p[s] + e0;
+  const float* __restrict__ g = t.g[s] + e0;
+  float* __restrict__ buf = t.buf[s] ? t.buf[s] + e0 : nullptr;
+  uint16_t* __restrict__ w = t.w16[s] ? t.w16[s] + e0 : nullptr;
+  const int64_t stride = kBlock;
+  int64_t tail = 0;
+  const bool vec = ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) |
+                     reinterpret_cast<uintptr_t>(buf)) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(w) & 7) == 0;
+  if (vec) {
+    const int64_t nv = n >> 2;
+    for (int64_t i = threadIdx.x; i < nv; i += stride) {
+      float4 pv = reinterpret_cast<float4*>(p)[i];
+      const float4 gv = reinterpret_cast<const float4*>(g)[i];
+      float4 bv = buf ? reinterpret_cast<float4*>(buf)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      const bool m = buf != nullptr;
+      sgd_elem(pv.x, gv.x, m ? &bv.x : nullptr, h);
+      sgd_elem(pv.y, gv.y, m ? &bv.y : nullptr, h);
+      sgd_elem(pv.z, gv.z, m ? &bv.z : nullptr, h);
+      sgd_elem(pv.w, gv.w, m ? &bv.w : nullptr, h);
+      reinterpret_cast<float4*>(p)[i] = pv;
+      if (buf) reinterpret_cast<float4*>(buf)[i] = bv;
+      if (w) {
+        uint2 o;
+        o.x = (uint32_t)f32_to_bf16_rne(pv.x) | ((uint32_t)f32_to_bf16_rne(pv.y) << 16);
+        o.y = (uint32_t)f32_to_bf16_rne(pv.z) | ((uint32_t)f32_to_bf16_rne(pv.w) << 16);
+        reinterpret_cast<uint2*>(w)[i] = o;
+      }
+    }
+    tail = nv << 2;
+  }
+  for (int64_t i = tail + threadIdx.x; i < n; i += stride) {
+    float pv = p[i];
+    sgd_elem(pv, g[i], buf ? buf + i : nullptr, h);
+    p[i] = pv;
+    if (w) w[i] = f32_to_bf16_rne(pv);
+  }
+}
+
+}  // namespace
+
+void sgd_step(float* const* p, const float* const* g, float* const* buf, uint16_t* const* w16, const int64_t* len,
+              int n_seg, float lr, float momentum, float dampening, float wd, bool nesterov, bool maximize,
+              bool first, hipStream_t stream) {
+  SgdHyper h{lr, momentum, dampening, wd, nesterov ? 1 : 0, maximize ? 1 : 0, first ? 1 : 0};
+  for (int s0 = 0; s0 < n_seg; s0 += kSgdSegs) {
+    const int m = n_seg - s0 < kSgdSegs ? n_seg - s0 : kSgdSegs;
+    SgdTable t{};
+    int32_t nb = 0;
+    for (int i = 0; i < m; ++i) {
+      t.p[i] = p[s0 + i];
+      t.g[i] = g[s0 + i];
+      t.buf[i] = buf[s0 + i];
+      t.w16[i] = w16[s0 + i];
+      t.len[i] = len[s0 + i];
+      t.start[i] = nb;
+      nb += (int32_t)((len[s0 + i] + kTile - 1) / kTile);
+    }
+    t.start[m] = nb;
+    t.n = m;
+    if (nb > 0) hipLaunchKernelGGL(sgd_kernel, dim3((unsigned)nb), dim3(kBlock), 0, stream, t, h);
+  }
+}
+
+}  // namespace grace

@@ -102,9 +102,52 @@ std::vector<Tensor> bn_act_bwd(const Tensor& dy, const Tensor& x, const c10::opt
   return {dx, dres, dg, db};
 }
 
+// Fused SGD over a list of fp32 parameters (dense, grads / momentum buffers / bf16 working copies
+// with the parameter's strides).  bufs / w16 entries may be None.
+void sgd_step(const std::vector<Tensor>& params, const std::vector<Tensor>& grads,
+              const std::vector<c10::optional<Tensor>>& bufs, const std::vector<c10::optional<Tensor>>& w16,
+              double lr, double momentum, double dampening, double wd, bool nesterov, bool maximize, bool first) {
+  const size_t n = params.size();
+  TORCH_CHECK(grads.size() == n && bufs.size() == n && w16.size() == n, "sgd_step: list lengths");
+  if (n == 0) return;
+  std::vector<float*> p(n), b(n);
+  std::vector<const float*> g(n);
+  std::vector<uint16_t*> w(n);
+  std::vector<int64_t> len(n);
+  for (size_t i = 0; i < n; ++i) {
+    const Tensor& t = params[i];
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_non_overlapping_and_dense(),
+                "sgd_step: parameters must be dense fp32 GPU tensors");
+    auto same = [&](const Tensor& u, at::ScalarType dt, const char* what) {
+      bool ok = u.is_cuda() && u.scalar_type() == dt && u.sizes() == t.sizes();
+      for (int64_t d = 0; ok && d < t.dim(); ++d)  // strides of size-1 dims do not move memory
+        ok = t.size(d) == 1 || u.stride(d) == t.stride(d);
+      TORCH_CHECK(ok, "sgd_step: ", what, " must match its parameter's shape, strides and expected dtype");
+    };
+    same(grads[i], at::kFloat, "grad");
+    p[i] = t.data_ptr<float>();
+    g[i] = grads[i].data_ptr<float>();
+    b[i] = nullptr;
+    if (bufs[i].has_value() && bufs[i]->defined()) {
+      same(*bufs[i], at::kFloat, "momentum buffer");
+      b[i] = bufs[i]->data_ptr<float>();
+    }
+    w[i] = nullptr;
+    if (w16[i].has_value() && w16[i]->defined()) {
+      same(*w16[i], at::kBFloat16, "bf16 working copy");
+      w[i] = reinterpret_cast<uint16_t*>(w16[i]->data_ptr());
+    }
+    len[i] = t.numel();
+  }
+  DevGuard guard(params[0].device());
+  grace::sgd_step(p.data(), g.data(), b.data(), w.data(), len.data(), (int)n, (float)lr, (float)momentum,
+                  (float)dampening, (float)wd, nesterov, maximize, first, cur_stream());
+}
+
 }  // namespace
 
 void grace_bind_nn(py::module& m) {
+  m.def("sgd_step", &sgd_step);
   m.def("bn_supported", &bn_supported);
   m.def("bn_act_fwd", &bn_act_fwd);
   m.def("bn_act_bwd", &bn_act_bwd);

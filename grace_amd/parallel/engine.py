@@ -211,7 +211,10 @@ class GraceEngine:
     @staticmethod
     def _gatherable(g: torch.Tensor, view: torch.Tensor) -> bool:
         # same shape and strides as the (dense) bucket view -> same dense memory image
-        return (g.is_cuda and g.dtype in (torch.float32, torch.bfloat16) and g.stride() == view.stride()
+        # (strides of size-1 dims do not move memory: a 1x1 conv's channels_last gradient and its
+        # contiguous bucket view are the same image)
+        return (g.is_cuda and g.dtype in (torch.float32, torch.bfloat16) and g.shape == view.shape
+                and all(a == b for a, b, n in zip(g.stride(), view.stride(), g.shape) if n > 1)
                 and _native.native_on(g.device))
 
     def _gather(self, b: Bucket) -> None:

@@ -37,6 +37,11 @@ class _DistributedOptimizer:
                                   sparse_params=sparse_params,
                                   grad_sources=weights.grad_sources() if weights is not None else None)
         self.weights = weights  # parallel/precision.BF16Weights: refreshed after every step
+        # FusedSGD writes the bf16 working copies inside its update kernel (no refresh pass)
+        self._fused_refresh = False
+        if weights is not None and hasattr(optimizer, "attach_working_copies"):
+            optimizer.attach_working_copies(weights)
+            self._fused_refresh = True
         self._synchronized = False
         self._should_sync = True
 
@@ -65,7 +70,7 @@ class _DistributedOptimizer:
                 self.synchronize()
         self._synchronized = False
         out = self._opt.step(closure)
-        if self.weights is not None:
+        if self.weights is not None and not self._fused_refresh:
             self.weights.refresh()
         return out
 
