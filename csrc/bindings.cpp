@@ -262,8 +262,9 @@ void qsgd_quantize(const Tensor& x, const Tensor& norms, double s, int64_t seed,
   CHECK_DEV(codes);
   CHECK_CONTIG(codes);
   TORCH_CHECK(codes.numel() >= x.numel(), "codes too small");
-  const int cb_ = (int)codes.element_size();
-  TORCH_CHECK(cb_ == 1 || cb_ == 2 || cb_ == 4, "codes must be int8/int16/int32");
+  // 1 int8, 2 int16, 4 int32, 3 fp16 integer levels (quant.hip)
+  const int cb_ = codes.scalar_type() == at::kHalf ? 3 : (int)codes.element_size();
+  TORCH_CHECK(cb_ == 1 || cb_ == 2 || cb_ == 3 || cb_ == 4, "codes must be int8/int16/int32/fp16");
   auto ct = make_ct(seg, cb, ce);
   DevGuard guard(x.device());
   grace::qsgd_quantize(ct, x.data_ptr<float>(), norms.data_ptr<float>(), (float)s, seed_arg(seed, step), codes.data_ptr(),
@@ -274,7 +275,8 @@ void qsgd_aggregate(const Tensor& base, int64_t rank_stride, int64_t codes_off, 
                     int64_t n_ranks, double s, double scale, const Tensor& out, bool accumulate, const Tensor& seg,
                     const Tensor& cb, const Tensor& ce, int64_t n_seg) {
   CHECK_F32(out);
-  check_rows(base, rank_stride, n_ranks, std::max(codes_off + out.numel() * code_bytes, norms_off + 4 * n_seg));
+  const int64_t code_size = code_bytes == 3 ? 2 : code_bytes;  // 3 = fp16 codes
+  check_rows(base, rank_stride, n_ranks, std::max(codes_off + out.numel() * code_size, norms_off + 4 * n_seg));
   auto ct = make_ct(seg, cb, ce);
   DevGuard guard(out.device());
   grace::qsgd_aggregate(ct, base.data_ptr<uint8_t>(), rank_stride, codes_off, norms_off, (int)code_bytes,

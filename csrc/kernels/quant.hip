@@ -18,6 +18,8 @@
 //
 // Every *_aggregate kernel decodes all W ranks' payloads (rank-strided rows of the all-gather
 // output, fixed rank order -> bit-identical on every rank) and writes scale * sum in ONE pass.
+#include <type_traits>
+
 #include "grace_common.h"
 #include "grace_kernels.h"
 
@@ -287,25 +289,22 @@ inline int grid_for(int64_t n) {
 
 }  // namespace
 
+// code_bytes: 1 = int8, 2 = int16, 4 = int32, 3 = fp16 (integer levels; exact up to 2048, the
+// all-reducible 16-bit code: RCCL has no int16 reduction)
 void qsgd_quantize(const ChunkTable& ct, const float* x, const float* norms, float s, SeedArg seed, void* codes,
                    int code_bytes, float* resid, hipStream_t stream) {
   if (ct.n_chunks == 0) return;
-  if (code_bytes == 1) {
+  auto go = [&](auto* typed) {
+    using T = std::remove_pointer_t<decltype(typed)>;
     if (resid)
-      qsgd_quant_kernel<int8_t, true><<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, norms, s, seed, (int8_t*)codes, resid);
+      qsgd_quant_kernel<T, true><<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, norms, s, seed, (T*)codes, resid);
     else
-      qsgd_quant_kernel<int8_t, false><<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, norms, s, seed, (int8_t*)codes, nullptr);
-  } else if (code_bytes == 2) {
-    if (resid)
-      qsgd_quant_kernel<int16_t, true><<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, norms, s, seed, (int16_t*)codes, resid);
-    else
-      qsgd_quant_kernel<int16_t, false><<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, norms, s, seed, (int16_t*)codes, nullptr);
-  } else {
-    if (resid)
-      qsgd_quant_kernel<int32_t, true><<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, norms, s, seed, (int32_t*)codes, resid);
-    else
-      qsgd_quant_kernel<int32_t, false><<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, norms, s, seed, (int32_t*)codes, nullptr);
-  }
+      qsgd_quant_kernel<T, false><<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, norms, s, seed, (T*)codes, nullptr);
+  };
+  if (code_bytes == 1) go((int8_t*)nullptr);
+  else if (code_bytes == 2) go((int16_t*)nullptr);
+  else if (code_bytes == 3) go((_Float16*)nullptr);
+  else go((int32_t*)nullptr);
 }
 
 void qsgd_aggregate(const ChunkTable& ct, const uint8_t* base, int64_t rank_stride, int64_t codes_off,
@@ -313,15 +312,15 @@ void qsgd_aggregate(const ChunkTable& ct, const uint8_t* base, int64_t rank_stri
                     hipStream_t stream) {
   if (ct.n_chunks == 0) return;
   const float inv_s = 1.f / s;
-  if (code_bytes == 1)
-    qsgd_aggregate_kernel<int8_t><<<ct.n_chunks, kBlock, 0, stream>>>(ct, base, rank_stride, codes_off, norms_off,
-                                                                      n_ranks, inv_s, scale, out, accumulate);
-  else if (code_bytes == 2)
-    qsgd_aggregate_kernel<int16_t><<<ct.n_chunks, kBlock, 0, stream>>>(ct, base, rank_stride, codes_off, norms_off,
-                                                                       n_ranks, inv_s, scale, out, accumulate);
-  else
-    qsgd_aggregate_kernel<int32_t><<<ct.n_chunks, kBlock, 0, stream>>>(ct, base, rank_stride, codes_off, norms_off,
-                                                                       n_ranks, inv_s, scale, out, accumulate);
+  auto go = [&](auto* typed) {
+    using T = std::remove_pointer_t<decltype(typed)>;
+    qsgd_aggregate_kernel<T><<<ct.n_chunks, kBlock, 0, stream>>>(ct, base, rank_stride, codes_off, norms_off, n_ranks,
+                                                                 inv_s, scale, out, accumulate);
+  };
+  if (code_bytes == 1) go((int8_t*)nullptr);
+  else if (code_bytes == 2) go((int16_t*)nullptr);
+  else if (code_bytes == 3) go((_Float16*)nullptr);
+  else go((int32_t*)nullptr);
 }
 
 void tern_quantize(const ChunkTable& ct, const int64_t* seg_start, const int64_t* word_off, const float* x,

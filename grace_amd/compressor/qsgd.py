@@ -12,7 +12,9 @@ s >= 128 (survey 2.14 #12).  Aggregation decodes all W ranks in one pass.
 Allreduce (BASELINE "QSGD 8-bit Allreduce"): *shared-scale* variant -- the per-segment norms
 are MAX-all-reduced first (one tiny collective for the whole bucket), every rank quantizes
 against the same norm, so integer levels are summable and RCCL sums them directly.  The code
-width is the smallest integer type holding s*W (int8 when s*W <= 127, e.g. s=15 at W=8).
+is the narrowest type whose SUM stays exact and that RCCL can reduce: int8 when s*W <= 127
+(e.g. s=15 at W=8), fp16 integer levels when s*W <= 2048 (the BASELINE s=127 config at W=2..8;
+RCCL has no int16 reduction), int32 beyond.
 """
 from __future__ import annotations
 
@@ -39,9 +41,14 @@ class QSGDCompressor(BucketCompressor):
         self.shared_scale = True
 
     def code_dtype(self, world_size: int = 1):
+        """Narrowest code type for the levels one all-reduced element can reach.  Shared-scale
+        (all-reduced) codes: int8, else fp16 -- integer sums are exact in fp16 up to 2048, and
+        RCCL (like gloo) has no int16 reduction -- else int32.  Gathered codes: int8 / int16."""
         levels = self.quantum_num * (world_size if self.shared_scale else 1)
         if levels <= 127:
             return torch.int8
+        if self.shared_scale:
+            return torch.float16 if levels <= 2048 else torch.int32
         if levels <= 32767:
             return torch.int16
         return torch.int32

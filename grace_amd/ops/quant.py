@@ -74,7 +74,7 @@ def qsgd_aggregate(base, rank_stride, codes_off, norms_off, code_dtype, n_ranks,
                    accumulate=False):
     if _native.use_native(out):
         t = _tables(layout, out.device)
-        esz = torch.empty((), dtype=code_dtype).element_size()
+        esz = 3 if code_dtype == torch.float16 else torch.empty((), dtype=code_dtype).element_size()
         _native.lib().qsgd_aggregate(base, rank_stride, codes_off, norms_off, esz, n_ranks, float(s), scale, out,
                                      accumulate, t["seg"], t["begin"], t["end"], layout.n_seg)
         return

@@ -288,3 +288,17 @@ def test_powersgd_fused_memory_matches_unfused():
         outs[mem_cls] = res
     for a, b in zip(outs[M.PowerSGDMemory], outs[Unfused]):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)
+
+
+def test_qsgd_code_dtypes_are_reducible():
+    """Shared-scale (all-reduced) codes never use int16: RCCL and gloo have no int16 reduction."""
+    from grace_amd.compressor.qsgd import QSGDCompressor
+
+    c = QSGDCompressor(127)
+    assert c.code_dtype(1) == torch.int8
+    assert c.code_dtype(4) == torch.int8 and QSGDCompressor(255).code_dtype(4) == torch.int16  # gathered: no reduction
+    c.enable_allreduce_mode()
+    assert c.code_dtype(1) == torch.int8
+    assert c.code_dtype(2) == torch.float16 and c.code_dtype(8) == torch.float16  # 1016 <= 2048: exact
+    assert c.code_dtype(32) == torch.int32
+    assert QSGDCompressor(15, shared_scale=True).code_dtype(8) == torch.int8

@@ -22,24 +22,28 @@ def _data(rank, shape=(31, 17), seed=0):
 
 def _same_on_all_ranks(t):
     W = dist.get_world_size()
+    t = t.detach().cpu().contiguous()
     out = [torch.empty_like(t) for _ in range(W)]
-    dist.all_gather(out, t.contiguous())
+    dist.all_gather(out, t)
     for o in out[1:]:
         assert torch.equal(o, out[0]), "result differs across ranks"
 
 
-def _body(rank, world):
+def _body(rank, world, device="cpu"):
+    """Every communicator x compressor pairing on W ranks.  device="cuda": each rank's tensors on
+    cuda:0 (native HIP kernels, gloo moving the GPU payloads) -- tests/test_gpu_multirank.py."""
     from grace_amd import grace_from_params
 
     xs = [_data(r) for r in range(world)]
-    x = xs[rank]
+    x = xs[rank].to(device)
 
     def run(params, name="w"):
         p = dict(params, world_size=world)
         grc = grace_from_params(p)
         out = grc.step(x.clone(), name)
+        assert out.device.type == torch.device(device).type
         _same_on_all_ranks(out)
-        return out
+        return out.cpu()
 
     # None: allreduce / allgather / broadcast all give the mean
     mean = sum(xs) / world
@@ -76,6 +80,9 @@ def _body(rank, world):
         out = run({"compressor": "qsgd", "quantum_num": 15, "communicator": comm}, "q")
         bound = max(t.norm() for t in xs) / 15
         assert (out - mean).abs().max() <= bound * (1 + 1e-4)
+    # s = 127 (BASELINE BERT config): s*W > 127 -> fp16 integer-level codes on the wire
+    out = run({"compressor": "qsgd", "quantum_num": 127, "communicator": "allreduce"}, "q127")
+    assert (out - mean).abs().max() <= max(t.norm() for t in xs) / 127 * (1 + 1e-4)
     # TernGrad / Natural / U8bit / Sketch run and agree across ranks
     for comp in ("terngrad", "natural", "u8bit", "sketch", "inceptionn", "adaq", "dgc"):
         comm = "allgather"
@@ -92,7 +99,7 @@ def _body(rank, world):
     grc = grace_from_params({"compressor": "topk", "compress_ratio": 0.05, "memory": "residual",
                              "communicator": "allgather", "world_size": world})
     for s in range(3):
-        out = grc.step(_data(rank, seed=s + 1), "w")
+        out = grc.step(_data(rank, seed=s + 1).to(device), "w")
         _same_on_all_ranks(out)
 
 
