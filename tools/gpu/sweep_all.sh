@@ -1,0 +1,11 @@
+#!/bin/bash
+# Every BASELINE workload (compressed + uncompressed reference) on one GPU, one process each.
+#   gpurun --timeout 1100 -- 'bash tools/gpu/sweep_all.sh'
+R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; export TMPDIR=/tmp; mkdir -p gpurun_out
+printf -- "%s\n" "--steps 30 --warmup 10" "--workload resnet50_none --steps 30 --warmup 10" \
+  "--workload vgg16_powersgd --steps 20 --warmup 10" "--workload vgg16_none --steps 20 --warmup 10" \
+  "--workload lstm_efsignsgd --steps 40 --warmup 10" "--workload lstm_none --steps 40 --warmup 10" \
+  "--workload bert_qsgd --steps 20 --warmup 10" "--workload bert_none --steps 20 --warmup 10" \
+  "--workload resnet9_dawn --steps 30 --warmup 10" "--workload resnet18_cifar_none --steps 30 --warmup 10" \
+  > gpurun_out/sweep_all.txt
+bash tools/bench_sweep.sh gpurun_out/sweep_all.txt
