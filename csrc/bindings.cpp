@@ -424,7 +424,7 @@ void powersgd_mq(const Tensor& x, const Tensor& small, const Tensor& out, const 
 }
 
 void gram_orthonormalize(const Tensor& buf, const Tensor& mats, int64_t which, int64_t n_mat, const Tensor& gtiles,
-                         const Tensor& gtile_begin, int64_t passes) {
+                         const Tensor& gtile_begin, int64_t passes, int64_t max_r) {
   CHECK_F32(buf);
   CHECK_I64(mats);
   CHECK_I32(gtiles);
@@ -436,7 +436,7 @@ void gram_orthonormalize(const Tensor& buf, const Tensor& mats, int64_t which, i
   auto T = at::empty({std::max<int64_t>(n_mat, 1) * 256}, buf.options());
   grace::gram_orthonormalize(buf.data_ptr<float>(), mats.data_ptr<int64_t>(), (int)n_mat, (int)which,
                              gtiles.data_ptr<int32_t>(), (int)nt, gtile_begin.data_ptr<int32_t>(),
-                             part.data_ptr<double>(), T.data_ptr<float>(), (int)passes, cur_stream());
+                             part.data_ptr<double>(), T.data_ptr<float>(), (int)passes, (int)max_r, cur_stream());
 }
 
 void powersgd_pqt(const Tensor& P, const Tensor& Q, const Tensor& out, const Tensor& mats, const Tensor& tiles,

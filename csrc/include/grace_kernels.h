@@ -84,9 +84,10 @@ void dgc_compact(const ChunkTable& ct, const float* x, const float* thr, float* 
 void powersgd_mq(const float* x, const float* small, float* out, int64_t out_len, const int64_t* mats,
                  const int32_t* tiles, int n_tiles, int mode, const float* comp_r, float beta, float gamma,
                  float* xout, hipStream_t stream);
+// max_r: largest rank r of the matrices (<= 4 selects the one-launch, one-workgroup-per-matrix form)
 void gram_orthonormalize(float* buf, const int64_t* mats, int n_mat, int which, const int32_t* gtiles,
                          int n_gtiles, const int32_t* gtile_begin, double* partials, float* T, int passes,
-                         hipStream_t stream);
+                         int max_r, hipStream_t stream);
 void powersgd_pqt(const float* P, const float* Q, float* out, const int64_t* mats, const int32_t* tiles, int n_tiles,
                   float* resid, hipStream_t stream);
 void philox_normal(float* out, int64_t n, SeedArg seed, hipStream_t stream);

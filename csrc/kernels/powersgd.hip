@@ -12,8 +12,9 @@
 //      from a second LDS tile.  Strip partial sums are combined with fp32 atomics (the output
 //      is only n*r or m*r floats).  Tall-skinny with r=4 is bandwidth bound (2 FLOP/byte):
 //      the MFMA work is ~25% utilised by construction but still ~3x faster than HBM needs.
-//  gram_orthonormalize  Gram matrices on MFMA (all tiles of all matrices in one launch), MGS in
-//                     the Gram metric per matrix, A <- A T; twice (CholQR2) -- see below
+//  gram_orthonormalize  r <= 4: one workgroup per matrix, one launch (fp64 Gram, MGS in the Gram
+//                     metric, in-place A <- A T, twice for CholQR2); r > 4: Gram tiles on MFMA
+//                     (all tiles of all matrices in one launch), per-matrix fix, apply -- see below
 //  powersgd_pqt       out = P Q^T: exactly one 16x16x4 MFMA per 16x16 output tile when r <= 4,
 //                     optionally fused with the residual update  r = x - P Q^T
 //  philox_normal      N(0,1) via Philox4x32 + Box-Muller (Q identical on every rank)
@@ -176,6 +177,25 @@ __global__ __launch_bounds__(kBlock) void gram_partial_kernel(const float* __res
   for (int e = threadIdx.x; e < 256; e += kBlock) o[e] = red[0][e] + red[1][e] + red[2][e] + red[3][e];
 }
 
+// Modified Gram-Schmidt expressed in the Gram metric: on entry Tm = I, G = A^T A; on exit the
+// columns of A*Tm are orthonormal (zero columns stay zero).  One thread (r <= 16).
+__device__ void mgs_gram_metric(const double (*G)[16], double (*Tm)[16], int r) {
+  for (int i = 0; i < r; ++i) {
+    double nn = 0.0;  // ||A t_i||^2 = t_i^T G t_i
+    for (int a = 0; a <= i; ++a)
+      for (int b = 0; b <= i; ++b) nn += Tm[a][i] * G[a][b] * Tm[b][i];
+    const double nrm = nn > 0.0 ? sqrt(nn) : 0.0;
+    const double inv = nrm > 1e-30 ? 1.0 / nrm : 0.0;  // zero column stays zero
+    for (int a = 0; a <= i; ++a) Tm[a][i] *= inv;
+    for (int j = i + 1; j < r; ++j) {
+      double pr = 0.0;  // <A t_i, A t_j> = t_i^T G t_j
+      for (int a = 0; a <= i; ++a)
+        for (int b = 0; b <= j; ++b) pr += Tm[a][i] * G[a][b] * Tm[b][j];
+      for (int a = 0; a <= i; ++a) Tm[a][j] -= pr * Tm[a][i];
+    }
+  }
+}
+
 // one 64-thread workgroup per matrix; T: fp32 [n_mat][16*16] (row i, col j: A_new[:, j] = sum_i A[:, i] T[i][j])
 __global__ __launch_bounds__(kWave) void gram_fix_kernel(const int64_t* __restrict__ mats,
                                                          const int32_t* __restrict__ gtile_begin,
@@ -194,23 +214,7 @@ __global__ __launch_bounds__(kWave) void gram_fix_kernel(const int64_t* __restri
     Tm[e >> 4][e & 15] = (e >> 4) == (e & 15) ? 1.0 : 0.0;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int i = 0; i < r; ++i) {
-      // ||A t_i||^2 = t_i^T G t_i
-      double nn = 0.0;
-      for (int a = 0; a <= i; ++a)
-        for (int b = 0; b <= i; ++b) nn += Tm[a][i] * G[a][b] * Tm[b][i];
-      const double nrm = nn > 0.0 ? sqrt(nn) : 0.0;
-      const double inv = nrm > 1e-30 ? 1.0 / nrm : 0.0;  // zero column stays zero
-      for (int a = 0; a <= i; ++a) Tm[a][i] *= inv;
-      for (int j = i + 1; j < r; ++j) {
-        double pr = 0.0;  // <A t_i, A t_j> = t_i^T G t_j
-        for (int a = 0; a <= i; ++a)
-          for (int b = 0; b <= j; ++b) pr += Tm[a][i] * G[a][b] * Tm[b][j];
-        for (int a = 0; a <= i; ++a) Tm[a][j] -= pr * Tm[a][i];
-      }
-    }
-  }
+  if (threadIdx.x == 0) mgs_gram_metric(G, Tm, r);
   __syncthreads();
   for (int e = threadIdx.x; e < 256; e += kWave) T[(int64_t)mi * 256 + e] = (float)Tm[e >> 4][e & 15];
 }
@@ -244,6 +248,95 @@ __global__ __launch_bounds__(kBlock) void gram_apply_kernel(float* __restrict__ 
 #pragma unroll
     for (int j = 0; j < 16; ++j)
       if (j < r) A[row * r + j] = o[j];
+  }
+}
+
+// r <= 4 (the PowerSGD ranks in use): the whole orthonormalisation of a matrix in ONE workgroup
+// and ONE launch for all matrices -- every pass is a Gram matrix from 16-B row loads (fp64 sums
+// of the 10 distinct products), MGS in the Gram metric, and the in-place A <- A T.  The
+// three-kernel form above costs 3 launches per pass (CholQR2: 6) of ~10 us each for matrices
+// of at most a few hundred KB; here the largest (VGG-16 fc6's 25088 x 4 Q) is one workgroup
+// streaming 400 KB per pass, the others run beside it.
+constexpr int kSmallR = 4;
+__global__ __launch_bounds__(kBlock) void gram_small_kernel(float* __restrict__ buf, const int64_t* __restrict__ mats,
+                                                            int which, int passes) {
+  const Mat mt = load_mat(mats, blockIdx.x);
+  const int64_t len = blk_len(mt, which);
+  const int r = (int)mt.r;
+  float* A = buf + blk_off(mt, which);
+  __shared__ double G[16][16];
+  __shared__ double Tm[16][16];
+  __shared__ double red[kBlock / kWave][10];
+  const bool vec = r == 4 && (reinterpret_cast<uintptr_t>(A) & 15) == 0;
+  auto load_row = [&](int64_t row, float (&a)[kSmallR]) {
+    if (vec) {
+      const float4 v = reinterpret_cast<const float4*>(A)[row];
+      a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
+    } else {
+#pragma unroll
+      for (int i = 0; i < kSmallR; ++i) a[i] = i < r ? A[row * r + i] : 0.f;
+    }
+  };
+  for (int pass = 0; pass < passes; ++pass) {
+    double s[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) s[k] = 0.0;
+#pragma unroll 4
+    for (int64_t row = threadIdx.x; row < len; row += kBlock) {
+      float a[kSmallR];
+      load_row(row, a);
+      int k = 0;
+#pragma unroll
+      for (int i = 0; i < kSmallR; ++i)
+#pragma unroll
+        for (int j = i; j < kSmallR; ++j) s[k++] += (double)a[i] * (double)a[j];
+    }
+#pragma unroll
+    for (int k = 0; k < 10; ++k) s[k] = wave_sum(s[k]);
+    if (lane_id() == 0)
+#pragma unroll
+      for (int k = 0; k < 10; ++k) red[wave_id()][k] = s[k];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int e = 0; e < 256; ++e) {
+        G[e >> 4][e & 15] = 0.0;
+        Tm[e >> 4][e & 15] = (e >> 4) == (e & 15) ? 1.0 : 0.0;
+      }
+      int k = 0;
+      for (int i = 0; i < kSmallR; ++i)
+        for (int j = i; j < kSmallR; ++j, ++k) {
+          double v = 0.0;
+          for (int w = 0; w < kBlock / kWave; ++w) v += red[w][k];  // fixed order: deterministic
+          G[i][j] = G[j][i] = v;
+        }
+      mgs_gram_metric(G, Tm, r);
+    }
+    __syncthreads();
+    float t[kSmallR][kSmallR];
+#pragma unroll
+    for (int i = 0; i < kSmallR; ++i)
+#pragma unroll
+      for (int j = 0; j < kSmallR; ++j) t[i][j] = (float)Tm[i][j];
+#pragma unroll 4
+    for (int64_t row = threadIdx.x; row < len; row += kBlock) {
+      float a[kSmallR], o[kSmallR];
+      load_row(row, a);
+#pragma unroll
+      for (int j = 0; j < kSmallR; ++j) {
+        float v = 0.f;
+#pragma unroll
+        for (int i = 0; i < kSmallR; ++i) v = fmaf(a[i], t[i][j], v);
+        o[j] = v;
+      }
+      if (vec) {
+        reinterpret_cast<float4*>(A)[row] = make_float4(o[0], o[1], o[2], o[3]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < kSmallR; ++j)
+          if (j < r) A[row * r + j] = o[j];
+      }
+    }
+    __syncthreads();  // the next pass reads what this one wrote (same workgroup)
   }
 }
 
@@ -333,8 +426,12 @@ void powersgd_mq(const float* x, const float* small, float* out, int64_t out_len
 
 void gram_orthonormalize(float* buf, const int64_t* mats, int n_mat, int which, const int32_t* gtiles,
                          int n_gtiles, const int32_t* gtile_begin, double* partials, float* T, int passes,
-                         hipStream_t stream) {
+                         int max_r, hipStream_t stream) {
   if (n_mat <= 0 || n_gtiles <= 0) return;
+  if (max_r <= kSmallR) {
+    gram_small_kernel<<<n_mat, kBlock, 0, stream>>>(buf, mats, which, passes);
+    return;
+  }
   for (int p = 0; p < passes; ++p) {
     gram_partial_kernel<<<n_gtiles, kBlock, 0, stream>>>(buf, mats, gtiles, which, partials);
     gram_fix_kernel<<<n_mat, kWave, 0, stream>>>(mats, gtile_begin, partials, T);

@@ -102,7 +102,12 @@ class PowerSGDCompressor(BucketCompressor):
             seed = fnv1a64(name.encode())
             q = PS.randn_shared(plan.q_total, seed if step_t is not None else mix_step(seed, step), x.device,
                                 step=step_t)
-            PS.orthogonalize(q, plan, which="q")
+            # The reference orthogonalises this fresh Gaussian Q (dist/compressor/powersgd.py:43).  That cannot
+            # change the result: MGS gives Q R^-1 with R upper triangular, so P = M Q R^-1 = P R^-1
+            # and the orthonormal factor of P R^-1 is that of P -- orthogonalize(P) below yields the
+            # same P-hat, hence the same Q = M^T P-hat and P-hat Q^T (up to rounding; a Gaussian Q is
+            # well conditioned).  Skipped: it was a 400 KB single-workgroup pass per step for
+            # VGG-16's 25088 x 4 Q.  (A warm-start Q is used as is, as in the reference.)
         p = PS.mq(x, q, plan, comp_r=comp_r, xout=xout)  # P = M Q for every matrix (one launch)
         if self.comm is not None and W > 1:
             self.comm.all_reduce(p)

@@ -133,7 +133,7 @@ def orthogonalize(buf: torch.Tensor, plan: Plan, which: str) -> None:
         # P = M Q can be ill-conditioned (near-low-rank gradients): CholQR2; the Gaussian Q
         # (condition number ~1) needs one pass
         _native.lib().gram_orthonormalize(buf, t["mat"], 0 if which == "p" else 1, plan.n_mat, t["gt_" + which],
-                                          t["gtb_" + which], 2 if which == "p" else 1)
+                                          t["gtb_" + which], 2 if which == "p" else 1, plan.rank)
         return
     for a in _views(buf, plan, which):
         r = a.shape[1]
