@@ -4,8 +4,10 @@ on every BatchNorm shape of ResNet-50 at batch 32 (bf16, channels_last).
 
     python benchmarks/bnact_bench.py [--batch 32] [--iters 50]
 
-Columns: shape, forward / backward microseconds for fused and stock, and the fused kernels'
-effective HBM rate (bytes the fused path must move / time).
+Columns: shape, forward / backward microseconds for the fused kernels (the default dispatch:
+single-launch where the grid fits co-resident, else two kernels), the fused kernels forced onto
+the two-kernel path, and stock (MIOpen + elementwise); the default path's effective HBM rate
+(bytes the two-kernel path must move / time).
 """
 import argparse
 import os
@@ -63,8 +65,12 @@ def main():
     ap.add_argument("--eager", action="store_true", help="time eager launches instead of graph replays")
     a = ap.parse_args()
     dev = "cuda"
-    tot = {"ff": 0.0, "fb": 0.0, "uf": 0.0, "ub": 0.0}
-    print(f"{'C':>5} {'H':>4} {'W':>4} relu res  cnt | fused fwd  bwd (us) | stock fwd  bwd (us) | fused GB/s fwd bwd")
+    from grace_amd.ops import _native
+
+    lib = _native.lib()
+    tot = {"ff": 0.0, "fb": 0.0, "tf": 0.0, "tb": 0.0, "uf": 0.0, "ub": 0.0}
+    print(f"{'C':>5} {'H':>4} {'W':>4} relu res  cnt  V f/b | fused fwd  bwd (us) | 2-kernel fwd  bwd | "
+          f"stock fwd  bwd (us) | fused GB/s fwd bwd")
     for (c, h, w, relu, res, cnt) in R50:
         m = BatchNormAct2d(c, relu=relu).to(dev)
         x = torch.randn(a.batch, c, h, w, device=dev, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
@@ -73,8 +79,9 @@ def main():
         xg = x.clone().requires_grad_(True)
         out = {}
         res_t = {}
-        for force in ("0", "1"):
-            os.environ["GRACE_AMD_FORCE_TORCH"] = force
+        for force in ("0", "2", "1"):
+            os.environ["GRACE_AMD_FORCE_TORCH"] = "1" if force == "1" else "0"
+            lib.bn_set_fused(force != "2")
 
             def fwd():
                 with torch.no_grad():
@@ -89,15 +96,20 @@ def main():
             tfb = timed(fb, a.iters, not a.eager)
             res_t[force] = (tf, tfb - tf)
         os.environ["GRACE_AMD_FORCE_TORCH"] = "0"
+        lib.bn_set_fused(True)
+        M = a.batch * h * w
+        vf, vb = lib.bn_fused_v(M, c, False), lib.bn_fused_v(M, c, True)
         nbytes = x.numel() * 2
         fwd_bytes = nbytes * (3 + (1 if res else 0))           # stats read, apply read+write (+res)
         bwd_bytes = nbytes * ((3 if relu else 2) * 2 + 1 + (1 if res else 0))  # reduce + dx reads, dx (+dres) write
-        (ff, fbk), (uf, ub) = res_t["0"], res_t["1"]
-        for k, v in (("ff", ff), ("fb", fbk), ("uf", uf), ("ub", ub)):
+        (ff, fbk), (tf2, tb2), (uf, ub) = res_t["0"], res_t["2"], res_t["1"]
+        for k, v in (("ff", ff), ("fb", fbk), ("tf", tf2), ("tb", tb2), ("uf", uf), ("ub", ub)):
             tot[k] += v * cnt
-        print(f"{c:5d} {h:4d} {w:4d} {str(relu)[0]:>4} {str(res)[0]:>3} {cnt:4d} | {ff:9.1f} {fbk:5.1f} | {uf:9.1f} {ub:5.1f} | "
-              f"{fwd_bytes / ff / 1e3:8.0f} {bwd_bytes / fbk / 1e3:5.0f}")
-    print(f"ResNet-50 total per step (us): fused fwd {tot['ff']:.0f} bwd {tot['fb']:.0f} | stock fwd {tot['uf']:.0f} bwd {tot['ub']:.0f}")
+        print(f"{c:5d} {h:4d} {w:4d} {str(relu)[0]:>4} {str(res)[0]:>3} {cnt:4d} {vf:2d}/{vb:<2d} | {ff:9.1f} {fbk:5.1f} | "
+              f"{tf2:12.1f} {tb2:5.1f} | {uf:9.1f} {ub:5.1f} | {fwd_bytes / ff / 1e3:8.0f} {bwd_bytes / fbk / 1e3:5.0f}")
+    print(f"ResNet-50 total per step (us): fused fwd {tot['ff']:.0f} bwd {tot['fb']:.0f} | two-kernel fwd {tot['tf']:.0f} "
+          f"bwd {tot['tb']:.0f} | stock fwd {tot['uf']:.0f} bwd {tot['ub']:.0f}")
+    print(f"single-launch spin timeouts: {lib.bn_spin_timeouts()}")
 
 
 if __name__ == "__main__":

@@ -44,7 +44,8 @@ constexpr int kMaxC = 2048;
 constexpr int kTileC = 256;       // channels per reduction tile (32 threads x 8 channels per row)
 constexpr int kMaxTiles = kMaxC / kTileC;
 constexpr int kMaxGroups = 64;
-constexpr int kSlotWords = kMaxTiles * (kMaxGroups + 1);
+constexpr int kTreeWords = kMaxTiles * (kMaxGroups + 1);
+constexpr int kSlotWords = kTreeWords + 2 * kMaxTiles;  // + per-tile generation word (+ pad)
 
 struct Bf8 {
   float v[8];
@@ -428,6 +429,325 @@ __global__ __launch_bounds__(kB) void bn_dx_kernel(const uint16_t* __restrict__ 
   }
 }
 
+
+// ---------------------------------------------------------------- single-launch variants
+// For the small/medium layers (ResNet-50 stages 2-4: 0.4-8 M elements) a BN pass is latency
+// bound: two launches, each with a serial reduction tail, for a few MB of data.  The fused
+// kernels keep the block's rows in REGISTERS (V 16-B vectors per thread per operand), run the
+// same arrival tree, and then every block waits for its tile's finisher to publish the
+// per-channel coefficients and finishes the elementwise pass from the registers: one launch,
+// one read of every operand.
+//
+// The wait needs every block of a tile co-resident.  The host only picks this path when the
+// whole grid fits in HALF of the device's occupancy for the kernel (hipOccupancy... x CUs), so
+// it still fits next to a persistent RCCL kernel; the spin is additionally bounded (~0.5 s,
+// s_sleep between polls) and a timed-out wait is counted in g_bn_spin_timeouts instead of
+// hanging the device (the results of that launch are then wrong, and the test suite fails on
+// the counter).
+__device__ unsigned g_bn_spin_timeouts;
+
+// Per-tile generation word (monotonic, never reset): every block reads it BEFORE its arrival in
+// the tree, the tile's finisher bumps it after publishing, the others wait for it to move.  The
+// hand-off follows cdna_hip_programming.md Guideline 16 R1 without fences: the finisher stores
+// the coefficients write-through (sc1) and drains every wave before the bump; consumers read
+// them with sc1 loads only, so no acquire (L1 invalidate) and no release (L2 writeback) is paid.
+struct Flag {
+  unsigned* gen;
+  unsigned g0;  // value seen at entry (thread 0 only)
+};
+
+__device__ __forceinline__ Flag tile_flag(const Red& R) {
+  Flag f;
+  f.gen = R.cnt + kTreeWords + 2 * blockIdx.y;
+  f.g0 = 0;
+  if (threadIdx.x == 0) f.g0 = __hip_atomic_load(f.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the value must be back before this block's arrival add (arrive() drains vmcnt first)
+  return f;
+}
+
+__device__ __forceinline__ void publish(const Flag& f) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its sc1 stores are done
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(f.gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void wait_published(const Flag& f) {
+  if (threadIdx.x == 0) {
+    unsigned spins = 0;
+    while (__hip_atomic_load(f.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == f.g0) {
+      __builtin_amdgcn_s_sleep(4);
+      if (++spins > (1u << 22)) {
+        atomicAdd(&g_bn_spin_timeouts, 1u);
+        break;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: keep loads below the poll
+  __syncthreads();
+}
+
+// published per-channel values: sc1 (agent-scope relaxed atomic) loads, never cached in L1
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Row addressing through buffer descriptors: the per-thread part (row phase + channel group) is
+// one 32-bit VGPR offset, the per-vector part (block base + u * rpi rows) a scalar soffset, so
+// holding V vectors in registers costs no per-vector address registers (flat 64-bit addresses
+// kept live across the reduction for the final stores pushed the V = 16 variant to 255 VGPRs).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+struct RowMap {
+  int voff;    // bytes: (rs * C + col) * 2
+  int sbase;   // bytes: block's first row * C * 2   (wave-uniform)
+  int sstep;   // bytes: rpi * C * 2                (wave-uniform)
+  int nvalid;  // vectors of this thread inside the tensor (<= V)
+  int64_t col;
+  bool active;
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ RowMap row_map(const Red& R, int V) {
+  const int cg = threadIdx.x % R.tprp, rs = threadIdx.x / R.tprp;
+  RowMap m;
+  m.active = cg < R.CT / 8;
+  m.col = (int64_t)blockIdx.y * R.CT + cg * 8;
+  const int64_t b0 = (int64_t)blockIdx.x * R.rows_per_blk;
+  m.voff = (int)(((int64_t)rs * R.C + m.col) * 2);
+  m.sbase = (int)(b0 * R.C * 2);
+  m.sstep = R.rpi * R.C * 2;
+  const int64_t left = R.M - (b0 + rs);  // rows from this thread's first row to the end
+  int nv = left <= 0 ? 0 : (int)((left + R.rpi - 1) / R.rpi);
+  m.nvalid = m.active ? (nv < V ? nv : V) : 0;
+  return m;
+}
+
+// Vectors past the end of the tensor (u >= nvalid) are pushed out of the descriptor's range
+// through the VGPR offset (+1 GiB; buffers here are < 2 GiB, so no 32-bit wrap): their loads
+// return 0 and their stores are dropped by the hardware range check -- no per-vector branches.
+__device__ __forceinline__ int voff_u(const RowMap& m, int u) { return u < m.nvalid ? m.voff : m.voff + 0x40000000; }
+
+template <int V>
+__device__ __forceinline__ void load_rows(const uint16_t* __restrict__ p, const Red& R, const RowMap& m, uint4 (&buf)[V]) {
+  const __amdgpu_buffer_rsrc_t rs = rsrc(p, R.M * R.C * 2);
+#pragma unroll
+  for (int u = 0; u < V; ++u) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff_u(m, u), m.sbase + u * m.sstep, 0);
+    buf[u] = make_uint4(v.x, v.y, v.z, v.w);
+  }
+}
+
+// Stores take the whole offset in the VGPR and soffset = 0: with a REGISTER soffset hipcc
+// (ROCm 7.2, gfx950) omits the wait state between a buffer_store_dwordx4 and a following VALU
+// overwrite of its data VGPRs, and the store then writes the overwritten value (measured:
+// d(residual) lanes corrupted exactly in the dword rewritten right after the store).
+__device__ __forceinline__ void store_raw(__amdgpu_buffer_rsrc_t rs, const RowMap& m, int u, const uint4 w) {
+  __builtin_amdgcn_raw_buffer_store_b128(u32x4{w.x, w.y, w.z, w.w}, rs, voff_u(m, u) + m.sbase + u * m.sstep, 0, 0);
+}
+
+__device__ __forceinline__ void store_row(__amdgpu_buffer_rsrc_t rs, const RowMap& m, int u, const float* v) {
+  uint4 o;
+  o.x = (uint32_t)f32_to_bf16_rne(v[0]) | ((uint32_t)f32_to_bf16_rne(v[1]) << 16);
+  o.y = (uint32_t)f32_to_bf16_rne(v[2]) | ((uint32_t)f32_to_bf16_rne(v[3]) << 16);
+  o.z = (uint32_t)f32_to_bf16_rne(v[4]) | ((uint32_t)f32_to_bf16_rne(v[5]) << 16);
+  o.w = (uint32_t)f32_to_bf16_rne(v[6]) | ((uint32_t)f32_to_bf16_rne(v[7]) << 16);
+  store_raw(rs, m, u, o);
+}
+
+// Per 16-bit half of a packed bf16 pair: 0xffff where the value is > 0 (0 < bits <= +inf:
+// the same set as the fp32 compare `y > 0.f`, NaNs excluded), else 0.
+__device__ __forceinline__ uint32_t relu_mask2(uint32_t y) {
+  const uint32_t l = y & 0xffffu, h = y >> 16;
+  return ((l - 1u) < 0x7f80u ? 0x0000ffffu : 0u) | ((h - 1u) < 0x7f80u ? 0xffff0000u : 0u);
+}
+
+// Opaque to the optimiser: the second pass must re-unpack the packed bf16 registers instead of
+// keeping the first pass's fp32 unpacked copies alive across the wait (2x the registers).
+template <int V>
+__device__ __forceinline__ void launder(uint4 (&b)[V]) {
+#pragma unroll
+  for (int u = 0; u < V; ++u) asm volatile("" : "+v"(b[u].x), "+v"(b[u].y), "+v"(b[u].z), "+v"(b[u].w));
+}
+
+__device__ __forceinline__ Bf8 unpack_bf8(const uint4 u) {
+  Bf8 r;
+  r.v[0] = __uint_as_float(u.x << 16);
+  r.v[1] = __uint_as_float(u.x & 0xffff0000u);
+  r.v[2] = __uint_as_float(u.y << 16);
+  r.v[3] = __uint_as_float(u.y & 0xffff0000u);
+  r.v[4] = __uint_as_float(u.z << 16);
+  r.v[5] = __uint_as_float(u.z & 0xffff0000u);
+  r.v[6] = __uint_as_float(u.w << 16);
+  r.v[7] = __uint_as_float(u.w & 0xffff0000u);
+  return r;
+}
+
+// stats finisher body shared by the two forward variants (store = how save[] is written)
+template <typename Store>
+__device__ __forceinline__ void finish_stats(const Red& R, const StatsOut& o, Store store) {
+  const int CT = R.CT, C = R.C;
+  const double* total = R.total + (size_t)blockIdx.y * 2 * CT;
+  const double inv_m = 1.0 / (double)R.M;
+  const double unbias = R.M > 1 ? (double)R.M / (double)(R.M - 1) : 1.0;
+  for (int cl = threadIdx.x; cl < CT; cl += kB) {
+    const int c = blockIdx.y * CT + cl;
+    const double mean = total[cl] * inv_m;
+    const double var = fmax(total[CT + cl] * inv_m - mean * mean, 0.0);
+    const float invstd = (float)(1.0 / sqrt(var + (double)o.eps));
+    const float ga = o.gamma ? o.gamma[c] : 1.f;
+    const float be = o.beta ? o.beta[c] : 0.f;
+    const float scale = ga * invstd;
+    store(o.save + c, (float)mean);
+    store(o.save + C + c, invstd);
+    store(o.save + 2 * C + c, scale);
+    store(o.save + 3 * C + c, be - (float)mean * scale);
+    if (o.running_mean) {
+      o.running_mean[c] = (1.f - o.momentum) * o.running_mean[c] + o.momentum * (float)mean;
+      o.running_var[c] = (1.f - o.momentum) * o.running_var[c] + o.momentum * (float)(var * unbias);
+    }
+  }
+  if (threadIdx.x == 0 && blockIdx.y == 0 && o.nbt) *o.nbt += 1;
+}
+
+template <int V, bool RELU, bool RES>
+__global__ __launch_bounds__(kB) void bn_fwd_fused_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
+                                                          Red R, StatsOut o, uint16_t* __restrict__ y) {
+  const RowMap m = row_map(R, V);
+  uint4 xb[V];
+  uint4 rb[RES ? V : 1];
+  load_rows<V>(x, R, m, xb);
+  if constexpr (RES) load_rows<V>(res, R, m, rb);  // in flight across the reduction
+  float s[8], q[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
+#pragma unroll
+  for (int u = 0; u < V; ++u) {
+    const Bf8 v = unpack_bf8(xb[u]);  // rows past the end are zeros: no effect on the sums
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s[j] += v.v[j];
+      q[j] = fmaf(v.v[j], v.v[j], q[j]);
+    }
+  }
+  const Flag f = tile_flag(R);
+  if (block_reduce_tree(R, s, q)) {
+    finish_stats(R, o, [](float* p, float v) { store_sc1(p, v); });
+    publish(f);
+  }
+  wait_published(f);
+  launder(xb);
+  float sc[8], sh[8];
+  if (m.active) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sc[j] = ld_sc1(o.save + 2 * R.C + m.col + j);
+      sh[j] = ld_sc1(o.save + 3 * R.C + m.col + j);
+    }
+  }
+  const __amdgpu_buffer_rsrc_t ys = rsrc(y, R.M * R.C * 2);
+#pragma unroll
+  for (int u = 0; u < V; ++u) {
+    const Bf8 v = unpack_bf8(xb[u]);
+    float out[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out[j] = fmaf(v.v[j], sc[j], sh[j]);
+    if constexpr (RES) {
+      const Bf8 rr = unpack_bf8(rb[u]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) out[j] += rr.v[j];
+    }
+    if constexpr (RELU) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) out[j] = fmaxf(out[j], 0.f);
+    }
+    store_row(ys, m, u, out);
+  }
+}
+
+template <int V, bool RELU, bool RES>
+__global__ __launch_bounds__(kB) void bn_bwd_fused_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
+                                                          const uint16_t* __restrict__ y, Red R, GradOut o,
+                                                          uint16_t* __restrict__ dx, uint16_t* __restrict__ dres) {
+  const RowMap m = row_map(R, V);
+  uint4 db[V], xb[V];
+  load_rows<V>(dy, R, m, db);
+  load_rows<V>(x, R, m, xb);
+  if constexpr (RELU) {  // db <- dz = dy * [y > 0], exact in bf16: y is not needed afterwards
+    uint4 yb[V];
+    load_rows<V>(y, R, m, yb);
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+      db[u].x &= relu_mask2(yb[u].x);
+      db[u].y &= relu_mask2(yb[u].y);
+      db[u].z &= relu_mask2(yb[u].z);
+      db[u].w &= relu_mask2(yb[u].w);
+    }
+  }
+  float mu[8], s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    mu[j] = m.active ? o.save[m.col + j] : 0.f;
+    s1[j] = s2[j] = 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < V; ++u) {
+    const Bf8 d = unpack_bf8(db[u]), v = unpack_bf8(xb[u]);  // zeros past the end
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s1[j] += d.v[j];
+      s2[j] = fmaf(d.v[j], v.v[j] - mu[j], s2[j]);
+    }
+  }
+  const Flag f = tile_flag(R);
+  if (block_reduce_tree(R, s1, s2)) {
+    const int CT = R.CT, C = R.C;
+    const double* total = R.total + (size_t)blockIdx.y * 2 * CT;
+    const double inv_m = 1.0 / (double)R.M;
+    for (int cl = threadIdx.x; cl < CT; cl += kB) {
+      const int c = blockIdx.y * CT + cl;
+      const double S1 = total[cl], S2 = total[CT + cl];
+      const float mean = o.save[c], invstd = o.save[C + c];
+      const float ga = o.gamma ? o.gamma[c] : 1.f;
+      const double dg = S2 * (double)invstd;
+      if (o.dgamma) o.dgamma[c] = (float)dg;
+      if (o.dbeta) o.dbeta[c] = (float)S1;
+      const double a = (double)ga * invstd;
+      const double b = -a * invstd * dg * inv_m;
+      store_sc1(o.coef + c, (float)a);
+      store_sc1(o.coef + C + c, (float)b);
+      store_sc1(o.coef + 2 * C + c, (float)(-a * S1 * inv_m - b * mean));
+    }
+    publish(f);
+  }
+  wait_published(f);
+  launder(db);
+  launder(xb);
+  float ca[8], cb[8], cc[8];
+  if (m.active) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ca[j] = ld_sc1(o.coef + m.col + j);
+      cb[j] = ld_sc1(o.coef + R.C + m.col + j);
+      cc[j] = ld_sc1(o.coef + 2 * R.C + m.col + j);
+    }
+  }
+  const __amdgpu_buffer_rsrc_t dxs = rsrc(dx, R.M * R.C * 2);
+  const __amdgpu_buffer_rsrc_t drs = rsrc(RES ? dres : dx, R.M * R.C * 2);
+#pragma unroll
+  for (int u = 0; u < V; ++u) {
+    const Bf8 d = unpack_bf8(db[u]), v = unpack_bf8(xb[u]);
+    const float* dz = d.v;
+    float out[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out[j] = fmaf(ca[j], dz[j], fmaf(cb[j], v.v[j], cc[j]));
+    store_row(dxs, m, u, out);
+    if constexpr (RES) store_raw(drs, m, u, db[u]);  // d(residual) = dz, already bf16-exact
+  }
+}
+
 // ---------------------------------------------------------------- host-side geometry
 // Arrival counters: a device pool of per-launch slots (kSlotWords counters each) taken
 // round-robin; the final blocks re-arm their tile's counters, so graph replays reuse a slot and
@@ -454,7 +774,8 @@ unsigned* next_slot(hipStream_t stream) {
 }
 
 // Grid and tree shape.  Target >= ~512 blocks (2 per CU) with 4..16 16-B vectors per thread.
-Red plan(int64_t M, int C) {
+// `fused_v` > 0: single-launch layout, exactly V row-vectors per thread (rows_per_blk = rpi*V).
+Red plan(int64_t M, int C, int fused_v = 0) {
   Red R{};
   R.M = M;
   R.C = C;
@@ -463,17 +784,22 @@ Red plan(int64_t M, int C) {
   R.tprp = 1;
   while (R.tprp < R.CT / 8) R.tprp <<= 1;
   R.rpi = kB / R.tprp;
-  const int64_t n_vec = M * C / 8;
-  int64_t vpt = n_vec / ((int64_t)kB * 512);
-  if (vpt < 4) vpt = 4;
-  if (vpt > 16) vpt = 16;
-  const int64_t per_blk = R.rpi * vpt;
-  int64_t nc = (M + per_blk - 1) / per_blk;
-  if (nc * tiles > 2048) nc = (2048 + tiles - 1) / tiles;
-  if (nc < 1) nc = 1;
-  int64_t rpb = (M + nc - 1) / nc;
-  rpb = (rpb + R.rpi - 1) / R.rpi * R.rpi;
-  nc = (M + rpb - 1) / rpb;
+  int64_t rpb;
+  if (fused_v > 0) {
+    rpb = (int64_t)R.rpi * fused_v;
+  } else {
+    const int64_t n_vec = M * C / 8;
+    int64_t vpt = n_vec / ((int64_t)kB * 512);
+    if (vpt < 4) vpt = 4;
+    if (vpt > 16) vpt = 16;
+    const int64_t per_blk = R.rpi * vpt;
+    int64_t nc = (M + per_blk - 1) / per_blk;
+    if (nc * tiles > 2048) nc = (2048 + tiles - 1) / tiles;
+    if (nc < 1) nc = 1;
+    rpb = (M + nc - 1) / nc;
+    rpb = (rpb + R.rpi - 1) / R.rpi * R.rpi;
+  }
+  const int64_t nc = (M + rpb - 1) / rpb;
   R.rows_per_blk = rpb;
   R.nchunks = (int)(nc < 1 ? 1 : nc);
   int gs = 1;
@@ -486,6 +812,93 @@ Red plan(int64_t M, int C) {
   R.gsize = gs;
   R.ngroups = ng;
   return R;
+}
+
+// Single-launch eligibility: the smallest V in {2, 4, 8, 16 (forward only)} whose grid fits in
+// half of the kernel's device-wide occupancy (see bn_fwd_fused_kernel); 0 = two-kernel path.
+constexpr int kFusedVs[4] = {2, 4, 8, 16};
+
+struct FusedCaps {
+  int cap[2][4] = {};  // [bwd][v index] resident-block budget
+  int target = 256;    // preferred maximum grid (= CUs)
+  bool init = false;
+};
+FusedCaps g_caps[64];
+
+template <typename K>
+int half_occupancy(K kernel, int cus) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kB, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return per_cu * cus / 2;
+}
+
+int g_fused_mode = -1;  // -1: from GRACE_BN_FUSED (default on), 0 off, 1 on
+
+template <int V>
+int fwd_cap(int cus) {
+  return std::min(std::min(half_occupancy(bn_fwd_fused_kernel<V, true, true>, cus),
+                           half_occupancy(bn_fwd_fused_kernel<V, true, false>, cus)),
+                  std::min(half_occupancy(bn_fwd_fused_kernel<V, false, true>, cus),
+                           half_occupancy(bn_fwd_fused_kernel<V, false, false>, cus)));
+}
+
+template <int V>
+int bwd_cap(int cus) {
+  return std::min(std::min(half_occupancy(bn_bwd_fused_kernel<V, true, true>, cus),
+                           half_occupancy(bn_bwd_fused_kernel<V, true, false>, cus)),
+                  std::min(half_occupancy(bn_bwd_fused_kernel<V, false, true>, cus),
+                           half_occupancy(bn_bwd_fused_kernel<V, false, false>, cus)));
+}
+
+bool fused_enabled() {
+  if (g_fused_mode < 0) {
+    const char* e = getenv("GRACE_BN_FUSED");
+    g_fused_mode = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_fused_mode == 1;
+}
+
+const FusedCaps& caps() {
+  int dev = 0;
+  GRACE_HIP_CHECK(hipGetDevice(&dev));
+  FusedCaps& c = g_caps[dev];
+  if (!c.init) {
+    int cus = 0;
+    GRACE_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    c.target = cus;
+    // the most register-hungry instance of each (direction, V) bounds that V
+    c.cap[0][0] = fwd_cap<2>(cus);
+    c.cap[0][1] = fwd_cap<4>(cus);
+    c.cap[0][2] = fwd_cap<8>(cus);
+    c.cap[0][3] = fwd_cap<16>(cus);
+    c.cap[1][0] = bwd_cap<2>(cus);
+    c.cap[1][1] = bwd_cap<4>(cus);
+    c.cap[1][2] = bwd_cap<8>(cus);
+    c.cap[1][3] = 0;  // 3 operands x 16 vectors: too many registers
+    c.init = true;
+  }
+  return c;
+}
+
+int pick_fused_v(int64_t M, int C, bool bwd) {
+  if (!fused_enabled() || M * C * 2 >= ((int64_t)1 << 31)) return 0;  // 32-bit buffer offsets
+  const FusedCaps& c = caps();
+  const int tiles = C / (C < kTileC ? C : kTileC);
+  for (int i = 0; i < 4; ++i) {
+    const Red R = plan(M, C, kFusedVs[i]);
+    const int64_t blocks = (int64_t)R.nchunks * tiles;
+    // Only full blocks (V >= 8) at 1/2 - 1 block per CU pay for the hand-off: measured on MI355X
+    // (benchmarks/bnact_bench.py, graph-replayed, ResNet-50 batch 32) V = 8/16 at 196-200 blocks
+    // beat the two-kernel path by 1.5-3.5 us per pass; V = 2/4 grids (196-784 blocks of thin
+    // blocks) lost 1-3 us, as did any grid of > 1 block per CU.
+    if (kFusedVs[i] < 8) continue;
+    if (c.cap[bwd][i] > 0 && blocks <= std::min(c.cap[bwd][i], c.target) && 2 * blocks >= c.target)
+      return kFusedVs[i];
+  }
+  return 0;
 }
 
 int64_t even(int64_t n) { return (n + 1) & ~(int64_t)1; }
@@ -523,14 +936,50 @@ int apply_grid(int64_t n_vec, int C) {
 
 bool bn_supported(int C) { return C > 0 && C % 8 == 0 && C <= kMaxC && (C <= kTileC || C % kTileC == 0); }
 
-int64_t bn_workspace_floats(int64_t M, int C) { return ws_floats(plan(M, C)); }
+int64_t bn_workspace_floats(int64_t M, int C) {
+  int64_t w = ws_floats(plan(M, C));
+  for (int v : kFusedVs) w = std::max(w, ws_floats(plan(M, C, v)));
+  return w;
+}
+
+int bn_fused_v(int64_t M, int C, bool bwd) { return pick_fused_v(M, C, bwd); }
+
+void bn_set_fused(bool on) { g_fused_mode = on ? 1 : 0; }
+
+unsigned bn_spin_timeouts() {
+  unsigned h = 0;
+  GRACE_HIP_CHECK(hipMemcpyFromSymbol(&h, HIP_SYMBOL(g_bn_spin_timeouts), sizeof(h), 0, hipMemcpyDeviceToHost));
+  return h;
+}
 
 void bn_act_forward(const uint16_t* x, const uint16_t* res, int64_t M, int C, const float* gamma, const float* beta,
                     float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps, bool relu,
                     float* save, float* ws, uint16_t* y, hipStream_t stream) {
+  StatsOut o{gamma, beta, running_mean, running_var, nbt, momentum, eps, save};
+  if (const int v = pick_fused_v(M, C, false)) {
+    Red R = plan(M, C, v);
+    bind_ws(R, ws, stream);
+    const dim3 grid(R.nchunks, C / R.CT);
+#define GRACE_BN_FWD(V)                                                                                        \
+  if (v == V) {                                                                                                \
+    if (relu && res)                                                                                           \
+      hipLaunchKernelGGL((bn_fwd_fused_kernel<V, true, true>), grid, dim3(kB), 0, stream, x, res, R, o, y);    \
+    else if (relu)                                                                                             \
+      hipLaunchKernelGGL((bn_fwd_fused_kernel<V, true, false>), grid, dim3(kB), 0, stream, x, res, R, o, y);   \
+    else if (res)                                                                                              \
+      hipLaunchKernelGGL((bn_fwd_fused_kernel<V, false, true>), grid, dim3(kB), 0, stream, x, res, R, o, y);   \
+    else                                                                                                       \
+      hipLaunchKernelGGL((bn_fwd_fused_kernel<V, false, false>), grid, dim3(kB), 0, stream, x, res, R, o, y);  \
+    return;                                                                                                    \
+  }
+    GRACE_BN_FWD(2)
+    GRACE_BN_FWD(4)
+    GRACE_BN_FWD(8)
+    GRACE_BN_FWD(16)
+#undef GRACE_BN_FWD
+  }
   Red R = plan(M, C);
   bind_ws(R, ws, stream);
-  StatsOut o{gamma, beta, running_mean, running_var, nbt, momentum, eps, save};
   hipLaunchKernelGGL(bn_stats_kernel, dim3(R.nchunks, C / R.CT), dim3(kB), 0, stream, x, R, o);
   const int64_t n_vec = M * C / 8;
   const int gb = apply_grid(n_vec, C);
@@ -547,9 +996,30 @@ void bn_act_forward(const uint16_t* x, const uint16_t* res, int64_t M, int C, co
 void bn_act_backward(const uint16_t* dy, const uint16_t* x, const uint16_t* y, int64_t M, int C, const float* gamma,
                      const float* save, bool relu, float* dgamma, float* dbeta, float* coef, float* ws,
                      uint16_t* dx, uint16_t* dres, hipStream_t stream) {
+  GradOut o{gamma, save, dgamma, dbeta, coef};
+  if (const int v = pick_fused_v(M, C, true)) {
+    Red R = plan(M, C, v);
+    bind_ws(R, ws, stream);
+    const dim3 grid(R.nchunks, C / R.CT);
+#define GRACE_BN_BWD(V)                                                                                           \
+  if (v == V) {                                                                                                   \
+    if (relu && dres)                                                                                             \
+      hipLaunchKernelGGL((bn_bwd_fused_kernel<V, true, true>), grid, dim3(kB), 0, stream, dy, x, y, R, o, dx, dres);   \
+    else if (relu)                                                                                                \
+      hipLaunchKernelGGL((bn_bwd_fused_kernel<V, true, false>), grid, dim3(kB), 0, stream, dy, x, y, R, o, dx, dres);  \
+    else if (dres)                                                                                                \
+      hipLaunchKernelGGL((bn_bwd_fused_kernel<V, false, true>), grid, dim3(kB), 0, stream, dy, x, y, R, o, dx, dres);  \
+    else                                                                                                          \
+      hipLaunchKernelGGL((bn_bwd_fused_kernel<V, false, false>), grid, dim3(kB), 0, stream, dy, x, y, R, o, dx, dres); \
+    return;                                                                                                       \
+  }
+    GRACE_BN_BWD(2)
+    GRACE_BN_BWD(4)
+    GRACE_BN_BWD(8)
+#undef GRACE_BN_BWD
+  }
   Red R = plan(M, C);
   bind_ws(R, ws, stream);
-  GradOut o{gamma, save, dgamma, dbeta, coef};
   const dim3 grid(R.nchunks, C / R.CT);
   if (relu)
     hipLaunchKernelGGL(bn_reduce_kernel<true>, grid, dim3(kB), 0, stream, dy, x, y, R, o);

@@ -153,11 +153,12 @@ def default_comm() -> Comm:
     if _DEFAULT is not None:
         return _DEFAULT
     if dist.is_available() and dist.is_initialized():
-        if os.environ.get("GRACE_AMD_COMM", "torch") == "native":
+        mode = os.environ.get("GRACE_AMD_COMM", "torch")
+        if mode in ("native", "native-inline"):
             from .native_comm import RcclComm
 
             # one communicator per process (cached: every caller shares its stream)
-            _DEFAULT = RcclComm.from_process_group()
+            _DEFAULT = RcclComm.from_process_group(inline=mode == "native-inline")
             return _DEFAULT
         return TorchComm()
     return LocalComm()

@@ -67,6 +67,43 @@ def test_native_comm_drives_grace(nccl_group):
     torch.testing.assert_close(out, torch.where(g >= 0, 1.0, -1.0))
 
 
+def test_native_inline_comm_in_graph(nccl_group):
+    """Inline mode: collectives on the caller's stream, so a whole training step with the RCCL
+    all-gather inside is captured in one HIP graph without an event fork/join (bench.py's
+    --comm native-inline); replays train exactly like the local (no-collective) comm."""
+    from grace_amd import grace_from_params
+    from grace_amd.parallel import DistributedOptimizer
+    from grace_amd.parallel.comm import LocalComm
+    from grace_amd.parallel.graph import GraphedStep
+    from grace_amd.parallel.native_comm import RcclComm
+
+    c = RcclComm.from_process_group(inline=True)
+    assert c.inline
+    p = {"compressor": "topk", "compress_ratio": 0.1, "memory": "residual", "communicator": "allgather"}
+    x, y = _data()
+    models = []
+    for comm in (LocalComm(), c):
+        m = _net()
+        o = DistributedOptimizer(torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.5),
+                                 grace_from_params(p, comm=comm), named_parameters=m.named_parameters())
+
+        def step():
+            o.zero_grad()
+            loss = F.cross_entropy(m(x), y)
+            loss.backward()
+            o.step()
+            return loss
+
+        run = GraphedStep(step, warmup=3)
+        for _ in range(5):
+            run()
+        torch.cuda.synchronize()
+        models.append(m)
+    for a, b in zip(models[0].parameters(), models[1].parameters()):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
+    c.check()
+
+
 def test_ddp_hook_gpu(nccl_group):
     from grace_amd import grace_from_params
     from grace_amd.parallel import GraceHookState, grace_comm_hook

@@ -43,7 +43,8 @@ def _reference(m, x, res, dy, relu):
 
 
 @pytest.mark.parametrize("shape", [(4, 64, 9, 9), (2, 256, 7, 5), (3, 2048, 3, 3), (1, 8, 2, 3), (8, 96, 4, 4),
-                                   (32, 128, 28, 28), (32, 1024, 14, 14), (16, 512, 17, 3), (32, 64, 112, 112)])
+                                   (32, 128, 28, 28), (32, 1024, 14, 14), (16, 512, 17, 3), (32, 64, 112, 112),
+                                   (32, 64, 56, 56), (32, 2048, 7, 7), (31, 512, 14, 13)])
 @pytest.mark.parametrize("relu,with_res", [(False, False), (True, False), (True, True), (False, True)])
 def test_bnact_matches_fp32_reference(shape, relu, with_res):
     assert _native.available()
@@ -70,6 +71,57 @@ def test_bnact_matches_fp32_reference(shape, relu, with_res):
     torch.testing.assert_close(xx.grad.float(), dx0, rtol=2e-2, atol=3e-2 * dx0.abs().max().item() + 1e-3)
     if res is not None:
         torch.testing.assert_close(rr.grad.float(), dr0, rtol=1e-2, atol=1e-2)
+
+
+@pytest.fixture
+def two_kernel_path():
+    _native.lib().bn_set_fused(False)
+    yield
+    _native.lib().bn_set_fused(True)
+
+
+def test_single_launch_path_selected():
+    """The co-resident single-launch kernels take the small/medium ResNet-50 shapes; the
+    largest stage-1 shapes keep the two-kernel path."""
+    C = _native.lib()
+    for (n, c, h, w) in [(32, 128, 28, 28), (32, 2048, 7, 7), (32, 512, 14, 14)]:
+        assert C.bn_fused_v(n * h * w, c, False) >= 8, (n, c, h, w)
+        assert C.bn_fused_v(n * h * w, c, True) >= 8, (n, c, h, w)
+    assert C.bn_fused_v(32 * 56 * 56, 64, False) == 16
+    assert C.bn_fused_v(32 * 112 * 112, 64, False) == 0
+    assert C.bn_fused_v(32 * 56 * 56, 256, True) == 0
+    assert C.bn_fused_v(32 * 7 * 7, 512, False) == 0  # thin grid: two kernels are faster
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 9, 9), (2, 256, 7, 5), (3, 2048, 3, 3), (32, 128, 28, 28)])
+@pytest.mark.parametrize("relu,with_res", [(False, False), (True, True)])
+def test_bnact_two_kernel_path_matches(shape, relu, with_res, two_kernel_path):
+    test_bnact_matches_fp32_reference(shape, relu, with_res)
+
+
+def test_single_launch_matches_two_kernel_path():
+    """Both layouts fold the same sums in a fixed (different) order: outputs agree to bf16
+    rounding, statistics to fp32 rounding."""
+    C = _native.lib()
+    outs = []
+    for fused in (True, False):
+        C.bn_set_fused(fused)
+        try:
+            m, x, res, dy = _case(32, 128, 28, 28, True, True, seed=5)
+            xx = x.clone().requires_grad_(True)
+            y = m(xx, res)
+            y.backward(dy)
+            torch.cuda.synchronize()
+            outs.append((y.float(), xx.grad.float(), m.weight.grad, m.bias.grad, m.running_var.clone()))
+        finally:
+            C.bn_set_fused(True)
+    for a, b in zip(*outs):
+        torch.testing.assert_close(a, b, rtol=1e-2, atol=2e-2)
+    assert C.bn_spin_timeouts() == 0
+
+
+def test_no_spin_timeouts():
+    assert _native.lib().bn_spin_timeouts() == 0
 
 
 def test_bnact_graph_replay():
