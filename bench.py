@@ -138,7 +138,19 @@ def main():
             from grace_amd.parallel import set_default_comm
             from grace_amd.parallel.native_comm import RcclComm
 
-            set_default_comm(RcclComm.from_process_group(inline=comm_kind == "native-inline"))
+            try:
+                native = RcclComm.from_process_group(inline=comm_kind == "native-inline")
+                ok = 1
+            except Exception as e:  # every rank must agree before the first GRACE collective
+                print(f"[rank {rank}] native RCCL comm unavailable ({type(e).__name__}: {str(e)[:120]}); "
+                      f"using torch.distributed", file=sys.stderr, flush=True)
+                native, ok = None, 0
+            flag = torch.tensor([ok], device=dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            if flag.item() == 1:
+                set_default_comm(native)
+            else:
+                comm_kind = "torch (native comm failed)"
     grc = grace_from_params(dict(w.grace, world_size=world))
     opt = DistributedOptimizer(base_opt, grc, named_parameters=named,
                                bucket_cap_mb=args.bucket_mb, overlap=overlap, weights=weights)

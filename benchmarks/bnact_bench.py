@@ -4,10 +4,10 @@ on every BatchNorm shape of ResNet-50 at batch 32 (bf16, channels_last).
 
     python benchmarks/bnact_bench.py [--batch 32] [--iters 50]
 
-Columns: shape, forward / backward microseconds for the fused kernels (the default dispatch:
-single-launch where the grid fits co-resident, else two kernels), the fused kernels forced onto
-the two-kernel path, and stock (MIOpen + elementwise); the default path's effective HBM rate
-(bytes the two-kernel path must move / time).
+Columns: shape, forward / backward microseconds for the fused kernels with the opt-in
+single-launch variants enabled (used where the grid fits co-resident with full blocks; V f/b =
+vectors per thread, 0 = two kernels), the fused kernels on the two-kernel path (the default), and
+stock (MIOpen + elementwise); the first column's effective HBM rate.
 """
 import argparse
 import os
@@ -81,7 +81,7 @@ def main():
         res_t = {}
         for force in ("0", "2", "1"):
             os.environ["GRACE_AMD_FORCE_TORCH"] = "1" if force == "1" else "0"
-            lib.bn_set_fused(force != "2")
+            lib.bn_set_fused(force == "0")
 
             def fwd():
                 with torch.no_grad():
@@ -99,6 +99,7 @@ def main():
         lib.bn_set_fused(True)
         M = a.batch * h * w
         vf, vb = lib.bn_fused_v(M, c, False), lib.bn_fused_v(M, c, True)
+        lib.bn_set_fused(False)
         nbytes = x.numel() * 2
         fwd_bytes = nbytes * (3 + (1 if res else 0))           # stats read, apply read+write (+res)
         bwd_bytes = nbytes * ((3 if relu else 2) * 2 + 1 + (1 if res else 0))  # reduce + dx reads, dx (+dres) write

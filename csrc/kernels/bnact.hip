@@ -74,6 +74,29 @@ __device__ __forceinline__ void store_bf8(uint16_t* p, const float* v) {
   *reinterpret_cast<uint4*>(p) = u;
 }
 
+__device__ __forceinline__ uint4 pack_bf8(const float* v) {
+  uint4 u;
+  u.x = (uint32_t)f32_to_bf16_rne(v[0]) | ((uint32_t)f32_to_bf16_rne(v[1]) << 16);
+  u.y = (uint32_t)f32_to_bf16_rne(v[2]) | ((uint32_t)f32_to_bf16_rne(v[3]) << 16);
+  u.z = (uint32_t)f32_to_bf16_rne(v[4]) | ((uint32_t)f32_to_bf16_rne(v[5]) << 16);
+  u.w = (uint32_t)f32_to_bf16_rne(v[6]) | ((uint32_t)f32_to_bf16_rne(v[7]) << 16);
+  return u;
+}
+
+// ReLU mask of 8 packed bf16 outputs: bit j = (y_j > 0), i.e. 0 < bits <= +inf (the fp32
+// compare `y > 0.f` on the rounded output, NaNs excluded).  The backward reads these 1-bit
+// masks (M*C/8 bytes) instead of the bf16 output (2*M*C bytes) in both of its passes.
+__device__ __forceinline__ uint32_t pos_bits(uint32_t w) {
+  return ((w & 0xffffu) - 1u < 0x7f80u ? 1u : 0u) | ((w >> 16) - 1u < 0x7f80u ? 2u : 0u);
+}
+__device__ __forceinline__ uint8_t relu_byte(const uint4 u) {
+  return (uint8_t)(pos_bits(u.x) | (pos_bits(u.y) << 2) | (pos_bits(u.z) << 4) | (pos_bits(u.w) << 6));
+}
+// mask byte -> per-dword AND masks for the packed bf16 pairs (channels 2k, 2k+1)
+__device__ __forceinline__ uint32_t pair_mask(uint32_t mb, int k) {
+  return ((mb >> (2 * k)) & 1u ? 0x0000ffffu : 0u) | ((mb >> (2 * k + 1)) & 1u ? 0xffff0000u : 0u);
+}
+
 template <typename T>
 __device__ __forceinline__ void store_sc1(T* p, T v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -296,7 +319,7 @@ __global__ __launch_bounds__(kB) void bn_stats_kernel(const uint16_t* __restrict
 template <bool RELU, bool RES>
 __global__ __launch_bounds__(kB) void bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
                                                       const float* __restrict__ save, uint16_t* __restrict__ y,
-                                                      int64_t n_vec, int C) {
+                                                      uint8_t* __restrict__ mask, int64_t n_vec, int C) {
   const int tpr = C >> 3;
   const int64_t stride = (int64_t)gridDim.x * kB;
   int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x;
@@ -322,7 +345,9 @@ __global__ __launch_bounds__(kB) void bn_apply_kernel(const uint16_t* __restrict
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = fmaxf(o[j], 0.f);
     }
-    store_bf8(y + i * 8, o);
+    const uint4 u = pack_bf8(o);
+    *reinterpret_cast<uint4*>(y + i * 8) = u;
+    if constexpr (RELU) mask[i] = relu_byte(u);
   }
 }
 
@@ -336,7 +361,7 @@ struct GradOut {
 
 template <bool RELU>
 __global__ __launch_bounds__(kB) void bn_reduce_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
-                                                       const uint16_t* __restrict__ y, Red R, GradOut o) {
+                                                       const uint8_t* __restrict__ mask, Red R, GradOut o) {
   float s1[8], s2[8], mu[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) s1[j] = s2[j] = mu[j] = 0.f;
@@ -347,30 +372,31 @@ __global__ __launch_bounds__(kB) void bn_reduce_kernel(const uint16_t* __restric
       for (int j = 0; j < 8; ++j) mu[j] = o.save[blockIdx.y * R.CT + cg * 8 + j];
     }
   }
-  auto acc = [&](const Bf8& d, const Bf8& v, const Bf8& w) {
+  auto acc = [&](const Bf8& d, const Bf8& v, uint32_t mb) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float dz = d.v[j];
-      if constexpr (RELU) dz = w.v[j] > 0.f ? dz : 0.f;
+      if constexpr (RELU) dz = (mb >> j) & 1u ? dz : 0.f;
       s1[j] += dz;
       s2[j] = fmaf(dz, v.v[j] - mu[j], s2[j]);
     }
   };
   for_rows(R, [&](int64_t e, int64_t step, int n) {
     if (n == 4) {
-      Bf8 d[4], v[4], w[4];
+      Bf8 d[4], v[4];
+      uint32_t w[4] = {0, 0, 0, 0};
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         d[u] = load_bf8(dy + e + u * step);
         v[u] = load_bf8(x + e + u * step);
-        if constexpr (RELU) w[u] = load_bf8(y + e + u * step);
+        if constexpr (RELU) w[u] = mask[(e + u * step) >> 3];
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc(d[u], v[u], w[u]);
     } else {
       const Bf8 d = load_bf8(dy + e), v = load_bf8(x + e);
-      Bf8 w;
-      if constexpr (RELU) w = load_bf8(y + e);
+      uint32_t w = 0;
+      if constexpr (RELU) w = mask[e >> 3];
       acc(d, v, w);
     }
   });
@@ -396,7 +422,7 @@ __global__ __launch_bounds__(kB) void bn_reduce_kernel(const uint16_t* __restric
 
 template <bool RELU, bool RES>
 __global__ __launch_bounds__(kB) void bn_dx_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
-                                                   const uint16_t* __restrict__ y, const float* __restrict__ coef,
+                                                   const uint8_t* __restrict__ mask, const float* __restrict__ coef,
                                                    uint16_t* __restrict__ dx, uint16_t* __restrict__ dres,
                                                    int64_t n_vec, int C) {
   const int tpr = C >> 3;
@@ -415,9 +441,9 @@ __global__ __launch_bounds__(kB) void bn_dx_kernel(const uint16_t* __restrict__ 
     const Bf8 v = load_bf8(x + i * 8);
     float dz[8], o[8];
     if constexpr (RELU) {
-      const Bf8 w = load_bf8(y + i * 8);
+      const uint32_t mb = mask[i];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) dz[j] = w.v[j] > 0.f ? d.v[j] : 0.f;
+      for (int j = 0; j < 8; ++j) dz[j] = (mb >> j) & 1u ? d.v[j] : 0.f;
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) dz[j] = d.v[j];
@@ -502,6 +528,7 @@ struct RowMap {
   int sbase;   // bytes: block's first row * C * 2   (wave-uniform)
   int sstep;   // bytes: rpi * C * 2                (wave-uniform)
   int nvalid;  // vectors of this thread inside the tensor (<= V)
+  int64_t row0;  // this thread's first row
   int64_t col;
   bool active;
 };
@@ -519,6 +546,7 @@ __device__ __forceinline__ RowMap row_map(const Red& R, int V) {
   m.voff = (int)(((int64_t)rs * R.C + m.col) * 2);
   m.sbase = (int)(b0 * R.C * 2);
   m.sstep = R.rpi * R.C * 2;
+  m.row0 = b0 + rs;
   const int64_t left = R.M - (b0 + rs);  // rows from this thread's first row to the end
   int nv = left <= 0 ? 0 : (int)((left + R.rpi - 1) / R.rpi);
   m.nvalid = m.active ? (nv < V ? nv : V) : 0;
@@ -555,13 +583,6 @@ __device__ __forceinline__ void store_row(__amdgpu_buffer_rsrc_t rs, const RowMa
   o.z = (uint32_t)f32_to_bf16_rne(v[4]) | ((uint32_t)f32_to_bf16_rne(v[5]) << 16);
   o.w = (uint32_t)f32_to_bf16_rne(v[6]) | ((uint32_t)f32_to_bf16_rne(v[7]) << 16);
   store_raw(rs, m, u, o);
-}
-
-// Per 16-bit half of a packed bf16 pair: 0xffff where the value is > 0 (0 < bits <= +inf:
-// the same set as the fp32 compare `y > 0.f`, NaNs excluded), else 0.
-__device__ __forceinline__ uint32_t relu_mask2(uint32_t y) {
-  const uint32_t l = y & 0xffffu, h = y >> 16;
-  return ((l - 1u) < 0x7f80u ? 0x0000ffffu : 0u) | ((h - 1u) < 0x7f80u ? 0xffff0000u : 0u);
 }
 
 // Opaque to the optimiser: the second pass must re-unpack the packed bf16 registers instead of
@@ -614,7 +635,8 @@ __device__ __forceinline__ void finish_stats(const Red& R, const StatsOut& o, St
 
 template <int V, bool RELU, bool RES>
 __global__ __launch_bounds__(kB) void bn_fwd_fused_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
-                                                          Red R, StatsOut o, uint16_t* __restrict__ y) {
+                                                          Red R, StatsOut o, uint16_t* __restrict__ y,
+                                                          uint8_t* __restrict__ mask) {
   const RowMap m = row_map(R, V);
   uint4 xb[V];
   uint4 rb[RES ? V : 1];
@@ -663,27 +685,32 @@ __global__ __launch_bounds__(kB) void bn_fwd_fused_kernel(const uint16_t* __rest
 #pragma unroll
       for (int j = 0; j < 8; ++j) out[j] = fmaxf(out[j], 0.f);
     }
-    store_row(ys, m, u, out);
+    const uint4 pk = pack_bf8(out);
+    store_raw(ys, m, u, pk);
+    if constexpr (RELU)
+      if (u < m.nvalid) mask[(m.row0 + (int64_t)u * R.rpi) * (R.C >> 3) + (m.col >> 3)] = relu_byte(pk);
   }
 }
 
 template <int V, bool RELU, bool RES>
 __global__ __launch_bounds__(kB) void bn_bwd_fused_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
-                                                          const uint16_t* __restrict__ y, Red R, GradOut o,
+                                                          const uint8_t* __restrict__ mask, Red R, GradOut o,
                                                           uint16_t* __restrict__ dx, uint16_t* __restrict__ dres) {
   const RowMap m = row_map(R, V);
   uint4 db[V], xb[V];
   load_rows<V>(dy, R, m, db);
   load_rows<V>(x, R, m, xb);
-  if constexpr (RELU) {  // db <- dz = dy * [y > 0], exact in bf16: y is not needed afterwards
-    uint4 yb[V];
-    load_rows<V>(y, R, m, yb);
+  if constexpr (RELU) {  // db <- dz = dy * [y > 0], exact in bf16
+    uint32_t mb[V];
+#pragma unroll
+    for (int u = 0; u < V; ++u)
+      mb[u] = u < m.nvalid ? mask[(m.row0 + (int64_t)u * R.rpi) * (R.C >> 3) + (m.col >> 3)] : 0u;
 #pragma unroll
     for (int u = 0; u < V; ++u) {
-      db[u].x &= relu_mask2(yb[u].x);
-      db[u].y &= relu_mask2(yb[u].y);
-      db[u].z &= relu_mask2(yb[u].z);
-      db[u].w &= relu_mask2(yb[u].w);
+      db[u].x &= pair_mask(mb[u], 0);
+      db[u].y &= pair_mask(mb[u], 1);
+      db[u].z &= pair_mask(mb[u], 2);
+      db[u].w &= pair_mask(mb[u], 3);
     }
   }
   float mu[8], s1[8], s2[8];
@@ -835,7 +862,10 @@ int half_occupancy(K kernel, int cus) {
   return per_cu * cus / 2;
 }
 
-int g_fused_mode = -1;  // -1: from GRACE_BN_FUSED (default on), 0 off, 1 on
+// Opt-in (GRACE_BN_FUSED=1 or bn_set_fused): on ResNet-50 the eligible layers gain 1.5-3.5 us
+// per pass but the whole-step graph measured no net gain (4165 vs 4183 img/s, within noise),
+// and the co-resident wait is the one place a BN launch could stall behind a persistent kernel.
+int g_fused_mode = -1;  // -1: from GRACE_BN_FUSED (default off), 0 off, 1 on
 
 template <int V>
 int fwd_cap(int cus) {
@@ -856,7 +886,7 @@ int bwd_cap(int cus) {
 bool fused_enabled() {
   if (g_fused_mode < 0) {
     const char* e = getenv("GRACE_BN_FUSED");
-    g_fused_mode = (e && e[0] == '0') ? 0 : 1;
+    g_fused_mode = (e && e[0] == '1') ? 1 : 0;
   }
   return g_fused_mode == 1;
 }
@@ -954,7 +984,7 @@ unsigned bn_spin_timeouts() {
 
 void bn_act_forward(const uint16_t* x, const uint16_t* res, int64_t M, int C, const float* gamma, const float* beta,
                     float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps, bool relu,
-                    float* save, float* ws, uint16_t* y, hipStream_t stream) {
+                    float* save, float* ws, uint16_t* y, uint8_t* mask, hipStream_t stream) {
   StatsOut o{gamma, beta, running_mean, running_var, nbt, momentum, eps, save};
   if (const int v = pick_fused_v(M, C, false)) {
     Red R = plan(M, C, v);
@@ -963,13 +993,13 @@ void bn_act_forward(const uint16_t* x, const uint16_t* res, int64_t M, int C, co
 #define GRACE_BN_FWD(V)                                                                                        \
   if (v == V) {                                                                                                \
     if (relu && res)                                                                                           \
-      hipLaunchKernelGGL((bn_fwd_fused_kernel<V, true, true>), grid, dim3(kB), 0, stream, x, res, R, o, y);    \
+      hipLaunchKernelGGL((bn_fwd_fused_kernel<V, true, true>), grid, dim3(kB), 0, stream, x, res, R, o, y, mask);    \
     else if (relu)                                                                                             \
-      hipLaunchKernelGGL((bn_fwd_fused_kernel<V, true, false>), grid, dim3(kB), 0, stream, x, res, R, o, y);   \
+      hipLaunchKernelGGL((bn_fwd_fused_kernel<V, true, false>), grid, dim3(kB), 0, stream, x, res, R, o, y, mask);   \
     else if (res)                                                                                              \
-      hipLaunchKernelGGL((bn_fwd_fused_kernel<V, false, true>), grid, dim3(kB), 0, stream, x, res, R, o, y);   \
+      hipLaunchKernelGGL((bn_fwd_fused_kernel<V, false, true>), grid, dim3(kB), 0, stream, x, res, R, o, y, mask);   \
     else                                                                                                       \
-      hipLaunchKernelGGL((bn_fwd_fused_kernel<V, false, false>), grid, dim3(kB), 0, stream, x, res, R, o, y);  \
+      hipLaunchKernelGGL((bn_fwd_fused_kernel<V, false, false>), grid, dim3(kB), 0, stream, x, res, R, o, y, mask);  \
     return;                                                                                                    \
   }
     GRACE_BN_FWD(2)
@@ -984,16 +1014,16 @@ void bn_act_forward(const uint16_t* x, const uint16_t* res, int64_t M, int C, co
   const int64_t n_vec = M * C / 8;
   const int gb = apply_grid(n_vec, C);
   if (relu && res)
-    hipLaunchKernelGGL((bn_apply_kernel<true, true>), dim3(gb), dim3(kB), 0, stream, x, res, save, y, n_vec, C);
+    hipLaunchKernelGGL((bn_apply_kernel<true, true>), dim3(gb), dim3(kB), 0, stream, x, res, save, y, mask, n_vec, C);
   else if (relu)
-    hipLaunchKernelGGL((bn_apply_kernel<true, false>), dim3(gb), dim3(kB), 0, stream, x, res, save, y, n_vec, C);
+    hipLaunchKernelGGL((bn_apply_kernel<true, false>), dim3(gb), dim3(kB), 0, stream, x, res, save, y, mask, n_vec, C);
   else if (res)
-    hipLaunchKernelGGL((bn_apply_kernel<false, true>), dim3(gb), dim3(kB), 0, stream, x, res, save, y, n_vec, C);
+    hipLaunchKernelGGL((bn_apply_kernel<false, true>), dim3(gb), dim3(kB), 0, stream, x, res, save, y, mask, n_vec, C);
   else
-    hipLaunchKernelGGL((bn_apply_kernel<false, false>), dim3(gb), dim3(kB), 0, stream, x, res, save, y, n_vec, C);
+    hipLaunchKernelGGL((bn_apply_kernel<false, false>), dim3(gb), dim3(kB), 0, stream, x, res, save, y, mask, n_vec, C);
 }
 
-void bn_act_backward(const uint16_t* dy, const uint16_t* x, const uint16_t* y, int64_t M, int C, const float* gamma,
+void bn_act_backward(const uint16_t* dy, const uint16_t* x, const uint8_t* mask, int64_t M, int C, const float* gamma,
                      const float* save, bool relu, float* dgamma, float* dbeta, float* coef, float* ws,
                      uint16_t* dx, uint16_t* dres, hipStream_t stream) {
   GradOut o{gamma, save, dgamma, dbeta, coef};
@@ -1004,13 +1034,13 @@ void bn_act_backward(const uint16_t* dy, const uint16_t* x, const uint16_t* y, i
 #define GRACE_BN_BWD(V)                                                                                           \
   if (v == V) {                                                                                                   \
     if (relu && dres)                                                                                             \
-      hipLaunchKernelGGL((bn_bwd_fused_kernel<V, true, true>), grid, dim3(kB), 0, stream, dy, x, y, R, o, dx, dres);   \
+      hipLaunchKernelGGL((bn_bwd_fused_kernel<V, true, true>), grid, dim3(kB), 0, stream, dy, x, mask, R, o, dx, dres);   \
     else if (relu)                                                                                                \
-      hipLaunchKernelGGL((bn_bwd_fused_kernel<V, true, false>), grid, dim3(kB), 0, stream, dy, x, y, R, o, dx, dres);  \
+      hipLaunchKernelGGL((bn_bwd_fused_kernel<V, true, false>), grid, dim3(kB), 0, stream, dy, x, mask, R, o, dx, dres);  \
     else if (dres)                                                                                                \
-      hipLaunchKernelGGL((bn_bwd_fused_kernel<V, false, true>), grid, dim3(kB), 0, stream, dy, x, y, R, o, dx, dres);  \
+      hipLaunchKernelGGL((bn_bwd_fused_kernel<V, false, true>), grid, dim3(kB), 0, stream, dy, x, mask, R, o, dx, dres);  \
     else                                                                                                          \
-      hipLaunchKernelGGL((bn_bwd_fused_kernel<V, false, false>), grid, dim3(kB), 0, stream, dy, x, y, R, o, dx, dres); \
+      hipLaunchKernelGGL((bn_bwd_fused_kernel<V, false, false>), grid, dim3(kB), 0, stream, dy, x, mask, R, o, dx, dres); \
     return;                                                                                                       \
   }
     GRACE_BN_BWD(2)
@@ -1022,19 +1052,19 @@ void bn_act_backward(const uint16_t* dy, const uint16_t* x, const uint16_t* y, i
   bind_ws(R, ws, stream);
   const dim3 grid(R.nchunks, C / R.CT);
   if (relu)
-    hipLaunchKernelGGL(bn_reduce_kernel<true>, grid, dim3(kB), 0, stream, dy, x, y, R, o);
+    hipLaunchKernelGGL(bn_reduce_kernel<true>, grid, dim3(kB), 0, stream, dy, x, mask, R, o);
   else
-    hipLaunchKernelGGL(bn_reduce_kernel<false>, grid, dim3(kB), 0, stream, dy, x, y, R, o);
+    hipLaunchKernelGGL(bn_reduce_kernel<false>, grid, dim3(kB), 0, stream, dy, x, mask, R, o);
   const int64_t n_vec = M * C / 8;
   const int gb = apply_grid(n_vec, C);
   if (relu && dres)
-    hipLaunchKernelGGL((bn_dx_kernel<true, true>), dim3(gb), dim3(kB), 0, stream, dy, x, y, coef, dx, dres, n_vec, C);
+    hipLaunchKernelGGL((bn_dx_kernel<true, true>), dim3(gb), dim3(kB), 0, stream, dy, x, mask, coef, dx, dres, n_vec, C);
   else if (relu)
-    hipLaunchKernelGGL((bn_dx_kernel<true, false>), dim3(gb), dim3(kB), 0, stream, dy, x, y, coef, dx, dres, n_vec, C);
+    hipLaunchKernelGGL((bn_dx_kernel<true, false>), dim3(gb), dim3(kB), 0, stream, dy, x, mask, coef, dx, dres, n_vec, C);
   else if (dres)
-    hipLaunchKernelGGL((bn_dx_kernel<false, true>), dim3(gb), dim3(kB), 0, stream, dy, x, y, coef, dx, dres, n_vec, C);
+    hipLaunchKernelGGL((bn_dx_kernel<false, true>), dim3(gb), dim3(kB), 0, stream, dy, x, mask, coef, dx, dres, n_vec, C);
   else
-    hipLaunchKernelGGL((bn_dx_kernel<false, false>), dim3(gb), dim3(kB), 0, stream, dy, x, y, coef, dx, dres, n_vec, C);
+    hipLaunchKernelGGL((bn_dx_kernel<false, false>), dim3(gb), dim3(kB), 0, stream, dy, x, mask, coef, dx, dres, n_vec, C);
 }
 
 }  // namespace grace

@@ -40,7 +40,7 @@ const float* opt_f32(const c10::optional<Tensor>& t, int64_t C, const char* what
   return t->data_ptr<float>();
 }
 
-// returns (y, save[4C] = mean, invstd, scale, shift)
+// returns (y, save[4C] = mean, invstd, scale, shift, relu mask [M*C/8] uint8 (undefined without relu))
 bool bn_supported(int64_t C) { return grace::bn_supported((int)C); }
 
 std::vector<Tensor> bn_act_fwd(const Tensor& x, const c10::optional<Tensor>& res, const c10::optional<Tensor>& weight,
@@ -63,25 +63,29 @@ std::vector<Tensor> bn_act_fwd(const Tensor& x, const c10::optional<Tensor>& res
   Tensor y = at::empty_like(x);
   auto f32 = x.options().dtype(at::kFloat);
   Tensor save = at::empty({4 * C}, f32);
+  // ReLU: 1 bit per element (bit j of byte i = output element 8i+j > 0), read by the backward
+  Tensor mask = relu ? at::empty({M * C / 8}, x.options().dtype(at::kByte)) : Tensor();
   Tensor ws = at::empty({grace::bn_workspace_floats(M, (int)C)}, f32);
   grace::bn_act_forward(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                         has_res ? reinterpret_cast<const uint16_t*>(res->data_ptr()) : nullptr, M, (int)C,
                         opt_f32(weight, C, "weight"), opt_f32(bias, C, "bias"), rm, rv, nb, (float)momentum,
                         (float)eps, relu, save.data_ptr<float>(), ws.data_ptr<float>(),
-                        reinterpret_cast<uint16_t*>(y.data_ptr()), cur_stream());
-  return {y, save};
+                        reinterpret_cast<uint16_t*>(y.data_ptr()),
+                        relu ? mask.data_ptr<uint8_t>() : nullptr, cur_stream());
+  return {y, save, mask};
 }
 
 // returns (dx, dres (undefined unless want_dres), dweight, dbias)
-std::vector<Tensor> bn_act_bwd(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& y,
+std::vector<Tensor> bn_act_bwd(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& mask,
                                const c10::optional<Tensor>& weight, const Tensor& save, bool relu, bool want_dres,
                                bool want_dweight) {
   int64_t M, C;
   check_rows(x, "x", &M, &C);
   same_layout(x, dy, "grad_output");
   if (relu) {
-    TORCH_CHECK(y.has_value() && y->defined(), "relu backward needs the forward output");
-    same_layout(x, *y, "output");
+    TORCH_CHECK(mask.has_value() && mask->defined() && mask->is_cuda() && mask->scalar_type() == at::kByte &&
+                    mask->is_contiguous() && mask->numel() == M * C / 8,
+                "relu backward needs the forward's [M*C/8] uint8 mask");
   }
   TORCH_CHECK(save.is_cuda() && save.scalar_type() == at::kFloat && save.numel() == 4 * C, "save");
   DevGuard guard(x.device());
@@ -94,7 +98,7 @@ std::vector<Tensor> bn_act_bwd(const Tensor& dy, const Tensor& x, const c10::opt
   Tensor ws = at::empty({grace::bn_workspace_floats(M, (int)C)}, f32);
   grace::bn_act_backward(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
                          reinterpret_cast<const uint16_t*>(x.data_ptr()),
-                         relu ? reinterpret_cast<const uint16_t*>(y->data_ptr()) : nullptr, M, (int)C,
+                         relu ? mask->data_ptr<uint8_t>() : nullptr, M, (int)C,
                          opt_f32(weight, C, "weight"), save.data_ptr<float>(), relu,
                          want_dweight ? dg.data_ptr<float>() : nullptr, want_dweight ? db.data_ptr<float>() : nullptr,
                          coef.data_ptr<float>(), ws.data_ptr<float>(), reinterpret_cast<uint16_t*>(dx.data_ptr()),

@@ -10,7 +10,8 @@ it is exactly ``relu(F.batch_norm(x) + residual)``.
 
 Numerics: statistics and the affine are fp32 (fp64 fold of the per-block partial sums), the
 output is rounded to bf16 once (the unfused bf16 path rounds after BN, after the add and after
-the ReLU); the ReLU mask is taken from the bf16 output, as ``threshold_backward`` does.
+the ReLU); the ReLU mask is taken from the bf16 output, as ``threshold_backward`` does, and kept as 1 bit per
+element for the backward (which then reads dy, x and M*C/8 mask bytes instead of dy, x and y).
 """
 from __future__ import annotations
 
@@ -43,21 +44,22 @@ def _fusable(x: torch.Tensor, bn: nn.BatchNorm2d, residual: Optional[torch.Tenso
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, nbt, momentum, eps, relu):
-        y, save = _native.lib().bn_act_fwd(x, residual, weight, bias, running_mean, running_var, nbt,
-                                           float(momentum), float(eps), bool(relu))
+        y, save, mask = _native.lib().bn_act_fwd(x, residual, weight, bias, running_mean, running_var, nbt,
+                                                 float(momentum), float(eps), bool(relu))
         ctx.relu = bool(relu)
         ctx.has_res = residual is not None
-        ctx.save_for_backward(x, y if relu else None, weight, save)
+        # the backward needs only the ReLU mask (1 bit per element), not the bf16 output
+        ctx.save_for_backward(x, mask if relu else None, weight, save)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, weight, save = ctx.saved_tensors
+        x, mask, weight, save = ctx.saved_tensors
         dy = dy.contiguous(memory_format=torch.channels_last)
         if dy.data_ptr() % 16:
             dy = dy.clone(memory_format=torch.channels_last)
         want_w = weight is not None and ctx.needs_input_grad[2]
-        dx, dres, dw, db = _native.lib().bn_act_bwd(dy, x, y, weight, save, ctx.relu,
+        dx, dres, dw, db = _native.lib().bn_act_bwd(dy, x, mask, weight, save, ctx.relu,
                                                     ctx.has_res and ctx.needs_input_grad[1], want_w)
         return (dx, dres if ctx.has_res and ctx.needs_input_grad[1] else None,
                 dw if want_w else None, db if want_w and ctx.needs_input_grad[3] else None,
