@@ -33,6 +33,8 @@
 //
 // Constraints (host-checked, other shapes use the PyTorch path): C % 8 == 0, C <= 2048, and
 // C % 256 == 0 when C > 256.
+#include <type_traits>
+
 #include "grace_common.h"
 #include "grace_kernels.h"
 
@@ -118,66 +120,51 @@ struct Red {
   unsigned* cnt;       // [tiles][kMaxGroups + 1]: group counters, top counter last
 };
 
-// Column fold of `rows` rows (stride C2 elements) for the columns this thread owns, fp64,
-// fixed order.  Thread t owns column t % C2 and rows r ≡ t / C2 (mod P) when C2 <= kB
-// (P = kB / C2 row phases, combined through LDS by the caller), else columns t and t + kB.
-template <typename T>
-__device__ __forceinline__ void fold_cols(const T* src, int rows, int C2, double (&acc)[2]) {
-  acc[0] = acc[1] = 0.0;
-  if (C2 <= kB) {
-    const int P = kB / C2, p = threadIdx.x / C2, c = threadIdx.x % C2;
-    if (p >= P) return;
-    int r = p;
-    for (; r + 7 * P < rows; r += 8 * P) {  // 8 independent loads in flight
-      T v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = src[(size_t)(r + u * P) * C2 + c];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) acc[0] += (double)v[u];
-    }
-    for (; r < rows; r += P) acc[0] += (double)src[(size_t)r * C2 + c];
-  } else {  // C2 == 2 * kB (CT = 256)
-    const int c = threadIdx.x;
-    int r = 0;
-    for (; r + 3 < rows; r += 4) {
-      T v[4][2];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        v[u][0] = src[(size_t)(r + u) * C2 + c];
-        v[u][1] = src[(size_t)(r + u) * C2 + c + kB];
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        acc[0] += (double)v[u][0];
-        acc[1] += (double)v[u][1];
-      }
-    }
-    for (; r < rows; ++r) {
-      acc[0] += (double)src[(size_t)r * C2 + c];
-      acc[1] += (double)src[(size_t)r * C2 + c + kB];
-    }
-  }
-}
-
-// Fold + combine the row phases; calls put(col, value) once per column (all threads enter).
+// Column fold of `rows` rows (row stride C2 elements, 16-B aligned) into fp64, fixed order.
+// The rows were published by other blocks (possibly on other XCDs), so after the acquire every
+// load misses the local L2: the fold is latency bound and issues ALL of a thread's loads before
+// the first use.  16-B loads: thread t owns vector column g = t % G (G = C2 / VW) and the rows
+// r = t / G (mod P), P = kB / G row phases (unrolled by U, independent); the phases are combined
+// through LDS (lds: kB * VW doubles) in phase order, so the result is run-to-run deterministic.
+// Calls put(col, value) once per column (all threads enter).
 template <typename T, typename Put>
 __device__ __forceinline__ void fold_block(const T* src, int rows, int C2, double* lds, Put put) {
-  double acc[2];
-  fold_cols(src, rows, C2, acc);
-  if (C2 <= kB) {
-    const int P = kB / C2;
-    lds[threadIdx.x] = acc[0];
-    __syncthreads();
-    if (threadIdx.x < C2) {
-      double v = lds[threadIdx.x];
-      for (int i = 1; i < P; ++i) v += lds[i * C2 + threadIdx.x];
-      put(threadIdx.x, v);
+  constexpr int VW = 16 / sizeof(T);
+  constexpr int U = 16 / (sizeof(T) / 4);  // 16 float4 or 8 double2 loads in flight
+  using V = typename std::conditional<sizeof(T) == 4, float4, double2>::type;
+  const int G = C2 / VW, P = kB / G;  // C2 <= 512: G <= 128 (float), 256 (double)
+  const int g = threadIdx.x % G, p = threadIdx.x / G;
+  double acc[VW];
+#pragma unroll
+  for (int j = 0; j < VW; ++j) acc[j] = 0.0;
+  if (p < P) {
+    const T* base = src + (size_t)g * VW;
+    for (int r = p; r < rows; r += U * P) {  // predicated: a short fold is still ONE round trip
+      V v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int rr = r + u * P;
+        if (rr < rows) v[u] = *reinterpret_cast<const V*>(base + (size_t)rr * C2);
+        else v[u] = V{};
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const T* e = reinterpret_cast<const T*>(&v[u]);
+#pragma unroll
+        for (int j = 0; j < VW; ++j) acc[j] += (double)e[j];
+      }
     }
-    __syncthreads();
-  } else {
-    put(threadIdx.x, acc[0]);
-    put(threadIdx.x + kB, acc[1]);
   }
+#pragma unroll
+  for (int j = 0; j < VW; ++j) lds[threadIdx.x * VW + j] = acc[j];
+  __syncthreads();
+  for (int c = threadIdx.x; c < C2; c += kB) {
+    const int gc = c / VW, j = c % VW;
+    double v = 0.0;
+    for (int i = 0; i < P; ++i) v += lds[(i * G + gc) * VW + j];
+    put(c, v);
+  }
+  __syncthreads();
 }
 
 // Every wave has drained its sc1 stores -> barrier -> one relaxed agent add.  True in every
@@ -202,9 +189,9 @@ __device__ __forceinline__ bool arrive(unsigned* counter, unsigned expected_last
 // Per-thread 8-channel accumulators -> this block's partial row -> the tile's arrival tree.
 // True in every thread of the tile's final block; totals then in total[tile][0..2CT).
 __device__ bool block_reduce_tree(const Red& R, const float* a, const float* b) {
-  __shared__ float sa[kB * 8];
+  __shared__ __align__(16) float sa[kB * 8];
   __shared__ float sb[kB * 8];
-  __shared__ double lds[kB];
+  double* lds = reinterpret_cast<double*>(sa);  // fold scratch (kB * 4 doubles), after sa is consumed
   const int CT = R.CT, C2 = 2 * CT, tile = blockIdx.y;
   const int cg = threadIdx.x % R.tprp, rs = threadIdx.x / R.tprp;
   if (cg < CT / 8) {
