@@ -46,7 +46,10 @@ def parse():
     ap.add_argument("--workload", default="resnet50_topk")
     ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (0 = workload default)")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
-    ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16", help="autocast compute dtype")
+    ap.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32",
+                    help="compute dtype; fp32 (default) = the reference harness's precision "
+                         "(pytorch_synthetic_benchmark.py:86,151-160: plain model(data), no autocast, "
+                         "TF32/xf32 disabled); bf16 = autocast, an explicitly labelled secondary run")
     ap.add_argument("--overlap", choices=["auto", "on", "off"], default="auto",
                     help="compress+communicate on a side stream during backward; auto = off under a "
                          "whole-step HIP graph (a forked capture costs ~0.9 ms/step on ROCm for ResNet-50, "
@@ -98,6 +101,9 @@ def main():
         os.environ.setdefault("MASTER_PORT", "29533")
         dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)  # RCCL over xGMI
     torch.backends.cudnn.benchmark = not args.no_benchmark_mode
+    # strict fp32: no reduced-precision (xf32) conv/GEMM paths
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.backends.cudnn.allow_tf32 = False
 
     w = WORKLOADS[args.workload]
     batch = args.batch or w.batch
@@ -202,13 +208,19 @@ def main():
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
+    # per-step device events (recorded on the stream, no host sync inside the timed region) give
+    # the reference harness's statistic: mean +- 1.96 std of img/s (pytorch_synthetic_benchmark.py:182-198)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    evs[0].record()
+    for i in range(args.steps):
         loss = run()
+        evs[i + 1].record()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -235,6 +247,9 @@ def main():
 
     samples = w.samples_per_batch(batch) * world * args.steps
     value = samples / elapsed
+    per_gpu = [w.samples_per_batch(batch) / (ms * 1e-3) for ms in step_ms if ms > 0]
+    mean_pg = sum(per_gpu) / max(1, len(per_gpu))
+    std_pg = (sum((v - mean_pg) ** 2 for v in per_gpu) / max(1, len(per_gpu))) ** 0.5
     if rank == 0:
         metric = HEADLINE_METRIC if w.name == "resnet50_topk" else f"{w.unit}/sec (whole node) {w.name}"
         out = {
@@ -265,6 +280,8 @@ def main():
                 "bf16_weights": weights is not None,
                 "optimizer": f"{'FusedSGD' if args.optimizer == 'fused' else 'torch.optim.SGD'}(lr={0.01 * world:g}, momentum=0.5)",
             },
+            "per_gpu": {"mean": round(mean_pg, 2), "ci95": round(1.96 * std_pg, 2),
+                        "note": f"{w.unit}/sec per GPU on rank 0, mean +- 1.96 std over {len(per_gpu)} steps"},
             "comm_wall_ms": round(float(ex.item()) * 1e3, 3),
             "final_loss": round(float(loss.float().item()), 4),
         }

@@ -134,18 +134,19 @@ void cast_segments_bf16(const float* const* src, uint16_t* const* dst, const int
                         hipStream_t stream);
 
 // ---------------------------------------------------------------- bnact.hip
-// fused training-mode BatchNorm (+ residual) (+ ReLU), channels_last bf16
+// fused training-mode BatchNorm (+ residual) (+ ReLU), channels_last bf16 / fp32
 bool bn_supported(int C);  // C % 8 == 0, C <= 2048, C % 256 == 0 above 256
 int64_t bn_workspace_floats(int64_t M, int C);  // `ws` size (fp32 words, 8-B aligned base)
 int bn_fused_v(int64_t M, int C, bool bwd);      // single-launch vectors/thread, 0 = two-kernel path
 void bn_set_fused(bool on);                       // runtime switch (default: env GRACE_BN_FUSED == 1)
 unsigned bn_spin_timeouts();                     // bounded co-residency waits that timed out (must stay 0)
-void bn_act_forward(const uint16_t* x, const uint16_t* res, int64_t M, int C, const float* gamma, const float* beta,
-                    float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps, bool relu,
-                    float* save, float* ws, uint16_t* y, uint8_t* relu_mask, hipStream_t stream);
-void bn_act_backward(const uint16_t* dy, const uint16_t* x, const uint8_t* relu_mask, int64_t M, int C, const float* gamma,
-                     const float* save, bool relu, float* dgamma, float* dbeta, float* coef, float* ws,
-                     uint16_t* dx, uint16_t* dres, hipStream_t stream);
+// x/res/y/dy/dx/dres: bf16 (uint16_t) or fp32 (`fp32`) elements; fp32 uses the two-kernel path
+void bn_act_forward(const void* x, const void* res, bool fp32, int64_t M, int C, const float* gamma,
+                    const float* beta, float* running_mean, float* running_var, int64_t* nbt, float momentum,
+                    float eps, bool relu, float* save, float* ws, void* y, uint8_t* relu_mask, hipStream_t stream);
+void bn_act_backward(const void* dy, const void* x, bool fp32, const uint8_t* relu_mask, int64_t M, int C,
+                     const float* gamma, const float* save, bool relu, float* dgamma, float* dbeta, float* coef,
+                     float* ws, void* dx, void* dres, hipStream_t stream);
 
 // ---------------------------------------------------------------- optim.hip
 constexpr int kSgdSegs = 64;

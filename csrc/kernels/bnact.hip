@@ -1,4 +1,4 @@
-// Fused training-mode BatchNorm (+ residual add) (+ ReLU) for channels_last bf16 activations.
+// Fused training-mode BatchNorm (+ residual add) (+ ReLU) for channels_last bf16 or fp32 activations.
 //
 // Why: in a ResNet-50 training step on MI355X the BN chain is the largest non-GEMM cost.  The
 // stock path runs, per BN layer, MIOpen mean/var + final + normalise forward, a ReLU kernel, a
@@ -97,6 +97,36 @@ __device__ __forceinline__ uint8_t relu_byte(const uint4 u) {
 // mask byte -> per-dword AND masks for the packed bf16 pairs (channels 2k, 2k+1)
 __device__ __forceinline__ uint32_t pair_mask(uint32_t mb, int k) {
   return ((mb >> (2 * k)) & 1u ? 0x0000ffffu : 0u) | ((mb >> (2 * k + 1)) & 1u ? 0xffff0000u : 0u);
+}
+
+// Element-type generic 8-channel row vectors for the two-kernel path: bf16 (one 16-B load) or
+// fp32 (two 16-B loads; the reference harness trains in fp32).
+__device__ __forceinline__ Bf8 ld8(const uint16_t* p) { return load_bf8(p); }
+__device__ __forceinline__ Bf8 ld8(const float* p) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  Bf8 r;
+  r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
+  r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
+  return r;
+}
+__device__ __forceinline__ void st8(uint16_t* p, const float* v) { store_bf8(p, v); }
+__device__ __forceinline__ void st8(float* p, const float* v) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+// store y and return its ReLU mask byte (taken from the value as stored, like threshold_backward)
+__device__ __forceinline__ uint8_t st8_mask(uint16_t* p, const float* v) {
+  const uint4 u = pack_bf8(v);
+  *reinterpret_cast<uint4*>(p) = u;
+  return relu_byte(u);
+}
+__device__ __forceinline__ uint8_t st8_mask(float* p, const float* v) {
+  st8(p, v);
+  uint32_t b = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) b |= (v[j] > 0.f ? 1u : 0u) << j;
+  return (uint8_t)b;
 }
 
 template <typename T>
@@ -252,7 +282,8 @@ __device__ __forceinline__ void for_rows(const Red& R, Body body) {
   for (; r < r1; r += R.rpi) body(r * R.C + col, (int64_t)0, 1);
 }
 
-__global__ __launch_bounds__(kB) void bn_stats_kernel(const uint16_t* __restrict__ x, Red R, StatsOut o) {
+template <typename T>
+__global__ __launch_bounds__(kB) void bn_stats_kernel(const T* __restrict__ x, Red R, StatsOut o) {
   float s[8], q[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
@@ -260,7 +291,7 @@ __global__ __launch_bounds__(kB) void bn_stats_kernel(const uint16_t* __restrict
     if (n == 4) {
       Bf8 v[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = load_bf8(x + e + u * step);
+      for (int u = 0; u < 4; ++u) v[u] = ld8(x + e + u * step);
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
@@ -269,7 +300,7 @@ __global__ __launch_bounds__(kB) void bn_stats_kernel(const uint16_t* __restrict
           q[j] = fmaf(v[u].v[j], v[u].v[j], q[j]);
         }
     } else {
-      const Bf8 v = load_bf8(x + e);
+      const Bf8 v = ld8(x + e);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         s[j] += v.v[j];
@@ -303,9 +334,9 @@ __global__ __launch_bounds__(kB) void bn_stats_kernel(const uint16_t* __restrict
 }
 
 // y = act(x*scale + shift [+ res]); scale/shift = save[2C..4C)
-template <bool RELU, bool RES>
-__global__ __launch_bounds__(kB) void bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
-                                                      const float* __restrict__ save, uint16_t* __restrict__ y,
+template <typename T, bool RELU, bool RES>
+__global__ __launch_bounds__(kB) void bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res,
+                                                      const float* __restrict__ save, T* __restrict__ y,
                                                       uint8_t* __restrict__ mask, int64_t n_vec, int C) {
   const int tpr = C >> 3;
   const int64_t stride = (int64_t)gridDim.x * kB;
@@ -319,12 +350,12 @@ __global__ __launch_bounds__(kB) void bn_apply_kernel(const uint16_t* __restrict
     sh[j] = save[3 * C + cg * 8 + j];
   }
   for (; i < n_vec; i += stride) {
-    const Bf8 v = load_bf8(x + i * 8);
+    const Bf8 v = ld8(x + i * 8);
     float o[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = fmaf(v.v[j], sc[j], sh[j]);
     if constexpr (RES) {
-      const Bf8 r = load_bf8(res + i * 8);
+      const Bf8 r = ld8(res + i * 8);
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] += r.v[j];
     }
@@ -332,9 +363,8 @@ __global__ __launch_bounds__(kB) void bn_apply_kernel(const uint16_t* __restrict
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = fmaxf(o[j], 0.f);
     }
-    const uint4 u = pack_bf8(o);
-    *reinterpret_cast<uint4*>(y + i * 8) = u;
-    if constexpr (RELU) mask[i] = relu_byte(u);
+    if constexpr (RELU) mask[i] = st8_mask(y + i * 8, o);
+    else st8(y + i * 8, o);
   }
 }
 
@@ -346,8 +376,8 @@ struct GradOut {
   float* coef;         // [3C]: a, b, c with dx = a*dz + b*x + c
 };
 
-template <bool RELU>
-__global__ __launch_bounds__(kB) void bn_reduce_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
+template <typename T, bool RELU>
+__global__ __launch_bounds__(kB) void bn_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                        const uint8_t* __restrict__ mask, Red R, GradOut o) {
   float s1[8], s2[8], mu[8];
 #pragma unroll
@@ -374,14 +404,14 @@ __global__ __launch_bounds__(kB) void bn_reduce_kernel(const uint16_t* __restric
       uint32_t w[4] = {0, 0, 0, 0};
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        d[u] = load_bf8(dy + e + u * step);
-        v[u] = load_bf8(x + e + u * step);
+        d[u] = ld8(dy + e + u * step);
+        v[u] = ld8(x + e + u * step);
         if constexpr (RELU) w[u] = mask[(e + u * step) >> 3];
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc(d[u], v[u], w[u]);
     } else {
-      const Bf8 d = load_bf8(dy + e), v = load_bf8(x + e);
+      const Bf8 d = ld8(dy + e), v = ld8(x + e);
       uint32_t w = 0;
       if constexpr (RELU) w = mask[e >> 3];
       acc(d, v, w);
@@ -407,10 +437,10 @@ __global__ __launch_bounds__(kB) void bn_reduce_kernel(const uint16_t* __restric
   }
 }
 
-template <bool RELU, bool RES>
-__global__ __launch_bounds__(kB) void bn_dx_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
+template <typename T, bool RELU, bool RES>
+__global__ __launch_bounds__(kB) void bn_dx_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                    const uint8_t* __restrict__ mask, const float* __restrict__ coef,
-                                                   uint16_t* __restrict__ dx, uint16_t* __restrict__ dres,
+                                                   T* __restrict__ dx, T* __restrict__ dres,
                                                    int64_t n_vec, int C) {
   const int tpr = C >> 3;
   const int64_t stride = (int64_t)gridDim.x * kB;
@@ -424,8 +454,8 @@ __global__ __launch_bounds__(kB) void bn_dx_kernel(const uint16_t* __restrict__ 
     cc[j] = coef[2 * C + cg * 8 + j];
   }
   for (; i < n_vec; i += stride) {
-    const Bf8 d = load_bf8(dy + i * 8);
-    const Bf8 v = load_bf8(x + i * 8);
+    const Bf8 d = ld8(dy + i * 8);
+    const Bf8 v = ld8(x + i * 8);
     float dz[8], o[8];
     if constexpr (RELU) {
       const uint32_t mb = mask[i];
@@ -437,8 +467,8 @@ __global__ __launch_bounds__(kB) void bn_dx_kernel(const uint16_t* __restrict__ 
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = fmaf(ca[j], dz[j], fmaf(cb[j], v.v[j], cc[j]));
-    store_bf8(dx + i * 8, o);
-    if constexpr (RES) store_bf8(dres + i * 8, dz);
+    st8(dx + i * 8, o);
+    if constexpr (RES) st8(dres + i * 8, dz);
   }
 }
 
@@ -969,10 +999,62 @@ unsigned bn_spin_timeouts() {
   return h;
 }
 
-void bn_act_forward(const uint16_t* x, const uint16_t* res, int64_t M, int C, const float* gamma, const float* beta,
-                    float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps, bool relu,
-                    float* save, float* ws, uint16_t* y, uint8_t* mask, hipStream_t stream) {
+namespace {
+
+template <typename T>
+void forward_2k(const T* x, const T* res, int64_t M, int C, const StatsOut& o, bool relu, float* save, float* ws,
+                T* y, uint8_t* mask, hipStream_t stream) {
+  Red R = plan(M, C);
+  bind_ws(R, ws, stream);
+  hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(R.nchunks, C / R.CT), dim3(kB), 0, stream, x, R, o);
+  const int64_t n_vec = M * C / 8;
+  const int gb = apply_grid(n_vec, C);
+  if (relu && res)
+    hipLaunchKernelGGL((bn_apply_kernel<T, true, true>), dim3(gb), dim3(kB), 0, stream, x, res, save, y, mask, n_vec, C);
+  else if (relu)
+    hipLaunchKernelGGL((bn_apply_kernel<T, true, false>), dim3(gb), dim3(kB), 0, stream, x, res, save, y, mask, n_vec, C);
+  else if (res)
+    hipLaunchKernelGGL((bn_apply_kernel<T, false, true>), dim3(gb), dim3(kB), 0, stream, x, res, save, y, mask, n_vec, C);
+  else
+    hipLaunchKernelGGL((bn_apply_kernel<T, false, false>), dim3(gb), dim3(kB), 0, stream, x, res, save, y, mask, n_vec, C);
+}
+
+template <typename T>
+void backward_2k(const T* dy, const T* x, const uint8_t* mask, int64_t M, int C, const GradOut& o, bool relu,
+                 const float* coef, float* ws, T* dx, T* dres, hipStream_t stream) {
+  Red R = plan(M, C);
+  bind_ws(R, ws, stream);
+  const dim3 grid(R.nchunks, C / R.CT);
+  if (relu)
+    hipLaunchKernelGGL((bn_reduce_kernel<T, true>), grid, dim3(kB), 0, stream, dy, x, mask, R, o);
+  else
+    hipLaunchKernelGGL((bn_reduce_kernel<T, false>), grid, dim3(kB), 0, stream, dy, x, mask, R, o);
+  const int64_t n_vec = M * C / 8;
+  const int gb = apply_grid(n_vec, C);
+  if (relu && dres)
+    hipLaunchKernelGGL((bn_dx_kernel<T, true, true>), dim3(gb), dim3(kB), 0, stream, dy, x, mask, coef, dx, dres, n_vec, C);
+  else if (relu)
+    hipLaunchKernelGGL((bn_dx_kernel<T, true, false>), dim3(gb), dim3(kB), 0, stream, dy, x, mask, coef, dx, dres, n_vec, C);
+  else if (dres)
+    hipLaunchKernelGGL((bn_dx_kernel<T, false, true>), dim3(gb), dim3(kB), 0, stream, dy, x, mask, coef, dx, dres, n_vec, C);
+  else
+    hipLaunchKernelGGL((bn_dx_kernel<T, false, false>), dim3(gb), dim3(kB), 0, stream, dy, x, mask, coef, dx, dres, n_vec, C);
+}
+
+}  // namespace
+
+void bn_act_forward(const void* xv, const void* resv, bool fp32, int64_t M, int C, const float* gamma,
+                    const float* beta, float* running_mean, float* running_var, int64_t* nbt, float momentum,
+                    float eps, bool relu, float* save, float* ws, void* yv, uint8_t* mask, hipStream_t stream) {
   StatsOut o{gamma, beta, running_mean, running_var, nbt, momentum, eps, save};
+  if (fp32) {  // two-kernel path only (the single-launch variants hold bf16 rows in registers)
+    forward_2k(static_cast<const float*>(xv), static_cast<const float*>(resv), M, C, o, relu, save, ws,
+               static_cast<float*>(yv), mask, stream);
+    return;
+  }
+  const uint16_t* x = static_cast<const uint16_t*>(xv);
+  const uint16_t* res = static_cast<const uint16_t*>(resv);
+  uint16_t* y = static_cast<uint16_t*>(yv);
   if (const int v = pick_fused_v(M, C, false)) {
     Red R = plan(M, C, v);
     bind_ws(R, ws, stream);
@@ -995,25 +1077,22 @@ void bn_act_forward(const uint16_t* x, const uint16_t* res, int64_t M, int C, co
     GRACE_BN_FWD(16)
 #undef GRACE_BN_FWD
   }
-  Red R = plan(M, C);
-  bind_ws(R, ws, stream);
-  hipLaunchKernelGGL(bn_stats_kernel, dim3(R.nchunks, C / R.CT), dim3(kB), 0, stream, x, R, o);
-  const int64_t n_vec = M * C / 8;
-  const int gb = apply_grid(n_vec, C);
-  if (relu && res)
-    hipLaunchKernelGGL((bn_apply_kernel<true, true>), dim3(gb), dim3(kB), 0, stream, x, res, save, y, mask, n_vec, C);
-  else if (relu)
-    hipLaunchKernelGGL((bn_apply_kernel<true, false>), dim3(gb), dim3(kB), 0, stream, x, res, save, y, mask, n_vec, C);
-  else if (res)
-    hipLaunchKernelGGL((bn_apply_kernel<false, true>), dim3(gb), dim3(kB), 0, stream, x, res, save, y, mask, n_vec, C);
-  else
-    hipLaunchKernelGGL((bn_apply_kernel<false, false>), dim3(gb), dim3(kB), 0, stream, x, res, save, y, mask, n_vec, C);
+  forward_2k(x, res, M, C, o, relu, save, ws, y, mask, stream);
 }
 
-void bn_act_backward(const uint16_t* dy, const uint16_t* x, const uint8_t* mask, int64_t M, int C, const float* gamma,
-                     const float* save, bool relu, float* dgamma, float* dbeta, float* coef, float* ws,
-                     uint16_t* dx, uint16_t* dres, hipStream_t stream) {
+void bn_act_backward(const void* dyv, const void* xv, bool fp32, const uint8_t* mask, int64_t M, int C,
+                     const float* gamma, const float* save, bool relu, float* dgamma, float* dbeta, float* coef,
+                     float* ws, void* dxv, void* dresv, hipStream_t stream) {
   GradOut o{gamma, save, dgamma, dbeta, coef};
+  if (fp32) {
+    backward_2k(static_cast<const float*>(dyv), static_cast<const float*>(xv), mask, M, C, o, relu, coef, ws,
+                static_cast<float*>(dxv), static_cast<float*>(dresv), stream);
+    return;
+  }
+  const uint16_t* dy = static_cast<const uint16_t*>(dyv);
+  const uint16_t* x = static_cast<const uint16_t*>(xv);
+  uint16_t* dx = static_cast<uint16_t*>(dxv);
+  uint16_t* dres = static_cast<uint16_t*>(dresv);
   if (const int v = pick_fused_v(M, C, true)) {
     Red R = plan(M, C, v);
     bind_ws(R, ws, stream);
@@ -1035,23 +1114,7 @@ void bn_act_backward(const uint16_t* dy, const uint16_t* x, const uint8_t* mask,
     GRACE_BN_BWD(8)
 #undef GRACE_BN_BWD
   }
-  Red R = plan(M, C);
-  bind_ws(R, ws, stream);
-  const dim3 grid(R.nchunks, C / R.CT);
-  if (relu)
-    hipLaunchKernelGGL(bn_reduce_kernel<true>, grid, dim3(kB), 0, stream, dy, x, mask, R, o);
-  else
-    hipLaunchKernelGGL(bn_reduce_kernel<false>, grid, dim3(kB), 0, stream, dy, x, mask, R, o);
-  const int64_t n_vec = M * C / 8;
-  const int gb = apply_grid(n_vec, C);
-  if (relu && dres)
-    hipLaunchKernelGGL((bn_dx_kernel<true, true>), dim3(gb), dim3(kB), 0, stream, dy, x, mask, coef, dx, dres, n_vec, C);
-  else if (relu)
-    hipLaunchKernelGGL((bn_dx_kernel<true, false>), dim3(gb), dim3(kB), 0, stream, dy, x, mask, coef, dx, dres, n_vec, C);
-  else if (dres)
-    hipLaunchKernelGGL((bn_dx_kernel<false, true>), dim3(gb), dim3(kB), 0, stream, dy, x, mask, coef, dx, dres, n_vec, C);
-  else
-    hipLaunchKernelGGL((bn_dx_kernel<false, false>), dim3(gb), dim3(kB), 0, stream, dy, x, mask, coef, dx, dres, n_vec, C);
+  backward_2k(dy, x, mask, M, C, o, relu, coef, ws, dx, dres, stream);
 }
 
 }  // namespace grace

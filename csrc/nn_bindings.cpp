@@ -14,7 +14,8 @@ using DevGuard = c10::hip::HIPGuardMasqueradingAsCUDA;
 
 // [M, C] row-major view of an NHWC (channels_last) or 2-D activation
 void check_rows(const Tensor& t, const char* what, int64_t* M, int64_t* C) {
-  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16, what, " must be a bf16 GPU tensor");
+  TORCH_CHECK(t.is_cuda() && (t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kFloat), what,
+              " must be a bf16 or fp32 GPU tensor");
   if (t.dim() == 4) {
     TORCH_CHECK(t.is_contiguous(at::MemoryFormat::ChannelsLast), what, " must be channels_last");
     *C = t.size(1);
@@ -28,7 +29,7 @@ void check_rows(const Tensor& t, const char* what, int64_t* M, int64_t* C) {
 }
 
 void same_layout(const Tensor& a, const Tensor& b, const char* what) {
-  TORCH_CHECK(a.sizes() == b.sizes() && a.strides() == b.strides() && b.scalar_type() == at::kBFloat16 &&
+  TORCH_CHECK(a.sizes() == b.sizes() && a.strides() == b.strides() && b.scalar_type() == a.scalar_type() &&
                   (reinterpret_cast<uintptr_t>(b.data_ptr()) & 15) == 0,
               what, " must match the input's shape, strides and dtype");
 }
@@ -66,12 +67,10 @@ std::vector<Tensor> bn_act_fwd(const Tensor& x, const c10::optional<Tensor>& res
   // ReLU: 1 bit per element (bit j of byte i = output element 8i+j > 0), read by the backward
   Tensor mask = relu ? at::empty({M * C / 8}, x.options().dtype(at::kByte)) : Tensor();
   Tensor ws = at::empty({grace::bn_workspace_floats(M, (int)C)}, f32);
-  grace::bn_act_forward(reinterpret_cast<const uint16_t*>(x.data_ptr()),
-                        has_res ? reinterpret_cast<const uint16_t*>(res->data_ptr()) : nullptr, M, (int)C,
+  grace::bn_act_forward(x.data_ptr(), has_res ? res->data_ptr() : nullptr, x.scalar_type() == at::kFloat, M, (int)C,
                         opt_f32(weight, C, "weight"), opt_f32(bias, C, "bias"), rm, rv, nb, (float)momentum,
                         (float)eps, relu, save.data_ptr<float>(), ws.data_ptr<float>(),
-                        reinterpret_cast<uint16_t*>(y.data_ptr()),
-                        relu ? mask.data_ptr<uint8_t>() : nullptr, cur_stream());
+                        y.data_ptr(), relu ? mask.data_ptr<uint8_t>() : nullptr, cur_stream());
   return {y, save, mask};
 }
 
@@ -96,13 +95,12 @@ std::vector<Tensor> bn_act_bwd(const Tensor& dy, const Tensor& x, const c10::opt
   Tensor db = want_dweight ? at::empty({C}, f32) : Tensor();
   Tensor coef = at::empty({3 * C}, f32);
   Tensor ws = at::empty({grace::bn_workspace_floats(M, (int)C)}, f32);
-  grace::bn_act_backward(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
-                         reinterpret_cast<const uint16_t*>(x.data_ptr()),
+  grace::bn_act_backward(dy.data_ptr(), x.data_ptr(), x.scalar_type() == at::kFloat,
                          relu ? mask->data_ptr<uint8_t>() : nullptr, M, (int)C,
                          opt_f32(weight, C, "weight"), save.data_ptr<float>(), relu,
                          want_dweight ? dg.data_ptr<float>() : nullptr, want_dweight ? db.data_ptr<float>() : nullptr,
-                         coef.data_ptr<float>(), ws.data_ptr<float>(), reinterpret_cast<uint16_t*>(dx.data_ptr()),
-                         want_dres ? reinterpret_cast<uint16_t*>(dres.data_ptr()) : nullptr, cur_stream());
+                         coef.data_ptr<float>(), ws.data_ptr<float>(), dx.data_ptr(),
+                         want_dres ? dres.data_ptr() : nullptr, cur_stream());
   return {dx, dres, dg, db};
 }
 

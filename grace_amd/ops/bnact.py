@@ -1,15 +1,16 @@
 """Fused training-mode BatchNorm (+ residual add) (+ ReLU) -- ``BatchNormAct2d``.
 
 A drop-in ``nn.BatchNorm2d`` subclass (same parameters, buffers and state_dict keys) whose
-``forward(x, residual=None)`` computes ``act(bn(x) + residual)``.  On a GPU with bf16
-channels_last activations (the autocast + channels_last training setup of bench.py) it runs the
+``forward(x, residual=None)`` computes ``act(bn(x) + residual)``.  On a GPU with bf16 or fp32
+channels_last activations (bench.py's fp32 default and its bf16 autocast run) it runs the
 four CDNA4 kernels of ``csrc/kernels/bnact.hip`` per layer (statistics with the running-stat /
 ``num_batches_tracked`` update folded in, apply, backward reduce, backward dx) instead of
 ~11 MIOpen + elementwise launches; everywhere else (CPU, fp32, eval mode, odd channel counts)
-it is exactly ``relu(F.batch_norm(x) + residual)``.
+it is exactly ``relu(F.batch_norm(x) + residual)``.  fp32 activations use the two-kernel path
+(the single-launch variants keep bf16 rows in registers).
 
-Numerics: statistics and the affine are fp32 (fp64 fold of the per-block partial sums), the
-output is rounded to bf16 once (the unfused bf16 path rounds after BN, after the add and after
+Numerics: statistics and the affine are fp32 (fp64 fold of the per-block partial sums); for
+bf16 the output is rounded to bf16 once (the unfused bf16 path rounds after BN, after the add and after
 the ReLU); the ReLU mask is taken from the bf16 output, as ``threshold_backward`` does, and kept as 1 bit per
 element for the backward (which then reads dy, x and M*C/8 mask bytes instead of dy, x and y).
 """
@@ -25,7 +26,7 @@ from . import _native
 
 
 def _fusable(x: torch.Tensor, bn: nn.BatchNorm2d, residual: Optional[torch.Tensor]) -> bool:
-    if not (x.is_cuda and x.dtype == torch.bfloat16 and _native.native_on(x.device)):
+    if not (x.is_cuda and x.dtype in (torch.bfloat16, torch.float32) and _native.native_on(x.device)):
         return False
     if x.dim() != 4 or not x.is_contiguous(memory_format=torch.channels_last):
         return False

@@ -11,14 +11,14 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-def _case(n, c, h, w, relu, with_res, seed=0):
+def _case(n, c, h, w, relu, with_res, seed=0, dtype=torch.bfloat16):
     g = torch.Generator(device="cpu").manual_seed(seed)
-    x = (torch.randn(n, c, h, w, generator=g) * 2 + 0.5).to(DEV, torch.bfloat16)
+    x = (torch.randn(n, c, h, w, generator=g) * 2 + 0.5).to(DEV, dtype)
     x = x.contiguous(memory_format=torch.channels_last)
     res = None
     if with_res:
-        res = torch.randn(n, c, h, w, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    dy = torch.randn(n, c, h, w, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        res = torch.randn(n, c, h, w, generator=g).to(DEV, dtype).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(n, c, h, w, generator=g).to(DEV, dtype).contiguous(memory_format=torch.channels_last)
     m = BatchNormAct2d(c, relu=relu).to(DEV)
     with torch.no_grad():
         m.weight.copy_(torch.rand(c, generator=g) + 0.5)
@@ -71,6 +71,33 @@ def test_bnact_matches_fp32_reference(shape, relu, with_res):
     torch.testing.assert_close(xx.grad.float(), dx0, rtol=2e-2, atol=3e-2 * dx0.abs().max().item() + 1e-3)
     if res is not None:
         torch.testing.assert_close(rr.grad.float(), dr0, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 9, 9), (3, 2048, 3, 3), (1, 8, 2, 3), (32, 128, 28, 28),
+                                   (32, 64, 56, 56), (32, 2048, 7, 7), (31, 512, 14, 13)])
+@pytest.mark.parametrize("relu,with_res", [(False, False), (True, False), (True, True), (False, True)])
+def test_bnact_fp32_matches_fp32_reference(shape, relu, with_res):
+    """fp32 activations (bench.py's default precision): two-kernel path, fp32 in and out."""
+    assert _native.available()
+    m, x, res, dy = _case(*shape, relu, with_res, dtype=torch.float32)
+    assert _fusable(x, m, res)
+    xx = x.clone().requires_grad_(True)
+    rr = res.clone().requires_grad_(True) if res is not None else None
+    y = m(xx, rr)
+    y.backward(dy)
+    torch.cuda.synchronize()
+    y0, dx0, dr0, dw0, db0, rm0, rv0 = _reference(m, x, res, dy, relu)
+    assert y.dtype == torch.float32 and y.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(y, y0, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(m.running_mean, rm0, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(m.running_var, rv0, rtol=1e-4, atol=1e-5)
+    M = x.numel() // x.shape[1]
+    scale = dy.abs().mean().item() * M ** 0.5
+    torch.testing.assert_close(m.bias.grad, db0, rtol=1e-4, atol=1e-4 * scale)
+    torch.testing.assert_close(m.weight.grad, dw0, rtol=1e-4, atol=1e-4 * scale)
+    torch.testing.assert_close(xx.grad, dx0, rtol=1e-3, atol=1e-4 * dx0.abs().max().item() + 1e-5)
+    if res is not None:
+        torch.testing.assert_close(rr.grad, dr0, rtol=1e-5, atol=1e-6)
 
 
 @pytest.fixture
