@@ -109,6 +109,48 @@ void topk_compact(const Tensor& x, const Tensor& seg, const Tensor& cb, const Te
                              cur_stream());
 }
 
+// two-pass Top-K (csrc/kernels/topk.hip topk_ef_bucket); x may alias g (NoneMemory, mode 0)
+void topk_ef(const Tensor& g, const Tensor& x, double beta, double gamma, int64_t mode, bool zero,
+             const Tensor& seg, const Tensor& cb, const Tensor& ce, const Tensor& seg_chunk_begin,
+             const Tensor& kseg, const Tensor& state, const Tensor& hist, const Tensor& ctr, const Tensor& ccnt,
+             const Tensor& out_off, const Tensor& out_val, const Tensor& out_idx, const Tensor& cand_val,
+             const Tensor& cand_idx) {
+  CHECK_F32(g);
+  CHECK_F32(x);
+  CHECK_I32(seg_chunk_begin);
+  CHECK_I32(kseg);
+  CHECK_I32(state);
+  CHECK_I32(hist);
+  CHECK_I32(ctr);
+  CHECK_I32(ccnt);
+  CHECK_I64(out_off);
+  CHECK_F32(out_val);
+  CHECK_I32(out_idx);
+  CHECK_F32(cand_val);
+  CHECK_I32(cand_idx);
+  const int n_seg = (int)kseg.numel();
+  const int64_t n = g.numel();
+  TORCH_CHECK(x.numel() == n, "x/g size mismatch");
+  TORCH_CHECK(n < ((int64_t)1 << 31), "bucket too large for int32 indices");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(g.data_ptr()) & 15) == 0 && (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0,
+              "g and x must be 16-byte aligned");
+  TORCH_CHECK(state.numel() >= 2 * n_seg && hist.numel() >= (int64_t)n_seg * 2048 && ctr.numel() >= 3 * n_seg,
+              "state / hist / ctr too small");
+  TORCH_CHECK(seg_chunk_begin.numel() == n_seg + 1 && ccnt.numel() >= 3 * seg.numel(), "chunk tables");
+  TORCH_CHECK(out_off.numel() == n_seg + 1, "out_off size");
+  TORCH_CHECK(cand_val.numel() >= n && cand_idx.numel() >= n, "candidate buffers must hold the bucket");
+  TORCH_CHECK(mode == 0 || x.data_ptr() != g.data_ptr(), "mode 1 needs a residual distinct from g");
+  TORCH_CHECK(!zero || x.data_ptr() != g.data_ptr(), "zeroing needs a residual distinct from g");
+  auto ct = make_ct(seg, cb, ce);
+  DevGuard guard(g.device());
+  grace::topk_ef_bucket(ct, seg_chunk_begin.data_ptr<int32_t>(), n_seg, g.data_ptr<float>(), x.data_ptr<float>(), n,
+                        (float)beta, (float)gamma, (int)mode, zero ? 1 : 0, kseg.data_ptr<int32_t>(),
+                        reinterpret_cast<grace::TopkState*>(state.data_ptr<int32_t>()), hist.data_ptr<int32_t>(),
+                        ctr.data_ptr<int32_t>(), ccnt.data_ptr<int32_t>(), out_off.data_ptr<int64_t>(),
+                        out_val.data_ptr<float>(), out_idx.data_ptr<int32_t>(), cand_val.data_ptr<float>(),
+                        cand_idx.data_ptr<int32_t>(), cur_stream());
+}
+
 void sparse_scatter_add(const Tensor& val, const Tensor& idx, const Tensor& out, double scale,
                         bool accumulate) {
   CHECK_F32(val);
@@ -739,6 +781,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("build_info", &build_info);
   m.def("topk_select", &topk_select);
   m.def("topk_compact", &topk_compact);
+  m.def("topk_ef", &topk_ef);
   m.def("sparse_scatter_add", &sparse_scatter_add);
   m.def("segment_stats", &segment_stats);
   m.def("randk_gather", &randk_gather);

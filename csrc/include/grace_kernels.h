@@ -22,6 +22,16 @@ void topk_select_bucket(const ChunkTable& ct, int n_seg, const float* g, const f
 void topk_compact_bucket(const ChunkTable& ct, int n_seg, const float* x, const TopkState* st,
                          const int64_t* out_off, int32_t* counters, float* out_val,
                          int32_t* out_idx, float* resid, int64_t idx_base, hipStream_t stream);
+// Two-pass Top-K with fused error feedback (the Top-K compressor): pass A compensates + digit-0
+// histogram; pass B splits every chunk into definite takes (front of the chunk's slice of cand_*)
+// and threshold-bin candidates (back of the slice); digits 1-2 run on the candidates; the
+// assemble kernel writes the payload.  ctr = 3 * n_seg int32, ccnt = 3 * n_chunks int32, cand_*
+// sized like x.  mode 0 -> x = g (copied when x != g), mode 1 -> x = beta * x + gamma * g;
+// zero: emitted entries of x are set to 0 (the residual update).  g and x 16-B aligned.
+void topk_ef_bucket(const ChunkTable& ct, const int32_t* seg_chunk_begin, int n_seg, const float* g, float* x,
+                    int64_t total, float beta, float gamma, int mode, int zero, const int32_t* kseg, TopkState* st,
+                    int32_t* hist, int32_t* ctr, int32_t* ccnt, const int64_t* out_off, float* out_val,
+                    int32_t* out_idx, float* cand_val, int32_t* cand_idx, hipStream_t stream);
 void sparse_scatter_add(const float* val, const int32_t* idx, int64_t K, float* out, float scale,
                         bool accumulate, hipStream_t stream);
 

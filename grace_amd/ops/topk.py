@@ -44,6 +44,26 @@ def _workspace(layout: SegmentLayout, ks: Sequence[int], device):
     return layout.cached(device, f"topk_ws:{hash(tuple(ks))}", build)
 
 
+TOPK_CHUNK = 16384  # elements per workgroup in the two streaming passes
+
+
+def _two_pass_ws(layout: SegmentLayout, device):
+    """Device state of the two-pass pipeline (csrc/kernels/topk.hip ``topk_ef_bucket``): candidate
+    buffers (value + index, one slice per chunk, sized like the bucket so any distribution fits),
+    per-chunk take/candidate/above-prefix counts and the 3 per-segment counters."""
+    def build():
+        n_chunks = layout.device_tables(device, TOPK_CHUNK)["n_chunks"]
+        i32 = dict(dtype=torch.int32, device=device)
+        return {
+            "ctr": torch.zeros(3 * layout.n_seg, **i32),
+            "ccnt": torch.zeros(3 * max(1, n_chunks), **i32),
+            "cand_val": torch.empty(max(1, layout.total), dtype=torch.float32, device=device),
+            "cand_idx": torch.empty(max(1, layout.total), **i32),
+        }
+
+    return layout.cached(device, "topk2_ws", build)
+
+
 def topk_ef(
     g: torch.Tensor,
     layout: SegmentLayout,
@@ -74,13 +94,13 @@ def topk_ef(
     if _native.use_native(g):
         C = _native.lib()
         ws = _workspace(layout, ks, g.device)
-        t = layout.device_tables(g.device)
+        w2 = _two_pass_ws(layout, g.device)
+        t = layout.device_tables(g.device, TOPK_CHUNK)
         x = resid if resid is not None else g
         mode = 1 if (resid is not None and resid_valid) else 0
-        C.topk_select(g, resid if mode == 1 else None, x, beta, gamma, mode, t["seg"], t["begin"], t["end"],
-                      ws["kseg"], ws["state"], ws["hist"])
-        C.topk_compact(x, t["seg"], t["begin"], t["end"], ws["state"], ws["out_off"], ws["counters"],
-                       vals, idx, resid, 0)
+        C.topk_ef(g, x, beta, gamma, mode, resid is not None, t["seg"], t["begin"], t["end"],
+                  t["seg_chunk_begin"], ws["kseg"], ws["state"], ws["hist"], w2["ctr"], w2["ccnt"],
+                  ws["out_off"], vals, idx, w2["cand_val"], w2["cand_idx"])
         return vals, idx
     # ---- PyTorch reference path (CPU / oracle)
     if resid is not None:
