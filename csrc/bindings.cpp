@@ -151,6 +151,18 @@ void topk_ef(const Tensor& g, const Tensor& x, double beta, double gamma, int64_
                         cand_idx.data_ptr<int32_t>(), cur_stream());
 }
 
+void sparse_scatter_add_dev(const Tensor& val, const Tensor& idx, const Tensor& count, const Tensor& out,
+                            double scale, bool accumulate) {
+  CHECK_F32(val);
+  CHECK_I32(idx);
+  CHECK_I32(count);
+  CHECK_F32(out);
+  TORCH_CHECK(val.numel() == idx.numel() && count.numel() >= 1, "val/idx size mismatch");
+  DevGuard guard(out.device());
+  grace::sparse_scatter_add_dev(val.data_ptr<float>(), idx.data_ptr<int32_t>(), count.data_ptr<int32_t>(),
+                                val.numel(), out.data_ptr<float>(), (float)scale, accumulate, cur_stream());
+}
+
 void sparse_scatter_add(const Tensor& val, const Tensor& idx, const Tensor& out, double scale,
                         bool accumulate) {
   CHECK_F32(val);
@@ -209,7 +221,8 @@ int64_t threshold_compact(const Tensor& g, const c10::optional<Tensor>& r, int64
   CHECK_F32(out_val);
   CHECK_I32(out_idx);
   CHECK_I32(counter);
-  TORCH_CHECK(out_val.numel() >= g.numel() && out_idx.numel() >= g.numel(), "capacity must be >= numel");
+  TORCH_CHECK(out_val.numel() == out_idx.numel() && counter.numel() >= 1, "capacity buffers / counter");
+  TORCH_CHECK(g.numel() < ((int64_t)1 << 31), "int32 indices");
   const float* rp = nullptr;
   if (mode == 1) {
     TORCH_CHECK(r.has_value(), "mode 1 needs r");
@@ -223,8 +236,8 @@ int64_t threshold_compact(const Tensor& g, const c10::optional<Tensor>& r, int64
   }
   DevGuard guard(g.device());
   grace::threshold_compact(g.data_ptr<float>(), rp, (int)mode, (float)beta, (float)gamma, g.numel(), (float)thr,
-                           out_val.data_ptr<float>(), out_idx.data_ptr<int32_t>(), counter.data_ptr<int32_t>(), wp,
-                           cur_stream());
+                           out_val.data_ptr<float>(), out_idx.data_ptr<int32_t>(), out_val.numel(),
+                           counter.data_ptr<int32_t>(), wp, cur_stream());
   return 0;
 }
 
@@ -402,7 +415,8 @@ void u8_aggregate(const Tensor& base, int64_t rank_stride, int64_t codes_off, in
 }
 
 // ------------------------------------------------------------------------------ DGC
-void dgc_sample(const Tensor& x, const Tensor& seg_off, const Tensor& samp_off, int64_t seed, const Tensor& samples) {
+void dgc_sample(const Tensor& x, const Tensor& seg_off, const Tensor& samp_off, int64_t seed,
+                const c10::optional<Tensor>& step, const Tensor& samples) {
   CHECK_F32(x);
   CHECK_I64(seg_off);
   CHECK_I64(samp_off);
@@ -410,7 +424,7 @@ void dgc_sample(const Tensor& x, const Tensor& seg_off, const Tensor& samp_off, 
   TORCH_CHECK(seg_off.numel() == samp_off.numel(), "offset tables");
   DevGuard guard(x.device());
   grace::dgc_sample(x.data_ptr<float>(), (int)seg_off.numel() - 1, seg_off.data_ptr<int64_t>(),
-                    samp_off.data_ptr<int64_t>(), samples.numel(), (uint64_t)seed, samples.data_ptr<float>(),
+                    samp_off.data_ptr<int64_t>(), samples.numel(), seed_arg(seed, step), samples.data_ptr<float>(),
                     cur_stream());
 }
 
@@ -432,18 +446,45 @@ void dgc_refine(const Tensor& x, const Tensor& state, const Tensor& target, int6
                     done.data_ptr<int32_t>(), cur_stream());
 }
 
+// capacity = out_val.numel(); vmask/umask (optional, DgcMemory fused): zeroed where sent
 void dgc_compact(const Tensor& x, const Tensor& thr, const Tensor& out_val, const Tensor& out_idx,
-                 const Tensor& counter, const Tensor& seg, const Tensor& cb, const Tensor& ce) {
+                 const Tensor& counter, const Tensor& seg, const Tensor& cb, const Tensor& ce,
+                 const c10::optional<Tensor>& vmask, const c10::optional<Tensor>& umask) {
   CHECK_F32(x);
   CHECK_F32(thr);
   CHECK_F32(out_val);
   CHECK_I32(out_idx);
   CHECK_I32(counter);
-  TORCH_CHECK(out_val.numel() >= x.numel() && out_idx.numel() >= x.numel(), "capacity");
+  TORCH_CHECK(out_val.numel() == out_idx.numel() && counter.numel() >= 1, "capacity buffers / counter");
+  TORCH_CHECK(x.numel() < ((int64_t)1 << 31), "int32 indices");
+  float* vp = nullptr;
+  float* up = nullptr;
+  if (vmask.has_value()) {
+    CHECK_F32((*vmask));
+    TORCH_CHECK(vmask->numel() == x.numel(), "vmask size");
+    vp = vmask->data_ptr<float>();
+  }
+  if (umask.has_value()) {
+    CHECK_F32((*umask));
+    TORCH_CHECK(umask->numel() == x.numel(), "umask size");
+    up = umask->data_ptr<float>();
+  }
   auto ct = make_ct(seg, cb, ce);
   DevGuard guard(x.device());
   grace::dgc_compact(ct, x.data_ptr<float>(), thr.data_ptr<float>(), out_val.data_ptr<float>(),
-                     out_idx.data_ptr<int32_t>(), counter.data_ptr<int32_t>(), cur_stream());
+                     out_idx.data_ptr<int32_t>(), out_val.numel(), counter.data_ptr<int32_t>(), vp, up, cur_stream());
+}
+
+void dgc_compensate(const Tensor& g, const Tensor& u, const Tensor& v, double momentum, bool first) {
+  CHECK_F32(g);
+  CHECK_F32(u);
+  CHECK_F32(v);
+  TORCH_CHECK(u.numel() == g.numel() && v.numel() == g.numel(), "u / v size");
+  TORCH_CHECK(((reinterpret_cast<uintptr_t>(g.data_ptr()) | reinterpret_cast<uintptr_t>(u.data_ptr()) |
+                reinterpret_cast<uintptr_t>(v.data_ptr())) & 15) == 0, "g / u / v must be 16-byte aligned");
+  DevGuard guard(g.device());
+  grace::dgc_compensate(g.data_ptr<float>(), u.data_ptr<float>(), v.data_ptr<float>(), (float)momentum, g.numel(),
+                        first, cur_stream());
 }
 
 // ------------------------------------------------------------------------------ PowerSGD
@@ -726,8 +767,23 @@ void adaq_compact(const Tensor& x, const Tensor& thr, const Tensor& goff, const 
   TORCH_CHECK(means.numel() == 2 * n_seg && counts.numel() == 2 * n_seg, "means/counts");
   DevGuard guard(x.device());
   grace::adaq_compact(ct, n_seg, seg_chunk_begin.data_ptr<int32_t>(), x.data_ptr<float>(), thr.data_ptr<float>(),
-                      goff.data_ptr<int32_t>(), cursor.data_ptr<int32_t>(), idx.data_ptr<int32_t>(),
+                      goff.data_ptr<int32_t>(), cursor.data_ptr<int32_t>(), idx.data_ptr<int32_t>(), idx.numel(),
                       psum.data_ptr<double>(), means.data_ptr<float>(), counts.data_ptr<int32_t>(), cur_stream());
+}
+
+// one rank's capacity payload (means, counts, idx[cap]) -> out
+void adaq_decode(const Tensor& means, const Tensor& counts, const Tensor& idx, const Tensor& goff_ws,
+                 const Tensor& out, double scale) {
+  CHECK_F32(means);
+  CHECK_I32(counts);
+  CHECK_I32(idx);
+  CHECK_I32(goff_ws);
+  CHECK_F32(out);
+  const int ng = (int)counts.numel();
+  TORCH_CHECK(means.numel() == ng && goff_ws.numel() >= ng + 1, "means / counts / workspace");
+  DevGuard guard(out.device());
+  grace::adaq_decode(ng, means.data_ptr<float>(), counts.data_ptr<int32_t>(), idx.data_ptr<int32_t>(), idx.numel(),
+                     goff_ws.data_ptr<int32_t>(), out.data_ptr<float>(), (float)scale, cur_stream());
 }
 
 // ------------------------------------------------------------------------------ INCEPTIONN
@@ -743,33 +799,35 @@ void inceptionn_count(const Tensor& x, int64_t e_b, int64_t mid, const Tensor& c
                           totals.data_ptr<int32_t>(), cur_stream());
 }
 
-void inceptionn_encode(const Tensor& x, int64_t e_b, int64_t mid, const Tensor& off, const Tensor& v32,
-                       const Tensor& v16, const Tensor& v8, const Tensor& codes) {
+void inceptionn_encode(const Tensor& x, int64_t e_b, int64_t mid, const Tensor& off, const Tensor& totals,
+                       const Tensor& stream, const Tensor& codes) {
   CHECK_F32(x);
   CHECK_I32(off);
-  CHECK_F32(v32);
-  CHECK_DT(v16, at::kShort);
-  CHECK_DT(v8, at::kByte);
+  CHECK_I32(totals);
+  CHECK_DT(stream, at::kByte);
   CHECK_DT(codes, at::kByte);
-  TORCH_CHECK(codes.numel() >= (x.numel() + 3) / 4, "codes size");
+  TORCH_CHECK(codes.numel() >= (x.numel() + 3) / 4 && totals.numel() >= 4, "codes / totals size");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(stream.data_ptr()) & 3) == 0, "stream must be 4-byte aligned");
   DevGuard guard(x.device());
   grace::inceptionn_encode(x.data_ptr<float>(), x.numel(), (int)e_b, (int)mid, off.data_ptr<int32_t>(),
-                           v32.data_ptr<float>(), reinterpret_cast<uint16_t*>(v16.data_ptr<int16_t>()),
-                           v8.data_ptr<uint8_t>(), codes.data_ptr<uint8_t>(), cur_stream());
+                           totals.data_ptr<int32_t>(), stream.data_ptr<uint8_t>(), stream.numel(),
+                           codes.data_ptr<uint8_t>(), cur_stream());
 }
 
-void inceptionn_decode(const Tensor& ptrs, const Tensor& code_ptrs, int64_t n_ranks, const Tensor& cnt,
-                       const Tensor& totals, double scale, const Tensor& out, bool accumulate) {
-  CHECK_I64(ptrs);
-  CHECK_I64(code_ptrs);
+// base: uint8 view of the rank rows (compressor._base.rank_rows)
+void inceptionn_decode(const Tensor& base, int64_t rank_stride, int64_t stream_off, int64_t codes_off,
+                       int64_t n_ranks, const Tensor& cnt, const Tensor& totals, double scale, const Tensor& out,
+                       bool accumulate) {
+  CHECK_DEV(base);
+  CHECK_DT(base, at::kByte);
   CHECK_I32(cnt);
   CHECK_I32(totals);
   CHECK_F32(out);
   const int64_t n = out.numel();
-  TORCH_CHECK(ptrs.numel() == 4 * n_ranks && code_ptrs.numel() == n_ranks, "pointer tables");
   TORCH_CHECK(cnt.numel() >= 4 * n_ranks * grace::inceptionn_tiles(n) && totals.numel() >= 4 * n_ranks, "workspace");
+  TORCH_CHECK(base.numel() >= (n_ranks - 1) * rank_stride + codes_off + (n + 3) / 4, "rank rows too small");
   DevGuard guard(out.device());
-  grace::inceptionn_decode(ptrs.data_ptr<int64_t>(), code_ptrs.data_ptr<int64_t>(), (int)n_ranks, n,
+  grace::inceptionn_decode(base.data_ptr<uint8_t>(), rank_stride, stream_off, codes_off, (int)n_ranks, n,
                            cnt.data_ptr<int32_t>(), totals.data_ptr<int32_t>(), (float)scale, out.data_ptr<float>(),
                            accumulate, cur_stream());
 }
@@ -783,6 +841,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("topk_compact", &topk_compact);
   m.def("topk_ef", &topk_ef);
   m.def("sparse_scatter_add", &sparse_scatter_add);
+  m.def("sparse_scatter_add_dev", &sparse_scatter_add_dev);
   m.def("segment_stats", &segment_stats);
   m.def("randk_gather", &randk_gather);
   m.def("randk_scatter", &randk_scatter);
@@ -800,6 +859,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dgc_sample", &dgc_sample);
   m.def("dgc_refine", &dgc_refine);
   m.def("dgc_compact", &dgc_compact);
+  m.def("dgc_compensate", &dgc_compensate);
   m.def("powersgd_mq", &powersgd_mq);
   m.def("gram_orthonormalize", &gram_orthonormalize);
   m.def("adaq_sample", &adaq_sample);
@@ -807,6 +867,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adaq_refine", &adaq_refine);
   m.def("adaq_offsets", &adaq_offsets);
   m.def("adaq_compact", &adaq_compact);
+  m.def("adaq_decode", &adaq_decode);
   m.def("inceptionn_tiles", &inceptionn_tiles);
   m.def("inceptionn_count", &inceptionn_count);
   m.def("inceptionn_encode", &inceptionn_encode);

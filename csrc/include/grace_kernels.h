@@ -34,6 +34,9 @@ void topk_ef_bucket(const ChunkTable& ct, const int32_t* seg_chunk_begin, int n_
                     int32_t* out_idx, float* cand_val, int32_t* cand_idx, hipStream_t stream);
 void sparse_scatter_add(const float* val, const int32_t* idx, int64_t K, float* out, float scale,
                         bool accumulate, hipStream_t stream);
+// K = min(*count, cap) read on the device (capacity payloads with an in-band count)
+void sparse_scatter_add_dev(const float* val, const int32_t* idx, const int32_t* count, int64_t cap, float* out,
+                            float scale, bool accumulate, hipStream_t stream);
 
 // ---------------------------------------------------------------- segstats.hip
 // per segment: [sum, sumsq, max|x|, sum|x|, sum(x<0), count(x<0)]
@@ -51,7 +54,8 @@ void randk_scatter(const float* vals, int64_t rank_stride, int n_ranks, int n_se
                    const int64_t* out_off, const int64_t* seeds, const int64_t* step, int64_t K, float* out,
                    float scale, bool accumulate, hipStream_t stream);
 void threshold_compact(const float* g, const float* r, int mode, float beta, float gamma, int64_t n, float thr,
-                       float* out_val, int32_t* out_idx, int32_t* counter, float* resid, hipStream_t stream);
+                       float* out_val, int32_t* out_idx, int64_t cap, int32_t* counter, float* resid,
+                       hipStream_t stream);
 
 // ---------------------------------------------------------------- signbits.hip
 void sign_pack(const ChunkTable& ct, const int64_t* seg_start, const int64_t* word_off, const float* g,
@@ -83,11 +87,12 @@ void u8_aggregate(const ChunkTable& ct, const uint8_t* base, int64_t rank_stride
 
 // ---------------------------------------------------------------- dgc.hip
 void dgc_sample(const float* x, int n_seg, const int64_t* seg_off, const int64_t* samp_off, int64_t n_samples,
-                uint64_t seed, float* samples, hipStream_t stream);
+                SeedArg seed, float* samples, hipStream_t stream);
 void dgc_refine(const ChunkTable& ct, int n_seg, const float* x, const TopkState* st, const float* target,
                 int max_iters, float* thr, int32_t* count, int32_t* done, hipStream_t stream);
 void dgc_compact(const ChunkTable& ct, const float* x, const float* thr, float* out_val, int32_t* out_idx,
-                 int32_t* counter, hipStream_t stream);
+                 int64_t cap, int32_t* counter, float* vmask, float* umask, hipStream_t stream);
+void dgc_compensate(const float* g, float* u, float* v, float momentum, int64_t n, bool first, hipStream_t stream);
 
 // ---------------------------------------------------------------- powersgd.hip
 // mats: int64 [n_mat][6] = (x_off, n, m, r, p_off, q_off); tiles: int32 [n_tiles][3]
@@ -118,10 +123,14 @@ void scale_inplace(float* x, int64_t n, float s, hipStream_t stream);
 // ---------------------------------------------------------------- inceptionn.hip
 int64_t inceptionn_tiles(int64_t n);
 void inceptionn_count(const float* x, int64_t n, int e_b, int mid, int32_t* cnt, int32_t* totals, hipStream_t stream);
-void inceptionn_encode(const float* x, int64_t n, int e_b, int mid, const int32_t* off, float* v32, uint16_t* v16,
-                       uint8_t* v8, uint8_t* codes, hipStream_t stream);
-void inceptionn_decode(const int64_t* ptrs, const int64_t* code_ptrs, int n_ranks, int64_t n, int32_t* cnt,
-                       int32_t* totals, float scale, float* out, bool accumulate, hipStream_t stream);
+// totals (device, written by inceptionn_count) -> unified value stream of cap_bytes (drops the
+// lowest classes first when they do not fit; cap_bytes >= 4 n never drops)
+void inceptionn_encode(const float* x, int64_t n, int e_b, int mid, const int32_t* off, const int32_t* totals,
+                       uint8_t* stream, int64_t cap_bytes, uint8_t* codes, hipStream_t stream_);
+// W rank-strided payloads (stream at stream_off, codes at codes_off of each row) decoded + summed
+void inceptionn_decode(const uint8_t* base, int64_t rank_stride, int64_t stream_off, int64_t codes_off, int n_ranks,
+                       int64_t n, int32_t* cnt, int32_t* totals, float scale, float* out, bool accumulate,
+                       hipStream_t stream);
 
 // ---------------------------------------------------------------- adaq.hip
 void adaq_sample(const float* x, int n_seg, const int64_t* seg_off, const int64_t* samp_off, int64_t n_samples,
@@ -133,8 +142,11 @@ void adaq_refine(const ChunkTable& ct, int n_seg, const float* x, const TopkStat
                  const float* target, int max_iters, float* thr, int32_t* count, int32_t* done, hipStream_t stream);
 void adaq_offsets(int n_seg, const int32_t* count, int32_t* goff, int32_t* cursor, hipStream_t stream);
 void adaq_compact(const ChunkTable& ct, int n_seg, const int32_t* seg_chunk_begin, const float* x, const float* thr,
-                  const int32_t* goff, int32_t* cursor, int32_t* idx, double* psum, float* means, int32_t* counts,
-                  hipStream_t stream);
+                  const int32_t* goff, int32_t* cursor, int32_t* idx, int64_t cap, double* psum, float* means,
+                  int32_t* counts, hipStream_t stream);
+// one rank's capacity payload -> out (+)= means[group] * scale at its indices (goff_ws: n_groups+1)
+void adaq_decode(int n_groups, const float* means, const int32_t* counts, const int32_t* idx, int64_t cap,
+                 int32_t* goff_ws, float* out, float scale, hipStream_t stream);
 
 // ---------------------------------------------------------------- ef.hip (bucket gather)
 constexpr int kGatherSegs = 120;

@@ -192,7 +192,7 @@ constexpr int kTile = kBlock * kPer;
 __global__ __launch_bounds__(kBlock) void adaq_compact_kernel(ChunkTable ct, const float* __restrict__ x,
                                                               const float* __restrict__ thr,
                                                               int32_t* __restrict__ cursor,
-                                                              int32_t* __restrict__ idx,
+                                                              int32_t* __restrict__ idx, int64_t cap,
                                                               double* __restrict__ psum) {
   __shared__ int lds[kBlock / kWave];
   __shared__ int bcast[2];
@@ -229,8 +229,15 @@ __global__ __launch_bounds__(kBlock) void adaq_compact_kernel(ChunkTable ct, con
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const int32_t i = (int32_t)(tb + (int64_t)j * kBlock + threadIdx.x);
-      if ((take0 >> j) & 1u) idx[p0++] = i;
-      if ((take1 >> j) & 1u) idx[p1++] = i;
+      // slots past the payload capacity are not written (the group's sent count is clamped)
+      if ((take0 >> j) & 1u) {
+        if (p0 < cap) idx[p0] = i;
+        ++p0;
+      }
+      if ((take1 >> j) & 1u) {
+        if (p1 < cap) idx[p1] = i;
+        ++p1;
+      }
     }
     __syncthreads();
   }
@@ -251,7 +258,7 @@ __global__ __launch_bounds__(kBlock) void adaq_compact_kernel(ChunkTable ct, con
 // one workgroup per segment: means of both sides from the chunk partials, in chunk order
 __global__ __launch_bounds__(kBlock) void adaq_means_kernel(const int32_t* __restrict__ seg_chunk_begin,
                                                             const double* __restrict__ psum,
-                                                            const int32_t* __restrict__ goff,
+                                                            const int32_t* __restrict__ goff, int64_t cap,
                                                             float* __restrict__ means, int32_t* __restrict__ counts) {
   const int s = blockIdx.x;
   const int c0 = seg_chunk_begin[s], c1 = seg_chunk_begin[s + 1];
@@ -273,8 +280,47 @@ __global__ __launch_bounds__(kBlock) void adaq_means_kernel(const int32_t* __res
     for (int w = 0; w < kBlock / kWave; ++w) t += red[threadIdx.x][w];
     const int g = 2 * s + (int)threadIdx.x;
     const int cnt = goff[g + 1] - goff[g];
-    counts[g] = cnt;
+    // in-band header: the SENT count (slots inside the capacity); the mean is over the selection
+    const int64_t hi = goff[g + 1] < cap ? goff[g + 1] : cap;
+    counts[g] = hi > goff[g] ? (int)(hi - goff[g]) : 0;
     means[g] = cnt > 0 ? (float)(t / cnt) : 0.f;
+  }
+}
+
+// decode one rank's payload: out[idx[j]] += means[group(j)] * scale for j < sum(counts), groups
+// laid out back to back (exclusive scan of the in-band counts; no host read of the size)
+__global__ __launch_bounds__(kBlock) void adaq_decode_scan_kernel(int n_groups, const int32_t* __restrict__ counts,
+                                                                  int32_t* __restrict__ goff) {
+  __shared__ int lds[kBlock / kWave];
+  int carry = 0;
+  for (int g0 = 0; g0 < n_groups; g0 += kBlock) {
+    const int g = g0 + threadIdx.x;
+    const int v = g < n_groups ? counts[g] : 0;
+    int tot = 0;
+    const int ex = block_exclusive_scan<kBlock>(v, lds, &tot);
+    if (g < n_groups) goff[g] = carry + ex;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) goff[n_groups] = carry;
+}
+
+__global__ __launch_bounds__(kBlock) void adaq_decode_kernel(int n_groups, const float* __restrict__ means,
+                                                             const int32_t* __restrict__ goff,
+                                                             const int32_t* __restrict__ idx, int64_t cap,
+                                                             float* __restrict__ out, float scale) {
+  const int64_t tot = goff[n_groups];
+  const int64_t K = tot < cap ? tot : cap;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < K; j += stride) {
+    int lo = 0, hi = n_groups;  // last group with goff[g] <= j
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (goff[mid] <= j)
+        lo = mid;
+      else
+        hi = mid;
+    }
+    out[idx[j]] += means[lo] * scale;
   }
 }
 
@@ -324,11 +370,17 @@ void adaq_offsets(int n_seg, const int32_t* count, int32_t* goff, int32_t* curso
 }
 
 void adaq_compact(const ChunkTable& ct, int n_seg, const int32_t* seg_chunk_begin, const float* x, const float* thr,
-                  const int32_t* goff, int32_t* cursor, int32_t* idx, double* psum, float* means, int32_t* counts,
-                  hipStream_t stream) {
+                  const int32_t* goff, int32_t* cursor, int32_t* idx, int64_t cap, double* psum, float* means,
+                  int32_t* counts, hipStream_t stream) {
   if (ct.n_chunks > 0)
-    adaq_compact_kernel<<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, thr, cursor, idx, psum);
-  if (n_seg > 0) adaq_means_kernel<<<n_seg, kBlock, 0, stream>>>(seg_chunk_begin, psum, goff, means, counts);
+    adaq_compact_kernel<<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, thr, cursor, idx, cap, psum);
+  if (n_seg > 0) adaq_means_kernel<<<n_seg, kBlock, 0, stream>>>(seg_chunk_begin, psum, goff, cap, means, counts);
+}
+
+void adaq_decode(int n_groups, const float* means, const int32_t* counts, const int32_t* idx, int64_t cap,
+                 int32_t* goff_ws, float* out, float scale, hipStream_t stream) {
+  adaq_decode_scan_kernel<<<1, kBlock, 0, stream>>>(n_groups, counts, goff_ws);
+  adaq_decode_kernel<<<grid_for(cap), kBlock, 0, stream>>>(n_groups, means, goff_ws, idx, cap, out, scale);
 }
 
 }  // namespace grace

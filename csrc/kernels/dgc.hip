@@ -11,7 +11,10 @@
 //                  workgroup-reduced, one atomic per workgroup
 //   dgc_adjust   : per segment, the reference's rule; marks converged segments done
 //   dgc_compact  : ballot compaction of |x| >= thr[seg] into (value, flat index)
-// The only host sync left is reading the final element count (payload size is data dependent).
+//   dgc_compact  : capacity-bounded (the payload has a fixed capacity and an in-band count, so
+//                  the exchange needs no host sync and is graph-capturable), DgcMemory's u / v
+//                  masking fused in
+//   dgc_compensate: DgcMemory's momentum correction + accumulation in one pass
 #include "grace_common.h"
 #include "grace_kernels.h"
 #include "grace_scan.h"
@@ -35,9 +38,10 @@ __device__ __forceinline__ int find_seg64(const int64_t* __restrict__ off, int n
 
 __global__ __launch_bounds__(kBlock) void dgc_sample_kernel(const float* __restrict__ x, int n_seg,
                                                             const int64_t* __restrict__ seg_off,
-                                                            const int64_t* __restrict__ samp_off, uint64_t seed,
+                                                            const int64_t* __restrict__ samp_off, SeedArg sa,
                                                             float* __restrict__ samples) {
   const int64_t S = samp_off[n_seg];
+  const uint64_t seed = sa.get();  // device step mixed in: fresh samples on every graph replay
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < S; j += stride) {
     const int s = find_seg64(samp_off, n_seg, j);
@@ -102,11 +106,15 @@ constexpr int kPer = 32;
 constexpr int kTile = kBlock * kPer;
 
 // |x| >= thr[seg] -> (value, flat index); one atomic per 256x32 tile (grace_scan.h)
+// cap: payload capacity -- entries selected past it are not sent (and, with the fused DgcMemory
+// masking, keep their u / v, so they are sent by a later step: spill instead of loss).
+// vmask / umask (optional): DgcMemory.update fused in -- v and u are zeroed where sent.
 __global__ __launch_bounds__(kBlock) void dgc_compact_kernel(ChunkTable ct, const float* __restrict__ x,
                                                              const float* __restrict__ thr,
                                                              float* __restrict__ out_val,
-                                                             int32_t* __restrict__ out_idx,
-                                                             int32_t* __restrict__ counter) {
+                                                             int32_t* __restrict__ out_idx, int64_t cap,
+                                                             int32_t* __restrict__ counter, float* vmask,
+                                                             float* __restrict__ umask) {
   __shared__ int lds[kBlock / kWave];
   __shared__ int bcast;
   const int c = blockIdx.x;
@@ -130,17 +138,53 @@ __global__ __launch_bounds__(kBlock) void dgc_compact_kernel(ChunkTable ct, cons
     if (tot > 0) {
       if (threadIdx.x == 0) bcast = atomicAdd(counter, tot);
       __syncthreads();
-      int p = bcast + pre;
+      int64_t p = (int64_t)bcast + pre;
 #pragma unroll
       for (int j = 0; j < kPer; ++j) {
         if ((take >> j) & 1u) {
-          out_val[p] = v[j];
-          out_idx[p] = (int32_t)(tb + (int64_t)j * kBlock + threadIdx.x);
+          if (p < cap) {
+            const int64_t i = tb + (int64_t)j * kBlock + threadIdx.x;
+            out_val[p] = v[j];
+            out_idx[p] = (int32_t)i;
+            if (vmask != nullptr) vmask[i] = 0.f;
+            if (umask != nullptr) umask[i] = 0.f;
+          }
           ++p;
         }
       }
     }
     __syncthreads();
+  }
+}
+
+// DgcMemory.compensate fused: u = m*u + g; v = v + u (first call: u = v = g).  One pass reading
+// g, u, v and writing u, v instead of three eager elementwise launches.
+__global__ __launch_bounds__(kBlock) void dgc_compensate_kernel(const float* __restrict__ g, float* __restrict__ u,
+                                                                float* __restrict__ v, float m, int64_t n,
+                                                                int first) {
+  const int64_t n4 = n >> 2;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  float4* u4 = reinterpret_cast<float4*>(u);
+  float4* v4 = reinterpret_cast<float4*>(v);
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4; i += stride) {
+    const float4 gg = g4[i];
+    if (first) {
+      u4[i] = gg;
+      v4[i] = gg;
+    } else {
+      float4 uu = u4[i], vv = v4[i];
+      uu = make_float4(fmaf(m, uu.x, gg.x), fmaf(m, uu.y, gg.y), fmaf(m, uu.z, gg.z), fmaf(m, uu.w, gg.w));
+      vv = make_float4(vv.x + uu.x, vv.y + uu.y, vv.z + uu.z, vv.w + uu.w);
+      u4[i] = uu;
+      v4[i] = vv;
+    }
+  }
+  for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+    const float gg = g[i];
+    const float uu = first ? gg : fmaf(m, u[i], gg);
+    u[i] = uu;
+    v[i] = first ? gg : v[i] + uu;
   }
 }
 
@@ -154,7 +198,7 @@ inline int grid_for(int64_t n) {
 }  // namespace
 
 void dgc_sample(const float* x, int n_seg, const int64_t* seg_off, const int64_t* samp_off, int64_t n_samples,
-                uint64_t seed, float* samples, hipStream_t stream) {
+                SeedArg seed, float* samples, hipStream_t stream) {
   if (n_samples <= 0) return;
   dgc_sample_kernel<<<grid_for(n_samples), kBlock, 0, stream>>>(x, n_seg, seg_off, samp_off, seed, samples);
 }
@@ -172,10 +216,15 @@ void dgc_refine(const ChunkTable& ct, int n_seg, const float* x, const TopkState
 }
 
 void dgc_compact(const ChunkTable& ct, const float* x, const float* thr, float* out_val, int32_t* out_idx,
-                 int32_t* counter, hipStream_t stream) {
+                 int64_t cap, int32_t* counter, float* vmask, float* umask, hipStream_t stream) {
   GRACE_HIP_CHECK(hipMemsetAsync(counter, 0, sizeof(int32_t), stream));
   if (ct.n_chunks == 0) return;
-  dgc_compact_kernel<<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, thr, out_val, out_idx, counter);
+  dgc_compact_kernel<<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, thr, out_val, out_idx, cap, counter, vmask, umask);
+}
+
+void dgc_compensate(const float* g, float* u, float* v, float momentum, int64_t n, bool first, hipStream_t stream) {
+  if (n <= 0) return;
+  dgc_compensate_kernel<<<grid_for((n + 3) / 4), kBlock, 0, stream>>>(g, u, v, momentum, n, first ? 1 : 0);
 }
 
 }  // namespace grace

@@ -8,7 +8,10 @@
 //   class 2  mid <= e < 127  16-bit fixed point (sign | 1.mantissa >> (127 - e)) >> 8
 //   class 1  e_b <= e < mid   8-bit fixed point (same) >> 16
 //   class 0  e < e_b          dropped
-// Payload: [v32 fp32 | v16 uint16 | v8 uint8 | class codes, 2 bits/element, 4 per byte].
+// Payload (fixed capacity, graph-capturable): [int32 header = class totals (0, n8, n16, n32) |
+// value stream of `cap` bytes: v32 fp32, v16 uint16, v8 uint8 back to back | class codes, 2
+// bits/element, 4 per byte].  The decoder recounts the classes from the codes, so it needs no
+// size exchange and no host read.
 //
 // The three value streams are ORDER-PRESERVING compactions (the decoder pairs the i-th class-c
 // code with the i-th class-c value), so the workgroup mapping is "contiguous per thread":
@@ -125,12 +128,39 @@ __global__ __launch_bounds__(kBlock) void inc_scan_kernel(int32_t* __restrict__ 
   if (threadIdx.x < 4) totals[src * 4 + threadIdx.x] = threadIdx.x == 0 ? 0 : carry[threadIdx.x];
 }
 
-// Encode pass 2.  off: scanned per-tile offsets of the single source.
+// Unified value stream of a capacity payload: [v32 fp32 (n32) | v16 (n16) | v8 (n8)] starting at
+// byte 0, 4 * n32 and 4 * n32 + 2 * n16 (n* = class totals, device-resident).  `cap` bytes of
+// stream: when the classes do not fit, the lowest-precision classes are dropped first (class 1,
+// then class 2 -> code 0), and class-3 values past cap / 4 in element order are dropped; the
+// decoder recounts from the codes, so it stays consistent.  cap >= 4 n never drops anything.
+struct IncPlan {
+  bool keep1, keep2;
+  int64_t cap3;
+  int64_t off16, off8;
+};
+
+__device__ __forceinline__ IncPlan inc_plan(const int32_t* tot, int64_t cap) {
+  const int64_t n8 = tot[1], n16 = tot[2], n32 = tot[3];
+  IncPlan p;
+  p.keep2 = 4 * n32 + 2 * n16 <= cap;
+  p.keep1 = p.keep2 && 4 * n32 + 2 * n16 + n8 <= cap;
+  p.cap3 = cap / 4;
+  p.off16 = 4 * (n32 < p.cap3 ? n32 : p.cap3);
+  p.off8 = p.off16 + (p.keep2 ? 2 * n16 : 0);
+  return p;
+}
+
+// Encode pass 2.  off: scanned per-tile offsets of the single source; tot: its class totals.
 __global__ __launch_bounds__(kBlock) void inc_encode_kernel(const float* __restrict__ x, int64_t n, int e_b, int mid,
                                                             const int32_t* __restrict__ off,
-                                                            float* __restrict__ v32, uint16_t* __restrict__ v16,
-                                                            uint8_t* __restrict__ v8, uint8_t* __restrict__ codes) {
+                                                            const int32_t* __restrict__ tot,
+                                                            uint8_t* __restrict__ stream, int64_t cap,
+                                                            uint8_t* __restrict__ codes) {
   __shared__ int lds[kBlock / kWave];
+  const IncPlan pl = inc_plan(tot, cap);
+  float* v32 = reinterpret_cast<float*>(stream);
+  uint16_t* v16 = reinterpret_cast<uint16_t*>(stream + pl.off16);
+  uint8_t* v8 = stream + pl.off8;
   const int64_t tile = blockIdx.x;
   const int64_t base = tile * kTile + (int64_t)threadIdx.x * kPer;
   uint32_t u[kPer];
@@ -153,15 +183,21 @@ __global__ __launch_bounds__(kBlock) void inc_encode_kernel(const float* __restr
 #pragma unroll
   for (int j = 0; j < kPer; ++j) {
     const int64_t i = base + j;
-    const int k = i < n ? inc_class(u[j], e_b, mid) : 0;
-    packed[j >> 4] |= (uint32_t)k << (2 * (j & 15));
+    int k = i < n ? inc_class(u[j], e_b, mid) : 0;
     if (k == 3) {
-      v32[o3++] = __uint_as_float(u[j]);
+      if (o3 < pl.cap3)
+        v32[o3] = __uint_as_float(u[j]);
+      else
+        k = 0;  // past the capacity (always the LAST class-3 elements in order)
+      ++o3;
     } else if (k == 2) {
-      v16[o2++] = (uint16_t)((inc_fixed(u[j]) >> 8) & 0xFFFFu);
+      if (pl.keep2) v16[o2++] = (uint16_t)((inc_fixed(u[j]) >> 8) & 0xFFFFu);
+      else k = 0;
     } else if (k == 1) {
-      v8[o1++] = (uint8_t)((inc_fixed(u[j]) >> 16) & 0xFFu);
+      if (pl.keep1) v8[o1++] = (uint8_t)((inc_fixed(u[j]) >> 16) & 0xFFu);
+      else k = 0;
     }
+    packed[j >> 4] |= (uint32_t)k << (2 * (j & 15));
   }
   // 32 elements -> 8 code bytes (element base+j at byte (base+j)/4, bits 2*(j%4))
 #pragma unroll
@@ -173,10 +209,14 @@ __global__ __launch_bounds__(kBlock) void inc_encode_kernel(const float* __restr
   }
 }
 
-// ptrs: int64 [W][4] = (v32, v16, v8, codes) device addresses; off: [W][n_tiles][4] scanned.
-__global__ __launch_bounds__(kBlock) void inc_decode_kernel(const int64_t* __restrict__ ptrs, int n_ranks, int64_t n,
-                                                            int64_t n_tiles, const int32_t* __restrict__ off,
-                                                            float scale, float* __restrict__ out, int accumulate) {
+// W rank-strided capacity payloads in ONE buffer: rank r's stream at base + r*stride + stream_off,
+// its codes at base + r*stride + codes_off (no per-rank pointer table: graph-capturable).
+// off: [W][n_tiles][4] scanned counts recounted from the codes; tot: [W][4] their totals.
+__global__ __launch_bounds__(kBlock) void inc_decode_kernel(const uint8_t* __restrict__ base_u8, int64_t stride,
+                                                            int64_t stream_off, int64_t codes_off, int n_ranks,
+                                                            int64_t n, int64_t n_tiles, const int32_t* __restrict__ off,
+                                                            const int32_t* __restrict__ tot, float scale,
+                                                            float* __restrict__ out, int accumulate) {
   __shared__ int lds[kBlock / kWave];
   const int64_t tile = blockIdx.x;
   const int64_t base = tile * kTile + (int64_t)threadIdx.x * kPer;
@@ -184,10 +224,13 @@ __global__ __launch_bounds__(kBlock) void inc_decode_kernel(const int64_t* __res
 #pragma unroll
   for (int j = 0; j < kPer; ++j) acc[j] = 0.f;
   for (int r = 0; r < n_ranks; ++r) {
-    const float* v32 = reinterpret_cast<const float*>(ptrs[4 * r + 0]);
-    const uint16_t* v16 = reinterpret_cast<const uint16_t*>(ptrs[4 * r + 1]);
-    const uint8_t* v8 = reinterpret_cast<const uint8_t*>(ptrs[4 * r + 2]);
-    const uint8_t* codes = reinterpret_cast<const uint8_t*>(ptrs[4 * r + 3]);
+    const uint8_t* row = base_u8 + (int64_t)r * stride;
+    const uint8_t* codes = row + codes_off;
+    // after the encoder's drops the codes ARE the kept classes: plain back-to-back layout
+    const int32_t* t = tot + 4 * r;
+    const float* v32 = reinterpret_cast<const float*>(row + stream_off);
+    const uint16_t* v16 = reinterpret_cast<const uint16_t*>(row + stream_off + 4 * (int64_t)t[3]);
+    const uint8_t* v8 = row + stream_off + 4 * (int64_t)t[3] + 2 * (int64_t)t[2];
     int k[kPer];
     int c1 = 0, c23 = 0;
 #pragma unroll
@@ -221,6 +264,40 @@ __global__ __launch_bounds__(kBlock) void inc_decode_kernel(const int64_t* __res
   }
 }
 
+// recount from codes: per-tile class counts of W rank-strided code arrays
+__global__ __launch_bounds__(kBlock) void inc_count_codes_kernel(const uint8_t* __restrict__ base_u8, int64_t stride,
+                                                                 int64_t codes_off, int64_t n, int64_t n_tiles,
+                                                                 int32_t* __restrict__ cnt) {
+  const int src = blockIdx.y;
+  const int64_t tile = blockIdx.x;
+  const uint8_t* codes = base_u8 + (int64_t)src * stride + codes_off;
+  const int64_t base = tile * kTile + (int64_t)threadIdx.x * kPer;
+  int c[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int64_t i = base + j;
+    if (i < n) {
+      const int k = code_at(codes, i);
+      c[1] += k == 1;
+      c[2] += k == 2;
+      c[3] += k == 3;
+    }
+  }
+  __shared__ int red[3][kBlock / kWave];
+#pragma unroll
+  for (int k = 1; k < 4; ++k) {
+    const int v = (int)wave_sum_u32((unsigned)c[k]);
+    if (lane_id() == 0) red[k - 1][wave_id()] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    int s = 0;
+    for (int w = 0; w < kBlock / kWave; ++w) s += red[threadIdx.x][w];
+    cnt[((int64_t)src * n_tiles + tile) * 4 + 1 + threadIdx.x] = s;
+  }
+  if (threadIdx.x == 3) cnt[((int64_t)src * n_tiles + tile) * 4] = 0;
+}
+
 }  // namespace
 
 int64_t inceptionn_tiles(int64_t n) { return (n + kTile - 1) / kTile; }
@@ -236,21 +313,23 @@ void inceptionn_count(const float* x, int64_t n, int e_b, int mid, int32_t* cnt,
   inc_scan_kernel<<<1, kBlock, 0, stream>>>(cnt, nt, totals);
 }
 
-void inceptionn_encode(const float* x, int64_t n, int e_b, int mid, const int32_t* off, float* v32, uint16_t* v16,
-                       uint8_t* v8, uint8_t* codes, hipStream_t stream) {
+void inceptionn_encode(const float* x, int64_t n, int e_b, int mid, const int32_t* off, const int32_t* totals,
+                       uint8_t* stream, int64_t cap_bytes, uint8_t* codes, hipStream_t stream_) {
   const int64_t nt = inceptionn_tiles(n);
   if (nt == 0) return;
-  inc_encode_kernel<<<(unsigned)nt, kBlock, 0, stream>>>(x, n, e_b, mid, off, v32, v16, v8, codes);
+  inc_encode_kernel<<<(unsigned)nt, kBlock, 0, stream_>>>(x, n, e_b, mid, off, totals, stream, cap_bytes, codes);
 }
 
-void inceptionn_decode(const int64_t* ptrs, const int64_t* code_ptrs, int n_ranks, int64_t n, int32_t* cnt,
-                       int32_t* totals, float scale, float* out, bool accumulate, hipStream_t stream) {
+void inceptionn_decode(const uint8_t* base, int64_t rank_stride, int64_t stream_off, int64_t codes_off, int n_ranks,
+                       int64_t n, int32_t* cnt, int32_t* totals, float scale, float* out, bool accumulate,
+                       hipStream_t stream) {
   const int64_t nt = inceptionn_tiles(n);
   if (nt == 0 || n_ranks <= 0) return;
-  inc_count_kernel<true><<<dim3((unsigned)nt, (unsigned)n_ranks), kBlock, 0, stream>>>(nullptr, code_ptrs, n, nt, 0, 0,
-                                                                                      cnt);
+  inc_count_codes_kernel<<<dim3((unsigned)nt, (unsigned)n_ranks), kBlock, 0, stream>>>(base, rank_stride, codes_off,
+                                                                                       n, nt, cnt);
   inc_scan_kernel<<<n_ranks, kBlock, 0, stream>>>(cnt, nt, totals);
-  inc_decode_kernel<<<(unsigned)nt, kBlock, 0, stream>>>(ptrs, n_ranks, n, nt, cnt, scale, out, accumulate ? 1 : 0);
+  inc_decode_kernel<<<(unsigned)nt, kBlock, 0, stream>>>(base, rank_stride, stream_off, codes_off, n_ranks, n, nt, cnt,
+                                                         totals, scale, out, accumulate ? 1 : 0);
 }
 
 }  // namespace grace

@@ -83,7 +83,7 @@ constexpr int kTile = kBlock * kPer;
 __global__ __launch_bounds__(kBlock) void threshold_compact_kernel(const float* g, const float* r, int mode,
                                                                    float beta, float gamma, int64_t n,
                                                                    float thr, float* __restrict__ out_val,
-                                                                   int32_t* __restrict__ out_idx,
+                                                                   int32_t* __restrict__ out_idx, int64_t cap,
                                                                    int32_t* __restrict__ counter,
                                                                    float* resid) {
   __shared__ int lds[kBlock / kWave];
@@ -104,24 +104,28 @@ __global__ __launch_bounds__(kBlock) void threshold_compact_kernel(const float* 
     }
     int tot = 0;
     const int pre = block_exclusive_scan<kBlock>(__popc(take), lds, &tot);
+    uint32_t sent = 0;  // selected AND inside the payload capacity
     if (tot > 0) {
       if (threadIdx.x == 0) bcast = atomicAdd(counter, tot);
       __syncthreads();
-      int p = bcast + pre;
+      int64_t p = (int64_t)bcast + pre;
 #pragma unroll
       for (int j = 0; j < kPer; ++j) {
         if ((take >> j) & 1u) {
-          out_val[p] = v[j];
-          out_idx[p] = (int32_t)(tb + (int64_t)j * kBlock + threadIdx.x);
+          if (p < cap) {
+            out_val[p] = v[j];
+            out_idx[p] = (int32_t)(tb + (int64_t)j * kBlock + threadIdx.x);
+            sent |= 1u << j;
+          }
           ++p;
         }
       }
     }
-    if (resid != nullptr) {
+    if (resid != nullptr) {  // spilled (selected past the capacity) entries stay in the residual
 #pragma unroll
       for (int j = 0; j < kPer; ++j) {
         const int64_t i = tb + (int64_t)j * kBlock + threadIdx.x;
-        if (i < n) resid[i] = ((take >> j) & 1u) ? 0.f : v[j];
+        if (i < n) resid[i] = ((sent >> j) & 1u) ? 0.f : v[j];
       }
     }
     __syncthreads();
@@ -153,13 +157,14 @@ void randk_scatter(const float* vals, int64_t rank_stride, int n_ranks, int n_se
 }
 
 void threshold_compact(const float* g, const float* r, int mode, float beta, float gamma, int64_t n, float thr,
-                       float* out_val, int32_t* out_idx, int32_t* counter, float* resid, hipStream_t stream) {
+                       float* out_val, int32_t* out_idx, int64_t cap, int32_t* counter, float* resid,
+                       hipStream_t stream) {
   GRACE_HIP_CHECK(hipMemsetAsync(counter, 0, sizeof(int32_t), stream));
   if (n <= 0) return;
   int64_t tiles = (n + kTile - 1) / kTile;
   if (tiles > 2048) tiles = 2048;
   threshold_compact_kernel<<<(int)tiles, kBlock, 0, stream>>>(g, r, mode, beta, gamma, n, thr, out_val, out_idx,
-                                                              counter, resid);
+                                                              cap, counter, resid);
 }
 
 }  // namespace grace

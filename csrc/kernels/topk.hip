@@ -598,6 +598,23 @@ __global__ __launch_bounds__(kBlock) void sparse_scatter_add_kernel(const float*
   }
 }
 
+// out[idx[j]] += val[j] * scale for j < min(*count, cap): the count lives in the payload's
+// in-band header (capacity payloads of the variable-size codecs: no host read of the size)
+__global__ __launch_bounds__(kBlock) void sparse_scatter_add_dev_kernel(const float* __restrict__ val,
+                                                                        const int32_t* __restrict__ idx,
+                                                                        const int32_t* __restrict__ count,
+                                                                        int64_t cap, float* __restrict__ out,
+                                                                        float scale, int accumulate) {
+  const int64_t c = *count;
+  const int64_t K = c < cap ? c : cap;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < K; j += stride) {
+    const int32_t t = idx[j];
+    const float add = val[j] * scale;
+    out[t] = accumulate ? out[t] + add : add;
+  }
+}
+
 }  // namespace
 
 void topk_select_bucket(const ChunkTable& ct, int n_seg, const float* g, const float* r, float* x,
@@ -645,6 +662,15 @@ void sparse_scatter_add(const float* val, const int32_t* idx, int64_t K, float* 
   int64_t blocks = (K + kBlock - 1) / kBlock;
   if (blocks > 4096) blocks = 4096;
   sparse_scatter_add_kernel<<<(int)blocks, kBlock, 0, stream>>>(val, idx, K, out, scale, accumulate ? 1 : 0);
+}
+
+void sparse_scatter_add_dev(const float* val, const int32_t* idx, const int32_t* count, int64_t cap, float* out,
+                            float scale, bool accumulate, hipStream_t stream) {
+  if (cap <= 0) return;
+  int64_t blocks = (cap + kBlock - 1) / kBlock;
+  if (blocks > 2048) blocks = 2048;
+  sparse_scatter_add_dev_kernel<<<(int)blocks, kBlock, 0, stream>>>(val, idx, count, cap, out, scale,
+                                                                    accumulate ? 1 : 0);
 }
 
 }  // namespace grace

@@ -11,11 +11,14 @@ Decompress writes plus_mean / minus_mean at the indices.
 MI355X (csrc/kernels/adaq.hip): every segment of a bucket and both sides at once, on the
 device -- Philox 1% sample, the segmented radix select of topk.hip for the initial thresholds,
 the refinement loop with both sides counted per pass over the bucket, ordered compaction of the
-indices and deterministic per-group means; one host read sizes the payload.  The PyTorch path
+indices and deterministic per-group means.  The payload has a FIXED index capacity (default 2 x
+the summed targets) and the per-group counts in-band, so nothing is read back to the host and the
+exchange is graph-capturable; the decoder scans the counts on the device.  The PyTorch path
 (per segment, torch RNG, sampling among the side's entries exactly as the reference) is the
 CPU oracle.  Payload [means fp32 (+,- per segment) | counts int32 (+,- per segment) | indices
 int32].  A side with no entries sends mean 0 and no index (the reference computes the mean of
-an empty set -> NaN).  Variable-size payload (Allgather).
+an empty set -> NaN).  Entries selected past the capacity are not sent (their group's mean still
+covers them).
 """
 from __future__ import annotations
 
@@ -54,9 +57,16 @@ def _side(vals_abs: torch.Tensor, ratio: float, gen) -> torch.Tensor:
 
 
 class AdaqCompressor(BucketCompressor):
-    def __init__(self, compress_ratio: float = 0.01):
-        super().__init__(tensors_size_are_same=False)
+    def __init__(self, compress_ratio: float = 0.01, capacity: float = 2.0):
+        super().__init__(tensors_size_are_same=True)  # fixed-capacity payload, counts in-band
         self.compress_ratio = compress_ratio
+        self.capacity = capacity
+
+    def _cap(self, lay) -> int:
+        """Index capacity: ``capacity`` x the summed per-side targets (<= ceil(n_i * ratio) + 1
+        per side), at most the bucket."""
+        tgt = sum(n * self.compress_ratio + 2 for n in lay.numels if n > 0)
+        return max(1, min(lay.total, int(math.ceil(self.capacity * tgt))))
 
     max_iters = 20
 
@@ -98,9 +108,8 @@ class AdaqCompressor(BucketCompressor):
         C.adaq_refine(x, ws["state"], ws["fallback"], ws["target"], self.max_iters, ws["thr"], ws["count"],
                       ws["done"], t["seg"], t["begin"], t["end"])
         C.adaq_offsets(ws["count"], ws["goff"], ws["cursor"])
-        total = int(ws["goff"][-1].item())  # payload size (data dependent): the one host read
         m, cnt, ix = self.payload(dev, [(torch.float32, (2 * lay.n_seg,)), (torch.int32, (2 * lay.n_seg,)),
-                                        (torch.int32, (total,))])
+                                        (torch.int32, (self._cap(lay),))])
         psum = torch.empty(max(1, 2 * t["n_chunks"]), dtype=torch.float64, device=dev)
         C.adaq_compact(x, ws["thr"], ws["goff"], ws["cursor"], ix, psum, m, cnt, t["seg"], t["begin"], t["end"],
                        t["seg_chunk_begin"])
@@ -127,17 +136,31 @@ class AdaqCompressor(BucketCompressor):
                 counts[2 * i + side] = chosen.numel()
                 idx_all.append((chosen + o).to(torch.int32))
         idx = torch.cat(idx_all) if idx_all else torch.empty(0, dtype=torch.int32, device=x.device)
+        cap = self._cap(lay)
         m, cnt, ix = self.payload(x.device, [(torch.float32, (2 * lay.n_seg,)), (torch.int32, (2 * lay.n_seg,)),
-                                             (torch.int32, (idx.numel(),))])
+                                             (torch.int32, (cap,))])
+        # groups back to back; the in-band counts are the entries inside the capacity
+        goff = torch.cumsum(counts.long(), 0) - counts.long()
+        counts = (torch.clamp(cap - goff, min=0)).minimum(counts.long()).to(torch.int32)
         m.copy_(means)
         cnt.copy_(counts)
-        ix.copy_(idx)
+        ix.zero_()
+        k = min(cap, idx.numel())
+        ix[:k] = idx[:k]
         return [m, cnt, ix], ctx
 
     def decompress_aggregate_impl(self, per_rank, ctx, n_ranks, scale):
-        out = self.out_buffer(ctx, per_rank[0][0].device, zero=True)
+        dev = per_rank[0][0].device
+        out = self.out_buffer(ctx, dev, zero=True)
+        if _native.use_native(out):
+            C = _native.lib()
+            ws = ctx.layout.cached(dev, "adaq_dec", lambda: torch.empty(2 * ctx.layout.n_seg + 1, dtype=torch.int32,
+                                                                        device=dev))
+            for means, counts, idx in per_rank:  # rank order: identical on every rank
+                C.adaq_decode(means, counts, idx, ws, out, scale)
+            return self.finish(out, ctx)
         for means, counts, idx in per_rank:
             reps = counts.to(device=means.device, dtype=torch.int64)
             v = torch.repeat_interleave(means, reps)  # [plus_0.., minus_0.., plus_1.., ...]
-            K.scatter_add(v, idx, out, scale, accumulate=True)
+            K.scatter_add(v, idx[: v.numel()], out, scale, accumulate=True)
         return self.finish(out, ctx)

@@ -8,42 +8,65 @@ then up to 10 refinements (x1.3 if more than 1.3*ratio*n entries pass, x0.7 if f
 Differences by design: the sample indices are drawn on the payload's device (the reference
 indexes a GPU tensor with a CPU index tensor, survey 2.14 #11), per-segment thresholds for
 flat buckets, the refinement runs on the device (csrc/kernels/dgc.hip: one count pass per
-iteration, segments that converged stop counting) and the sparse payload is
-fp32 values + int32 indices.  ``ctx.selected`` (flat indices) replaces the dense mask.
+iteration, segments that converged stop counting) and the sparse payload is a FIXED-capacity
+[header | fp32 values | int32 indices] buffer with the count in-band (ops/cappayload.py): no
+host read of the size, so DGC steps are graph-capturable.  ``capacity`` (default 2.0 x the
+summed per-segment targets) bounds the bytes on the wire; entries selected past it keep their
+DgcMemory u / v and are sent later.  With DgcMemory the momentum correction, the selection and
+the u / v masking run as one fused native sequence (``fused_compress``).
 """
 from __future__ import annotations
 
-from dataclasses import dataclass, field
-
 import torch
 
-from ..core import layout_of
+from ..ops import _native
+from ..ops import cappayload as P
 from ..ops import dgc as D
-from ..ops import topk as K
 from ._base import BucketCompressor, Ctx
 
 
 class DgcCompressor(BucketCompressor):
-    def __init__(self, compress_ratio: float = 0.01, sample_ratio: float = 0.01, max_iters: int = 10):
-        super().__init__(tensors_size_are_same=False)
+    def __init__(self, compress_ratio: float = 0.01, sample_ratio: float = 0.01, max_iters: int = 10,
+                 capacity: float = 2.0):
+        super().__init__(tensors_size_are_same=True)  # fixed-capacity payload (ops/cappayload.py)
         self.compress_ratio = compress_ratio
         self.sample_ratio = sample_ratio
         self.max_iters = max_iters
+        self.capacity = capacity
+
+    def _select(self, g, ctx, name, vmask=None, umask=None):
+        cap = D.dgc_capacity(ctx.layout, self.compress_ratio, self.capacity)
+        seed, step = self.next_rng(name, g.device)
+        hdr, vals, idx = D.dgc_select(g, ctx.layout, self.compress_ratio, self.sample_ratio, self.max_iters,
+                                      seed, cap, step, vmask, umask)
+        ctx.extra["sent"] = (hdr, idx)
+        return [hdr, vals, idx], ctx
 
     def compress(self, tensor, name):
         ctx = self.ctx(tensor, name)
+        return self._select(self.flat(tensor), ctx, name)
+
+    def fused_compress(self, tensor, name, memory):
+        """DgcMemory fused: one pass u = m*u + g, v += u (csrc/kernels/dgc.hip dgc_compensate), the
+        selection on v, and the u / v masking of DgcMemory.update inside the compaction."""
+        from ..memory.dgc import DgcMemory
+
+        if not isinstance(memory, DgcMemory) or not _native.use_native(tensor):
+            return None
+        if memory.gradient_clipping:
+            tensor = memory._clip(tensor, name)
         g = self.flat(tensor)
-        vals, idx = D.dgc_select(g, ctx.layout, self.compress_ratio, self.sample_ratio, self.max_iters,
-                                 self.next_seed(name))
-        ctx.extra["selected"] = idx
-        return [vals, idx], ctx
+        u, v, first = memory.state_buffers(name, g)
+        _native.lib().dgc_compensate(g, u, v, memory.momentum, first)
+        ctx = self.ctx(tensor, name)
+        return self._select(v, ctx, name, vmask=v, umask=u)
 
     def decompress_aggregate_impl(self, per_rank, ctx, n_ranks, scale):
-        out = self.out_buffer(ctx, per_rank[0][0].device, zero=True)
-        for v, i in per_rank:
-            K.scatter_add(v, i, out, scale, accumulate=True)
+        out = self.out_buffer(ctx, per_rank[0][1].device, zero=True)
+        for hdr, v, i in per_rank:  # rank order: identical on every rank
+            P.scatter_capped(hdr, v, i, out, scale, accumulate=True)
         return self.finish(out, ctx)
 
 
-# DgcMemory reads ctx.selected
-Ctx.selected = property(lambda self: self.extra["selected"].long())
+# DgcMemory (generic, unfused path) reads the sent entries from ctx.extra["sent"]
+Ctx.selected = property(lambda self: self.extra["sent"])

@@ -13,11 +13,15 @@ the position of the leading one (tfp find_bins over powers of two in the referen
 MI355X: csrc/kernels/inceptionn.hip -- a per-tile class count + device scan, then ONE encode
 pass writes the 2-bit codes and the three order-preserving compacted streams; the decoder
 recounts classes from every rank's codes and decodes + sums all W ranks in one pass (rank
-order, deterministic).  One host read of the three class totals sizes the payload (the size is
-data dependent, as in the reference).  The PyTorch path below is the CPU oracle (bit-identical).
+order, deterministic).  The payload has a FIXED capacity (ops/cappayload.py idea): an int32
+header with the class totals, ONE value stream of 4 * ceil(capacity * n) bytes holding the fp32,
+16-bit and 8-bit values back to back, and the codes -- no host read of a size, graph-capturable.
+capacity 1.0 (default) always fits (every element as fp32); below it the lowest-precision
+classes are dropped first when the step's values do not fit.  The PyTorch path below is the CPU
+oracle (bit-identical).
 The class codes are packed little-endian 4 per byte (element 4j+t at bits 2t of byte j) instead
 of the reference's quarter-split layout (wire-format detail, same information).
-Payload [fp32 v32 | int16 v16 | uint8 v8 | uint8 classes].  Variable size.
+Payload [int32 header (0, n8, n16, n32) | value stream | uint8 classes].
 """
 from __future__ import annotations
 
@@ -43,26 +47,31 @@ def _leading_bin(v: torch.Tensor) -> torch.Tensor:
 
 
 class INCEPTIONNCompressor(BucketCompressor):
-    def __init__(self, error_bound: float = 2e-10):
-        super().__init__(tensors_size_are_same=False)
+    def __init__(self, error_bound: float = 2e-10, capacity: float = 1.0):
+        super().__init__(tensors_size_are_same=True)  # fixed-capacity payload
         self.error_bound = error_bound
         self.e_b = 127 + int(math.log(error_bound / 2, 10))
         self.mid = self.e_b + math.ceil((127 - self.e_b) / 2)
+        self.capacity = capacity
+
+    def _cap_bytes(self, n: int) -> int:
+        """Value-stream bytes: 4 * ceil(capacity * n) (1.0 = every element fits as fp32)."""
+        return 4 * max(1, int(math.ceil(self.capacity * n)))
+
+    def _payload(self, dev, n):
+        return self.payload(dev, [(torch.int32, (4,)), (torch.uint8, (self._cap_bytes(n),)),
+                                  (torch.uint8, ((n + 3) // 4,))])
 
     def _native_compress(self, x, ctx):
         C = _native.lib()
         n = x.numel()
         nt = C.inceptionn_tiles(n)
-        lay = ctx.layout
-        ws = lay.cached(x.device, "inceptionn_enc", lambda: {
-            "cnt": torch.empty(max(1, 4 * nt), dtype=torch.int32, device=x.device),
-            "tot": torch.empty(4, dtype=torch.int32, device=x.device)})
-        C.inceptionn_count(x, self.e_b, self.mid, ws["cnt"], ws["tot"])
-        _, n8, n16, n32 = (int(v) for v in ws["tot"].tolist())  # payload size: one host read
-        a, b, c, d = self.payload(x.device, [(torch.float32, (n32,)), (torch.int16, (n16,)), (torch.uint8, (n8,)),
-                                             (torch.uint8, ((n + 3) // 4,))])
-        C.inceptionn_encode(x, self.e_b, self.mid, ws["cnt"], a, b, c, d)
-        return [a, b, c, d]
+        ws = ctx.layout.cached(x.device, "inceptionn_enc", lambda: torch.empty(max(1, 4 * nt), dtype=torch.int32,
+                                                                              device=x.device))
+        hdr, stream, codes = self._payload(x.device, n)
+        C.inceptionn_count(x, self.e_b, self.mid, ws, hdr)  # class totals -> the in-band header
+        C.inceptionn_encode(x, self.e_b, self.mid, ws, hdr, stream, codes)
+        return [hdr, stream, codes]
 
     def compress(self, tensor, name):
         ctx = self.ctx(tensor, name)
@@ -76,27 +85,45 @@ class INCEPTIONNCompressor(BucketCompressor):
         c32 = expo >= 127
         c16 = (expo >= self.mid) & (expo < 127)
         c8 = (expo >= self.e_b) & (expo < self.mid)
+        n = x.numel()
+        n32, n16, n8 = int(c32.sum()), int(c16.sum()), int(c8.sum())
+        cap = self._cap_bytes(n)
+        # capacity plan (same as csrc/kernels/inceptionn.hip inc_plan): drop class 8, then 16,
+        # then the last class-32 elements
+        keep2 = 4 * n32 + 2 * n16 <= cap
+        keep1 = keep2 and 4 * n32 + 2 * n16 + n8 <= cap
+        cap3 = cap // 4
+        if n32 > cap3:
+            pos = torch.cumsum(c32.long(), 0) - 1
+            c32 = c32 & (pos < cap3)
+        if not keep2:
+            c16 = torch.zeros_like(c16)
+        if not keep1:
+            c8 = torch.zeros_like(c8)
         shift = (127 - expo).clamp(0, 63)
         fixed = (sign >> 8) | (((mant >> 1) | 0x400000) >> shift)
-        v16 = ((fixed >> 8) & 0xFFFF)[c16]
-        v8 = ((fixed >> 16) & 0xFF)[c8]
+        v16 = ((fixed >> 8) & 0xFFFF)[c16].to(torch.int32).to(torch.int16)
+        v8 = ((fixed >> 16) & 0xFF)[c8].to(torch.uint8)
         v32 = x[c32]
         code = c8.long() * 1 + c16.long() * 2 + c32.long() * 3
-        n = x.numel()
         npad = (n + 3) // 4 * 4
         cp = torch.zeros(npad, dtype=torch.int64, device=x.device)
         cp[:n] = code
         packed = (cp.view(-1, 4) << torch.tensor([0, 2, 4, 6], device=x.device)).sum(1)
-        a, b, c, d = self.payload(x.device, [(torch.float32, (v32.numel(),)), (torch.int16, (v16.numel(),)),
-                                             (torch.uint8, (v8.numel(),)), (torch.uint8, (packed.numel(),))])
-        a.copy_(v32)
-        b.copy_(v16.to(torch.int32).to(torch.int16))
-        c.copy_(v8.to(torch.uint8))
-        d.copy_(packed.to(torch.uint8))
-        return [a, b, c, d], ctx
+        hdr, stream, codes = self._payload(x.device, n)
+        hdr.copy_(torch.tensor([0, n8, n16, n32], dtype=torch.int32))
+        stream.zero_()
+        body = torch.cat([v32.view(torch.uint8), v16.view(torch.uint8), v8])
+        stream[: body.numel()] = body
+        codes.copy_(packed.to(torch.uint8))
+        return [hdr, stream, codes], ctx
 
-    def _decode(self, v32, v16, v8, packed, n, device):
+    def _decode(self, stream, packed, n, device):
         codes = ((packed.to(torch.int64).unsqueeze(1) >> torch.tensor([0, 2, 4, 6], device=device)) & 3).view(-1)[:n]
+        n32, n16, n8 = int((codes == 3).sum()), int((codes == 2).sum()), int((codes == 1).sum())
+        v32 = stream[: 4 * n32].view(torch.float32)
+        v16 = stream[4 * n32: 4 * n32 + 2 * n16].view(torch.int16)
+        v8 = stream[4 * n32 + 2 * n16: 4 * n32 + 2 * n16 + n8]
         out = torch.zeros(n, dtype=torch.float32, device=device)
         # 16-bit class
         w = v16.to(torch.int64) & 0xFFFF
@@ -123,19 +150,19 @@ class INCEPTIONNCompressor(BucketCompressor):
 
     def decompress_aggregate_impl(self, per_rank, ctx, n_ranks, scale):
         dev = per_rank[0][0].device
-        if _native.use_native(per_rank[0][3]):
+        n = ctx.layout.total
+        if _native.use_native(per_rank[0][2]):
             C = _native.lib()
-            n = ctx.layout.total
             out = self.out_buffer(ctx, dev)
-            ptrs = torch.tensor([t.data_ptr() for p in per_rank for t in p], dtype=torch.int64).to(dev)
-            cptr = torch.tensor([p[3].data_ptr() for p in per_rank], dtype=torch.int64).to(dev)
-            cnt = torch.empty(max(1, 4 * n_ranks * C.inceptionn_tiles(n)), dtype=torch.int32, device=dev)
-            tot = torch.empty(4 * n_ranks, dtype=torch.int32, device=dev)
-            C.inceptionn_decode(ptrs, cptr, n_ranks, cnt, tot, scale, out, False)
+            base, stride, offs = self.rows(per_rank)
+            ws = ctx.layout.cached(dev, f"inceptionn_dec:{n_ranks}", lambda: (
+                torch.empty(max(1, 4 * n_ranks * C.inceptionn_tiles(n)), dtype=torch.int32, device=dev),
+                torch.empty(4 * n_ranks, dtype=torch.int32, device=dev)))
+            C.inceptionn_decode(base, stride, offs[1], offs[2], n_ranks, ws[0], ws[1], scale, out, False)
             return self.finish(out, ctx)
         out = self.out_buffer(ctx, dev, zero=True)
-        for v32, v16, v8, packed in per_rank:
-            out += self._decode(v32, v16, v8, packed, ctx.layout.total, dev)
+        for _hdr, stream, packed in per_rank:
+            out += self._decode(stream, packed, n, dev)
         if scale != 1.0:
             out *= scale
         return self.finish(out, ctx)

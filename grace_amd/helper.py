@@ -8,7 +8,8 @@ Broadcast receives the rank, Threshold defaults to 0.01 (survey 2.14 #3, #4, #13
 
 Recognised keys: compressor, memory, communicator, world_size, compress_ratio, lr,
 quantum_num, threshold, momentum (signum), dgc_momentum, gradient_clipping, compress_rank,
-warm_start, error_bound, quantiles, beta, gamma, fp16_dtype.
+warm_start, error_bound, quantiles, beta, gamma, fp16_dtype, capacity (payload capacity of the
+variable-size codecs threshold / dgc / adaq / inceptionn, ops/cappayload.py).
 """
 from __future__ import annotations
 
@@ -26,8 +27,8 @@ COMPRESSORS: Dict[str, Callable[[Dict[str, Any]], Any]] = {
         str(p.get("fp16_dtype", "fp16")), torch.float16)),
     "topk": lambda p: Z.TopKCompressor(p.get("compress_ratio", 0.01)),
     "randomk": lambda p: Z.RandomKCompressor(p.get("compress_ratio", 0.01)),
-    "threshold": lambda p: Z.ThresholdCompressor(p.get("threshold", 0.01)),
-    "dgc": lambda p: Z.DgcCompressor(p.get("compress_ratio", 0.01)),
+    "threshold": lambda p: Z.ThresholdCompressor(p.get("threshold", 0.01), capacity=p.get("capacity", 1.0)),
+    "dgc": lambda p: Z.DgcCompressor(p.get("compress_ratio", 0.01), capacity=p.get("capacity", 2.0)),
     "qsgd": lambda p: Z.QSGDCompressor(p.get("quantum_num", 127)),
     "terngrad": lambda p: Z.TernGradCompressor(),
     "signsgd": lambda p: Z.SignSGDCompressor(),
@@ -38,8 +39,8 @@ COMPRESSORS: Dict[str, Callable[[Dict[str, Any]], Any]] = {
     "powersgd": lambda p: Z.PowerSGDCompressor(rank=p.get("compress_rank", 1),
                                                warm_start=p.get("warm_start", False),
                                                world_size=p.get("world_size")),
-    "adaq": lambda p: Z.AdaqCompressor(p.get("compress_ratio", 0.01)),
-    "inceptionn": lambda p: Z.INCEPTIONNCompressor(p.get("error_bound", 2e-10)),
+    "adaq": lambda p: Z.AdaqCompressor(p.get("compress_ratio", 0.01), capacity=p.get("capacity", 2.0)),
+    "inceptionn": lambda p: Z.INCEPTIONNCompressor(p.get("error_bound", 2e-10), capacity=p.get("capacity", 1.0)),
     "sketch": lambda p: Z.SketchCompressor(p.get("quantiles", 64)),
     "u8bit": lambda p: Z.U8bitCompressor(),
 }

@@ -1,7 +1,8 @@
 """DGC threshold selection (native: csrc/kernels/dgc.hip + the segmented radix select)."""
 from __future__ import annotations
 
-from typing import Tuple
+import math
+from typing import Optional, Tuple
 
 import torch
 
@@ -16,12 +17,25 @@ def _sizes(layout: SegmentLayout, ratio: float, sample_ratio: float):
     return ns, ks
 
 
+def dgc_capacity(layout: SegmentLayout, ratio: float, capacity: float) -> int:
+    """Payload capacity: ``capacity`` x the summed per-segment targets max(1, ratio * n_i)
+    (the refinement aims at [0.7, 1.3] x target; 2.0 leaves room for the segments that end the
+    10 refinements outside that band), never more than the bucket."""
+    tgt = sum(max(1.0, n * ratio) for n in layout.numels if n > 0)
+    return max(1, min(layout.total, int(math.ceil(capacity * tgt))))
+
+
 def dgc_select(x: torch.Tensor, layout: SegmentLayout, ratio: float, sample_ratio: float, max_iters: int,
-               seed: int) -> Tuple[torch.Tensor, torch.Tensor]:
-    from ..parallel.comm import PayloadBuilder
+               seed: int, cap: int, step: Optional[torch.Tensor] = None, vmask: Optional[torch.Tensor] = None,
+               umask: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """DGC selection of |x| >= thr_i per segment into a capacity payload (header, values, indices).
+    ``step``: device step counter mixed into the sampling seed on the device (graph replays draw
+    fresh samples); ``vmask`` / ``umask``: DgcMemory's v / u, zeroed at the SENT entries."""
+    from .cappayload import sparse_payload
 
     ns, ks = _sizes(layout, ratio, sample_ratio)
     dev = x.device
+    hdr, v, i = sparse_payload(dev, cap)
     if _native.use_native(x):
         C = _native.lib()
         slay = layout.cached(dev, f"dgc_sample_layout:{sample_ratio}",
@@ -37,32 +51,24 @@ def dgc_select(x: torch.Tensor, layout: SegmentLayout, ratio: float, sample_rati
                 "count": torch.empty(layout.n_seg, dtype=torch.int32, device=dev),
                 "done": torch.empty(layout.n_seg, dtype=torch.int32, device=dev),
                 "samples": torch.empty(max(1, slay.total), dtype=torch.float32, device=dev),
-                "cnt": torch.zeros(1, dtype=torch.int32, device=dev),
             }
 
         ws = layout.cached(dev, f"dgc_ws:{ratio}:{sample_ratio}", build)
         sd = seed & 0xFFFFFFFFFFFFFFFF
         sd = sd - (1 << 64) if sd >= (1 << 63) else sd
         samples = ws["samples"][: slay.total]
-        C.dgc_sample(x, t["offsets"], ws["samp_off"], sd, samples)
+        C.dgc_sample(x, t["offsets"], ws["samp_off"], sd, step, samples)
         tw = _topk_ws(slay, ks, dev)
         C.topk_select(samples, None, samples, 1.0, 1.0, 0, st["seg"], st["begin"], st["end"], tw["kseg"],
                       tw["state"], tw["hist"])
         C.dgc_refine(x, tw["state"], ws["target"], max_iters, ws["thr"], ws["count"], ws["done"], t["seg"],
                      t["begin"], t["end"])
-        cap_v = torch.empty(x.numel(), dtype=torch.float32, device=dev)
-        cap_i = torch.empty(x.numel(), dtype=torch.int32, device=dev)
-        C.dgc_compact(x, ws["thr"], cap_v, cap_i, ws["cnt"], t["seg"], t["begin"], t["end"])
-        s = int(ws["cnt"].item())
-        v, i = PayloadBuilder(dev, [(torch.float32, (s,)), (torch.int32, (s,))]).tensors
-        if s:
-            v.copy_(cap_v[:s])
-            i.copy_(cap_i[:s])
-        return v, i
+        C.dgc_compact(x, ws["thr"], v, i, hdr[:1], t["seg"], t["begin"], t["end"], vmask, umask)
+        return hdr, v, i
     # ---- PyTorch reference path (per segment, reference dgc.py:12-43 semantics)
     gen = torch.Generator(device=dev)
     gen.manual_seed(seed & 0x7FFFFFFFFFFFFFFF)
-    vals, idxs = [], []
+    idxs = []
     for (si, o, n), s, k in zip(layout.segments(), ns, ks):
         if n == 0:
             continue
@@ -82,11 +88,15 @@ def dgc_select(x: torch.Tensor, layout: SegmentLayout, ratio: float, sample_rati
             mask = seg.abs() >= thr
             sel = mask.sum()
         (ii,) = torch.where(mask)
-        vals.append(seg[ii])
-        idxs.append((ii + o).to(torch.int32))
-    cat_v = torch.cat(vals) if vals else torch.empty(0, device=dev)
-    cat_i = torch.cat(idxs) if idxs else torch.empty(0, dtype=torch.int32, device=dev)
-    v, i = PayloadBuilder(dev, [(torch.float32, (cat_v.numel(),)), (torch.int32, (cat_i.numel(),))]).tensors
-    v.copy_(cat_v)
-    i.copy_(cat_i)
-    return v, i
+        idxs.append(ii + o)
+    cat_i = torch.cat(idxs) if idxs else torch.empty(0, dtype=torch.int64, device=dev)
+    hdr.zero_()
+    hdr[0] = cat_i.numel()
+    hdr[1] = cap
+    s_ = cat_i[:cap]
+    v[: s_.numel()] = x[s_]
+    i[: s_.numel()] = s_.to(torch.int32)
+    for m in (vmask, umask):
+        if m is not None:
+            m[s_] = 0.0
+    return hdr, v, i

@@ -8,9 +8,9 @@ launch).
 
 Requirements on the step (checked by construction in grace_amd):
 * static shapes and static input buffers (copy new data into them before ``replay``);
-* no host synchronisation inside the step -- Top-K / Random-K / sign / QSGD / TernGrad /
-  Natural / PowerSGD exchanges qualify; Threshold / DGC / Adaq / INCEPTIONN (data-dependent
-  payload sizes read back to the host) do not and must run eagerly;
+* no host synchronisation inside the step -- every built-in codec qualifies except Sketch; the
+  variable-size ones (Threshold / DGC / Adaq / INCEPTIONN) exchange FIXED-capacity payloads with
+  an in-band count (ops/cappayload.py), so no payload size is read back to the host;
 * steady state before capture: the warm-up steps allocate residual / momentum state, so the
   captured kernels read and update it in place on every replay;
 * per-step randomness must advance on replay: Random-K indices, QSGD/TernGrad/Natural rounding
@@ -27,9 +27,8 @@ import torch
 
 #: stochastic codecs whose native kernels read a device step counter
 _DEVICE_STEPPED = ("RandomKCompressor", "QSGDCompressor", "TernGradCompressor", "NaturalCompressor",
-                   "PowerSGDCompressor")
-_HOST_SYNC = ("ThresholdCompressor", "DgcCompressor", "AdaqCompressor", "INCEPTIONNCompressor",
-              "SketchCompressor")
+                   "PowerSGDCompressor", "DgcCompressor", "AdaqCompressor")
+_HOST_SYNC = ("SketchCompressor",)
 
 
 def graph_safe(grc, allow_static_seeds: bool = False) -> Optional[str]:

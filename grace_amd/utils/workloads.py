@@ -85,6 +85,11 @@ WORKLOADS: Dict[str, Workload] = {
         "resnet50_none", "resnet50", 32, "images",
         {"compressor": "none", "memory": "none", "communicator": "allreduce"},
         _img_batch(224, 1000), _img_loss, channels_last=True),
+    # DGC 1% + DgcMemory (momentum correction) via Allgather: fixed-capacity payload, graph-capturable
+    "resnet50_dgc": Workload(
+        "resnet50_dgc", "resnet50", 32, "images",
+        {"compressor": "dgc", "compress_ratio": 0.01, "memory": "dgc", "communicator": "allgather"},
+        _img_batch(224, 1000), _img_loss, channels_last=True),
     "resnet18_cifar_none": Workload(
         "resnet18_cifar_none", "resnet18_cifar", 128, "images",
         {"compressor": "none", "memory": "none", "communicator": "allreduce"},

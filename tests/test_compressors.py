@@ -137,11 +137,36 @@ def test_dgc_selects_about_ratio():
     x = _x(20000)
     c = Z.DgcCompressor(0.01)
     payload, ctx = c.compress(x, "d")
-    n = payload[0].numel()
+    hdr = payload[0]
+    n = int(hdr[0])
     assert 0.5 * 200 <= n <= 1.5 * 200
+    assert payload[1].numel() == 400  # capacity 2 x target: fixed payload size
     dec = c.decompress(payload, ctx)
     sel = dec != 0
+    assert sel.sum() == n
     assert torch.equal(dec[sel], x[sel])
+
+
+def test_capacity_payload_fixed_size_and_spill():
+    """Threshold with capacity < selected: the payload size is fixed, the header holds the
+    selected count, and the spilled entries stay in the residual (error feedback keeps them)."""
+    from grace_amd.ops import cappayload as P
+
+    x = _x(5000)
+    full = Z.ThresholdCompressor(0.5)
+    p_full, _ = full.compress(x, "t")
+    n_sel = int((x.abs() > 0.5).sum())
+    assert int(p_full[0][0]) == n_sel and p_full[1].numel() == 5000
+    c = Z.ThresholdCompressor(0.5, capacity=0.05)
+    mem = M.ResidualMemory()
+    grc = Allgather(c, mem, comm=LocalComm())
+    out = grc.step(x.clone(), "t")
+    cap = P.capacity(5000, 0.05)
+    assert (out != 0).sum() == cap < n_sel
+    r = mem.residuals["t"]
+    # sent + residual == input; residual still holds the spilled large entries
+    torch.testing.assert_close(out + r, x)
+    assert int((r.abs() > 0.5).sum()) == n_sel - cap
 
 
 def test_powersgd_matches_oracle_w1():

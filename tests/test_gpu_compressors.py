@@ -137,10 +137,13 @@ def test_dgc_gpu_selects_about_ratio():
     c = Z.DgcCompressor(0.01)
     payload, ctx = c.compress(flat.cuda(), "gpu_bucket")
     big = lay.numels[-1]
-    idx = payload[1].cpu().long()
+    hdr, vals, idx = (t.cpu() for t in payload)
+    n = min(int(hdr[0]), vals.numel())
+    assert int(hdr[0]) <= vals.numel(), "capacity overflow on N(0,1) data"
+    idx = idx[:n].long()
     n_big = ((idx >= lay.offsets[-2]) & (idx < lay.offsets[-1])).sum().item()
     assert 0.5 * 0.01 * big <= n_big <= 1.5 * 0.01 * big
-    assert torch.equal(payload[0].cpu(), flat[idx])
+    assert torch.equal(vals[:n], flat[idx])
 
 
 @pytest.mark.parametrize("rank", [1, 2, 4])
@@ -285,11 +288,34 @@ def test_inceptionn_native_bit_exact():
     pg, ctx_g = comp.compress(x.cuda(), "inc_bucket")
     for a, b in zip(pc, pg):
         assert a.dtype == b.dtype and a.numel() == b.numel()
-        assert torch.equal(a, b.cpu())
+    # header (class totals) and codes bit-exact; the value stream up to its used bytes (the
+    # capacity tail past them is never read and left unwritten on the GPU)
+    assert torch.equal(pc[0], pg[0].cpu()) and torch.equal(pc[2], pg[2].cpu())
+    _, n8, n16, n32 = pc[0].tolist()
+    used = 4 * n32 + 2 * n16 + n8
+    assert torch.equal(pc[1][:used], pg[1][:used].cpu())
     others = [comp.compress(x * s, "inc_bucket")[0] for s in (0.5, -3.0)]
     ref = comp.decompress_aggregate([pc] + others, ctx_c, 3)
     got = comp.decompress_aggregate([pg] + [[t.cuda() for t in o] for o in others], ctx_g, 3)
     assert torch.equal(got.cpu(), ref)
+
+
+def test_inceptionn_capacity_drops_lowest_classes_first():
+    """capacity < 1: the 8-bit class is dropped before the 16-bit one; GPU == CPU oracle."""
+    g = torch.Generator().manual_seed(12)
+    n = 100_000
+    x = torch.randn(n, generator=g) * torch.logspace(-9, 1, n)[torch.randperm(n, generator=g)]
+    register_layout("inc_cap", SegmentLayout.from_tensors([x]))
+    full = Z.INCEPTIONNCompressor(2e-10)
+    _, n8, n16, n32 = full.compress(x, "inc_cap")[0][0].tolist()
+    cap = (4 * n32 + 2 * n16 + n8 // 2) / (4 * n)  # room for v32 + v16, not for all of v8
+    comp = Z.INCEPTIONNCompressor(2e-10, capacity=cap)
+    pc, ctx_c = comp.compress(x, "inc_cap")
+    pg, ctx_g = comp.compress(x.cuda(), "inc_cap")
+    assert torch.equal(pc[2], pg[2].cpu())
+    codes = ((pc[2].long().unsqueeze(1) >> torch.tensor([0, 2, 4, 6])) & 3).view(-1)[:n]
+    assert int((codes == 1).sum()) == 0 and int((codes == 2).sum()) == n16 and int((codes == 3).sum()) == n32
+    torch.testing.assert_close(comp.decompress(pg, ctx_g).cpu(), comp.decompress(pc, ctx_c), rtol=0, atol=0)
 
 
 def test_adaq_native_properties():
@@ -308,7 +334,8 @@ def test_adaq_native_properties():
     comp = Z.AdaqCompressor(0.05)
     payload, ctx = comp.compress(x.cuda(), "adaq_bucket")
     m, cnt, ix = (t.cpu() for t in payload)
-    assert ix.numel() == int(cnt.sum())
+    assert ix.numel() == comp._cap(lay) >= int(cnt.sum())  # fixed capacity, in-band counts
+    ix = ix[: int(cnt.sum())]
     pos = 0
     for s, o, n in lay.segments():
         seg = x[o:o + n]
