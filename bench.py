@@ -72,6 +72,10 @@ def parse():
                     help="HIP graphs: full = whole step (fwd+bwd+GRACE+RCCL+optimizer) captured; compute = "
                          "forward+backward graphed, GRACE + optimizer eager; auto = full for graph-safe "
                          "GRACE pipelines (any world size), eager otherwise")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="process group: nccl = RCCL over xGMI (one GPU per rank); gloo = host transport, lets "
+                         "several ranks share one GPU (multi-rank rehearsal on a 1-GPU box; --comm torch, no "
+                         "whole-step graph: gloo collectives are not capturable)")
     ap.add_argument("--comm", choices=["auto", "torch", "native", "native-inline"], default="auto",
                     help="collective runtime: torch = ProcessGroupNCCL (RCCL, its own stream: an event "
                          "fork/join per collective); native = grace_amd RCCL runtime on its comm stream; "
@@ -94,12 +98,18 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU")
+    gloo = args.backend == "gloo"
+    if gloo:  # ranks may share GPUs
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1 or args.force_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
-        dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)  # RCCL over xGMI
+        if gloo:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)  # RCCL over xGMI
     torch.backends.cudnn.benchmark = not args.no_benchmark_mode
     # strict fp32: no reduced-precision (xf32) conv/GEMM paths
     torch.backends.cuda.matmul.allow_tf32 = False
@@ -132,6 +142,10 @@ def main():
         probe = grace_from_params(dict(w.grace, world_size=world))
         mode = "full" if graph_safe(probe) is None else "off"
         del probe
+        if gloo and world > 1:
+            mode = "compute"  # gloo collectives cannot be captured
+    if gloo and world > 1 and mode == "full":
+        raise SystemExit("--graph full needs a capturable collective (--backend nccl)")
     if args.no_overlap:
         args.overlap = "off"
     overlap = args.overlap == "on" or (args.overlap == "auto" and mode != "full")
@@ -140,6 +154,8 @@ def main():
         comm_kind = args.comm
         if comm_kind == "auto":
             comm_kind = "native-inline" if (mode == "full" and not overlap) else "torch"
+        if gloo:
+            comm_kind = "torch"
         if comm_kind != "torch":
             from grace_amd.parallel import set_default_comm
             from grace_amd.parallel.native_comm import RcclComm
@@ -192,6 +208,7 @@ def main():
     except Exception as e:  # capture unsupported -> stay eager
         graph_note = f"failed: {type(e).__name__}: {str(e)[:120]}"
         torch.cuda.synchronize()
+        opt.abort_step()  # a capture that raised mid-backward leaves buckets half launched
         fwd_model, run = model, step
     if dist.is_initialized():  # every rank must run the same mode (collective sequences must match)
         ok = torch.tensor([0 if graph_note.startswith("failed") else 1], device=dev)
@@ -201,7 +218,10 @@ def main():
 
     def barrier():
         if world > 1:
-            dist.barrier(device_ids=[local])
+            if gloo:
+                dist.barrier()
+            else:
+                dist.barrier(device_ids=[local])
 
     for _ in range(args.warmup):
         run()
@@ -271,6 +291,7 @@ def main():
                 "per_gpu_batch": batch,
                 "seq_len": w.seq_len,
                 "parallelism": f"dp{world}",
+                "backend": "gloo (ranks share GPUs: rehearsal, not a scaling number)" if gloo else "nccl (RCCL)",
                 "grace": w.grace,
                 "bucket_mb": args.bucket_mb,
                 "overlap": overlap,

@@ -95,10 +95,23 @@ class GraceEngine:
     def __init__(self, params: Sequence[Tuple[str, torch.nn.Parameter]], grc: Communicator,
                  bucket_cap_mb: float = 64.0, backward_passes_per_step: int = 1, overlap: bool = True,
                  sparse_params: Sequence[str] = (), debug: Optional[bool] = None,
-                 grad_sources: Optional[Dict[int, torch.Tensor]] = None):
+                 grad_sources: Optional[Dict[int, torch.Tensor]] = None,
+                 group_collectives: Optional[bool] = None):
         from ..utils import debug as _dbg
+        from .comm import GroupedComm
 
         self.grc = grc
+        # one RCCL group per step for the buckets' collectives (GroupedComm) when nothing is to
+        # be gained from issuing them early: no overlap with backward and more than one rank
+        if group_collectives is None:
+            group_collectives = (not overlap) and grc.comm.world_size > 1
+        if group_collectives and not isinstance(grc.comm, GroupedComm):
+            gc = GroupedComm(grc.comm)
+            grc.comm = gc
+            for part in (grc.compressor, grc.memory):
+                if hasattr(part, "bind_comm"):
+                    part.bind_comm(gc)
+        self.grouped = isinstance(grc.comm, GroupedComm)
         self.debug = _dbg.ExchangeChecker(getattr(grc, "comm", None)) if (
             debug if debug is not None else _dbg.enabled_from_env()) else None
         self.overlap = overlap
@@ -306,6 +319,12 @@ class GraceEngine:
                             b.views[i].copy_(p.grad)
                         p.grad = b.views[i]
                 self._launch(b)
+        if self.grouped:
+            if self.stream is not None:
+                with torch.cuda.stream(self.stream):
+                    self.grc.comm.flush()
+            else:
+                self.grc.comm.flush()
         cur = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
         if self.stream is not None:
             cur.wait_stream(self.stream)
@@ -322,6 +341,18 @@ class GraceEngine:
             b.reset()
         if self._sparse:
             self._finish_sparse()
+        self.in_flight = 0
+
+    def abort_step(self):
+        """Forget a partially launched step (e.g. a HIP-graph capture that raised mid-backward):
+        handles, contexts, fired flags, handed-over gradients, pass counters, deferred
+        collectives.  The engine is then ready for a fresh eager step."""
+        for b in self.buckets:
+            b.reset()
+        self._passes.clear()
+        self._sparse_pending.clear()
+        if self.grouped:
+            self.grc.comm._pending = []
         self.in_flight = 0
 
     def zero_grad(self, set_to_none: bool = True):

@@ -22,7 +22,8 @@ from .engine import GraceEngine
 
 class _DistributedOptimizer:
     def __init__(self, optimizer, grace, named_parameters=None, backward_passes_per_step: int = 1,
-                 bucket_cap_mb: float = 64.0, overlap: bool = True, sparse_params=(), weights=None):
+                 bucket_cap_mb: float = 64.0, overlap: bool = True, sparse_params=(), weights=None,
+                 group_collectives=None):
         self._opt = optimizer
         if named_parameters is None:
             params = [p for g in optimizer.param_groups for p in g["params"]]
@@ -35,7 +36,8 @@ class _DistributedOptimizer:
         self.engine = GraceEngine(named_parameters, grace, bucket_cap_mb=bucket_cap_mb,
                                   backward_passes_per_step=backward_passes_per_step, overlap=overlap,
                                   sparse_params=sparse_params,
-                                  grad_sources=weights.grad_sources() if weights is not None else None)
+                                  grad_sources=weights.grad_sources() if weights is not None else None,
+                                  group_collectives=group_collectives)
         self.weights = weights  # parallel/precision.BF16Weights: refreshed after every step
         # FusedSGD writes the bf16 working copies inside its update kernel (no refresh pass)
         self._fused_refresh = False
@@ -73,6 +75,12 @@ class _DistributedOptimizer:
         if self.weights is not None and not self._fused_refresh:
             self.weights.refresh()
         return out
+
+    def abort_step(self):
+        """Drop a partially launched exchange (e.g. a failed HIP-graph capture) so the next
+        eager step starts clean."""
+        self.engine.abort_step()
+        self._synchronized = False
 
     def zero_grad(self, set_to_none: bool = True):
         # default (torch's): .grad = None; backward hands every fresh gradient over and ONE native

@@ -79,7 +79,7 @@ def test_zero_grad_race_guard():
     o.zero_grad()
 
 
-def _dp_body(rank, world, params):
+def _dp_body(rank, world, params, group=False):
     from grace_amd import grace_from_params
     from grace_amd.parallel import DistributedOptimizer, broadcast_parameters
 
@@ -90,7 +90,8 @@ def _dp_body(rank, world, params):
         torch.testing.assert_close(a, b)
     grc = grace_from_params(dict(params, world_size=world))
     opt = DistributedOptimizer(torch.optim.SGD(m.parameters(), lr=0.05), grc, named_parameters=m.named_parameters(),
-                               bucket_cap_mb=0.002)
+                               bucket_cap_mb=0.002, group_collectives=group)
+    assert opt.engine.grouped == bool(group)
     ref_opt = torch.optim.SGD(ref.parameters(), lr=0.05)
     for s in range(3):
         x, y = _batch(rank, s)
@@ -124,6 +125,19 @@ def _dp_body(rank, world, params):
 ])
 def test_distributed_optimizer_gloo(params):
     run_distributed(_dp_body, 2, params)
+
+
+@pytest.mark.parametrize("params", [
+    {"compressor": "none", "communicator": "allreduce"},
+    {"compressor": "topk", "compress_ratio": 0.1, "memory": "residual", "communicator": "allgather"},
+    {"compressor": "powersgd", "compress_rank": 2, "memory": "powersgd", "communicator": "allreduce"},
+    {"compressor": "dgc", "compress_ratio": 0.1, "memory": "dgc", "communicator": "allgather"},
+])
+def test_grouped_collectives_gloo(params):
+    """GroupedComm: every bucket's collective deferred to synchronize() and issued together
+    (one RCCL group on the native runtime); blocking in-compress collectives (PowerSGD) flush
+    first.  Same results as the ungrouped path (plain SGD reference for None)."""
+    run_distributed(_dp_body, 2, params, True)
 
 
 def _ddp_body(rank, world):

@@ -104,6 +104,97 @@ def test_native_inline_comm_in_graph(nccl_group):
     c.check()
 
 
+def test_native_group_collectives(nccl_group):
+    """RcclComm.group(): all-gathers and sum all-reduces in ONE ncclGroupStart/End (the path
+    GroupedComm.flush takes for a step's buckets), forked and inline, also inside a HIP graph."""
+    from grace_amd.parallel.comm import GroupedComm
+    from grace_amd.parallel.native_comm import RcclComm
+
+    for inline in (False, True):
+        c = RcclComm.from_process_group(inline=inline)
+        gc = GroupedComm(c)
+        a = torch.arange(1000, dtype=torch.float32, device="cuda")
+        b = torch.randn(333, device="cuda")
+        oa = torch.empty(1000, device="cuda")
+        ob = torch.empty(333, device="cuda")
+        r = torch.full((77,), 3.0, device="cuda")
+        ws = [gc.all_gather_into(oa, a, async_op=True), gc.all_reduce(r, async_op=True),
+              gc.all_gather_into(ob, b, async_op=True)]
+        assert gc.pending == 3
+        gc.flush()
+        assert gc.pending == 0
+        for w in ws:
+            w.wait()
+        torch.cuda.synchronize()
+        torch.testing.assert_close(oa, a)
+        torch.testing.assert_close(ob, b)
+        torch.testing.assert_close(r, torch.full((77,), 3.0, device="cuda"))
+    # grouped collectives captured in a graph (inline comm, as under bench.py --graph full)
+    c = RcclComm.from_process_group(inline=True)
+    gc = GroupedComm(c)
+    src = torch.randn(4096, device="cuda")
+    out = torch.empty(4096, device="cuda")
+    red = torch.zeros(64, device="cuda")
+
+    def body():
+        w1 = gc.all_gather_into(out, src, async_op=True)
+        w2 = gc.all_reduce(red, async_op=True)
+        gc.flush()
+        w1.wait()
+        w2.wait()
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        body()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        body()
+    src.normal_()
+    g.replay()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out, src)
+    c.check()
+
+
+def test_engine_groups_bucket_collectives_in_graph(nccl_group):
+    """DistributedOptimizer with several buckets and group_collectives=True on the inline native
+    comm, whole step captured: trains exactly like the ungrouped local comm."""
+    from grace_amd import grace_from_params
+    from grace_amd.parallel import DistributedOptimizer
+    from grace_amd.parallel.comm import LocalComm
+    from grace_amd.parallel.graph import GraphedStep
+    from grace_amd.parallel.native_comm import RcclComm
+
+    c = RcclComm.from_process_group(inline=True)
+    p = {"compressor": "topk", "compress_ratio": 0.1, "memory": "residual", "communicator": "allgather"}
+    x, y = _data()
+    models = []
+    for comm, grp in ((LocalComm(), False), (c, True)):
+        m = _net()
+        o = DistributedOptimizer(torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.5),
+                                 grace_from_params(p, comm=comm), named_parameters=m.named_parameters(),
+                                 bucket_cap_mb=0.002, overlap=False, group_collectives=grp)
+        assert o.engine.grouped == grp and len(o.engine.buckets) > 1
+
+        def step():
+            o.zero_grad()
+            loss = F.cross_entropy(m(x), y)
+            loss.backward()
+            o.step()
+            return loss
+
+        run = GraphedStep(step, warmup=3)
+        for _ in range(5):
+            run()
+        torch.cuda.synchronize()
+        models.append(m)
+    for a, b in zip(models[0].parameters(), models[1].parameters()):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
+    c.check()
+
+
 def test_ddp_hook_gpu(nccl_group):
     from grace_amd import grace_from_params
     from grace_amd.parallel import GraceHookState, grace_comm_hook
