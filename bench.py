@@ -65,7 +65,9 @@ def parse():
                     help="gather: zero_grad(set_to_none) + one native gather launch per bucket; "
                          "accumulate: bucket memset + AccumulateGrad adds into bucket views")
     ap.add_argument("--no-benchmark-mode", action="store_true", help="disable MIOpen find (cudnn.benchmark)")
-    ap.add_argument("--exposed-steps", type=int, default=3, help="untimed steps measuring exposed GRACE time")
+    ap.add_argument("--exposed-steps", type=int, default=3,
+                    help="untimed eager steps after the timed region: GraceProfiler split of the exchange "
+                         "(compress / comm / decompress ms, bytes on the wire) and the exposed exchange time")
     ap.add_argument("--force-dist", action="store_true",
                     help="initialise the RCCL process group even for one GPU (exercises the collective path)")
     ap.add_argument("--graph", choices=["auto", "full", "compute", "off"], default="auto",
@@ -246,14 +248,22 @@ def main():
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
 
-    # untimed: exposed GRACE time (compress tail + collective + decompress + optimizer after
-    # a fully synchronized backward) -- the "comm wall-time" split of the reference harness
-    # (pytorch_synthetic_benchmark.py:166-167)
+    # untimed: the reference harness's "comm wall-time" split (pytorch_synthetic_benchmark.py:
+    # 166-167) -- eager steps with the GraceProfiler attached: compress (compensate + compress +
+    # residual update), comm (collective issue -> completion as seen by the consuming stream),
+    # decompress (decode + aggregate into the bucket), bytes on the wire per rank; plus the
+    # EXPOSED exchange time: opt.step() (exchange + optimizer) after a fully synchronised backward
+    from grace_amd.utils.profiler import GraceProfiler
+
+    prof = GraceProfiler(roctx=False)
+    opt.engine.grc.profiler = prof
     exposed = []
-    for _ in range(args.exposed_steps):
+    for i in range(args.exposed_steps):
         opt.zero_grad(set_to_none=set_to_none)
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp, cache_enabled=False):
             l2 = w.loss(fwd_model, data)
+        if i == 0:
+            prof.reset()
         l2.backward()
         torch.cuda.synchronize()
         barrier()
@@ -261,6 +271,9 @@ def main():
         opt.step()
         torch.cuda.synchronize()
         exposed.append(time.perf_counter() - t)
+        prof.step()
+    opt.engine.grc.profiler = None
+    split = prof.report() if args.exposed_steps else {}
     ex = torch.tensor([sum(exposed) / max(1, len(exposed))], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(ex, op=dist.ReduceOp.MAX)
@@ -303,7 +316,10 @@ def main():
             },
             "per_gpu": {"mean": round(mean_pg, 2), "ci95": round(1.96 * std_pg, 2),
                         "note": f"{w.unit}/sec per GPU on rank 0, mean +- 1.96 std over {len(per_gpu)} steps"},
-            "comm_wall_ms": round(float(ex.item()) * 1e3, 3),
+            "exchange_ms": {k.replace("_ms_per_step", ""): round(v, 4) for k, v in split.items()
+                            if k.endswith("_ms_per_step")},
+            "bytes_on_wire_per_rank": int(split.get("bytes_per_step", 0)),
+            "exposed_exchange_ms": round(float(ex.item()) * 1e3, 3),
             "final_loss": round(float(loss.float().item()), 4),
         }
         print(json.dumps(out), flush=True)

@@ -22,8 +22,10 @@
 #include <rccl/rccl.h>
 
 #include <atomic>
+#include <chrono>
 #include <cstring>
 #include <memory>
+#include <shared_mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -69,6 +71,12 @@ ncclDataType_t nccl_dtype(const Tensor& t) {
   throw std::runtime_error("unsupported dtype for RCCL");
 }
 
+// bool tensors travel as bytes; only max / min keep them 0/1 (a "sum" would produce 2, 3, ...)
+void check_bool_op(const Tensor& t, const std::string& op) {
+  if (t.scalar_type() == at::kBool && op != "max" && op != "min")
+    throw std::runtime_error("bool all_reduce supports only max / min (logical or / and)");
+}
+
 ncclRedOp_t nccl_op(const std::string& op) {
   if (op == "sum") return ncclSum;
   if (op == "max") return ncclMax;
@@ -89,8 +97,10 @@ class Work {
     if (done_ != nullptr && !g_exiting.load()) (void)hipEventDestroy(done_);
   }
   hipEvent_t event() const { return done_; }
-  void wait() {  // stream-level: the caller's current stream waits, the host does not
-    if (done_ != nullptr) HIP_OK(hipStreamWaitEvent(current_stream(), done_, 0));
+  void wait() {  // stream-level: the caller's current stream (on the comm's device) waits
+    if (done_ == nullptr) return;
+    c10::hip::HIPGuardMasqueradingAsCUDA guard(device_);
+    HIP_OK(hipStreamWaitEvent(current_stream(), done_, 0));
   }
   bool is_completed() {
     if (done_ == nullptr) return true;
@@ -144,6 +154,7 @@ class RcclComm {
   uintptr_t stream_ptr() const { return reinterpret_cast<uintptr_t>(stream_); }
 
   std::shared_ptr<Work> all_gather(const Tensor& out, const Tensor& in) {
+    std::shared_lock<std::shared_timed_mutex> lk(mu_);
     check(out);
     check(in);
     TORCH_CHECK(out.numel() == in.numel() * world_, "all_gather: out must be world_size x in");
@@ -154,13 +165,16 @@ class RcclComm {
   }
 
   std::shared_ptr<Work> all_reduce(const Tensor& t, const std::string& op) {
+    std::shared_lock<std::shared_timed_mutex> lk(mu_);
     check(t);
+    check_bool_op(t, op);
     begin();
     RCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t), nccl_op(op), comm_, s_));
     return end();
   }
 
   std::shared_ptr<Work> broadcast(const Tensor& t, int root) {
+    std::shared_lock<std::shared_timed_mutex> lk(mu_);
     check(t);
     begin();
     RCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t), root, comm_, s_));
@@ -168,8 +182,10 @@ class RcclComm {
   }
 
   std::shared_ptr<Work> reduce_scatter(const Tensor& out, const Tensor& in, const std::string& op) {
+    std::shared_lock<std::shared_timed_mutex> lk(mu_);
     check(out);
     check(in);
+    check_bool_op(in, op);
     TORCH_CHECK(in.numel() == out.numel() * world_, "reduce_scatter: in must be world_size x out");
     begin();
     RCCL_CHECK(ncclReduceScatter(in.data_ptr(), out.data_ptr(), out.numel(), nccl_dtype(in), nccl_op(op), comm_,
@@ -180,12 +196,16 @@ class RcclComm {
   // Batched: all_gathers of (out_i, in_i) pairs and in-place sum all_reduces in ONE group.
   std::shared_ptr<Work> group(const std::vector<std::pair<Tensor, Tensor>>& gathers,
                               const std::vector<Tensor>& reduces) {
+    std::shared_lock<std::shared_timed_mutex> lk(mu_);
     for (auto& g : gathers) {
       check(g.first);
       check(g.second);
       TORCH_CHECK(g.first.numel() == g.second.numel() * world_, "group all_gather size");
     }
-    for (auto& t : reduces) check(t);
+    for (auto& t : reduces) {
+      check(t);
+      check_bool_op(t, "sum");
+    }
     begin();
     RCCL_CHECK(ncclGroupStart());
     for (auto& g : gathers)
@@ -198,15 +218,26 @@ class RcclComm {
   }
 
   std::string check_async_error() {
+    std::shared_lock<std::shared_timed_mutex> lk(mu_);
+    if (comm_ == nullptr) return aborted_.load() ? std::string("communicator aborted") : std::string();
     ncclResult_t r = ncclSuccess;
     RCCL_CHECK(ncclCommGetAsyncError(comm_, &r));
     return r == ncclSuccess ? std::string() : std::string(ncclGetErrorString(r));
   }
 
+  // Callable from a watchdog thread while the training thread issues collectives: issue paths
+  // hold mu_ shared (enqueue only, never a wait), abort takes it exclusively, so comm_ is never
+  // freed under a running ncclXxx call.  An enqueue stuck inside RCCL must not make the abort
+  // hang as well: after a bounded wait the communicator is aborted anyway (ncclCommAbort is the
+  // documented way to unblock it) and later issue calls fail on aborted_.
   void abort() {
-    if (comm_ != nullptr) {
-      (void)ncclCommAbort(comm_);
-      comm_ = nullptr;
+    aborted_.store(true);
+    std::unique_lock<std::shared_timed_mutex> lk(mu_, std::defer_lock);
+    const bool locked = lk.try_lock_for(std::chrono::seconds(5));
+    ncclComm_t c = comm_;
+    if (c != nullptr) {
+      (void)ncclCommAbort(c);
+      if (locked) comm_ = nullptr;
     }
   }
 
@@ -214,13 +245,16 @@ class RcclComm {
   void check(const Tensor& t) {
     TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "RCCL tensors must be contiguous GPU tensors");
     TORCH_CHECK(t.get_device() == device_, "tensor on the wrong device");
-    TORCH_CHECK(comm_ != nullptr, "communicator aborted");
+    TORCH_CHECK(comm_ != nullptr && !aborted_.load(), "communicator aborted");
   }
   // Forked (default): the comm stream waits on the caller's stream, the collective runs there
   // and overlaps whatever the caller does next.  Inline: the collective is issued on the
   // caller's current stream -- inside a whole-step HIP graph that is one more node in a single
   // chain instead of an event fork + join (a forked capture costs ~0.4 ms/step on MI355X).
   void begin() {
+    // the caller's current stream is looked up on the COMM's device (a different current device
+    // would record the fork / run an inline collective on another device's stream)
+    guard_.emplace(device_);
     if (inline_) {
       s_ = current_stream();
       return;
@@ -230,15 +264,17 @@ class RcclComm {
     HIP_OK(hipStreamWaitEvent(stream_, fork_, 0));
   }
   std::shared_ptr<Work> end() {
+    std::shared_ptr<Work> w;
     if (inline_) {
       hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
       HIP_OK(hipStreamIsCapturing(s_, &st));
-      auto w = std::make_shared<Work>(device_, st == hipStreamCaptureStatusNone);
+      w = std::make_shared<Work>(device_, st == hipStreamCaptureStatusNone);
       if (w->event() != nullptr) HIP_OK(hipEventRecord(w->event(), s_));
-      return w;
+    } else {
+      w = std::make_shared<Work>(device_);
+      HIP_OK(hipEventRecord(w->event(), stream_));
     }
-    auto w = std::make_shared<Work>(device_);
-    HIP_OK(hipEventRecord(w->event(), stream_));
+    guard_.reset();
     return w;
   }
 
@@ -253,6 +289,9 @@ class RcclComm {
   hipStream_t s_ = nullptr;  // stream of the collective being issued
   bool inline_ = false;
   hipEvent_t fork_;
+  c10::optional<c10::hip::HIPGuardMasqueradingAsCUDA> guard_;  // device of the collective in flight
+  std::shared_timed_mutex mu_;
+  std::atomic<bool> aborted_{false};
 };
 
 void bind(py::module& m) {

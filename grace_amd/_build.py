@@ -12,6 +12,13 @@ Usage::
 
     python -m grace_amd._build            # build (incremental)
     python -m grace_amd._build --clean    # rebuild everything
+    python -m grace_amd._build --asan     # host-side AddressSanitizer preset -> build/asan/_C.so
+
+The ASan preset instruments the HOST code only (bindings, argument validation, the RCCL runtime
+in csrc/comm): every ``-fsanitize=`` sits directly after ``-Xarch_host`` (GPU code objects are
+never sanitized -- GPU ASan / xnack+ is not available on the MI355X pool).  Run host-side checks
+with tools/asan_host_check.sh (preloads clang's ASan runtime, loads the instrumented library
+through ``GRACE_AMD_NATIVE_SO``).
 """
 from __future__ import annotations
 
@@ -29,6 +36,10 @@ ROOT = Path(__file__).resolve().parent.parent
 CSRC = ROOT / "csrc"
 BUILD = ROOT / "build" / "native"
 OUT = ROOT / "grace_amd" / "_C.so"
+BUILD_ASAN = ROOT / "build" / "asan_obj"
+OUT_ASAN = ROOT / "build" / "asan" / "_C.so"
+ASAN_COMPILE = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-pointer", "-g"]
+ASAN_LINK = ["-Xarch_host", "-fsanitize=address", "-shared-libasan"]
 ARCH = os.environ.get("GRACE_OFFLOAD_ARCH", "gfx950")
 
 
@@ -96,19 +107,23 @@ def _compile(hipcc, flags, src: Path, obj: Path):
     return src.name, time.time() - t0
 
 
-def build(clean: bool = False, verbose: bool = True) -> Path:
+def build(clean: bool = False, verbose: bool = True, asan: bool = False) -> Path:
     tlib, tinc, abi = _torch_paths()
     hipcc = _hipcc()
-    if clean and BUILD.exists():
-        shutil.rmtree(BUILD)
-    BUILD.mkdir(parents=True, exist_ok=True)
+    build_dir, out = (BUILD_ASAN, OUT_ASAN) if asan else (BUILD, OUT)
+    if clean and build_dir.exists():
+        shutil.rmtree(build_dir)
+    build_dir.mkdir(parents=True, exist_ok=True)
+    out.parent.mkdir(parents=True, exist_ok=True)
     flags = _common_flags(tinc, abi)
+    if asan:
+        flags = [f for f in flags if f != "-O3"] + ["-O1", *ASAN_COMPILE]
     headers = list((CSRC / "include").rglob("*.h"))
     dep_mtime = max([h.stat().st_mtime for h in headers] + [Path(__file__).stat().st_mtime])
     srcs = _sources()
     objs, todo = [], []
     for s in srcs:
-        o = BUILD / (s.relative_to(CSRC).as_posix().replace("/", "__") + ".o")
+        o = build_dir / (s.relative_to(CSRC).as_posix().replace("/", "__") + ".o")
         objs.append(o)
         if _needs_rebuild(s, o, dep_mtime):
             todo.append((s, o))
@@ -121,9 +136,10 @@ def build(clean: bool = False, verbose: bool = True) -> Path:
                 if verbose:
                     print(f"[grace_amd build] {name}: {dt:.1f}s", flush=True)
     newest_obj = max(o.stat().st_mtime for o in objs)
-    if todo or not OUT.exists() or OUT.stat().st_mtime < newest_obj:
+    if todo or not out.exists() or out.stat().st_mtime < newest_obj:
         link = [
-            hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(OUT), *map(str, objs),
+            hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *(ASAN_LINK if asan else []), "-o", str(out),
+            *map(str, objs),
             f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
             "-ltorch_python", "-lamdhip64", "-lrccl", f"-Wl,-rpath,{tlib}",
         ]
@@ -131,15 +147,16 @@ def build(clean: bool = False, verbose: bool = True) -> Path:
         if proc.returncode != 0:
             raise RuntimeError(f"link failed\n{' '.join(link)}\n{proc.stdout}\n{proc.stderr}")
         if verbose:
-            print(f"[grace_amd build] linked {OUT.relative_to(ROOT)}", flush=True)
-    return OUT
+            print(f"[grace_amd build] linked {out.relative_to(ROOT)}", flush=True)
+    return out
 
 
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--clean", action="store_true")
+    ap.add_argument("--asan", action="store_true", help="host-side AddressSanitizer build (build/asan/_C.so)")
     args = ap.parse_args(argv)
-    build(clean=args.clean)
+    build(clean=args.clean, asan=args.asan)
 
 
 if __name__ == "__main__":

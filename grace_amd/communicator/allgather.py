@@ -72,5 +72,9 @@ class Allgather(Communicator):
     def async_send(self, tensors, name):
         return allgather_send(self.comm, self.compressor, tensors, self.world_size)
 
+    def wait_comm(self, handles):
+        if handles[3] is not None:
+            handles[3].wait()
+
     def wait_receive(self, handles, ctx):
         return allgather_recv(handles, self.compressor, ctx, self.world_size)

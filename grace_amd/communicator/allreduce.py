@@ -55,6 +55,15 @@ class Allreduce(Communicator):
                 works.append((self.comm.all_reduce(flat, async_op=True), flat, idxs))
         return ("ar", (tensors, works))
 
+    def wait_comm(self, handles):
+        kind, h = handles
+        if kind == "ag":
+            if h[3] is not None:
+                h[3].wait()
+            return
+        for w, _, _ in h[1]:
+            w.wait()
+
     def wait_receive(self, handles, ctx):
         kind, handles = handles
         if kind == "ag":

@@ -56,6 +56,11 @@ class Broadcast(Communicator):
             bufs.append(b)
         return bufs, rank_specs, works
 
+    def wait_comm(self, handles):
+        for w in handles[2]:
+            if w is not None:
+                w.wait()
+
     def wait_receive(self, handles, ctx):
         bufs, rank_specs, works = handles
         for w in works:

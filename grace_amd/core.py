@@ -147,6 +147,7 @@ class Communicator(Stateful, ABC):
         self.compressor = compressor
         self.memory = memory
         self.profiler = None  # grace_amd.utils.profiler.GraceProfiler (opt-in)
+        self._comm_t0 = {}  # id(handles) -> profiler start event of the collective
         self.comm = comm if comm is not None else default_comm()
         self.world_size = int(world_size) if world_size is not None else self.comm.world_size
         if self.world_size != self.comm.world_size:
@@ -185,12 +186,24 @@ class Communicator(Stateful, ABC):
         payload, ctx = self.compress_step(tensor, name)
         prof = self._prof()
         prof.add_bytes(sum(t.numel() * t.element_size() for t in payload))
-        with prof.phase("comm_issue", name):
-            return self.async_send(payload, name), ctx
+        t0 = prof.start()
+        handles = self.async_send(payload, name)
+        if t0 is not None:
+            self.__dict__.setdefault("_comm_t0", {})[id(handles)] = t0
+        return handles, ctx
 
     def receive_step(self, handles, ctx):
-        with self._prof().phase("comm_wait_decompress", ""):
+        prof = self._prof()
+        t0 = self.__dict__.get("_comm_t0", {}).pop(id(handles), None)
+        if t0 is not None:  # comm = issue -> collective complete on this stream
+            self.wait_comm(handles)
+            prof.stop("comm", t0)
+        with prof.phase("decompress", ""):
             return self.wait_receive(handles, ctx)
+
+    def wait_comm(self, handles) -> None:
+        """Make the current stream wait for the collective(s) of ``handles`` (idempotent; the
+        decode in ``wait_receive`` then finds them complete).  Default: nothing separable."""
 
     @abstractmethod
     def async_send(self, tensors: Sequence[torch.Tensor], name: str):

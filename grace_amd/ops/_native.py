@@ -34,7 +34,19 @@ def lib():
     try:
         import torch  # noqa: F401  (loads libamdhip64 / librccl from torch/lib first)
 
-        _lib = importlib.import_module("grace_amd._C")
+        alt = os.environ.get("GRACE_AMD_NATIVE_SO")  # e.g. the ASan preset build/asan/_C.so
+        if alt:
+            import importlib.machinery
+            import importlib.util
+            import sys
+
+            spec = importlib.util.spec_from_loader(
+                "grace_amd._C", importlib.machinery.ExtensionFileLoader("grace_amd._C", alt))
+            _lib = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(_lib)
+            sys.modules["grace_amd._C"] = _lib
+        else:
+            _lib = importlib.import_module("grace_amd._C")
     except Exception as e:  # pragma: no cover - depends on build state
         _err = e
         return lib()

@@ -96,7 +96,7 @@ class GraceEngine:
                  bucket_cap_mb: float = 64.0, backward_passes_per_step: int = 1, overlap: bool = True,
                  sparse_params: Sequence[str] = (), debug: Optional[bool] = None,
                  grad_sources: Optional[Dict[int, torch.Tensor]] = None,
-                 group_collectives: Optional[bool] = None):
+                 group_collectives: Optional[bool] = None, watchdog=None):
         from ..utils import debug as _dbg
         from .comm import GroupedComm
 
@@ -112,6 +112,10 @@ class GraceEngine:
                 if hasattr(part, "bind_comm"):
                     part.bind_comm(gc)
         self.grouped = isinstance(grc.comm, GroupedComm)
+        # failure detection (parallel/launch.py Watchdog): every synchronize() tracks the step's
+        # collectives and raises in the training thread if an earlier one missed its deadline;
+        # RCCL async errors (peer death) are polled on the native comm
+        self.watchdog = watchdog
         self.debug = _dbg.ExchangeChecker(getattr(grc, "comm", None)) if (
             debug if debug is not None else _dbg.enabled_from_env()) else None
         self.overlap = overlap
@@ -342,6 +346,13 @@ class GraceEngine:
         if self._sparse:
             self._finish_sparse()
         self.in_flight = 0
+        if self.watchdog is not None:
+            self.watchdog.check()
+            check = getattr(self.grc.comm, "check", None)
+            if callable(check):
+                check()
+            if self.device.type == "cuda" and not torch.cuda.is_current_stream_capturing():
+                self.watchdog.track_stream("GRACE exchange")
 
     def abort_step(self):
         """Forget a partially launched step (e.g. a HIP-graph capture that raised mid-backward):

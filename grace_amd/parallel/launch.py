@@ -50,7 +50,11 @@ class Watchdog:
     ``track(work, what)`` registers a handle; a daemon thread polls ``work.is_completed()`` and
     records a failure when the deadline passes.  ``check()`` (call it once per step, e.g. from
     the optimizer) raises ``TimeoutError`` in the training thread; with ``abort=comm`` the
-    native RCCL communicator is aborted so the stuck kernels are torn down.
+    native RCCL communicator is aborted so the stuck kernels are torn down (from the watchdog
+    thread: a training thread blocked on the hung collective cannot do it itself; the native
+    runtime serialises abort against in-flight issue calls, csrc/comm/rccl_comm.cpp).
+    ``track_stream(what)`` records an event on the current stream -- the engine calls it after
+    each step's collectives so a dead peer becomes a TimeoutError instead of a silent hang.
     """
 
     def __init__(self, timeout_s: float = 120.0, poll_s: float = 0.5, abort=None):
@@ -69,6 +73,19 @@ class Watchdog:
             return
         with self._lock:
             self._items.append((time.monotonic() + self.timeout_s, work, what))
+
+    def track_stream(self, what: str = "step collectives"):
+        """Track completion of everything queued so far on the current stream."""
+        if not torch.cuda.is_available():
+            return
+        ev = torch.cuda.Event()
+        ev.record()
+
+        class _Ev:
+            def is_completed(self_inner):
+                return ev.query()
+
+        self.track(_Ev(), what)
 
     def _run(self):
         while not self._stop.wait(self.poll_s):

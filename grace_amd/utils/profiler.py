@@ -4,7 +4,8 @@ The reference only has ad-hoc ``torch.cuda.synchronize(); time.time(); print`` i
 Horovod QSGD compressor (/root/reference/grace_dl/torch/compressor/qsgd.py:14-15, 33-34) and
 commented compute/communication prints in the benchmark (pytorch_synthetic_benchmark.py:
 166-167).  Here every phase of the pipeline (compress = compensate+compress+update, comm =
-collective issue->completion, decompress = decompress+aggregate) is bracketed by a pair of
+collective issue->completion as seen by the consuming stream, decompress = decompress +
+aggregate) is bracketed by a pair of
 ``torch.cuda.Event`` s recorded on the stream that runs it, plus a roctx range (visible in
 ``rocprofv3 --marker-trace``).  Events are resolved only when ``report()`` is called.
 
@@ -49,6 +50,21 @@ class GraceProfiler:
                 torch.cuda.nvtx.range_pop()
             self._pending.append((name, start, end))
 
+    def start(self):
+        """Event marking the start of a span that ends in another call (``stop``)."""
+        if not self.enabled or not torch.cuda.is_available():
+            return None
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+
+    def stop(self, name: str, start) -> None:
+        if start is None:
+            return
+        end = torch.cuda.Event(enable_timing=True)
+        end.record()
+        self._pending.append((name, start, end))
+
     def add_bytes(self, n: int):
         self.bytes_sent += int(n)
 
@@ -82,6 +98,12 @@ class _Null:
     @contextlib.contextmanager
     def phase(self, name, tag=""):
         yield
+
+    def start(self):
+        return None
+
+    def stop(self, name, start):
+        pass
 
     def add_bytes(self, n):
         pass

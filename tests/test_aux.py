@@ -52,6 +52,86 @@ def test_checkpoint_resume_preserves_grace_state(tmp_path):
         torch.testing.assert_close(a, b)
 
 
+def _ckpt_w2_body(rank, world, path):
+    from grace_amd import grace_from_params
+    from grace_amd.parallel import DistributedOptimizer
+    from grace_amd.utils import checkpoint
+
+    params = {"compressor": "topk", "compress_ratio": 0.2, "memory": "residual", "communicator": "allgather",
+              "world_size": world}
+
+    def make():
+        m = _model()
+        return m, DistributedOptimizer(torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9),
+                                       grace_from_params(params), named_parameters=m.named_parameters())
+
+    m1, o1 = make()
+    _train(m1, o1, 3, 10 * rank)  # rank-specific data: rank-specific residuals
+    res1 = {k: v.clone() for k, v in o1.engine.grc.memory.residuals.items()}
+    checkpoint.save(path, m1, o1)  # per-rank GRACE state by default at W > 1
+    assert os.path.exists(checkpoint.grace_path(path, rank))
+    m2, o2 = make()
+    checkpoint.load(path, m2, o2)
+    res2 = o2.engine.grc.memory.residuals
+    assert res1.keys() == res2.keys()
+    for k in res1:
+        assert torch.equal(res1[k], res2[k]), "rank got back another rank's residual"
+    # residuals really differ across ranks (else the test proves nothing)
+    k0 = sorted(res1)[0]
+    out = [torch.empty_like(res1[k0]) for _ in range(world)]
+    dist.all_gather(out, res1[k0].contiguous())
+    assert not torch.equal(out[0], out[1])
+    _train(m1, o1, 2, 100 + rank)
+    _train(m2, o2, 2, 100 + rank)
+    for a, b in zip(m1.parameters(), m2.parameters()):
+        torch.testing.assert_close(a, b)
+
+
+def test_checkpoint_per_rank_grace_state_w2(tmp_path):
+    run_distributed(_ckpt_w2_body, 2, str(tmp_path / "ck.pt"))
+
+
+def test_checkpoint_bf16_masters_roundtrip(tmp_path):
+    """BF16Weights: the fp32 masters (not the bf16 working copies) are saved and restored."""
+    from grace_amd import grace_from_params
+    from grace_amd.parallel import DistributedOptimizer
+    from grace_amd.parallel.precision import BF16Weights
+    from grace_amd.utils import checkpoint
+
+    def make():
+        m = _model()
+        w = BF16Weights(m)
+        o = DistributedOptimizer(torch.optim.SGD(list(w.master_parameters(m)), lr=0.1, momentum=0.9),
+                                 grace_from_params({"compressor": "none", "communicator": "allreduce"}),
+                                 named_parameters=list(w.named_master_parameters(m)), weights=w)
+        return m, w, o
+
+    def train(m, o, steps, seed0):
+        for s in range(steps):
+            g = torch.Generator().manual_seed(seed0 + s)
+            x, y = torch.randn(8, 10, generator=g), torch.randint(0, 3, (8,), generator=g)
+            o.zero_grad()
+            with torch.autocast("cpu", dtype=torch.bfloat16):
+                loss = F.cross_entropy(m(x), y)
+            loss.backward()
+            o.step()
+
+    m1, w1, o1 = make()
+    train(m1, o1, 3, 0)
+    path = str(tmp_path / "ck.pt")
+    checkpoint.save(path, m1, o1, weights=w1)
+    m2, w2, o2 = make()
+    checkpoint.load(path, m2, o2, weights=w2)
+    for a, b in zip(w1.masters, w2.masters):
+        assert a.dtype == torch.float32 and torch.equal(a, b)
+    for a, b in zip(w1.working, w2.working):
+        assert torch.equal(a, b)
+    train(m1, o1, 2, 50)
+    train(m2, o2, 2, 50)
+    for a, b in zip(w1.masters, w2.masters):
+        torch.testing.assert_close(a, b)
+
+
 def test_checkpoint_loader_is_weights_only(tmp_path):
     from grace_amd.utils import checkpoint
 
@@ -133,3 +213,34 @@ def test_packing_helpers_roundtrip_and_reference_format():
     # reference layout: quarters (n=4 pads 4 more entries 0..3 -> 2 bytes)
     enc = P.encode_byte(torch.tensor([1, 2, 3, 0]))
     assert enc.tolist() == [1 + 4 * 3 + 16 * 0 + 64 * 2, 2 + 4 * 0 + 16 * 1 + 64 * 3]
+
+
+def test_profiler_splits_comm_and_decompress():
+    """GraceProfiler phases: compress / comm / decompress are separate entries (bench.py reports
+    them as the exchange split); CPU: events are no-ops, bytes are still counted."""
+    from grace_amd import grace_from_params
+    from grace_amd.utils.profiler import GraceProfiler
+
+    grc = grace_from_params({"compressor": "fp16", "communicator": "allreduce"})
+    grc.profiler = GraceProfiler()
+    h, ctx = grc.send_step(torch.randn(256), "x")
+    out = grc.receive_step(h, ctx)
+    grc.profiler.step()
+    assert out.shape == (256,)
+    assert grc.profiler.report()["bytes_per_step"] == 512
+
+
+def test_engine_watchdog_raises_in_training_thread():
+    from grace_amd import grace_from_params
+    from grace_amd.parallel import DistributedOptimizer
+    from grace_amd.parallel.launch import Watchdog
+
+    m = _model()
+    wd = Watchdog(timeout_s=60, poll_s=0.05)
+    o = DistributedOptimizer(torch.optim.SGD(m.parameters(), lr=0.1), grace_from_params({"compressor": "none"}),
+                             named_parameters=m.named_parameters(), watchdog=wd)
+    _train(m, o, 1, 0)  # healthy
+    wd._failure = "all_gather of bucket 0 did not complete within 60s"  # injected
+    with pytest.raises(TimeoutError):
+        _train(m, o, 1, 1)
+    wd.close()

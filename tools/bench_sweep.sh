@@ -8,5 +8,5 @@ while IFS= read -r v; do
   if [ $rc -ne 0 ]; then echo "$v FAILED rc=$rc"; tail -5 gpurun_out/sweep_last.log; exit 1; fi
   grep '"metric"' gpurun_out/sweep_last.log | python3 -c "
 import sys,json; d=json.loads(sys.stdin.read())
-print('$v', '|', d['value'], d['unit'], '|', d['ms_per_step'], 'ms |', d['config'].get('hip_graph'), '| overlap', d['config'].get('overlap'), '| comm', d.get('comm_wall_ms'))"
+print('$v', '|', d['value'], d['unit'], '|', d['ms_per_step'], 'ms |', d['config'].get('hip_graph'), '| overlap', d['config'].get('overlap'), '| exposed', d.get('exposed_exchange_ms'), '| split', d.get('exchange_ms'), '| wire B', d.get('bytes_on_wire_per_rank'))"
 done < "$1"
