@@ -36,13 +36,11 @@ def lib():
 
         alt = os.environ.get("GRACE_AMD_NATIVE_SO")  # e.g. the ASan preset build/asan/_C.so
         if alt:
-            import importlib.machinery
-            import importlib.util
             import sys
+            from importlib import machinery, util
 
-            spec = importlib.util.spec_from_loader(
-                "grace_amd._C", importlib.machinery.ExtensionFileLoader("grace_amd._C", alt))
-            _lib = importlib.util.module_from_spec(spec)
+            spec = util.spec_from_loader("grace_amd._C", machinery.ExtensionFileLoader("grace_amd._C", alt))
+            _lib = util.module_from_spec(spec)
             spec.loader.exec_module(_lib)
             sys.modules["grace_amd._C"] = _lib
         else:

@@ -244,3 +244,13 @@ def test_engine_watchdog_raises_in_training_thread():
     with pytest.raises(TimeoutError):
         _train(m, o, 1, 1)
     wd.close()
+
+
+def test_native_library_loads_on_cpu_host():
+    """The built extension imports on the host (no GPU needed for the module itself)."""
+    from grace_amd.ops import _native
+
+    if not os.path.exists(os.path.join(os.path.dirname(os.path.dirname(__file__)), "grace_amd", "_C.so")):
+        pytest.skip("extension not built")
+    assert _native.available(), _native._err
+    assert "gfx950" in _native.lib().build_info()
