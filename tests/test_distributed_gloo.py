@@ -29,6 +29,38 @@ def _same_on_all_ranks(t):
         assert torch.equal(o, out[0]), "result differs across ranks"
 
 
+def _replay_mean(params, xs, name, device):
+    """mean over ranks r of decompress(compress_r(x_r)) with codec objects bound to rank r."""
+    from grace_amd import grace_from_params
+    from grace_amd.parallel.comm import LocalComm
+
+    dec = []
+    for r, x in enumerate(xs):
+        c = grace_from_params(dict(params, world_size=1), comm=LocalComm()).compressor
+        c.rank = r
+        payload, ctx = c.compress(x.to(device).clone(), name)
+        dec.append(c.decompress(payload, ctx).cpu())
+    return sum(dec) / len(xs)
+
+
+def _powersgd_oracle(xs, rank, name, device):
+    from grace_amd.ops import powersgd as PS
+    from grace_amd.ops.randomk import fnv1a64, mix_step
+
+    n, m = xs[0].shape
+    W = len(xs)
+    seed = fnv1a64(name.encode())
+    if device == "cpu":
+        q = PS.randn_shared(m * rank, mix_step(seed, 1), "cpu").view(m, rank)
+    else:  # native: device step counter 1 mixed in on the device
+        q = PS.randn_shared(m * rank, seed, device, step=torch.ones(1, dtype=torch.int64, device=device)).cpu()
+        q = q.view(m, rank)
+    p = sum(x @ q for x in xs) / W
+    p = O.gram_schmidt(p)
+    q2 = sum(x.t() @ p for x in xs) / W
+    return p @ q2.t()
+
+
 def _body(rank, world, device="cpu"):
     """Every communicator x compressor pairing on W ranks.  device="cuda": each rank's tensors on
     cuda:0 (native HIP kernels, gloo moving the GPU payloads) -- tests/test_gpu_multirank.py."""
@@ -83,14 +115,19 @@ def _body(rank, world, device="cpu"):
     # s = 127 (BASELINE BERT config): s*W > 127 -> fp16 integer-level codes on the wire
     out = run({"compressor": "qsgd", "quantum_num": 127, "communicator": "allreduce"}, "q127")
     assert (out - mean).abs().max() <= max(t.norm() for t in xs) / 127 * (1 + 1e-4)
-    # TernGrad / Natural / U8bit / Sketch run and agree across ranks
+    # TernGrad / Natural / U8bit / Sketch / INCEPTIONN / Adaq / DGC: the W-rank result equals the
+    # rank-ordered average of every rank's OWN decode, replayed locally on each rank with a codec
+    # object carrying that rank's id (same per-(name, rank, step) seeds as the real rank used)
     for comp in ("terngrad", "natural", "u8bit", "sketch", "inceptionn", "adaq", "dgc"):
-        comm = "allgather"
-        out = run({"compressor": comp, "communicator": comm, "compress_ratio": 0.05}, comp)
-        assert torch.isfinite(out).all()
-    # PowerSGD (W-averaged P and Q)
+        p = {"compressor": comp, "communicator": "allgather", "compress_ratio": 0.05}
+        out = run(p, comp)
+        exp = _replay_mean(p, xs, comp, device)
+        torch.testing.assert_close(out, exp, rtol=1e-5, atol=1e-6)
+    # PowerSGD (W-averaged P and Q, shared Q on every rank): P = mean_r(M_r Q), orthonormalised,
+    # Q' = mean_r(M_r^T P); result P Q'^T (oracle with the same Q)
     out = run({"compressor": "powersgd", "compress_rank": 2, "communicator": "allreduce"}, "ps")
-    assert torch.isfinite(out).all()
+    exp = _powersgd_oracle(xs, 2, "ps", device)
+    torch.testing.assert_close(out, exp, rtol=1e-4, atol=1e-5)
     # DGC memory with clipping (batched scalar allreduce)
     out = run({"compressor": "dgc", "memory": "dgc", "gradient_clipping": True, "communicator": "allgather",
                "compress_ratio": 0.05}, "dg")
@@ -103,6 +140,6 @@ def _body(rank, world, device="cpu"):
         _same_on_all_ranks(out)
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_communicators_gloo(world):
     run_distributed(_body, world)

@@ -227,8 +227,21 @@ def test_gram_orthonormalize_orthogonal_and_rank_deficient():
     torch.testing.assert_close(b[po:po + n * r], ref[po:po + n * r], rtol=1e-4, atol=1e-5)
 
 
-def test_powersgd_fused_memory_gpu_matches_cpu_unfused():
+def test_powersgd_fused_memory_gpu_matches_cpu_unfused(monkeypatch):
+    """Fused GPU PowerSGD (+ memory) == unfused CPU PowerSGD with the SAME Q: the CPU path's Q
+    is drawn by the native Philox generator with the host-mixed seed, which is bit-identical to
+    the GPU's (base seed, device step) draw (tests/test_gpu_graph_rng.py)."""
     from grace_amd.core import register_layout
+    from grace_amd.ops import powersgd as PS
+
+    real = PS.randn_shared
+
+    def shared_q(n, seed, device, step=None):
+        if torch.device(device).type == "cpu":
+            return real(n, seed, "cuda").cpu()
+        return real(n, seed, device, step=step)
+
+    monkeypatch.setattr(PS, "randn_shared", shared_q)
 
     class Unfused(M.PowerSGDMemory):
         pass
@@ -246,12 +259,8 @@ def test_powersgd_fused_memory_gpu_matches_cpu_unfused():
             res.append(grc.step(x.to(dev), "psgd_gpu").cpu())
         res.append(mem.residuals["psgd_gpu"].reshape(-1).cpu())
         outs[dev] = res
-    # different RNG streams for Q (Philox vs torch): compare energy and the EF invariant instead
-    for o in outs["cuda"]:
-        assert torch.isfinite(o).all()
-    gen = torch.Generator().manual_seed(2)
-    x_last = torch.cat([torch.randn(*sh, generator=gen).flatten() for sh in shapes])
-    assert outs["cuda"][2].norm() <= (x_last.norm() + outs["cuda"][3].norm()) * 1.01
+    for a, b in zip(outs["cuda"], outs["cpu"]):  # 3 decoded steps + the final residual
+        torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-4)
 
 
 def test_segment_stats_large_unaligned_segment():
