@@ -490,7 +490,7 @@ void dgc_compensate(const Tensor& g, const Tensor& u, const Tensor& v, double mo
 // ------------------------------------------------------------------------------ PowerSGD
 void powersgd_mq(const Tensor& x, const Tensor& small, const Tensor& out, const Tensor& mats, const Tensor& tiles,
                  int64_t mode, const c10::optional<Tensor>& comp_r, double beta, double gamma,
-                 const c10::optional<Tensor>& xout) {
+                 const c10::optional<Tensor>& xout, int64_t max_r) {
   CHECK_F32(x);
   CHECK_F32(small);
   CHECK_F32(out);
@@ -503,7 +503,7 @@ void powersgd_mq(const Tensor& x, const Tensor& small, const Tensor& out, const 
   DevGuard guard(x.device());
   grace::powersgd_mq(x.data_ptr<float>(), small.data_ptr<float>(), out.data_ptr<float>(), out.numel(),
                      mats.data_ptr<int64_t>(), tiles.data_ptr<int32_t>(), (int)(tiles.numel() / 3), (int)mode,
-                     opt_f32(comp_r), (float)beta, (float)gamma, opt_f32_mut(xout), cur_stream());
+                     opt_f32(comp_r), (float)beta, (float)gamma, opt_f32_mut(xout), (int)max_r, cur_stream());
 }
 
 void gram_orthonormalize(const Tensor& buf, const Tensor& mats, int64_t which, int64_t n_mat, const Tensor& gtiles,
@@ -523,7 +523,7 @@ void gram_orthonormalize(const Tensor& buf, const Tensor& mats, int64_t which, i
 }
 
 void powersgd_pqt(const Tensor& P, const Tensor& Q, const Tensor& out, const Tensor& mats, const Tensor& tiles,
-                  const c10::optional<Tensor>& resid) {
+                  const c10::optional<Tensor>& resid, int64_t max_r) {
   CHECK_F32(P);
   CHECK_F32(Q);
   CHECK_F32(out);
@@ -532,7 +532,8 @@ void powersgd_pqt(const Tensor& P, const Tensor& Q, const Tensor& out, const Ten
   if (resid.has_value()) TORCH_CHECK(resid->numel() == out.numel(), "resid size");
   DevGuard guard(out.device());
   grace::powersgd_pqt(P.data_ptr<float>(), Q.data_ptr<float>(), out.data_ptr<float>(), mats.data_ptr<int64_t>(),
-                      tiles.data_ptr<int32_t>(), (int)(tiles.numel() / 3), opt_f32_mut(resid), cur_stream());
+                      tiles.data_ptr<int32_t>(), (int)(tiles.numel() / 3), opt_f32_mut(resid), (int)max_r,
+                      cur_stream());
 }
 
 void philox_normal(const Tensor& out, int64_t seed, const c10::optional<Tensor>& step) {

@@ -4,19 +4,15 @@
 //   P = M Q ; orthogonalize(P) ; Q = M^T P ; decompress P Q^T     (M: n x m, Q: m x r, r <= 4 typ.)
 // Here every matrix of a bucket is processed by ONE launch per product:
 //
-//  powersgd_mq<MODE>  MODE 0: P = M Q    MODE 1: Q = M^T P
-//      Work list of 64 x 1024 (MODE 0) / 1024 x 64 (MODE 1) strips of M.  A 256-thread workgroup
-//      stages 64x64 fp32 sub-tiles of M in LDS (coalesced 256-B row reads, +1 padding against
-//      bank conflicts), each wave runs v_mfma_f32_16x16x4_f32 on a 16-row (MODE 0) or 16-column
-//      (MODE 1) slice: 16 MFMAs per sub-tile, the small operand (Q or P, r padded to 16) comes
-//      from a second LDS tile.  Strip partial sums are combined with fp32 atomics (the output
-//      is only n*r or m*r floats).  Tall-skinny with r=4 is bandwidth bound (2 FLOP/byte):
-//      the MFMA work is ~25% utilised by construction but still ~3x faster than HBM needs.
+//  ps_mq / ps_mtp     P = M Q / Q = M^T P: bandwidth-shaped VALU kernels (see below) -- with
+//                     r <= 16 the products are 2r FLOP per element, far below the MFMA break-even;
+//                     the round-1 MFMA versions (r padded to the 16-wide N tile) measured 0.25-1.8 %
+//                     matrix-core utilisation and 2.6-4.4 TB/s.
 //  gram_orthonormalize  r <= 4: one workgroup per matrix, one launch (fp64 Gram, MGS in the Gram
 //                     metric, in-place A <- A T, twice for CholQR2); r > 4: Gram tiles on MFMA
-//                     (all tiles of all matrices in one launch), per-matrix fix, apply -- see below
-//  powersgd_pqt       out = P Q^T: exactly one 16x16x4 MFMA per 16x16 output tile when r <= 4,
-//                     optionally fused with the residual update  r = x - P Q^T
+//                     (all tiles of all matrices in one launch, v_mfma_f32_16x16x4_f32 on the
+//                     r x r Gram), per-matrix fix, apply -- see below
+//  ps_pqt             out = P Q^T, optionally fused with the residual update r = x - P Q^T
 //  philox_normal      N(0,1) via Philox4x32 + Box-Muller (Q identical on every rank)
 #include "grace_common.h"
 #include "grace_kernels.h"
@@ -41,93 +37,268 @@ __device__ __forceinline__ Mat load_mat(const int64_t* __restrict__ mats, int i)
   return Mat{p[0], p[1], p[2], p[3], p[4], p[5]};
 }
 
-// tiles: int32 [n_tiles][3] = (matrix, block index along the output dim, strip index)
-// COMP (MODE 0 only; every element of M is staged by exactly one workgroup there):
-//   0: M = x      1: M = x, stored to xout      2: M = beta*r + gamma*x, stored to xout
-// i.e. the PowerSGD error-feedback compensate (memory/powersgd.py) fused into the first
-// product instead of a separate read-read-write pass over the bucket.
-template <int MODE, int COMP>
-__global__ __launch_bounds__(kBlock) void mq_kernel(const float* __restrict__ x, const float* __restrict__ small,
-                                                    float* __restrict__ out, const int64_t* __restrict__ mats,
-                                                    const int32_t* __restrict__ tiles, const float* cr, float beta,
-                                                    float gamma, float* xout) {
-  __shared__ float ms[kT * kLd];
-  __shared__ float ss[kT * kRPad];
-  const int* tl = tiles + 3 * blockIdx.x;
-  const Mat mt = load_mat(mats, tl[0]);
-  const int64_t n = mt.n, m = mt.m, r = mt.r;
-  const int lane = lane_id(), w = wave_id();
-  // MODE 0: output rows [ob, ob+64), reduce over cols [s0, s1)
-  // MODE 1: output cols [ob, ob+64), reduce over rows [s0, s1)
-  const int64_t ob = (int64_t)tl[1] * kT;
-  const int64_t red_len = MODE == 0 ? m : n;
-  const int64_t s0 = (int64_t)tl[2] * kStrip;
-  const int64_t s1 = s0 + kStrip < red_len ? s0 + kStrip : red_len;
-  const float* S = small + (MODE == 0 ? mt.q_off : mt.p_off);  // [red_len][r]
-  // Software pipeline: the global loads of sub-tile k+1 are issued into registers before the
-  // MFMAs of sub-tile k run, so HBM latency overlaps the matrix-core work.
-  constexpr int kPer = kT * kT / kBlock;  // 16 elements of M per thread per sub-tile
-  float pg[kPer], pr[kPer];
-  auto elem = [&](int64_t sb, int it, int64_t& gi) -> bool {
-    const int idx = it * kBlock + threadIdx.x;
-    const int64_t gr = (MODE == 0 ? ob : sb) + (idx >> 6), gc = (MODE == 0 ? sb : ob) + (idx & 63);
-    gi = mt.x_off + gr * m + gc;
-    return gr < n && gc < m;
-  };
-  auto fetch = [&](int64_t sb) {
-#pragma unroll
-    for (int it = 0; it < kPer; ++it) {
-      int64_t gi;
-      const bool ok = elem(sb, it, gi);
-      pg[it] = ok ? x[gi] : 0.f;
-      if (COMP == 2) pr[it] = ok ? cr[gi] : 0.f;
-    }
-  };
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  fetch(s0);
-  for (int64_t sb = s0; sb < s1; sb += kT) {
-    __syncthreads();
-#pragma unroll
-    for (int it = 0; it < kPer; ++it) {
-      const int idx = it * kBlock + threadIdx.x;
-      float v = pg[it];
-      if (COMP == 2) v = fmaf(beta, pr[it], gamma * v);
-      if (COMP != 0) {
-        int64_t gi;
-        if (elem(sb, it, gi)) xout[gi] = v;
-      }
-      ms[(idx >> 6) * kLd + (idx & 63)] = v;
-    }
-    // small operand rows [sb, sb+64) of S, r padded to 16 with zeros
-    for (int it = 0; it < kT * kRPad / kBlock; ++it) {
-      const int idx = it * kBlock + threadIdx.x;
-      const int kk = idx >> 4, j = idx & 15;
-      const int64_t gk = sb + kk;
-      ss[idx] = (j < r && gk < s1) ? S[gk * r + j] : 0.f;
-    }
-    __syncthreads();
-    if (sb + kT < s1) fetch(sb + kT);
-#pragma unroll 4
-    for (int kk = 0; kk < kT; kk += 4) {
-      const int ka = kk + (lane >> 4);
-      float a;
-      if (MODE == 0)
-        a = ms[(16 * w + (lane & 15)) * kLd + ka];  // A[i][k] = M[row i][col k]
-      else
-        a = ms[ka * kLd + 16 * w + (lane & 15)];  // A[i][k] = M^T[col i][row k]
-      const float bv = ss[ka * kRPad + (lane & 15)];
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv, acc, 0, 0, 0);
+// ---- Bandwidth-shaped tall-skinny products for the PowerSGD ranks (r <= 16), VALU.
+// With r = 4 a product is 8 FLOP per 4-byte element of M: ~0.5 ms of VALU for all of VGG-16 at
+// the chip's fp32 rate against ~0.1 ms of HBM time -- it is the BYTES that set the speed, so
+// these kernels read M exactly once with 16-B loads (rows whose start is not 16-B aligned use
+// the 4-B path), keep the small operand in registers / scalar loads, and write each result once:
+//   ps_mq    P[i,:] = sum_k M[i,k] Q[k,:]   block = 16 rows (4 per wave) x 2048-column strip;
+//            per-wave row sums reduced with cross-lane adds, one atomic per (row, j) per strip;
+//            COMP fuses the PowerSGD error-feedback compensate (M = beta*r + gamma*x -> xout)
+//   ps_mtp   Q[k,:] = sum_i M[i,k] P[i,:]   thread = 4 columns (1 unaligned), block = 256-row strip;
+//            P rows are wave-uniform (scalar loads), one atomic per (column, j) per strip
+//   ps_pqt   out = P Q^T, resid -= out       thread = 4 columns, Q rows in registers, 32-row strip
+// (The MFMA versions of these -- 64x64 LDS-staged tiles with r padded to the 16-wide MFMA N --
+// ran at 2.6-4.4 TB/s; MFMA utilisation 0.25-1.8 %, profiles/r1_pmc_powersgd.txt.)
+constexpr int kRB0 = 16, kCS0 = 2048;     // ps_mq: rows per block, columns per strip
+constexpr int kCBV = 1024, kCBS = 256;    // ps_mtp / ps_pqt: columns per block (16-B / 4-B path)
+constexpr int kRSP = 32;                  // rows per strip: ps_pqt (ps_mtp: per-matrix, from the tile table)
+constexpr int kPB = 8;                    // rows per batch: independent 16-B loads in flight per thread
+
+__device__ __forceinline__ bool mat_vec(const Mat& mt) { return ((mt.x_off | mt.m) & 3) == 0; }
+
+template <int R>
+__device__ __forceinline__ void load_small_row(const float* __restrict__ S, int64_t row, int r, float (&v)[R]) {
+  if constexpr (R == 4) {
+    if (r == 4 && (reinterpret_cast<uintptr_t>(S) & 15) == 0) {
+      const float4 q = *reinterpret_cast<const float4*>(S + row * 4);
+      v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+      return;
     }
   }
-  // C/D: col j = lane & 15, row i = (lane >> 4) * 4 + reg
-  const int j = lane & 15;
-  if (j < r) {
-    float* O = out + (MODE == 0 ? mt.p_off : mt.q_off);
-    const int64_t olen = MODE == 0 ? n : m;
+  {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int64_t oi = ob + 16 * w + (lane >> 4) * 4 + q;
-      if (oi < olen) atomicAdd(&O[oi * r + j], acc[q]);
+    for (int j = 0; j < R; ++j) v[j] = j < r ? S[row * r + j] : 0.f;
+  }
+}
+
+template <int R, int COMP>
+__global__ __launch_bounds__(kBlock) void ps_mq_kernel(const float* __restrict__ x, const float* __restrict__ Qall,
+                                                       float* __restrict__ Pall, const int64_t* __restrict__ mats,
+                                                       const int32_t* __restrict__ tiles, const float* cr, float beta,
+                                                       float gamma, float* xout) {
+  const int* tl = tiles + 3 * blockIdx.x;
+  const Mat mt = load_mat(mats, tl[0]);
+  const int64_t n = mt.n, m = mt.m;
+  const int r = (int)mt.r;
+  const float* Q = Qall + mt.q_off;
+  const int lane = lane_id(), w = wave_id();
+  const int64_t row0 = (int64_t)tl[1] * kRB0 + 4 * w;
+  const int64_t c0 = (int64_t)tl[2] * kCS0;
+  const int64_t c1 = c0 + kCS0 < m ? c0 + kCS0 : m;
+  float acc[4][R];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int j = 0; j < R; ++j) acc[a][j] = 0.f;
+  if (mat_vec(mt)) {
+    constexpr int kCU = 2;  // column chunks per iteration: 4 rows x 2 chunks (x2 with COMP 2) loads in flight
+    for (int64_t cb = c0 + 4 * lane; cb < c1; cb += 4 * kWave * kCU) {
+      float4 mv[kCU][4], rv[kCU][4];
+#pragma unroll
+      for (int k = 0; k < kCU; ++k)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int64_t c = cb + (int64_t)k * 4 * kWave, row = row0 + rr;
+          mv[k][rr] = make_float4(0.f, 0.f, 0.f, 0.f);
+          rv[k][rr] = mv[k][rr];
+          if (row < n && c < c1) {
+            const int64_t gi = mt.x_off + row * m + c;
+            mv[k][rr] = *reinterpret_cast<const float4*>(x + gi);
+            if (COMP == 2) rv[k][rr] = *reinterpret_cast<const float4*>(cr + gi);
+          }
+        }
+#pragma unroll
+      for (int k = 0; k < kCU; ++k) {
+        const int64_t c = cb + (int64_t)k * 4 * kWave;
+        if (c >= c1) break;
+        float q[4][R];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) load_small_row<R>(Q, c + t, r, q[t]);
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          float4 v = mv[k][rr];
+          if (COMP == 2)
+            v = make_float4(fmaf(beta, rv[k][rr].x, gamma * v.x), fmaf(beta, rv[k][rr].y, gamma * v.y),
+                            fmaf(beta, rv[k][rr].z, gamma * v.z), fmaf(beta, rv[k][rr].w, gamma * v.w));
+          const int64_t row = row0 + rr;
+          if (COMP != 0 && row < n) *reinterpret_cast<float4*>(xout + mt.x_off + row * m + c) = v;
+          const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int j = 0; j < R; ++j) acc[rr][j] = fmaf(e[t], q[t][j], acc[rr][j]);
+        }
+      }
+    }
+  } else {
+    for (int64_t c = c0 + lane; c < c1; c += kWave) {
+      float q[R];
+      load_small_row<R>(Q, c, r, q);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int64_t row = row0 + rr;
+        if (row < n) {
+          const int64_t gi = mt.x_off + row * m + c;
+          float v = x[gi];
+          if (COMP == 2) v = fmaf(beta, cr[gi], gamma * v);
+          if (COMP != 0) xout[gi] = v;
+#pragma unroll
+          for (int j = 0; j < R; ++j) acc[rr][j] = fmaf(v, q[j], acc[rr][j]);
+        }
+      }
+    }
+  }
+  float* P = Pall + mt.p_off;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+#pragma unroll
+    for (int j = 0; j < R; ++j) acc[rr][j] = wave_sum(acc[rr][j]);
+    const int64_t row = row0 + rr;
+    if (lane < r && row < n) {
+      float v = 0.f;
+#pragma unroll
+      for (int j = 0; j < R; ++j) v = lane == j ? acc[rr][j] : v;
+      atomicAdd(&P[row * r + lane], v);
+    }
+  }
+}
+
+// ps_mtp geometry: a block owns 1024 contiguous columns (16-B path: 256 threads x 4; 4-B path:
+// 256 columns) of a row strip whose length is chosen per matrix on the host (enough workgroups for
+// every matrix); each thread accumulates its columns over the strip with kPB independent 16-B
+// loads in flight, the block's partial Q is transposed through LDS into address order, and the
+// strip's atomics go out as contiguous wave-wide runs (per-lane atomics 64 B apart measured 1.8
+// TB/s for VGG-16 fc6; a block covering only 1 KB of each row read slower than one covering 4 KB).
+template <int R>
+__global__ __launch_bounds__(kBlock) void ps_mtp_kernel(const float* __restrict__ x, const float* __restrict__ Pall,
+                                                        float* __restrict__ Qall, const int64_t* __restrict__ mats,
+                                                        const int32_t* __restrict__ tiles) {
+  __shared__ float red[kCBV * R];
+  const int* tl = tiles + 3 * blockIdx.x;
+  const Mat mt = load_mat(mats, tl[0]);
+  const int64_t n = mt.n, m = mt.m;
+  const int r = (int)mt.r;
+  const float* P = Pall + mt.p_off;
+  float* Q = Qall + mt.q_off;
+  // tl[2] = (first row / 32) << 16 | (rows / 32)
+  const int64_t r0 = (int64_t)(tl[2] >> 16) * 32;
+  const int64_t r1 = r0 + (int64_t)(tl[2] & 0xffff) * 32 < n ? r0 + (int64_t)(tl[2] & 0xffff) * 32 : n;
+  if (mat_vec(mt)) {  // block-uniform branch
+    const int64_t cb = (int64_t)tl[1] * kCBV;
+    const int64_t c = cb + 4 * threadIdx.x;
+    const bool act = c < m;
+    float acc[4][R];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int j = 0; j < R; ++j) acc[t][j] = 0.f;
+    for (int64_t rb = r0; rb < r1; rb += kPB) {
+      float4 mv[kPB];
+#pragma unroll
+      for (int u = 0; u < kPB; ++u)
+        mv[u] = (act && rb + u < r1) ? *reinterpret_cast<const float4*>(x + mt.x_off + (rb + u) * m + c)
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int u = 0; u < kPB; ++u) {
+        if (rb + u >= r1) break;
+        float p[R];
+        load_small_row<R>(P, rb + u, r, p);
+        const float e[4] = {mv[u].x, mv[u].y, mv[u].z, mv[u].w};
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int j = 0; j < R; ++j) acc[t][j] = fmaf(e[t], p[j], acc[t][j]);
+      }
+    }
+    // LDS image of the block's Q rows in address order: (local column, j) at local_col * r + j
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int j = 0; j < R; ++j)
+        if (j < r) red[(4 * threadIdx.x + t) * r + j] = acc[t][j];
+    __syncthreads();
+    const int64_t ncols = m - cb < kCBV ? m - cb : kCBV;
+    for (int e = threadIdx.x; e < ncols * r; e += kBlock) atomicAdd(&Q[cb * r + e], red[e]);
+  } else {
+    const int64_t c = (int64_t)tl[1] * kCBS + threadIdx.x;
+    if (c >= m) return;
+    float acc[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) acc[j] = 0.f;
+    for (int64_t row = r0; row < r1; ++row) {
+      const float v = x[mt.x_off + row * m + c];
+      float p[R];
+      load_small_row<R>(P, row, r, p);
+#pragma unroll
+      for (int j = 0; j < R; ++j) acc[j] = fmaf(v, p[j], acc[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+      if (j < r) atomicAdd(&Q[c * r + j], acc[j]);
+  }
+}
+
+template <int R>
+__global__ __launch_bounds__(kBlock) void ps_pqt_kernel(const float* __restrict__ Pall, const float* __restrict__ Qall,
+                                                        float* __restrict__ out, const int64_t* __restrict__ mats,
+                                                        const int32_t* __restrict__ tiles, float* __restrict__ resid) {
+  const int* tl = tiles + 3 * blockIdx.x;
+  const Mat mt = load_mat(mats, tl[0]);
+  const int64_t n = mt.n, m = mt.m;
+  const int r = (int)mt.r;
+  const float* P = Pall + mt.p_off;
+  const float* Q = Qall + mt.q_off;
+  const int64_t r0 = (int64_t)tl[1] * kRSP;
+  const int64_t r1 = r0 + kRSP < n ? r0 + kRSP : n;
+  if (mat_vec(mt)) {
+    const int64_t c = (int64_t)tl[2] * kCBV + 4 * threadIdx.x;
+    if (c >= m) return;
+    float q[4][R];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) load_small_row<R>(Q, c + t, r, q[t]);
+    for (int64_t rb = r0; rb < r1; rb += kPB) {
+      float4 rv[kPB];
+      if (resid != nullptr) {
+#pragma unroll
+        for (int u = 0; u < kPB; ++u)
+          if (rb + u < r1) rv[u] = *reinterpret_cast<const float4*>(resid + mt.x_off + (rb + u) * m + c);
+      }
+#pragma unroll
+      for (int u = 0; u < kPB; ++u) {
+        const int64_t row = rb + u;
+        if (row >= r1) break;
+        float p[R];
+        load_small_row<R>(P, row, r, p);
+        float o[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          float v = 0.f;
+#pragma unroll
+          for (int j = 0; j < R; ++j) v = fmaf(p[j], q[t][j], v);
+          o[t] = v;
+        }
+        const int64_t gi = mt.x_off + row * m + c;
+        *reinterpret_cast<float4*>(out + gi) = make_float4(o[0], o[1], o[2], o[3]);
+        if (resid != nullptr)
+          *reinterpret_cast<float4*>(resid + gi) =
+              make_float4(rv[u].x - o[0], rv[u].y - o[1], rv[u].z - o[2], rv[u].w - o[3]);
+      }
+    }
+  } else {
+    const int64_t c = (int64_t)tl[2] * kCBS + threadIdx.x;
+    if (c >= m) return;
+    float q[R];
+    load_small_row<R>(Q, c, r, q);
+    for (int64_t row = r0; row < r1; ++row) {
+      float p[R];
+      load_small_row<R>(P, row, r, p);
+      float v = 0.f;
+#pragma unroll
+      for (int j = 0; j < R; ++j) v = fmaf(p[j], q[j], v);
+      const int64_t gi = mt.x_off + row * m + c;
+      out[gi] = v;
+      if (resid != nullptr) resid[gi] -= v;
     }
   }
 }
@@ -196,6 +367,34 @@ __device__ void mgs_gram_metric(const double (*G)[16], double (*Tm)[16], int r) 
   }
 }
 
+// mgs_gram_metric for r <= 4 with register arrays (unrolled, predicated on the runtime r)
+__device__ __forceinline__ void mgs_gram_metric_reg(const double (&G)[4][4], double (&Tm)[4][4], int r) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (i >= r) break;
+    double nn = 0.0;
+#pragma unroll
+    for (int a = 0; a <= i; ++a)
+#pragma unroll
+      for (int b = 0; b <= i; ++b) nn += Tm[a][i] * G[a][b] * Tm[b][i];
+    const double nrm = nn > 0.0 ? sqrt(nn) : 0.0;
+    const double inv = nrm > 1e-30 ? 1.0 / nrm : 0.0;  // zero column stays zero
+#pragma unroll
+    for (int a = 0; a <= i; ++a) Tm[a][i] *= inv;
+#pragma unroll
+    for (int j = i + 1; j < 4; ++j) {
+      if (j >= r) break;
+      double pr = 0.0;
+#pragma unroll
+      for (int a = 0; a <= i; ++a)
+#pragma unroll
+        for (int b = 0; b <= j; ++b) pr += Tm[a][i] * G[a][b] * Tm[b][j];
+#pragma unroll
+      for (int a = 0; a <= i; ++a) Tm[a][j] -= pr * Tm[a][i];
+    }
+  }
+}
+
 // one 64-thread workgroup per matrix; T: fp32 [n_mat][16*16] (row i, col j: A_new[:, j] = sum_i A[:, i] T[i][j])
 __global__ __launch_bounds__(kWave) void gram_fix_kernel(const int64_t* __restrict__ mats,
                                                          const int32_t* __restrict__ gtile_begin,
@@ -258,14 +457,14 @@ __global__ __launch_bounds__(kBlock) void gram_apply_kernel(float* __restrict__ 
 // of at most a few hundred KB; here the largest (VGG-16 fc6's 25088 x 4 Q) is one workgroup
 // streaming 400 KB per pass, the others run beside it.
 constexpr int kSmallR = 4;
+constexpr int kGramLds = 16384;  // floats of a block staged in LDS (64 KB)
 __global__ __launch_bounds__(kBlock) void gram_small_kernel(float* __restrict__ buf, const int64_t* __restrict__ mats,
                                                             int which, int passes) {
   const Mat mt = load_mat(mats, blockIdx.x);
   const int64_t len = blk_len(mt, which);
   const int r = (int)mt.r;
   float* A = buf + blk_off(mt, which);
-  __shared__ double G[16][16];
-  __shared__ double Tm[16][16];
+  __shared__ double Tm[kSmallR][kSmallR];
   __shared__ double red[kBlock / kWave][10];
   const bool vec = r == 4 && (reinterpret_cast<uintptr_t>(A) & 15) == 0;
   auto load_row = [&](int64_t row, float (&a)[kSmallR]) {
@@ -277,6 +476,33 @@ __global__ __launch_bounds__(kBlock) void gram_small_kernel(float* __restrict__ 
       for (int i = 0; i < kSmallR; ++i) a[i] = i < r ? A[row * r + i] : 0.f;
     }
   };
+  // A block of <= 64 KB (every P of VGG-16 / ResNet-50) is staged in LDS once: the passes then
+  // run on LDS instead of re-streaming the rows with one dependent global load per thread per
+  // 256 rows (latency bound: 37 us per call for VGG-16 before)
+  __shared__ float4 sA[kGramLds / 4];
+  const bool in_lds = vec && len * 4 <= kGramLds;
+  if (in_lds) {  // all of a thread's rows (<= 16) in flight at once, then into LDS
+    float4 st[kGramLds / 4 / kBlock];
+#pragma unroll
+    for (int k = 0; k < kGramLds / 4 / kBlock; ++k) {
+      const int64_t row = threadIdx.x + (int64_t)k * kBlock;
+      st[k] = row < len ? reinterpret_cast<const float4*>(A)[row] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < kGramLds / 4 / kBlock; ++k) {
+      const int64_t row = threadIdx.x + (int64_t)k * kBlock;
+      if (row < len) sA[row] = st[k];
+    }
+    __syncthreads();
+  }
+  auto row_of = [&](int64_t row, float (&a)[kSmallR]) {
+    if (in_lds) {
+      const float4 v = sA[row];
+      a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
+    } else {
+      load_row(row, a);
+    }
+  };
   for (int pass = 0; pass < passes; ++pass) {
     double s[10];
 #pragma unroll
@@ -284,7 +510,7 @@ __global__ __launch_bounds__(kBlock) void gram_small_kernel(float* __restrict__ 
 #pragma unroll 4
     for (int64_t row = threadIdx.x; row < len; row += kBlock) {
       float a[kSmallR];
-      load_row(row, a);
+      row_of(row, a);
       int k = 0;
 #pragma unroll
       for (int i = 0; i < kSmallR; ++i)
@@ -298,18 +524,28 @@ __global__ __launch_bounds__(kBlock) void gram_small_kernel(float* __restrict__ 
       for (int k = 0; k < 10; ++k) red[wave_id()][k] = s[k];
     __syncthreads();
     if (threadIdx.x == 0) {
-      for (int e = 0; e < 256; ++e) {
-        G[e >> 4][e & 15] = 0.0;
-        Tm[e >> 4][e & 15] = (e >> 4) == (e & 15) ? 1.0 : 0.0;
-      }
+      // the 4 x 4 Gram and the MGS coefficients in REGISTERS (fully unrolled): the LDS-resident
+      // version ran ~8 us per pass of dependent LDS round trips in this single thread
+      double g[kSmallR][kSmallR], tm[kSmallR][kSmallR];
       int k = 0;
+#pragma unroll
       for (int i = 0; i < kSmallR; ++i)
+#pragma unroll
         for (int j = i; j < kSmallR; ++j, ++k) {
           double v = 0.0;
+#pragma unroll
           for (int w = 0; w < kBlock / kWave; ++w) v += red[w][k];  // fixed order: deterministic
-          G[i][j] = G[j][i] = v;
+          g[i][j] = g[j][i] = v;
         }
-      mgs_gram_metric(G, Tm, r);
+#pragma unroll
+      for (int i = 0; i < kSmallR; ++i)
+#pragma unroll
+        for (int j = 0; j < kSmallR; ++j) tm[i][j] = i == j ? 1.0 : 0.0;
+      mgs_gram_metric_reg(g, tm, r);
+#pragma unroll
+      for (int i = 0; i < kSmallR; ++i)
+#pragma unroll
+        for (int j = 0; j < kSmallR; ++j) Tm[i][j] = tm[i][j];
     }
     __syncthreads();
     float t[kSmallR][kSmallR];
@@ -320,7 +556,7 @@ __global__ __launch_bounds__(kBlock) void gram_small_kernel(float* __restrict__ 
 #pragma unroll 4
     for (int64_t row = threadIdx.x; row < len; row += kBlock) {
       float a[kSmallR], o[kSmallR];
-      load_row(row, a);
+      row_of(row, a);
 #pragma unroll
       for (int j = 0; j < kSmallR; ++j) {
         float v = 0.f;
@@ -328,7 +564,9 @@ __global__ __launch_bounds__(kBlock) void gram_small_kernel(float* __restrict__ 
         for (int i = 0; i < kSmallR; ++i) v = fmaf(a[i], t[i][j], v);
         o[j] = v;
       }
-      if (vec) {
+      if (in_lds && pass + 1 < passes) {
+        sA[row] = make_float4(o[0], o[1], o[2], o[3]);  // the next pass reads LDS
+      } else if (vec) {
         reinterpret_cast<float4*>(A)[row] = make_float4(o[0], o[1], o[2], o[3]);
       } else {
 #pragma unroll
@@ -337,53 +575,6 @@ __global__ __launch_bounds__(kBlock) void gram_small_kernel(float* __restrict__ 
       }
     }
     __syncthreads();  // the next pass reads what this one wrote (same workgroup)
-  }
-}
-
-// out[x_off + row*m + col] = sum_j P[row][j] Q[col][j]; tiles: (matrix, row block of 16, col block of 256).
-// Each wave computes four 16x16 MFMA tiles (64 columns); the 16 x 256 workgroup tile is staged in
-// LDS so every store instruction writes 64 consecutive floats of one row (256 B) instead of four
-// 64-B row pieces.  With ``resid`` (holding x) the residual r = x - P Q^T is updated in the same pass.
-constexpr int kPqtCols = 256;
-__global__ __launch_bounds__(kBlock) void pqt_kernel(const float* __restrict__ P, const float* __restrict__ Q,
-                                                     float* __restrict__ out, const int64_t* __restrict__ mats,
-                                                     const int32_t* __restrict__ tiles, float* resid) {
-  __shared__ float tile[16][kPqtCols + 1];
-  const int* tl = tiles + 3 * blockIdx.x;
-  const Mat mt = load_mat(mats, tl[0]);
-  const int64_t n = mt.n, m = mt.m, r = mt.r;
-  const float* Pm = P + mt.p_off;
-  const float* Qm = Q + mt.q_off;
-  const int lane = lane_id(), w = wave_id();
-  const int64_t row0 = (int64_t)tl[1] * 16;
-  const int64_t cbase = (int64_t)tl[2] * kPqtCols;
-#pragma unroll
-  for (int cb = 0; cb < 4; ++cb) {
-    const int lc0 = 64 * w + 16 * cb;  // local column of this 16x16 tile
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int k0 = 0; k0 < r; k0 += 4) {
-      const int k = k0 + (lane >> 4);
-      const int64_t ar = row0 + (lane & 15), bc = cbase + lc0 + (lane & 15);
-      const float a = (ar < n && k < r) ? Pm[ar * r + k] : 0.f;  // A[i][k] = P[row i][k]
-      const float b = (bc < m && k < r) ? Qm[bc * r + k] : 0.f;  // B[k][j] = Q[col j][k]
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) tile[(lane >> 4) * 4 + q][lc0 + (lane & 15)] = acc[q];
-  }
-  __syncthreads();
-  const int64_t col = cbase + threadIdx.x;
-  if (col < m) {
-#pragma unroll 4
-    for (int rr = 0; rr < 16; ++rr) {
-      const int64_t row = row0 + rr;
-      if (row < n) {
-        const int64_t gi = mt.x_off + row * m + col;
-        const float v = tile[rr][threadIdx.x];
-        out[gi] = v;
-        if (resid != nullptr) resid[gi] -= v;
-      }
-    }
   }
 }
 
@@ -409,19 +600,29 @@ __global__ __launch_bounds__(kBlock) void philox_normal_kernel(float* __restrict
 
 }  // namespace
 
+template <int R>
+void launch_mq(const float* x, const float* small, float* out, const int64_t* mats, const int32_t* tiles, int n_tiles,
+               int mode, const float* comp_r, float beta, float gamma, float* xout, hipStream_t stream) {
+  if (mode == 1)
+    ps_mtp_kernel<R><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles);
+  else if (xout == nullptr)
+    ps_mq_kernel<R, 0><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles, nullptr, 0.f, 0.f, nullptr);
+  else if (comp_r == nullptr)
+    ps_mq_kernel<R, 1><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles, nullptr, 0.f, 0.f, xout);
+  else
+    ps_mq_kernel<R, 2><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles, comp_r, beta, gamma, xout);
+}
+
 void powersgd_mq(const float* x, const float* small, float* out, int64_t out_len, const int64_t* mats,
                  const int32_t* tiles, int n_tiles, int mode, const float* comp_r, float beta, float gamma,
-                 float* xout, hipStream_t stream) {
+                 float* xout, int max_r, hipStream_t stream) {
   GRACE_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(float) * out_len, stream));
   if (n_tiles <= 0) return;
-  if (mode == 1)
-    mq_kernel<1, 0><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles, nullptr, 0.f, 0.f, nullptr);
-  else if (xout == nullptr)
-    mq_kernel<0, 0><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles, nullptr, 0.f, 0.f, nullptr);
-  else if (comp_r == nullptr)
-    mq_kernel<0, 1><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles, nullptr, 0.f, 0.f, xout);
-  else
-    mq_kernel<0, 2><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles, comp_r, beta, gamma, xout);
+  if (max_r <= 1) launch_mq<1>(x, small, out, mats, tiles, n_tiles, mode, comp_r, beta, gamma, xout, stream);
+  else if (max_r <= 2) launch_mq<2>(x, small, out, mats, tiles, n_tiles, mode, comp_r, beta, gamma, xout, stream);
+  else if (max_r <= 4) launch_mq<4>(x, small, out, mats, tiles, n_tiles, mode, comp_r, beta, gamma, xout, stream);
+  else if (max_r <= 8) launch_mq<8>(x, small, out, mats, tiles, n_tiles, mode, comp_r, beta, gamma, xout, stream);
+  else launch_mq<16>(x, small, out, mats, tiles, n_tiles, mode, comp_r, beta, gamma, xout, stream);
 }
 
 void gram_orthonormalize(float* buf, const int64_t* mats, int n_mat, int which, const int32_t* gtiles,
@@ -440,9 +641,13 @@ void gram_orthonormalize(float* buf, const int64_t* mats, int n_mat, int which, 
 }
 
 void powersgd_pqt(const float* P, const float* Q, float* out, const int64_t* mats, const int32_t* tiles, int n_tiles,
-                  float* resid, hipStream_t stream) {
+                  float* resid, int max_r, hipStream_t stream) {
   if (n_tiles <= 0) return;
-  pqt_kernel<<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid);
+  if (max_r <= 1) ps_pqt_kernel<1><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid);
+  else if (max_r <= 2) ps_pqt_kernel<2><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid);
+  else if (max_r <= 4) ps_pqt_kernel<4><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid);
+  else if (max_r <= 8) ps_pqt_kernel<8><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid);
+  else ps_pqt_kernel<16><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid);
 }
 
 void philox_normal(float* out, int64_t n, SeedArg seed, hipStream_t stream) {

@@ -34,17 +34,27 @@ class Plan:
         key = str(device)
         t = self._dev.get(key)
         if t is None:
+            # work tables of csrc/kernels/powersgd.hip (ps_mq: 16 rows x 2048 columns; ps_mtp:
+            # 1024 / 256 columns x per-matrix row strips; ps_pqt: 32 rows x 1024 / 256 columns)
             t0, t1, tp = [], [], []
             for i, (xo, n, m, r, po, qo) in enumerate(self.mats):
-                for rb in range((n + 63) // 64):
-                    for sidx in range((m + 1023) // 1024):
-                        t0.append((i, rb, sidx))
-                for cb in range((m + 63) // 64):
-                    for sidx in range((n + 1023) // 1024):
-                        t1.append((i, cb, sidx))
+                cb = 1024 if (xo % 4 == 0 and m % 4 == 0) else 256
                 for rb in range((n + 15) // 16):
-                    for cb in range((m + 255) // 256):
-                        tp.append((i, rb, cb))
+                    for sidx in range((m + 2047) // 2048):
+                        t0.append((i, rb, sidx))
+                # ps_mtp: 1024 (16-B path) / 256 (4-B path) column blocks; rows split into strips of a
+                # multiple of 32 rows so that the matrix yields >= ~1024 workgroups (too few waves
+                # left the product latency bound)
+                ncb = (m + cb - 1) // cb
+                n32 = (n + 31) // 32
+                strips = max(1, min(n32, -(-1024 // ncb)))
+                per = -(-n32 // strips)
+                for c in range(ncb):
+                    for s0 in range(0, n32, per):
+                        t1.append((i, c, (s0 << 16) | min(per, n32 - s0)))
+                for rb in range((n + 31) // 32):
+                    for c in range((m + cb - 1) // cb):
+                        tp.append((i, rb, c))
 
             def it(lst):
                 return torch.tensor(lst, dtype=torch.int32, device=device).view(-1) if lst else \
@@ -155,7 +165,7 @@ def mq(x: torch.Tensor, q: torch.Tensor, plan: Plan, comp_r: Optional[torch.Tens
     p = torch.empty(plan.p_total, dtype=torch.float32, device=x.device)
     if _native.use_native(x):
         t = plan.tables(x.device)
-        _native.lib().powersgd_mq(x, q, p, t["mat"], t["tiles0"], 0, comp_r, beta, gamma, xout)
+        _native.lib().powersgd_mq(x, q, p, t["mat"], t["tiles0"], 0, comp_r, beta, gamma, xout, plan.rank)
         return p
     for (xo, n, m, r, po, qo) in plan.mats:
         mx = x[xo:xo + n * m]
@@ -172,7 +182,7 @@ def mtp(x: torch.Tensor, p: torch.Tensor, plan: Plan) -> torch.Tensor:
     q = torch.empty(plan.q_total, dtype=torch.float32, device=x.device)
     if _native.use_native(x):
         t = plan.tables(x.device)
-        _native.lib().powersgd_mq(x, p, q, t["mat"], t["tiles1"], 1, None, 1.0, 1.0, None)
+        _native.lib().powersgd_mq(x, p, q, t["mat"], t["tiles1"], 1, None, 1.0, 1.0, None, plan.rank)
         return q
     for (xo, n, m, r, po, qo) in plan.mats:
         torch.mm(x[xo:xo + n * m].view(n, m).t(), p[po:po + n * r].view(n, r), out=q[qo:qo + m * r].view(m, r))
@@ -184,7 +194,7 @@ def pqt(p: torch.Tensor, q: torch.Tensor, plan: Plan, out: torch.Tensor, resid: 
     resid[matrix i] -= P_i Q_i^T in the same pass (PowerSGD residual update)."""
     if _native.use_native(out):
         t = plan.tables(out.device)
-        _native.lib().powersgd_pqt(p, q, out, t["mat"], t["tilesp"], resid)
+        _native.lib().powersgd_pqt(p, q, out, t["mat"], t["tilesp"], resid, plan.rank)
         return
     for (xo, n, m, r, po, qo) in plan.mats:
         o = out[xo:xo + n * m].view(n, m)
