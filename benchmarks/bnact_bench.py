@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Per-shape timing of the fused BN(+add)(+ReLU) kernels vs the stock MIOpen + elementwise path,
-on every BatchNorm shape of ResNet-50 at batch 32 (bf16, channels_last).
+on every BatchNorm shape of ResNet-50 at batch 32 (bf16 or fp32, channels_last).
 
-    python benchmarks/bnact_bench.py [--batch 32] [--iters 50]
+    python benchmarks/bnact_bench.py [--batch 32] [--iters 50] [--dtype fp32]
 
 Columns: shape, forward / backward microseconds for the fused kernels with the opt-in
 single-launch variants enabled (used where the grid fits co-resident with full blocks; V f/b =
@@ -63,6 +63,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--eager", action="store_true", help="time eager launches instead of graph replays")
+    ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
     a = ap.parse_args()
     dev = "cuda"
     from grace_amd.ops import _native
@@ -73,7 +74,8 @@ def main():
           f"stock fwd  bwd (us) | fused GB/s fwd bwd")
     for (c, h, w, relu, res, cnt) in R50:
         m = BatchNormAct2d(c, relu=relu).to(dev)
-        x = torch.randn(a.batch, c, h, w, device=dev, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        x = torch.randn(a.batch, c, h, w, device=dev,
+                        dtype=torch.bfloat16 if a.dtype == "bf16" else torch.float32).contiguous(memory_format=torch.channels_last)
         r = torch.randn_like(x) if res else None
         dy = torch.randn_like(x)
         xg = x.clone().requires_grad_(True)
@@ -100,7 +102,7 @@ def main():
         M = a.batch * h * w
         vf, vb = lib.bn_fused_v(M, c, False), lib.bn_fused_v(M, c, True)
         lib.bn_set_fused(False)
-        nbytes = x.numel() * 2
+        nbytes = x.numel() * x.element_size()
         fwd_bytes = nbytes * (3 + (1 if res else 0))           # stats read, apply read+write (+res)
         bwd_bytes = nbytes * ((3 if relu else 2) * 2 + 1 + (1 if res else 0))  # reduce + dx reads, dx (+dres) write
         (ff, fbk), (tf2, tb2), (uf, ub) = res_t["0"], res_t["2"], res_t["1"]

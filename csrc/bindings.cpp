@@ -587,6 +587,39 @@ void sketch_decode(const Tensor& base, int64_t rank_stride, int64_t bins_off, in
                        (int)n_ranks, (float)scale, out.data_ptr<float>(), cur_stream());
 }
 
+// tables (all int32 / fp32, per segment): ranks/slot/st_* [n_seg][max_slots], nrank/nuniq [n_seg],
+// lo_idx/hi_idx/w/edges [n_seg][q+1]; h0 [n_seg][2048] and h [n_seg][max_slots][128] zero on entry
+// (and left zero on exit)
+void quantile_select(const Tensor& x, const Tensor& seg, const Tensor& cb, const Tensor& ce, int64_t n_seg,
+                     int64_t max_slots, const Tensor& ranks, const Tensor& nrank, const Tensor& h0, const Tensor& h,
+                     const Tensor& st_pfx, const Tensor& st_rank, const Tensor& slot, const Tensor& uniq,
+                     const Tensor& nuniq, int64_t q, const Tensor& lo_idx, const Tensor& hi_idx, const Tensor& w,
+                     const Tensor& edges) {
+  CHECK_F32(x);
+  CHECK_F32(w);
+  CHECK_F32(edges);
+  for (const Tensor* t : {&ranks, &nrank, &h0, &h, &st_pfx, &st_rank, &slot, &uniq, &nuniq, &lo_idx, &hi_idx}) {
+    CHECK_I32((*t));
+  }
+  TORCH_CHECK(max_slots >= 1 && max_slots <= 256, "max_slots must be in [1, 256] (one select thread per rank)");
+  const int64_t ms = n_seg * max_slots;
+  TORCH_CHECK(ranks.numel() >= ms && st_pfx.numel() >= ms && st_rank.numel() >= ms && slot.numel() >= ms &&
+                  uniq.numel() >= ms, "per-rank tables too small");
+  TORCH_CHECK(nrank.numel() >= n_seg && nuniq.numel() >= n_seg, "per-segment tables too small");
+  TORCH_CHECK(h0.numel() >= n_seg * 2048 && h.numel() >= ms * 128, "histograms too small");
+  const int64_t ne = n_seg * (q + 1);
+  TORCH_CHECK(lo_idx.numel() >= ne && hi_idx.numel() >= ne && w.numel() >= ne && edges.numel() >= ne,
+              "edge tables too small");
+  auto ct = make_ct(seg, cb, ce);
+  DevGuard guard(x.device());
+  grace::quantile_select(ct, (int)n_seg, x.data_ptr<float>(), (int)max_slots, ranks.data_ptr<int32_t>(),
+                         nrank.data_ptr<int32_t>(), h0.data_ptr<int32_t>(), h.data_ptr<int32_t>(),
+                         reinterpret_cast<uint32_t*>(st_pfx.data_ptr<int32_t>()), st_rank.data_ptr<int32_t>(),
+                         slot.data_ptr<int32_t>(), reinterpret_cast<uint32_t*>(uniq.data_ptr<int32_t>()),
+                         nuniq.data_ptr<int32_t>(), (int)q, lo_idx.data_ptr<int32_t>(), hi_idx.data_ptr<int32_t>(),
+                         w.data_ptr<float>(), edges.data_ptr<float>(), cur_stream());
+}
+
 // ------------------------------------------------------------------------------ segment stats
 void segment_stats(const Tensor& x, const c10::optional<Tensor>& r, int64_t mode, double beta, double gamma,
                    const c10::optional<Tensor>& xout, const Tensor& seg, const Tensor& cb, const Tensor& ce,
@@ -879,6 +912,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("decode16_sum", &decode16_sum);
   m.def("sketch_encode", &sketch_encode);
   m.def("sketch_decode", &sketch_decode);
+  m.def("quantile_select", &quantile_select);
   m.def("axpby", &axpby);
   m.def("scale_", &scale_);
   m.def("gather_segments", &gather_segments);

@@ -116,6 +116,13 @@ void sketch_encode(const ChunkTable& ct, const float* x, const float* edges, int
 void sketch_decode(const ChunkTable& ct, const uint8_t* base, int64_t rank_stride, int64_t bins_off, int64_t means_off,
                    int q, int bin_bytes, int n_ranks, float scale, float* out, hipStream_t stream);
 
+// ---------------------------------------------------------------- quantile.hip
+// exact order statistics of every segment at the given sorted ranks + interpolated sketch edges
+void quantile_select(const ChunkTable& ct, int n_seg, const float* x, int max_slots, const int32_t* ranks,
+                     const int32_t* nrank, int32_t* h0, int32_t* h, uint32_t* st_pfx, int32_t* st_rank, int32_t* slot,
+                     uint32_t* uniq, int32_t* nuniq, int q, const int32_t* lo_idx, const int32_t* hi_idx,
+                     const float* w, float* edges, hipStream_t stream);
+
 // ---------------------------------------------------------------- ef.hip (elementwise)
 void axpby(const float* x, const float* y, float* out, int64_t n, float a, float b, hipStream_t stream);
 void scale_inplace(float* x, int64_t n, float s, hipStream_t stream);

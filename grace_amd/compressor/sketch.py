@@ -50,6 +50,60 @@ def segmented_quantile_edges(x: torch.Tensor, lay, q: int) -> torch.Tensor:
     return (a * (1 - w) + b * w).contiguous()
 
 
+_QSEL_CHUNK = 65536  # elements per workgroup of the selection passes (LDS setup amortised)
+
+
+def _qsel_tables(lay, q: int, dev: torch.device):
+    """Per-layout tables of the native selection: the sorted distinct ranks floor/ceil(j (n-1)/q)
+    of every segment, the positions of each edge's two ranks among them, the interpolation
+    weights (float64 positions rounded to fp32 exactly as ``segmented_quantile_edges``) and the
+    zero-initialised histograms / state the kernels leave clean after every call."""
+    def build():
+        n = torch.tensor(lay.numels, dtype=torch.float64)
+        probs = torch.linspace(0, 1, q + 1, dtype=torch.float64)
+        pos = probs[None, :] * (n[:, None] - 1).clamp_min(0)
+        lo, hi = pos.floor(), pos.ceil()
+        w = (pos - lo).float()
+        per = []
+        for i in range(lay.n_seg):
+            per.append(sorted(set(lo[i].long().tolist()) | set(hi[i].long().tolist())) if lay.numels[i] else [])
+        ms = max(1, max(len(r) for r in per))
+        if ms > 256:
+            return None
+        ranks = torch.zeros(lay.n_seg, ms, dtype=torch.int32)
+        lo_idx = torch.zeros(lay.n_seg, q + 1, dtype=torch.int32)
+        hi_idx = torch.zeros(lay.n_seg, q + 1, dtype=torch.int32)
+        for i, r in enumerate(per):
+            if not r:
+                continue
+            ranks[i, :len(r)] = torch.tensor(r, dtype=torch.int32)
+            where = {v: j for j, v in enumerate(r)}
+            lo_idx[i] = torch.tensor([where[int(v)] for v in lo[i].tolist()], dtype=torch.int32)
+            hi_idx[i] = torch.tensor([where[int(v)] for v in hi[i].tolist()], dtype=torch.int32)
+        z = lambda *shape: torch.zeros(*shape, dtype=torch.int32, device=dev)
+        return {"max_slots": ms, "ranks": ranks.to(dev), "nrank": torch.tensor([len(r) for r in per], dtype=torch.int32,
+                                                                               device=dev),
+                "lo_idx": lo_idx.to(dev), "hi_idx": hi_idx.to(dev), "w": w.contiguous().to(dev),
+                "h0": z(lay.n_seg * 2048), "h": z(lay.n_seg * ms * 128), "st_pfx": z(lay.n_seg * ms),
+                "st_rank": z(lay.n_seg * ms), "slot": z(lay.n_seg * ms), "uniq": z(lay.n_seg * ms),
+                "nuniq": z(lay.n_seg)}
+    return lay.cached(dev, f"qsel:{q}", build)
+
+
+def native_quantile_edges(x: torch.Tensor, lay, q: int):
+    """[n_seg, q+1] edges from the HIP multi-rank radix select (csrc/kernels/quantile.hip), or
+    None when the layout needs more than 256 distinct ranks per segment (q > 127)."""
+    tb = _qsel_tables(lay, q, x.device)
+    if tb is None:
+        return None
+    ct = lay.device_tables(x.device, _QSEL_CHUNK)
+    edges = torch.empty(lay.n_seg, q + 1, device=x.device)
+    _native.lib().quantile_select(x, ct["seg"], ct["begin"], ct["end"], lay.n_seg, tb["max_slots"], tb["ranks"],
+                                  tb["nrank"], tb["h0"], tb["h"], tb["st_pfx"], tb["st_rank"], tb["slot"],
+                                  tb["uniq"], tb["nuniq"], q, tb["lo_idx"], tb["hi_idx"], tb["w"], edges)
+    return edges
+
+
 class SketchCompressor(BucketCompressor):
     reduce_by_allgather = True
     allreduce_compatible = True
@@ -65,7 +119,9 @@ class SketchCompressor(BucketCompressor):
         bdt = torch.uint8 if q < 256 else torch.int16
         bins, means = self.payload(x.device, [(bdt, (lay.total,)), (torch.float32, (q * lay.n_seg,))])
         if _native.use_native(x) and q <= 1024:
-            edges = segmented_quantile_edges(x, lay, q)
+            edges = native_quantile_edges(x, lay, q)
+            if edges is None:
+                edges = segmented_quantile_edges(x, lay, q)
             sums = torch.zeros(lay.n_seg * q, device=x.device)
             cnts = torch.zeros(lay.n_seg * q, device=x.device)
             t = lay.device_tables(x.device)

@@ -28,7 +28,7 @@ import torch
 #: stochastic codecs whose native kernels read a device step counter
 _DEVICE_STEPPED = ("RandomKCompressor", "QSGDCompressor", "TernGradCompressor", "NaturalCompressor",
                    "PowerSGDCompressor", "DgcCompressor", "AdaqCompressor")
-_HOST_SYNC = ("SketchCompressor",)
+_HOST_SYNC = ()
 
 
 def graph_safe(grc, allow_static_seeds: bool = False) -> Optional[str]:
@@ -36,6 +36,12 @@ def graph_safe(grc, allow_static_seeds: bool = False) -> Optional[str]:
     name = type(grc.compressor).__name__
     if name in _HOST_SYNC:
         return f"{name} reads payload sizes back to the host"
+    if name == "SketchCompressor":
+        from ..ops import _native
+
+        # the native multi-rank select (q <= 127) is capturable; the sort fallback is not
+        if grc.compressor.quantiles > 127 or not _native.available():
+            return f"{name} with {grc.compressor.quantiles} quantiles sorts the bucket (no native select)"
     if not grc.compressor.tensors_size_are_same:
         return f"{name} has variable-size payloads"
     if name in _DEVICE_STEPPED and not allow_static_seeds:
