@@ -1,5 +1,6 @@
 """Per-layer fp32 convolution timing for the ResNet-50 b32 step: MIOpen channels-last vs NCHW,
-and 1x1 convs as plain hipBLASLt GEMMs over the channels-last activation ([N*H*W, Cin] x Wᵀ).
+and 1x1 convs as plain hipBLASLt GEMMs over the channels-last activation ([N*H*W, Cin] x Wᵀ) ("mm")
+and on the hand-written f32 MFMA GEMM (grace_amd.ops.conv, "mf").
 
 Prints, for every unique conv shape (with its multiplicity in the network), fwd and fwd+bwd
 ms per call for each path, and the whole-network totals weighted by multiplicity.
@@ -11,8 +12,14 @@ from __future__ import annotations
 import argparse
 import collections
 
+import os
+import sys
+
 import torch
 import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from grace_amd.ops.conv import _Conv1x1Fn  # noqa: E402
 
 
 def resnet50_convs(batch):
@@ -67,6 +74,9 @@ class _MM1x1(torch.autograd.Function):
         return gx, gw
 
 
+PATHS = ("cl", "nchw", "mm", "mf")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32)
@@ -79,19 +89,21 @@ def main():
     dt = torch.float32 if args.dtype == "fp32" else torch.bfloat16
     dev = torch.device("cuda")
     tot = collections.defaultdict(float)
-    print(f"{'shape (N,Cin,H,W,Cout,k,s)':34} {'x':>2} " + " ".join(f"{p + ' ' + m:>12}" for p in ("cl", "nchw", "mm")
+    print(f"{'shape (N,Cin,H,W,Cout,k,s)':34} {'x':>2} " + " ".join(f"{p + ' ' + m:>12}" for p in PATHS
                                                             for m in ("fwd", "f+b")))
     for shp, cnt in sorted(resnet50_convs(args.batch).items(), key=lambda kv: -kv[0][4] * kv[0][1]):
         n, cin, h, w, cout, k, s = shp
         row = {}
-        for path in ("cl", "nchw", "mm"):
-            if path == "mm" and (k != 1 or s != 1):
+        for path in PATHS:
+            if path in ("mm", "mf") and (k != 1 or s != 1):
                 continue
             mf = torch.channels_last if path != "nchw" else torch.contiguous_format
             x = torch.randn(n, cin, h, w, device=dev, dtype=dt).to(memory_format=mf).requires_grad_(True)
             wt = (torch.randn(cout, cin, k, k, device=dev, dtype=dt) * 0.05).to(memory_format=mf).requires_grad_(True)
             if path == "mm":
                 f = lambda: _MM1x1.apply(x, wt)
+            elif path == "mf":
+                f = lambda: _Conv1x1Fn.apply(x, wt)
             else:
                 f = lambda: F.conv2d(x, wt, stride=s, padding=k // 2)
             y = f()
@@ -103,7 +115,7 @@ def main():
                 out = f()
                 gx, gw = torch.autograd.grad(out, (x, wt), gy)
             row[path + " f+b"] = timed(fb, args.iters)
-            if path == "mm":  # numerics vs the MIOpen conv
+            if path in ("mm", "mf"):  # numerics vs the MIOpen conv
                 ref = F.conv2d(x.detach().contiguous(), wt.detach().contiguous())
                 err = (y.detach() - ref).abs().max().item() / ref.abs().max().item()
                 assert err < 1e-4, (shp, err)
@@ -111,9 +123,9 @@ def main():
             tot[key] += cnt * v
         best_fb = min(v for kk, v in row.items() if kk.endswith("f+b"))
         tot["best f+b"] += cnt * best_fb
-        tot["cl f+b (mm where 1x1 s1)"] += cnt * row.get("mm f+b", row["cl f+b"])
+        tot["cl f+b (mf where 1x1 s1)"] += cnt * row.get("mf f+b", row["cl f+b"])
         print(f"{str(shp):34} {cnt:>2} " + " ".join(f"{row.get(p + ' ' + m, float('nan')):12.3f}"
-                                                   for p in ("cl", "nchw", "mm") for m in ("fwd", "f+b")))
+                                                   for p in PATHS for m in ("fwd", "f+b")))
     print("totals (ms per network step, weighted by multiplicity):")
     for key, v in tot.items():
         print(f"  {key:30} {v:8.3f}")

@@ -326,15 +326,24 @@ void qsgd_quantize(const Tensor& x, const Tensor& norms, double s, int64_t seed,
                        cb_, opt_f32_mut(resid), cur_stream());
 }
 
+// shared_norms: [n_seg] norms used for every rank (shared-scale codes; the rows then hold codes only)
 void qsgd_aggregate(const Tensor& base, int64_t rank_stride, int64_t codes_off, int64_t norms_off, int64_t code_bytes,
                     int64_t n_ranks, double s, double scale, const Tensor& out, bool accumulate, const Tensor& seg,
-                    const Tensor& cb, const Tensor& ce, int64_t n_seg) {
+                    const Tensor& cb, const Tensor& ce, int64_t n_seg, const c10::optional<Tensor>& shared_norms) {
   CHECK_F32(out);
   const int64_t code_size = code_bytes == 3 ? 2 : code_bytes;  // 3 = fp16 codes
-  check_rows(base, rank_stride, n_ranks, std::max(codes_off + out.numel() * code_size, norms_off + 4 * n_seg));
+  const float* sn = nullptr;
+  if (shared_norms.has_value()) {
+    CHECK_F32((*shared_norms));
+    TORCH_CHECK(shared_norms->numel() >= n_seg, "shared_norms too small");
+    sn = shared_norms->data_ptr<float>();
+    check_rows(base, rank_stride, n_ranks, codes_off + out.numel() * code_size);
+  } else {
+    check_rows(base, rank_stride, n_ranks, std::max(codes_off + out.numel() * code_size, norms_off + 4 * n_seg));
+  }
   auto ct = make_ct(seg, cb, ce);
   DevGuard guard(out.device());
-  grace::qsgd_aggregate(ct, base.data_ptr<uint8_t>(), rank_stride, codes_off, norms_off, (int)code_bytes,
+  grace::qsgd_aggregate(ct, base.data_ptr<uint8_t>(), rank_stride, codes_off, norms_off, sn, (int)code_bytes,
                         (int)n_ranks, (float)s, (float)scale, out.data_ptr<float>(), accumulate, cur_stream());
 }
 
@@ -618,6 +627,32 @@ void quantile_select(const Tensor& x, const Tensor& seg, const Tensor& cb, const
                          slot.data_ptr<int32_t>(), reinterpret_cast<uint32_t*>(uniq.data_ptr<int32_t>()),
                          nuniq.data_ptr<int32_t>(), (int)q, lo_idx.data_ptr<int32_t>(), hi_idx.data_ptr<int32_t>(),
                          w.data_ptr<float>(), edges.data_ptr<float>(), cur_stream());
+}
+
+// ------------------------------------------------------------------------------ fp32 MFMA GEMM
+// Operands are raw row-strided views of the given tensors' storage (see gemm_f32.hip):
+// kcontig: X(r, k) = x[r*ld + k] over r < rows, k < K; else X(r, k) = x[k*ld + r].
+static void check_operand(const Tensor& x, bool kc, int64_t ld, int64_t rows, int64_t K, const char* what) {
+  CHECK_DEV(x);
+  CHECK_DT(x, at::kFloat);
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && ld % 4 == 0, what, ": 16-B alignment");
+  TORCH_CHECK(kc ? (K % 4 == 0) : (rows % 4 == 0), what, ": the contiguous extent must be a multiple of 4");
+  const int64_t need = kc ? (rows - 1) * ld + K : (K - 1) * ld + rows;
+  TORCH_CHECK(x.numel() >= need && ld >= (kc ? K : rows), what, ": view exceeds the tensor");
+}
+
+void gemm_f32(const Tensor& A, bool a_kc, int64_t lda, const Tensor& B, bool b_kc, int64_t ldb, const Tensor& C,
+              int64_t ldc, int64_t M, int64_t N, int64_t K, int64_t splits) {
+  check_operand(A, a_kc, lda, M, K, "A");
+  check_operand(B, b_kc, ldb, N, K, "B");
+  CHECK_DEV(C);
+  CHECK_DT(C, at::kFloat);
+  TORCH_CHECK(C.numel() >= (M - 1) * ldc + N && ldc >= N, "C too small");
+  TORCH_CHECK(splits == 0 || splits == 1 || ldc == N, "split-K needs a dense C");
+  TORCH_CHECK(M < (1LL << 31) && N < (1LL << 31) && K < (1LL << 31), "GEMM dims must fit int32");
+  DevGuard guard(C.device());
+  grace::gemm_f32(A.data_ptr<float>(), a_kc, lda, B.data_ptr<float>(), b_kc, ldb, C.data_ptr<float>(), ldc, (int)M,
+                  (int)N, (int)K, (int)splits, cur_stream());
 }
 
 // ------------------------------------------------------------------------------ segment stats
@@ -913,6 +948,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sketch_encode", &sketch_encode);
   m.def("sketch_decode", &sketch_decode);
   m.def("quantile_select", &quantile_select);
+  m.def("gemm_f32", &gemm_f32);
   m.def("axpby", &axpby);
   m.def("scale_", &scale_);
   m.def("gather_segments", &gather_segments);

@@ -69,8 +69,8 @@ void sign_unpack(const ChunkTable& ct, const int64_t* seg_start, const int64_t* 
 void qsgd_quantize(const ChunkTable& ct, const float* x, const float* norms, float s, SeedArg seed, void* codes,
                    int code_bytes, float* resid, hipStream_t stream);
 void qsgd_aggregate(const ChunkTable& ct, const uint8_t* base, int64_t rank_stride, int64_t codes_off,
-                    int64_t norms_off, int code_bytes, int n_ranks, float s, float scale, float* out, bool accumulate,
-                    hipStream_t stream);
+                    int64_t norms_off, const float* shared_norms, int code_bytes, int n_ranks, float s, float scale,
+                    float* out, bool accumulate, hipStream_t stream);
 void tern_quantize(const ChunkTable& ct, const int64_t* seg_start, const int64_t* word_off, const float* x,
                    const float* clips, const float* scal, SeedArg seed, uint64_t* words, float* resid,
                    hipStream_t stream);
@@ -122,6 +122,12 @@ void quantile_select(const ChunkTable& ct, int n_seg, const float* x, int max_sl
                      const int32_t* nrank, int32_t* h0, int32_t* h, uint32_t* st_pfx, int32_t* st_rank, int32_t* slot,
                      uint32_t* uniq, int32_t* nuniq, int q, const int32_t* lo_idx, const int32_t* hi_idx,
                      const float* w, float* edges, hipStream_t stream);
+
+// ---------------------------------------------------------------- gemm_f32.hip
+// C[m][n] (+)= sum_k A(m,k) B(n,k) on the f32 MFMA; X(r,k) = x[r*ld+k] (kcontig) or x[k*ld+r];
+// splits > 1: split-K with f32 atomics into C (zeroed here; needs ldc == N)
+void gemm_f32(const float* A, bool a_kcontig, int64_t lda, const float* B, bool b_kcontig, int64_t ldb, float* C,
+              int64_t ldc, int M, int N, int K, int splits, hipStream_t stream);
 
 // ---------------------------------------------------------------- ef.hip (elementwise)
 void axpby(const float* x, const float* y, float* out, int64_t n, float a, float b, hipStream_t stream);

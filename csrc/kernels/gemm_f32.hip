@@ -1,0 +1,291 @@
+// fp32 GEMM on the CDNA4 f32-input matrix cores (v_mfma_f32_32x32x2_f32), for the convolutions of
+// the fp32 training step (the reference harness's precision: examples/torch/
+// pytorch_synthetic_benchmark.py:86 trains torchvision ResNet-50 in fp32).
+//
+//   C[m][n] (+)= sum_k A(m, k) * B(n, k)          exact f32 (an fmaf chain per output, no xf32)
+//
+// Each operand is either K-CONTIGUOUS (X(r, k) = x[r*ld + k]) or MN-CONTIGUOUS (X(r, k) =
+// x[k*ld + r]), which covers the three GEMMs of a 1x1 convolution over channels_last
+// activations [M = N*H*W, C]:
+//   forward        Y[M][Cout]  = X[M][Cin] . W[Cout][Cin]^T       A K-contig, B K-contig
+//   backward-data  dX[M][Cin]  = dY[M][Cout] . W[Cout][Cin]       A K-contig, B MN-contig
+//   weight grad    dW[Cout][Cin] = dY^T . X  (K = M, split-K)     A MN-contig, B MN-contig
+//
+// Tiling for 64-wide waves: a 256-thread workgroup owns a BM x BN tile (128x128, 128x64 or
+// 64x128) as a 2x2 grid of waves, each wave a (BM/2)x(BN/2) grid of 32x32 MFMA blocks with f32x16
+// accumulators.  K advances in BK = 32 slices through two LDS stages (one barrier per slice:
+// the next slice's global loads are in flight while the MFMAs consume the current one).
+//   LDS images:  K-contig operand  [r][k], rows of 36 floats: 16-B stores of the 16-B global
+//                loads, and ONE ds_read_b128 per lane per 8-k group (conflict-free: the 4-float
+//                pad spreads the 16 lanes of each b128 group over all 64 banks)
+//                MN-contig operand [k][r]: 16-B stores, four ds_read_b32 per 8-k group
+//                (32 consecutive r per half-wave: conflict-free)
+// The k order inside an 8-k group is permuted per lane half -- the MFMA slot k=h of step s takes
+// actual k = 8g + 4h + s -- identically for A and B, so each lane's 4 operands of a group are 4
+// consecutive k (the single 16-B read) and the sum is unchanged.
+// Blocks are remapped so each XCD (blocks are dealt round-robin to the 8 XCDs) walks a contiguous
+// run of tiles, n fastest: neighbouring tiles share A rows in that XCD's L2.
+// Split-K (weight gradients: K = N*H*W up to 10^5 against a small output) accumulates with f32
+// atomics into a zeroed C.
+#include <algorithm>
+
+#include "grace_common.h"
+#include "grace_kernels.h"
+
+namespace grace {
+namespace {
+
+constexpr int kGB = 256;  // threads per workgroup (4 waves)
+constexpr int BK = 32;    // k per LDS stage
+constexpr int LDK = 36;   // row pitch (floats) of a K-contig LDS image
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+struct GemmParams {
+  const float* A;
+  const float* B;
+  float* C;
+  int M, N, K;
+  int64_t lda, ldb, ldc;
+  int tiles_m, tiles_n, splits, k_per_split;
+  int atomic;
+  int c_vec;  // C rows 16-B aligned (ldc % 4 == 0, C 16-B aligned): float4 stores
+};
+
+template <int R, bool KC>
+struct Operand {
+  static constexpr int NV = R * BK / 4 / kGB;          // float4 per thread per stage
+  static constexpr int LDS = KC ? R * LDK : BK * R;    // floats per stage
+  static constexpr int TPR = R / 4;                    // MN-contig: threads per k row
+  float4 v[NV];
+
+  __device__ __forceinline__ void load(const float* __restrict__ x, int64_t ld, int r0, int rmax, int k0, int kmax) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      int r, k;
+      if constexpr (KC) {
+        r = r0 + threadIdx.x / 8 + 32 * i;
+        k = k0 + 4 * (threadIdx.x % 8);
+      } else {
+        r = r0 + 4 * (threadIdx.x % TPR);
+        k = k0 + threadIdx.x / TPR + (kGB / TPR) * i;
+      }
+      v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (r < rmax && k < kmax) {
+        v[i] = KC ? *reinterpret_cast<const float4*>(x + (int64_t)r * ld + k)
+                  : *reinterpret_cast<const float4*>(x + (int64_t)k * ld + r);
+      }
+    }
+  }
+  __device__ __forceinline__ void store(float* lds) const {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      if constexpr (KC) {
+        const int r = threadIdx.x / 8 + 32 * i, k = 4 * (threadIdx.x % 8);
+        *reinterpret_cast<float4*>(lds + r * LDK + k) = v[i];
+      } else {
+        const int r = 4 * (threadIdx.x % TPR), k = threadIdx.x / TPR + (kGB / TPR) * i;
+        *reinterpret_cast<float4*>(lds + k * R + r) = v[i];
+      }
+    }
+  }
+  // the lane's 4 operands of 8-k group g: k = 8g + 4h + s, s = 0..3, row r
+  __device__ __forceinline__ float4 frag(const float* lds, int r, int g, int h) const {
+    const int k = 8 * g + 4 * h;
+    if constexpr (KC) {
+      return *reinterpret_cast<const float4*>(lds + r * LDK + k);
+    } else {
+      return make_float4(lds[k * R + r], lds[(k + 1) * R + r], lds[(k + 2) * R + r], lds[(k + 3) * R + r]);
+    }
+  }
+};
+
+__device__ __forceinline__ float f4get(const float4& v, int s) { return s == 0 ? v.x : s == 1 ? v.y : s == 2 ? v.z : v.w; }
+
+template <int BM, int BN, bool AKC, bool BKC>
+__global__ __launch_bounds__(kGB, 2) void gemm_f32_kernel(GemmParams p) {
+  using OA = Operand<BM, AKC>;
+  using OB = Operand<BN, BKC>;
+  constexpr int STAGE = OA::LDS + OB::LDS;
+  constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 32, FN = WN / 32;
+  constexpr int CP = BN + 4;  // padded row pitch of the staged C tile (epilogue)
+  constexpr int LDS_TOTAL = 2 * STAGE > BM * CP ? 2 * STAGE : BM * CP;
+  __shared__ __align__(16) float lds[LDS_TOTAL];
+
+  int b = blockIdx.x;
+  const int nb = gridDim.x;
+  if ((nb & 7) == 0) b = (b & 7) * (nb >> 3) + (b >> 3);  // XCD-contiguous tile runs
+  const int split = b % p.splits;
+  const int t = b / p.splits;
+  const int tn = t % p.tiles_n, tm = t / p.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kb = split * p.k_per_split;
+  const int ke = min(p.K, kb + p.k_per_split);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = w & 1, wn = w >> 1;
+  const int lr = lane & 31, lh = lane >> 5;
+
+  f32x16 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  OA oa;
+  OB ob;
+  if (kb < ke) {
+    oa.load(p.A, p.lda, m0, p.M, kb, ke);
+    ob.load(p.B, p.ldb, n0, p.N, kb, ke);
+    oa.store(lds);
+    ob.store(lds + OA::LDS);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int k0 = kb; k0 < ke; k0 += BK) {
+    const bool more = k0 + BK < ke;
+    if (more) {
+      oa.load(p.A, p.lda, m0, p.M, k0 + BK, ke);
+      ob.load(p.B, p.ldb, n0, p.N, k0 + BK, ke);
+    }
+    const float* As = lds + cur * STAGE;
+    const float* Bs = As + OA::LDS;
+#pragma unroll
+    for (int g = 0; g < BK / 8; ++g) {
+      float4 fa[FM], fb[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) fa[i] = oa.frag(As, wm * WM + i * 32 + lr, g, lh);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) fb[j] = ob.frag(Bs, wn * WN + j * 32 + lr, g, lh);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(fa[i], s), f4get(fb[j], s), acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      oa.store(lds + (cur ^ 1) * STAGE);
+      ob.store(lds + (cur ^ 1) * STAGE + OA::LDS);
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // C/D map of the 32x32 f32 MFMA: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+  if (!p.atomic) {
+    // stage the tile through LDS (the k-loop's stages are free after its last barrier) and
+    // store 16 B per lane: BN/4 lanes cover a full C row segment
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          lds[(wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * CP + wn * WN + j * 32 + lr] = acc[i][j][r];
+    __syncthreads();
+    constexpr int TPR = BN / 4;
+    const int cq = threadIdx.x % TPR;
+    const int col = n0 + 4 * cq;
+    for (int rr = threadIdx.x / TPR; rr < BM; rr += kGB / TPR) {
+      const int row = m0 + rr;
+      if (row >= p.M) break;
+      const float4 v = *reinterpret_cast<const float4*>(lds + rr * CP + 4 * cq);
+      float* dst = p.C + (int64_t)row * p.ldc + col;
+      if (p.c_vec && col + 3 < p.N) {
+        *reinterpret_cast<float4*>(dst) = v;
+      } else {
+        if (col < p.N) dst[0] = v.x;
+        if (col + 1 < p.N) dst[1] = v.y;
+        if (col + 2 < p.N) dst[2] = v.z;
+        if (col + 3 < p.N) dst[3] = v.w;
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = n0 + wn * WN + j * 32 + lr;
+      if (col >= p.N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (row < p.M) {
+          float* dst = p.C + (int64_t)row * p.ldc + col;
+          atomicAdd(dst, acc[i][j][r]);
+        }
+      }
+    }
+}
+
+template <int BM, int BN, bool AKC, bool BKC>
+void launch_cfg(GemmParams p, hipStream_t stream) {
+  p.tiles_m = (p.M + BM - 1) / BM;
+  p.tiles_n = (p.N + BN - 1) / BN;
+  const int64_t blocks = (int64_t)p.tiles_m * p.tiles_n * p.splits;
+  gemm_f32_kernel<BM, BN, AKC, BKC><<<(unsigned)blocks, kGB, 0, stream>>>(p);
+}
+
+inline int64_t ntiles(int M, int N, int bm, int bn) { return (int64_t)((M + bm - 1) / bm) * ((N + bn - 1) / bn); }
+
+// tile shape: the largest of 128x128 / 128x64 / 64x128 / 64x64 that still gives >= 1.5 workgroups
+// per CU (small-M layers, e.g. the 7x7 stage at M = 1568, otherwise leave most of the chip idle)
+template <bool AKC, bool BKC>
+void launch_layout(GemmParams p, hipStream_t stream) {
+  const int64_t want = 384;
+  const int64_t t128 = ntiles(p.M, p.N, 128, 128) * p.splits;
+  const int64_t tm = ntiles(p.M, p.N, 128, 64) * p.splits, tn = ntiles(p.M, p.N, 64, 128) * p.splits;
+  if (p.M > 64 && p.N > 64 && t128 >= want)
+    launch_cfg<128, 128, AKC, BKC>(p, stream);
+  else if (p.M > 64 && tm >= want && (p.N <= 64 || tm >= tn))
+    launch_cfg<128, 64, AKC, BKC>(p, stream);
+  else if (p.N > 64 && tn >= want)
+    launch_cfg<64, 128, AKC, BKC>(p, stream);
+  else
+    launch_cfg<64, 64, AKC, BKC>(p, stream);
+}
+
+}  // namespace
+
+void gemm_f32(const float* A, bool a_kcontig, int64_t lda, const float* B, bool b_kcontig, int64_t ldb, float* C,
+              int64_t ldc, int M, int N, int K, int splits, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return;
+  GemmParams p{};
+  p.A = A;
+  p.B = B;
+  p.C = C;
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  p.lda = lda;
+  p.ldb = ldb;
+  p.ldc = ldc;
+  if (splits == 0) {  // auto: split K when even 64x64 tiles leave CUs idle (f32 atomics into C)
+    const int64_t tiles = ntiles(M, N, 64, 64);
+    splits = 1;
+    if (tiles < 256 && K >= 512 && ldc == N) splits = (int)std::min<int64_t>((384 + tiles - 1) / tiles, K / 256);
+  }
+  if (splits < 1) splits = 1;
+  int kps = (K + splits - 1) / splits;
+  kps = (kps + BK - 1) / BK * BK;
+  splits = K > 0 ? (K + kps - 1) / kps : 1;
+  p.splits = splits;
+  p.k_per_split = kps;
+  p.atomic = splits > 1;
+  p.c_vec = (reinterpret_cast<uintptr_t>(C) % 16 == 0) && (ldc % 4 == 0);
+  if (p.atomic) GRACE_HIP_CHECK(hipMemsetAsync(C, 0, sizeof(float) * (size_t)M * ldc, stream));  // ldc == N (host-checked)
+  if (a_kcontig && b_kcontig)
+    launch_layout<true, true>(p, stream);
+  else if (a_kcontig && !b_kcontig)
+    launch_layout<true, false>(p, stream);
+  else if (!a_kcontig && !b_kcontig)
+    launch_layout<false, false>(p, stream);
+  else
+    launch_layout<false, true>(p, stream);
+}
+
+}  // namespace grace

@@ -63,25 +63,77 @@ __global__ __launch_bounds__(kBlock) void qsgd_quant_kernel(ChunkTable ct, const
   }
 }
 
+// 4 codes of one rank as floats (one 4/8/16-B load)
 template <typename CodeT>
+__device__ __forceinline__ float4 load_codes4(const CodeT* p) {
+  if constexpr (sizeof(CodeT) == 1) {
+    const uint32_t u = *reinterpret_cast<const uint32_t*>(p);
+    return make_float4((float)(int8_t)(u & 0xff), (float)(int8_t)((u >> 8) & 0xff), (float)(int8_t)((u >> 16) & 0xff),
+                       (float)(int8_t)(u >> 24));
+  } else if constexpr (sizeof(CodeT) == 2) {
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    CodeT c[4];
+    *reinterpret_cast<uint2*>(c) = u;
+    return make_float4((float)c[0], (float)c[1], (float)c[2], (float)c[3]);
+  } else {
+    const int4 u = *reinterpret_cast<const int4*>(p);
+    return make_float4((float)u.x, (float)u.y, (float)u.z, (float)u.w);
+  }
+}
+
+// out[i] (+)= scale * sum_r norm_r[seg] / s * code_r[i].  `shared_norms` (shared-scale all-reduced
+// codes: one norm for every rank) replaces the per-rank norms of the payload rows.  VEC: the
+// codes and out are 16-B aligned at element 0 (host-checked), so the chunk body runs 4
+// elements per thread with one vector load per rank.
+template <typename CodeT, bool VEC>
 __global__ __launch_bounds__(kBlock) void qsgd_aggregate_kernel(ChunkTable ct, const uint8_t* __restrict__ base,
                                                                 int64_t rank_stride, int64_t codes_off,
-                                                                int64_t norms_off, int n_ranks, float inv_s,
-                                                                float scale, float* __restrict__ out,
-                                                                int accumulate) {
+                                                                int64_t norms_off, const float* __restrict__ shared_norms,
+                                                                int n_ranks, float inv_s, float scale,
+                                                                float* __restrict__ out, int accumulate) {
   const int c = blockIdx.x;
   const int sg = ct.seg[c];
   const int64_t b = ct.begin[c], e = ct.end[c];
-  for (int64_t i = b + threadIdx.x; i < e; i += kBlock) {
+  auto norm = [&](int r) {
+    return shared_norms ? shared_norms[sg]
+                        : reinterpret_cast<const float*>(base + (int64_t)r * rank_stride + norms_off)[sg];
+  };
+  auto scalar = [&](int64_t i) {
     float acc = 0.f;
     for (int r = 0; r < n_ranks; ++r) {
-      const uint8_t* rb = base + (int64_t)r * rank_stride;
-      const float nrm = reinterpret_cast<const float*>(rb + norms_off)[sg];
-      const CodeT q = reinterpret_cast<const CodeT*>(rb + codes_off)[i];
-      acc += nrm * inv_s * (float)q;
+      const CodeT q = reinterpret_cast<const CodeT*>(base + (int64_t)r * rank_stride + codes_off)[i];
+      acc += norm(r) * inv_s * (float)q;
     }
     acc *= scale;
     out[i] = accumulate ? out[i] + acc : acc;
+  };
+  if constexpr (!VEC) {
+    for (int64_t i = b + threadIdx.x; i < e; i += kBlock) scalar(i);
+  } else {
+    const int64_t a0 = ((b + 3) & ~(int64_t)3) < e ? ((b + 3) & ~(int64_t)3) : e;
+    const int64_t a1 = a0 + ((e - a0) & ~(int64_t)3);
+    for (int64_t i = b + threadIdx.x; i < a0; i += kBlock) scalar(i);
+    for (int64_t i = a1 + threadIdx.x; i < e; i += kBlock) scalar(i);
+    for (int64_t i = a0 + 4 * (int64_t)threadIdx.x; i < a1; i += 4 * kBlock) {
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int r = 0; r < n_ranks; ++r) {
+        const float f = norm(r) * inv_s;
+        const float4 q = load_codes4(reinterpret_cast<const CodeT*>(base + (int64_t)r * rank_stride + codes_off) + i);
+        acc.x += f * q.x;
+        acc.y += f * q.y;
+        acc.z += f * q.z;
+        acc.w += f * q.w;
+      }
+      float4 o = make_float4(acc.x * scale, acc.y * scale, acc.z * scale, acc.w * scale);
+      if (accumulate) {
+        const float4 p = *reinterpret_cast<const float4*>(out + i);
+        o.x += p.x;
+        o.y += p.y;
+        o.z += p.z;
+        o.w += p.w;
+      }
+      *reinterpret_cast<float4*>(out + i) = o;
+    }
   }
 }
 
@@ -308,14 +360,22 @@ void qsgd_quantize(const ChunkTable& ct, const float* x, const float* norms, flo
 }
 
 void qsgd_aggregate(const ChunkTable& ct, const uint8_t* base, int64_t rank_stride, int64_t codes_off,
-                    int64_t norms_off, int code_bytes, int n_ranks, float s, float scale, float* out, bool accumulate,
-                    hipStream_t stream) {
+                    int64_t norms_off, const float* shared_norms, int code_bytes, int n_ranks, float s, float scale,
+                    float* out, bool accumulate, hipStream_t stream) {
   if (ct.n_chunks == 0) return;
   const float inv_s = 1.f / s;
+  const bool vec = ((reinterpret_cast<uintptr_t>(base) + codes_off) % 16 == 0) && (rank_stride % 16 == 0) &&
+                   (reinterpret_cast<uintptr_t>(out) % 16 == 0);
   auto go = [&](auto* typed) {
     using T = std::remove_pointer_t<decltype(typed)>;
-    qsgd_aggregate_kernel<T><<<ct.n_chunks, kBlock, 0, stream>>>(ct, base, rank_stride, codes_off, norms_off, n_ranks,
-                                                                 inv_s, scale, out, accumulate);
+    if (vec)
+      qsgd_aggregate_kernel<T, true><<<ct.n_chunks, kBlock, 0, stream>>>(ct, base, rank_stride, codes_off, norms_off,
+                                                                         shared_norms, n_ranks, inv_s, scale, out,
+                                                                         accumulate);
+    else
+      qsgd_aggregate_kernel<T, false><<<ct.n_chunks, kBlock, 0, stream>>>(ct, base, rank_stride, codes_off, norms_off,
+                                                                          shared_norms, n_ranks, inv_s, scale, out,
+                                                                          accumulate);
   };
   if (code_bytes == 1) go((int8_t*)nullptr);
   else if (code_bytes == 2) go((int16_t*)nullptr);

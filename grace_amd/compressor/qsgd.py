@@ -87,20 +87,11 @@ class QSGDCompressor(BucketCompressor):
         return self._encode(self.flat(tensor), ctx, name, memory), ctx
 
     def _agg(self, per_rank, ctx, n_ranks, scale, norms=None):
-        from ..parallel.comm import PayloadBuilder
-
-        if norms is not None:  # shared-scale payloads carry no norm: re-attach ours
-            rows = []
-            for p in per_rank:
-                pb = PayloadBuilder(p[0].device, [(p[0].dtype, tuple(p[0].shape)), (torch.float32, (ctx.layout.n_seg,))])
-                pb.tensors[0].copy_(p[0])
-                pb.tensors[1].copy_(norms)
-                rows.append(pb.tensors)
-            per_rank = rows
         base, stride, offs = self.rows(per_rank)
         out = self.out_buffer(ctx, base.device)
-        Q.qsgd_aggregate(base, stride, offs[0], offs[1], per_rank[0][0].dtype, n_ranks, self.quantum_num, ctx.layout,
-                         out, scale)
+        # shared-scale payloads carry codes only: every row is decoded against the shared norms
+        Q.qsgd_aggregate(base, stride, offs[0], offs[1] if norms is None else 0, per_rank[0][0].dtype, n_ranks,
+                         self.quantum_num, ctx.layout, out, scale, shared_norms=norms)
         return self.finish(out, ctx)
 
     def decompress_aggregate_impl(self, per_rank, ctx, n_ranks, scale):

@@ -15,6 +15,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.bnact import BatchNormAct2d
+from ..ops.conv import Conv1x1F32
 
 
 def _conv3x3(cin, cout, stride=1):
@@ -22,6 +23,10 @@ def _conv3x3(cin, cout, stride=1):
 
 
 def _conv1x1(cin, cout, stride=1):
+    # stride-1 1x1 convs are plain GEMMs over channels_last activations: Conv1x1F32 can run them on
+    # the hand-written f32 MFMA GEMM (opt-in, GRACE_CONV_MFMA=1; nn.Conv2d state_dict either way)
+    if stride == 1:
+        return Conv1x1F32(cin, cout)
     return nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
 
 

@@ -71,19 +71,21 @@ def qsgd_quantize(x: torch.Tensor, layout: SegmentLayout, norms: torch.Tensor, s
 
 
 def qsgd_aggregate(base, rank_stride, codes_off, norms_off, code_dtype, n_ranks, s, layout, out, scale,
-                   accumulate=False):
+                   accumulate=False, shared_norms=None):
+    """Decode-sum of W payload rows.  ``shared_norms``: the shared-scale variant's all-reduced
+    norms, used for every row (the rows then carry codes only; ``norms_off`` is ignored)."""
     if _native.use_native(out):
         t = _tables(layout, out.device)
         esz = 3 if code_dtype == torch.float16 else torch.empty((), dtype=code_dtype).element_size()
         _native.lib().qsgd_aggregate(base, rank_stride, codes_off, norms_off, esz, n_ranks, float(s), scale, out,
-                                     accumulate, t["seg"], t["begin"], t["end"], layout.n_seg)
+                                     accumulate, t["seg"], t["begin"], t["end"], layout.n_seg, shared_norms)
         return
     esz = torch.empty((), dtype=code_dtype).element_size()
     acc = torch.zeros(layout.total, dtype=torch.float32, device=out.device)
     for r in range(n_ranks):
         row = base[r * rank_stride:]
         q = row[codes_off:codes_off + esz * layout.total].view(code_dtype).float()
-        nrm = row[norms_off:norms_off + 4 * layout.n_seg].view(torch.float32)
+        nrm = shared_norms if shared_norms is not None else row[norms_off:norms_off + 4 * layout.n_seg].view(torch.float32)
         acc += expand(nrm, layout) / s * q
     acc *= scale
     if accumulate:
