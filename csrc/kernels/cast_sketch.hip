@@ -68,47 +68,129 @@ __global__ __launch_bounds__(kBlock) void decode16_sum_kernel(const uint8_t* __r
   }
 }
 
-// bins: uint8 (q <= 256) or uint16; edges: [n_seg][q+1]; sums/counts: [n_seg][q] (zeroed)
+// first index >= b whose address is 16-B aligned for a float array (clamped to e)
+__device__ __forceinline__ int64_t vec4_begin(const void* x, int64_t b, int64_t e) {
+  const int64_t mis = (int64_t)((reinterpret_cast<uintptr_t>(x) >> 2) & 3);
+  const int64_t a = b + ((4 - ((b + mis) & 3)) & 3);
+  return a < e ? a : e;
+}
+
+__device__ __forceinline__ uint32_t sk_key(float v) {  // ascending order-preserving key
+  const uint32_t u = __float_as_uint(v);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// bins: uint8 (q <= 256) or uint16; edges: [n_seg][q+1]; sums/counts: [n_seg][q] (zeroed).
+// Bin = (#edges <= v) - 1 clamped to [0, q-1] (torch.searchsorted(right=True) - 1).  The edges
+// are staged in LDS with a 2048-entry table over the top 11 bits of the order-preserving key:
+// start[d] = #edges whose key is below bucket d, so an element only scans the few edges inside
+// its own bucket (quantile edges spread over the value range: ~1-2 per populated bucket) --
+// this pass is VALU-issue bound, a per-element binary search was 4x slower.  Bin codes are
+// stored 4 per 4/8-B store; per-bin sums / counts in per-wave LDS copies, folded once per
+// workgroup into one global atomic per bin.
 template <typename BinT>
 __global__ __launch_bounds__(kBlock) void sketch_encode_kernel(ChunkTable ct, const float* __restrict__ x,
                                                                const float* __restrict__ edges, int q,
                                                                BinT* __restrict__ bins, float* __restrict__ sums,
                                                                float* __restrict__ counts) {
-  __shared__ float le[kMaxQ + 1];
-  __shared__ float ls[kMaxQ];
-  __shared__ float lc[kMaxQ];
+  constexpr int NW = kBlock / kWave;
+  __shared__ float le[kMaxQ + 2];
+  __shared__ uint16_t start[2048];
+  __shared__ float ls[NW][kMaxQ];
+  __shared__ uint32_t lc[NW][kMaxQ];
   const int c = blockIdx.x;
   const int sg = ct.seg[c];
   const int64_t b = ct.begin[c], e = ct.end[c];
   const float* E = edges + (int64_t)sg * (q + 1);
   for (int i = threadIdx.x; i <= q; i += kBlock) le[i] = E[i];
-  for (int i = threadIdx.x; i < q; i += kBlock) {
-    ls[i] = 0.f;
-    lc[i] = 0.f;
+  if (threadIdx.x == 0) le[q + 1] = __int_as_float(0x7fc00000);  // NaN sentinel: `<= v` is false
+  for (int i = threadIdx.x; i < NW * q; i += kBlock) {
+    ls[i / q][i % q] = 0.f;
+    lc[i / q][i % q] = 0u;
   }
   __syncthreads();
-  for (int64_t i = b + threadIdx.x; i < e; i += kBlock) {
-    const float v = x[i];
-    // bin = (#edges <= v) - 1 clamped to [0, q-1]
-    int lo = 0, hi = q + 1;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (le[mid] <= v)
-        lo = mid + 1;
+  for (int d = threadIdx.x; d < 2048; d += kBlock) {  // lower bound of bucket d among the edge keys
+    const uint32_t lo = (uint32_t)d << 21;
+    int l = 0, r = q + 1;
+    while (l < r) {
+      const int m = (l + r) >> 1;
+      if (sk_key(le[m]) < lo)
+        l = m + 1;
       else
-        hi = mid;
+        r = m;
     }
-    int bin = lo - 1;
-    bin = bin < 0 ? 0 : (bin > q - 1 ? q - 1 : bin);
+    start[d] = (uint16_t)l;
+  }
+  __syncthreads();
+  float* wls = ls[wave_id()];
+  uint32_t* wlc = lc[wave_id()];
+  auto bin_of = [&](float v) {
+    int cnt = start[sk_key(v) >> 21];
+    while (le[cnt] <= v) ++cnt;  // stops at the NaN sentinel (index q + 1) at the latest
+    const int bb = cnt - 1;
+    return bb < 0 ? 0 : (bb > q - 1 ? q - 1 : bb);
+  };
+  auto one = [&](int64_t i) {
+    const float v = x[i];
+    const int bin = bin_of(v);
     bins[i] = (BinT)bin;
-    atomicAdd(&ls[bin], v);
-    atomicAdd(&lc[bin], 1.f);
+    atomicAdd(&wls[bin], v);
+    atomicAdd(&wlc[bin], 1u);
+  };
+  const int64_t a0 = vec4_begin(x, b, e);
+  const int64_t a1 = a0 + ((e - a0) & ~(int64_t)3);
+  for (int64_t i = b + threadIdx.x; i < a0; i += kBlock) one(i);
+  for (int64_t i = a1 + threadIdx.x; i < e; i += kBlock) one(i);
+  const bool vec_bins = ((reinterpret_cast<uintptr_t>(bins + a0)) % (4 * sizeof(BinT))) == 0;
+  // 8 x 16 B in flight per thread before any use: one vector at a time left every wave waiting
+  // on HBM latency with ~12 KB in flight per CU (this pass was latency bound, not LDS bound)
+  constexpr int U = 8;
+  for (int64_t i0 = a0 + 4 * (int64_t)threadIdx.x; i0 < a1; i0 += 4 * kBlock * U) {
+   float4 xs[U];
+#pragma unroll
+   for (int u = 0; u < U; ++u) {
+     const int64_t i = i0 + (int64_t)u * 4 * kBlock;
+     xs[u] = i < a1 ? *reinterpret_cast<const float4*>(x + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+   }
+#pragma unroll
+   for (int u = 0; u < U; ++u) {
+    const int64_t i = i0 + (int64_t)u * 4 * kBlock;
+    if (i >= a1) break;
+    const float4 v4 = xs[u];
+    const float v[4] = {v4.x, v4.y, v4.z, v4.w};
+    int bn[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bn[j] = bin_of(v[j]);
+      atomicAdd(&wls[bn[j]], v[j]);
+      atomicAdd(&wlc[bn[j]], 1u);
+    }
+    if (vec_bins) {
+      if constexpr (sizeof(BinT) == 1) {
+        *reinterpret_cast<uint32_t*>(bins + i) =
+            (uint32_t)bn[0] | ((uint32_t)bn[1] << 8) | ((uint32_t)bn[2] << 16) | ((uint32_t)bn[3] << 24);
+      } else {
+        *reinterpret_cast<uint2*>(bins + i) = make_uint2((uint32_t)bn[0] | ((uint32_t)bn[1] << 16),
+                                                         (uint32_t)bn[2] | ((uint32_t)bn[3] << 16));
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bins[i + j] = (BinT)bn[j];
+    }
+   }
   }
   __syncthreads();
   for (int i = threadIdx.x; i < q; i += kBlock) {
-    if (lc[i] != 0.f) {
-      atomicAdd(&sums[(int64_t)sg * q + i], ls[i]);
-      atomicAdd(&counts[(int64_t)sg * q + i], lc[i]);
+    float sv = 0.f;
+    uint32_t cv = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      sv += ls[w][i];
+      cv += lc[w][i];
+    }
+    if (cv != 0) {
+      atomicAdd(&sums[(int64_t)sg * q + i], sv);
+      atomicAdd(&counts[(int64_t)sg * q + i], (float)cv);
     }
   }
 }
@@ -121,7 +203,7 @@ __global__ __launch_bounds__(kBlock) void sketch_decode_kernel(ChunkTable ct, co
   const int c = blockIdx.x;
   const int sg = ct.seg[c];
   const int64_t b = ct.begin[c], e = ct.end[c];
-  for (int64_t i = b + threadIdx.x; i < e; i += kBlock) {
+  auto one = [&](int64_t i) {
     float acc = 0.f;
     for (int r = 0; r < n_ranks; ++r) {
       const uint8_t* rb = base + (int64_t)r * rank_stride;
@@ -129,6 +211,39 @@ __global__ __launch_bounds__(kBlock) void sketch_decode_kernel(ChunkTable ct, co
       acc += reinterpret_cast<const float*>(rb + means_off)[(int64_t)sg * q + bin];
     }
     out[i] = acc * scale;
+  };
+  const bool vec = (reinterpret_cast<uintptr_t>(base + bins_off) % (4 * sizeof(BinT))) == 0 &&
+                   (rank_stride % (4 * sizeof(BinT))) == 0;
+  const int64_t a0 = vec ? vec4_begin(out, b, e) : e;
+  const int64_t a1 = a0 + ((e - a0) & ~(int64_t)3);
+  for (int64_t i = b + threadIdx.x; i < a0; i += kBlock) one(i);
+  for (int64_t i = a1 + threadIdx.x; i < e; i += kBlock) one(i);
+  for (int64_t i = a0 + 4 * (int64_t)threadIdx.x; i < a1; i += 4 * kBlock) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 4
+    for (int r = 0; r < n_ranks; ++r) {
+      const uint8_t* rb = base + (int64_t)r * rank_stride;
+      const float* M = reinterpret_cast<const float*>(rb + means_off) + (int64_t)sg * q;
+      uint32_t bn[4];
+      if constexpr (sizeof(BinT) == 1) {
+        const uint32_t u = *reinterpret_cast<const uint32_t*>(rb + bins_off + i);
+        bn[0] = u & 0xff;
+        bn[1] = (u >> 8) & 0xff;
+        bn[2] = (u >> 16) & 0xff;
+        bn[3] = u >> 24;
+      } else {
+        const uint2 u = *reinterpret_cast<const uint2*>(rb + bins_off + 2 * i);
+        bn[0] = u.x & 0xffff;
+        bn[1] = u.x >> 16;
+        bn[2] = u.y & 0xffff;
+        bn[3] = u.y >> 16;
+      }
+      acc.x += M[bn[0]];
+      acc.y += M[bn[1]];
+      acc.z += M[bn[2]];
+      acc.w += M[bn[3]];
+    }
+    *reinterpret_cast<float4*>(out + i) = make_float4(acc.x * scale, acc.y * scale, acc.z * scale, acc.w * scale);
   }
 }
 

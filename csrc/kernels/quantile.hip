@@ -13,8 +13,9 @@
 //                      residual rank; targets with the same prefix share a SLOT (ranks are sorted,
 //                      so equal prefixes are adjacent); the histogram is left zeroed
 //   qsel_hist<D>       D = 1..3: one pass, the element's known prefix is looked up among the
-//                      segment's slots (binary search in LDS) and digit D is counted in that slot's
-//                      128-bin LDS histogram (only elements sharing a target's prefix count)
+//                      segment's slots (open-addressing LDS hash table) and digit D is
+//                      counted in that slot's 128-bin LDS histogram (only elements sharing a
+//                      target's prefix count)
 //   qsel_select<D>     per slot: wave scan of its 128 bins; targets refine prefix and rank; the
 //                      last digit resolves the full key = the exact value, and the same kernel
 //                      emits the interpolated edges (unfused mul/add: torch's rounding)
@@ -107,7 +108,13 @@ __global__ __launch_bounds__(kHBlock) void qsel_hist0_kernel(ChunkTable ct, cons
 }
 
 // Count digit D of every element whose known (32 - shift - bits)-bit prefix is one of the
-// segment's slot prefixes.  Dynamic LDS: [max_slots] prefixes + [max_slots][128] counts.
+// segment's slot prefixes.  Slots are found through an open-addressing LDS hash table (4096
+// entries for <= 256 slots: ~1 probe), so the common miss costs a hash, one LDS read and one
+// compare -- these passes are VALU-issue bound, not memory bound, so every instruction per
+// element counts.  Dynamic LDS: [max_slots] prefixes + [max_slots][128] counts.
+constexpr int kHash = 4096;
+__device__ __forceinline__ uint32_t qhash(uint32_t p) { return (p * 0x9E3779B1u) >> 20; }
+
 template <int D>
 __global__ __launch_bounds__(kHBlock) void qsel_hist_kernel(ChunkTable ct, const float* __restrict__ x, int max_slots,
                                                             const uint32_t* __restrict__ uniq,
@@ -116,30 +123,37 @@ __global__ __launch_bounds__(kHBlock) void qsel_hist_kernel(ChunkTable ct, const
   constexpr int shift = QDigit<D>::shift;
   constexpr int hi = shift + QDigit<D>::bits;  // the known prefix is key >> hi
   extern __shared__ __align__(16) uint32_t dyn[];
+  __shared__ int32_t tab[kHash];  // slot + 1, 0 = empty
   uint32_t* up = dyn;
   int32_t* lh = reinterpret_cast<int32_t*>(dyn + max_slots);
   const int seg = ct.seg[blockIdx.x];
   const int nu = nuniq[seg];
   if (nu == 0) return;  // block-uniform
   const uint32_t* su = uniq + (int64_t)seg * max_slots;
-  for (int i = threadIdx.x; i < nu; i += kHBlock) up[i] = su[i];
+  for (int i = threadIdx.x; i < kHash; i += kHBlock) tab[i] = 0;
   for (int i = threadIdx.x; i < nu * 128; i += kHBlock) lh[i] = 0;
   __syncthreads();
-  const uint32_t lo_p = up[0], hi_p = up[nu - 1];
+  for (int sl = threadIdx.x; sl < nu; sl += kHBlock) {
+    const uint32_t p = su[sl];
+    up[sl] = p;
+    uint32_t idx = qhash(p);
+    while (atomicCAS(&tab[idx], 0, sl + 1) != 0) idx = (idx + 1) & (kHash - 1);
+  }
+  __syncthreads();
   const int64_t b = ct.begin[blockIdx.x], e = ct.end[blockIdx.x];
   auto count = [&](float v) {
     const uint32_t k = ord_key(v);
     const uint32_t p = k >> hi;
-    if (p < lo_p || p > hi_p) return;
-    int l = 0, r = nu - 1;  // slot prefixes are strictly ascending
-    while (l < r) {
-      const int m = (l + r) >> 1;
-      if (up[m] < p)
-        l = m + 1;
-      else
-        r = m;
+    uint32_t idx = qhash(p);
+    int32_t ent = tab[idx];
+    while (ent != 0) {
+      if (up[ent - 1] == p) {
+        atomicAdd(&lh[(ent - 1) * 128 + ((k >> shift) & 127)], 1);
+        return;
+      }
+      idx = (idx + 1) & (kHash - 1);
+      ent = tab[idx];
     }
-    if (up[l] == p) atomicAdd(&lh[l * 128 + ((k >> shift) & 127)], 1);
   };
   const int64_t a0 = aligned_begin(x, b, e);
   const int64_t a1 = a0 + ((e - a0) & ~(int64_t)3);
@@ -147,19 +161,21 @@ __global__ __launch_bounds__(kHBlock) void qsel_hist_kernel(ChunkTable ct, const
   for (int64_t i = a1 + threadIdx.x; i < e; i += kHBlock) count(x[i]);
   const float4* x4 = reinterpret_cast<const float4*>(x + a0);
   const int64_t nv = (a1 - a0) >> 2;
-  for (int64_t v = threadIdx.x; v < nv; v += 2 * kHBlock) {
-    const float4 p = x4[v];
-    const bool two = v + kHBlock < nv;
-    const float4 q = two ? x4[v + kHBlock] : make_float4(0.f, 0.f, 0.f, 0.f);
-    count(p.x);
-    count(p.y);
-    count(p.z);
-    count(p.w);
-    if (two) {
-      count(q.x);
-      count(q.y);
-      count(q.z);
-      count(q.w);
+  constexpr int U = 8;  // 8 x 16 B in flight per thread before the (LDS-bound) counting
+  for (int64_t v0 = threadIdx.x; v0 < nv; v0 += (int64_t)U * kHBlock) {
+    float4 xs[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t v = v0 + (int64_t)u * kHBlock;
+      xs[u] = v < nv ? x4[v] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (v0 + (int64_t)u * kHBlock >= nv) break;
+      count(xs[u].x);
+      count(xs[u].y);
+      count(xs[u].z);
+      count(xs[u].w);
     }
   }
   __syncthreads();
@@ -289,9 +305,10 @@ void quantile_select(const ChunkTable& ct, int n_seg, const float* x, int max_sl
   static bool lds_attr = false;  // > 64 KB of dynamic LDS has to be opted into per kernel
   if (!lds_attr) {
     const int mx = 150 * 1024;
-    GRACE_HIP_CHECK(hipFuncSetAttribute((const void*)qsel_hist_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, mx));
-    GRACE_HIP_CHECK(hipFuncSetAttribute((const void*)qsel_hist_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, mx));
-    GRACE_HIP_CHECK(hipFuncSetAttribute((const void*)qsel_hist_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, mx));
+    const int mxh = 140 * 1024;  // + 16 KB static hash table <= 160 KB; max_slots <= 256 needs 132 KB
+    GRACE_HIP_CHECK(hipFuncSetAttribute((const void*)qsel_hist_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, mxh));
+    GRACE_HIP_CHECK(hipFuncSetAttribute((const void*)qsel_hist_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, mxh));
+    GRACE_HIP_CHECK(hipFuncSetAttribute((const void*)qsel_hist_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, mxh));
     GRACE_HIP_CHECK(hipFuncSetAttribute((const void*)qsel_select_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, mx));
     GRACE_HIP_CHECK(hipFuncSetAttribute((const void*)qsel_select_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, mx));
     GRACE_HIP_CHECK(hipFuncSetAttribute((const void*)qsel_select_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, mx));

@@ -51,6 +51,7 @@ def segmented_quantile_edges(x: torch.Tensor, lay, q: int) -> torch.Tensor:
 
 
 _QSEL_CHUNK = 65536  # elements per workgroup of the selection passes (LDS setup amortised)
+_CODEC_CHUNK = 32768  # encode / decode: per-workgroup LDS bin tables amortised over 32K elements
 
 
 def _qsel_tables(lay, q: int, dev: torch.device):
@@ -124,7 +125,7 @@ class SketchCompressor(BucketCompressor):
                 edges = segmented_quantile_edges(x, lay, q)
             sums = torch.zeros(lay.n_seg * q, device=x.device)
             cnts = torch.zeros(lay.n_seg * q, device=x.device)
-            t = lay.device_tables(x.device)
+            t = lay.device_tables(x.device, _CODEC_CHUNK)
             _native.lib().sketch_encode(x, edges, q, bins, sums, cnts, t["seg"], t["begin"], t["end"])
             torch.where(cnts > 0, sums / cnts.clamp_min(1), torch.zeros_like(sums), out=means)
             return [bins, means], ctx
@@ -144,7 +145,7 @@ class SketchCompressor(BucketCompressor):
         if _native.use_native(per_rank[0][0]):
             base, stride, offs = self.rows(per_rank)
             out = self.out_buffer(ctx, base.device)
-            t = lay.device_tables(base.device)
+            t = lay.device_tables(base.device, _CODEC_CHUNK)
             _native.lib().sketch_decode(base, stride, offs[0], offs[1], q, per_rank[0][0].element_size(), n_ranks,
                                         scale, out, t["seg"], t["begin"], t["end"], lay.n_seg)
             return self.finish(out, ctx)
