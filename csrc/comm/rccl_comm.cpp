@@ -193,6 +193,27 @@ class RcclComm {
     return end();
   }
 
+  // out[p] <- chunk `rank` of rank p's in (equal chunks of numel / world): one send and one recv
+  // per peer in one group -- on a fully connected xGMI node every pair has its own link
+  std::shared_ptr<Work> all_to_all(const Tensor& out, const Tensor& in) {
+    std::shared_lock<std::shared_timed_mutex> lk(mu_);
+    check(out);
+    check(in);
+    TORCH_CHECK(out.numel() == in.numel() && in.numel() % world_ == 0, "all_to_all: equal sizes, divisible by W");
+    TORCH_CHECK(out.scalar_type() == in.scalar_type(), "dtype mismatch");
+    const int64_t chunk = in.numel() / world_;
+    const size_t esz = in.element_size();
+    auto dt = nccl_dtype(in);
+    begin();
+    RCCL_CHECK(ncclGroupStart());
+    for (int p = 0; p < world_; ++p) {
+      RCCL_CHECK(ncclSend(static_cast<const char*>(in.data_ptr()) + p * chunk * esz, chunk, dt, p, comm_, s_));
+      RCCL_CHECK(ncclRecv(static_cast<char*>(out.data_ptr()) + p * chunk * esz, chunk, dt, p, comm_, s_));
+    }
+    RCCL_CHECK(ncclGroupEnd());
+    return end();
+  }
+
   // Batched: all_gathers of (out_i, in_i) pairs and in-place sum all_reduces in ONE group.
   std::shared_ptr<Work> group(const std::vector<std::pair<Tensor, Tensor>>& gathers,
                               const std::vector<Tensor>& reduces) {
@@ -310,6 +331,7 @@ void bind(py::module& m) {
       .def("broadcast", &RcclComm::broadcast)
       .def("reduce_scatter", &RcclComm::reduce_scatter, py::arg("out"), py::arg("inp"), py::arg("op") = "sum")
       .def("group", &RcclComm::group)
+      .def("all_to_all", &RcclComm::all_to_all)
       .def("check_async_error", &RcclComm::check_async_error)
       .def_property("inline", &RcclComm::is_inline, &RcclComm::set_inline)
       .def("abort", &RcclComm::abort);

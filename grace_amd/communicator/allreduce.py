@@ -39,6 +39,9 @@ class Allreduce(Communicator):
     def async_send(self, tensors, name):
         if self._via_allgather:
             return ("ag", allgather_send(self.comm, self.compressor, tensors, self.world_size))
+        rs = getattr(self.compressor, "rs_mode", None)
+        if rs is not None and rs(self.world_size):  # QSGD: int8 all-to-all + int16 all-gather
+            return ("rs", self.compressor.rs_send(self.comm, tensors[0]))
         tensors = list(tensors)
         works = []
         by_dtype = OrderedDict()
@@ -57,6 +60,9 @@ class Allreduce(Communicator):
 
     def wait_comm(self, handles):
         kind, h = handles
+        if kind == "rs":
+            h[1].wait()
+            return
         if kind == "ag":
             if h[3] is not None:
                 h[3].wait()
@@ -68,6 +74,8 @@ class Allreduce(Communicator):
         kind, handles = handles
         if kind == "ag":
             return allgather_recv(handles, self.compressor, ctx, self.world_size)
+        if kind == "rs":
+            return self.compressor.rs_receive(self.comm, handles, ctx, self.world_size)
         tensors, works = handles
         for w, flat, idxs in works:
             w.wait()

@@ -11,10 +11,17 @@ s >= 128 (survey 2.14 #12).  Aggregation decodes all W ranks in one pass.
 
 Allreduce (BASELINE "QSGD 8-bit Allreduce"): *shared-scale* variant -- the per-segment norms
 are MAX-all-reduced first (one tiny collective for the whole bucket), every rank quantizes
-against the same norm, so integer levels are summable and RCCL sums them directly.  The code
-is the narrowest type whose SUM stays exact and that RCCL can reduce: int8 when s*W <= 127
-(e.g. s=15 at W=8), fp16 integer levels when s*W <= 2048 (the BASELINE s=127 config at W=2..8;
-RCCL has no int16 reduction), int32 beyond.
+against the same norm, so integer levels are summable.  Two wire formats:
+
+* reduce-scatter in the compressed domain (default when W > 1, s <= 127 and s*W <= 32767): the
+  int8 codes go through ONE all-to-all (chunk p to rank p: each pair of GPUs on its own xGMI
+  link), each rank sums its chunk's W code rows into exact int16 level sums, and ONE all-gather
+  returns the int16 sums.  Bytes received per rank: (W-1)/W * (1 + 2) B per element, against
+  (W-1)/W * 2 * 2 B for a ring all-reduce of 16-bit codes -- and the 8-bit codes stay 8-bit on
+  the wire at any W (the reference's int8 payload, qsgd.py:27).
+* plain all-reduce of the codes in the narrowest type whose SUM stays exact and that RCCL can
+  reduce: int8 when s*W <= 127 (e.g. s=15 at W=8), fp16 integer levels when s*W <= 2048 (RCCL
+  has no int16 reduction), int32 beyond.
 """
 from __future__ import annotations
 
@@ -27,11 +34,18 @@ from ._base import BucketCompressor
 
 
 class QSGDCompressor(BucketCompressor):
-    def __init__(self, quantum_num: int = 127, shared_scale: bool = False):
+    def __init__(self, quantum_num: int = 127, shared_scale: bool = False, reduce_scatter: bool = True):
         super().__init__()
         self.quantum_num = int(quantum_num)
         self.shared_scale = shared_scale
+        self.reduce_scatter = bool(reduce_scatter)
         self.comm = None
+
+    def rs_mode(self, world_size: int) -> bool:
+        """Compressed-domain reduce-scatter + all-gather (int8 codes out, int16 sums back)."""
+        return (self.shared_scale and self.reduce_scatter and world_size > 1 and self.quantum_num <= 127
+                and self.quantum_num * world_size <= 32767 and self.comm is not None
+                and hasattr(self.comm, "all_to_all"))
 
     @property
     def allreduce_compatible(self):
@@ -56,8 +70,11 @@ class QSGDCompressor(BucketCompressor):
     def _encode(self, g, ctx, name, memory=None):
         lay = ctx.layout
         W = self.comm.world_size if (self.shared_scale and self.comm is not None) else 1
-        cdt = self.code_dtype(W)
-        codes, norms = self.payload(g.device, [(cdt, (lay.total,)), (torch.float32, (lay.n_seg,))])
+        rs = self.rs_mode(W)
+        cdt = torch.int8 if rs else self.code_dtype(W)
+        # reduce-scatter mode: codes padded to W equal 16-B chunks (the pad is never decoded)
+        ncode = -(-lay.total // (16 * W)) * 16 * W if rs else lay.total
+        codes, norms = self.payload(g.device, [(cdt, (ncode,)), (torch.float32, (lay.n_seg,))])
         r = None
         if memory is None:
             stats = S.segment_stats(g, lay)
@@ -70,11 +87,28 @@ class QSGDCompressor(BucketCompressor):
         if self.shared_scale and W > 1:
             self.comm.all_reduce(norms, op="max")
         seed, step = self.next_rng(name, x.device)
-        Q.qsgd_quantize(x, lay, norms, self.quantum_num, seed, codes, resid=r, step=step)
+        Q.qsgd_quantize(x, lay, norms, self.quantum_num, seed, codes[:lay.total], resid=r, step=step)
         if self.shared_scale:
             ctx.extra["norms"] = norms
             return [codes]
         return [codes, norms]
+
+    # ---------------------------------------------------------------- reduce-scatter wire format
+    def rs_send(self, comm, codes):
+        """Phase 1: all-to-all of the int8 codes (async)."""
+        recv = torch.empty_like(codes)
+        return recv, comm.all_to_all(recv, codes, async_op=True)
+
+    def rs_receive(self, comm, handle, ctx, world_size):
+        """Phase 2: exact int16 sums of this rank's chunk, all-gathered; one decode pass."""
+        recv, work = handle
+        work.wait()
+        W = world_size
+        part = recv.view(W, -1).sum(0, dtype=torch.int16)
+        full = torch.empty(recv.numel(), dtype=torch.int16, device=recv.device)
+        comm.all_gather_into(full.view(torch.uint8), part.view(torch.uint8))  # bytes: no int16 collective needed
+        scale = 1.0 / W if self.average else 1.0
+        return self._agg([[full]], ctx, 1, scale, ctx.extra.get("norms"))
 
     def compress(self, tensor, name):
         ctx = self.ctx(tensor, name)

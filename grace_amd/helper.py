@@ -29,7 +29,7 @@ COMPRESSORS: Dict[str, Callable[[Dict[str, Any]], Any]] = {
     "randomk": lambda p: Z.RandomKCompressor(p.get("compress_ratio", 0.01)),
     "threshold": lambda p: Z.ThresholdCompressor(p.get("threshold", 0.01), capacity=p.get("capacity", 1.0)),
     "dgc": lambda p: Z.DgcCompressor(p.get("compress_ratio", 0.01), capacity=p.get("capacity", 2.0)),
-    "qsgd": lambda p: Z.QSGDCompressor(p.get("quantum_num", 127)),
+    "qsgd": lambda p: Z.QSGDCompressor(p.get("quantum_num", 127), reduce_scatter=p.get("qsgd_reduce_scatter", True)),
     "terngrad": lambda p: Z.TernGradCompressor(),
     "signsgd": lambda p: Z.SignSGDCompressor(),
     "signum": lambda p: Z.SignumCompressor(p.get("momentum", 0.9)),

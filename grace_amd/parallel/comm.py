@@ -57,6 +57,10 @@ class Comm:
     def broadcast(self, t: torch.Tensor, src: int, async_op: bool = False) -> Work:
         raise NotImplementedError
 
+    def all_to_all(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False) -> Work:
+        """Chunk p of ``out`` <- chunk ``rank`` of rank p's ``inp`` (W equal chunks)."""
+        raise NotImplementedError
+
     def barrier(self) -> None:
         pass
 
@@ -75,6 +79,10 @@ class LocalComm(Comm):
         return Work()
 
     def broadcast(self, t, src, async_op=False):
+        return Work()
+
+    def all_to_all(self, out, inp, async_op=False):
+        out.view(-1).copy_(inp.view(-1))
         return Work()
 
 
@@ -107,6 +115,15 @@ class TorchComm(Comm):
     def broadcast(self, t, src, async_op=False):
         gsrc = dist.get_global_rank(self.group, src) if self.group is not None else src
         w = dist.broadcast(t, gsrc, group=self.group, async_op=async_op)
+        return Work([w] if async_op else [])
+
+    def all_to_all(self, out, inp, async_op=False):
+        if self._gloo and out.is_cuda:  # gloo's all-to-all is host-only: stage through the CPU
+            o = torch.empty(out.numel(), dtype=out.dtype)
+            dist.all_to_all_single(o, inp.reshape(-1).cpu(), group=self.group)
+            out.view(-1).copy_(o)
+            return Work()
+        w = dist.all_to_all_single(out.view(-1), inp.view(-1), group=self.group, async_op=async_op)
         return Work([w] if async_op else [])
 
     def barrier(self):
@@ -171,6 +188,10 @@ class GroupedComm(Comm):
     def broadcast(self, t, src, async_op=False):
         self.flush()
         return self.inner.broadcast(t, src, async_op)
+
+    def all_to_all(self, out, inp, async_op=False):
+        self.flush()
+        return self.inner.all_to_all(out, inp, async_op)
 
     def barrier(self):
         self.flush()

@@ -73,6 +73,12 @@ class LoopbackComm(Comm):
         out.view(-1).copy_(red[self.rank])
         return Work()
 
+    def all_to_all(self, out, inp, async_op=False):
+        ts = self.group._exchange(self.rank, inp.reshape(-1))
+        W = self.world_size
+        out.view(W, -1).copy_(torch.stack([x.to(out.device).view(W, -1)[self.rank] for x in ts]))
+        return Work()
+
     def barrier(self):
         self.group._barrier.wait()
 

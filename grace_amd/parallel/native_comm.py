@@ -89,6 +89,10 @@ class RcclComm(_comm.Comm):
         self._mark(t)
         return self._ret(self._c.broadcast(t, src), async_op)
 
+    def all_to_all(self, out, inp, async_op=False):
+        self._mark(out, inp)
+        return self._ret(self._c.all_to_all(out.view(-1), inp.view(-1)), async_op)
+
     def reduce_scatter(self, out, inp, op="sum", async_op=False):
         self._mark(out, inp)
         return self._ret(self._c.reduce_scatter(out, inp, op), async_op)

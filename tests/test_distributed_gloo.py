@@ -112,9 +112,13 @@ def _body(rank, world, device="cpu"):
         out = run({"compressor": "qsgd", "quantum_num": 15, "communicator": comm}, "q")
         bound = max(t.norm() for t in xs) / 15
         assert (out - mean).abs().max() <= bound * (1 + 1e-4)
-    # s = 127 (BASELINE BERT config): s*W > 127 -> fp16 integer-level codes on the wire
+    # s = 127 (BASELINE BERT config): int8 codes all-to-all + int16 level sums all-gathered
+    # (compressed-domain reduce-scatter), bit-identical to the all-reduce of fp16 integer levels
     out = run({"compressor": "qsgd", "quantum_num": 127, "communicator": "allreduce"}, "q127")
     assert (out - mean).abs().max() <= max(t.norm() for t in xs) / 127 * (1 + 1e-4)
+    ref = run({"compressor": "qsgd", "quantum_num": 127, "communicator": "allreduce",
+               "qsgd_reduce_scatter": False}, "q127")
+    assert torch.equal(out, ref)
     # TernGrad / Natural / U8bit / Sketch / INCEPTIONN / Adaq / DGC: the W-rank result equals the
     # rank-ordered average of every rank's OWN decode, replayed locally on each rank with a codec
     # object carrying that rank's id (same per-(name, rank, step) seeds as the real rank used)
