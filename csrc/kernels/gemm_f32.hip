@@ -13,9 +13,10 @@
 //
 // Tiling for 64-wide waves: a 256-thread workgroup owns a BM x BN tile (128x128, 128x64 or
 // 64x128) as a 2x2 grid of waves, each wave a (BM/2)x(BN/2) grid of 32x32 MFMA blocks with f32x16
-// accumulators.  K advances in BK = 32 slices through two LDS stages (one barrier per slice:
-// the next slice's global loads are in flight while the MFMAs consume the current one).
-//   LDS images:  K-contig operand  [r][k], rows of 36 floats: 16-B stores of the 16-B global
+// accumulators.  K advances in BK = 16 slices through two LDS stages (one barrier per slice:
+// the next slice's global loads are in flight while the MFMAs consume the current one; 20 KB
+// stages leave room for 3 workgroups per CU).
+//   LDS images:  K-contig operand  [r][k], rows of 20 floats: 16-B stores of the 16-B global
 //                loads, and ONE ds_read_b128 per lane per 8-k group (conflict-free: the 4-float
 //                pad spreads the 16 lanes of each b128 group over all 64 banks)
 //                MN-contig operand [k][r]: 16-B stores, four ds_read_b32 per 8-k group
@@ -36,8 +37,8 @@ namespace grace {
 namespace {
 
 constexpr int kGB = 256;  // threads per workgroup (4 waves)
-constexpr int BK = 32;    // k per LDS stage
-constexpr int LDK = 36;   // row pitch (floats) of a K-contig LDS image
+constexpr int BK = 16;    // k per LDS stage (2 x 8-k groups): 20 KB stages -> 3 workgroups per CU
+constexpr int LDK = 20;   // row pitch (floats) of a K-contig LDS image (conflict-free b128 reads)
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -64,8 +65,8 @@ struct Operand {
     for (int i = 0; i < NV; ++i) {
       int r, k;
       if constexpr (KC) {
-        r = r0 + threadIdx.x / 8 + 32 * i;
-        k = k0 + 4 * (threadIdx.x % 8);
+        r = r0 + threadIdx.x / (BK / 4) + (kGB / (BK / 4)) * i;
+        k = k0 + 4 * (threadIdx.x % (BK / 4));
       } else {
         r = r0 + 4 * (threadIdx.x % TPR);
         k = k0 + threadIdx.x / TPR + (kGB / TPR) * i;
@@ -81,7 +82,7 @@ struct Operand {
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       if constexpr (KC) {
-        const int r = threadIdx.x / 8 + 32 * i, k = 4 * (threadIdx.x % 8);
+        const int r = threadIdx.x / (BK / 4) + (kGB / (BK / 4)) * i, k = 4 * (threadIdx.x % (BK / 4));
         *reinterpret_cast<float4*>(lds + r * LDK + k) = v[i];
       } else {
         const int r = 4 * (threadIdx.x % TPR), k = threadIdx.x / TPR + (kGB / TPR) * i;
@@ -103,13 +104,14 @@ struct Operand {
 __device__ __forceinline__ float f4get(const float4& v, int s) { return s == 0 ? v.x : s == 1 ? v.y : s == 2 ? v.z : v.w; }
 
 template <int BM, int BN, bool AKC, bool BKC>
-__global__ __launch_bounds__(kGB, 2) void gemm_f32_kernel(GemmParams p) {
+__global__ __launch_bounds__(kGB, 3) void gemm_f32_kernel(GemmParams p) {
   using OA = Operand<BM, AKC>;
   using OB = Operand<BN, BKC>;
   constexpr int STAGE = OA::LDS + OB::LDS;
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 32, FN = WN / 32;
-  constexpr int CP = BN + 4;  // padded row pitch of the staged C tile (epilogue)
-  constexpr int LDS_TOTAL = 2 * STAGE > BM * CP ? 2 * STAGE : BM * CP;
+  constexpr int CP = WN + 4;                  // padded row pitch of a wave's staged 32-row C slab
+  constexpr int CSTAGE = 4 * 32 * CP;        // the 4 waves' slabs (epilogue)
+  constexpr int LDS_TOTAL = 2 * STAGE > CSTAGE ? 2 * STAGE : CSTAGE;
   __shared__ __align__(16) float lds[LDS_TOTAL];
 
   int b = blockIdx.x;
@@ -176,32 +178,41 @@ __global__ __launch_bounds__(kGB, 2) void gemm_f32_kernel(GemmParams p) {
 
   // C/D map of the 32x32 f32 MFMA: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
   if (!p.atomic) {
-    // stage the tile through LDS (the k-loop's stages are free after its last barrier) and
-    // store 16 B per lane: BN/4 lanes cover a full C row segment
+    // each wave stages its 32-row slabs through its own LDS region (the k-loop's stages are free
+    // after the last barrier) and stores 16 B per lane: WN/4 lanes cover a row segment
+    float* slab = lds + w * 32 * CP;
+    constexpr int LPR = WN / 4;          // lanes per staged row
+    constexpr int RPI = kWave / LPR;     // rows per wave instruction
+    const int cq = lane % LPR;
+    const int col = n0 + wn * WN + 4 * cq;
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
+    for (int i = 0; i < FM; ++i) {
 #pragma unroll
       for (int j = 0; j < FN; ++j)
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          lds[(wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * CP + wn * WN + j * 32 + lr] = acc[i][j][r];
-    __syncthreads();
-    constexpr int TPR = BN / 4;
-    const int cq = threadIdx.x % TPR;
-    const int col = n0 + 4 * cq;
-    for (int rr = threadIdx.x / TPR; rr < BM; rr += kGB / TPR) {
-      const int row = m0 + rr;
-      if (row >= p.M) break;
-      const float4 v = *reinterpret_cast<const float4*>(lds + rr * CP + 4 * cq);
-      float* dst = p.C + (int64_t)row * p.ldc + col;
-      if (p.c_vec && col + 3 < p.N) {
-        *reinterpret_cast<float4*>(dst) = v;
-      } else {
-        if (col < p.N) dst[0] = v.x;
-        if (col + 1 < p.N) dst[1] = v.y;
-        if (col + 2 < p.N) dst[2] = v.z;
-        if (col + 3 < p.N) dst[3] = v.w;
+        for (int r = 0; r < 16; ++r) slab[((r & 3) + 8 * (r >> 2) + 4 * lh) * CP + j * 32 + lr] = acc[i][j][r];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int rr = lane / LPR; rr < 32; rr += RPI) {
+        const int row = m0 + wm * WM + i * 32 + rr;
+        if (row < p.M) {
+          const float4 v = *reinterpret_cast<const float4*>(slab + rr * CP + 4 * cq);
+          float* dst = p.C + (int64_t)row * p.ldc + col;
+          if (p.c_vec && col + 3 < p.N) {
+            *reinterpret_cast<float4*>(dst) = v;
+          } else {
+            if (col < p.N) dst[0] = v.x;
+            if (col + 1 < p.N) dst[1] = v.y;
+            if (col + 2 < p.N) dst[2] = v.z;
+            if (col + 3 < p.N) dst[3] = v.w;
+          }
+        }
       }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     return;
   }
