@@ -13,10 +13,9 @@
 //
 // Tiling for 64-wide waves: a 256-thread workgroup owns a BM x BN tile (128x128, 128x64 or
 // 64x128) as a 2x2 grid of waves, each wave a (BM/2)x(BN/2) grid of 32x32 MFMA blocks with f32x16
-// accumulators.  K advances in BK = 16 slices through two LDS stages (one barrier per slice:
-// the next slice's global loads are in flight while the MFMAs consume the current one; 20 KB
-// stages leave room for 3 workgroups per CU).
-//   LDS images:  K-contig operand  [r][k], rows of 20 floats: 16-B stores of the 16-B global
+// accumulators.  K advances in BK = 32 slices through two LDS stages (one barrier per slice:
+// the next slice's global loads are in flight while the MFMAs consume the current one).
+//   LDS images:  K-contig operand  [r][k], rows of 36 floats: 16-B stores of the 16-B global
 //                loads, and ONE ds_read_b128 per lane per 8-k group (conflict-free: the 4-float
 //                pad spreads the 16 lanes of each b128 group over all 64 banks)
 //                MN-contig operand [k][r]: 16-B stores, four ds_read_b32 per 8-k group
@@ -37,8 +36,8 @@ namespace grace {
 namespace {
 
 constexpr int kGB = 256;  // threads per workgroup (4 waves)
-constexpr int BK = 16;    // k per LDS stage (2 x 8-k groups): 20 KB stages -> 3 workgroups per CU
-constexpr int LDK = 20;   // row pitch (floats) of a K-contig LDS image (conflict-free b128 reads)
+constexpr int BK = 32;    // k per LDS stage (4 x 8-k groups; BK = 16 with 4 workgroups per CU measured slower)
+constexpr int LDK = 36;   // row pitch (floats) of a K-contig LDS image (conflict-free b128 reads)
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -104,7 +103,7 @@ struct Operand {
 __device__ __forceinline__ float f4get(const float4& v, int s) { return s == 0 ? v.x : s == 1 ? v.y : s == 2 ? v.z : v.w; }
 
 template <int BM, int BN, bool AKC, bool BKC>
-__global__ __launch_bounds__(kGB, 3) void gemm_f32_kernel(GemmParams p) {
+__global__ __launch_bounds__(kGB, 2) void gemm_f32_kernel(GemmParams p) {
   using OA = Operand<BM, AKC>;
   using OB = Operand<BN, BKC>;
   constexpr int STAGE = OA::LDS + OB::LDS;
