@@ -53,6 +53,12 @@ def test_native_rccl_comm_single_rank(nccl_group):
     c.broadcast(t, 0).wait()
     torch.cuda.synchronize()
     torch.testing.assert_close(out, t)
+    # all-to-all (send/recv group; the QSGD reduce-scatter wire format): identity at W = 1, int8
+    codes = torch.arange(-64, 64, dtype=torch.int8, device="cuda")
+    recv = torch.empty_like(codes)
+    c.all_to_all(recv, codes, async_op=True).wait()
+    torch.cuda.synchronize()
+    assert torch.equal(recv, codes)
     assert c.world_size == 1
     c.check()
 
