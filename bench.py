@@ -203,7 +203,8 @@ def main():
     run = step
     try:
         if mode == "full":
-            run = GraphedStep(step, warmup=max(3, args.warmup // 2))
+            run = GraphedStep(step, warmup=max(3, args.warmup // 2),
+                              capture_error_mode="thread_local" if world > 1 else "global")
             graph_note = "full"
         elif mode == "compute":
             with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp, cache_enabled=False):

@@ -57,9 +57,15 @@ class GraphedStep:
 
     ``fn`` must perform a full training step on static buffers (zero_grad, forward, backward,
     optimizer.step) and return the loss tensor.
+
+    ``capture_error_mode`` is passed to ``torch.cuda.graph``.  With collectives inside the
+    step (W > 1) use ``"thread_local"``: RCCL's proxy thread makes HIP calls of its own while
+    the training thread captures, and under the default ``"global"`` mode such a call from
+    ANY thread invalidates the capture.
     """
 
-    def __init__(self, fn: Callable[[], torch.Tensor], warmup: int = 3, pool=None):
+    def __init__(self, fn: Callable[[], torch.Tensor], warmup: int = 3, pool=None,
+                 capture_error_mode: str = "global"):
         self.fn = fn
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
@@ -69,7 +75,7 @@ class GraphedStep:
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, pool=pool):
+        with torch.cuda.graph(self.graph, pool=pool, capture_error_mode=capture_error_mode):
             self.loss = fn()
         torch.cuda.synchronize()
 

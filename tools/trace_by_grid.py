@@ -17,10 +17,9 @@ def main():
     a = ap.parse_args()
     acc = collections.defaultdict(list)
     for r in csv.DictReader(open(a.csv)):
-        k = r["Kernel_Name"]
+        k = re.sub(r"\(.*", "", r["Kernel_Name"].replace("(anonymous namespace)::", ""))[:60]
         if a.match not in k:
             continue
-        k = re.sub(r"\(.*", "", k.replace("(anonymous namespace)::", ""))[:60]
         grid = (r.get("Grid_Size_X", "?"), r.get("Grid_Size_Y", "?"))
         acc[(k, grid)].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     rows = sorted(acc.items(), key=lambda kv: -sum(kv[1]))
