@@ -80,12 +80,13 @@ def parse():
                     help="process group: nccl = RCCL over xGMI (one GPU per rank); gloo = host transport, lets "
                          "several ranks share one GPU (multi-rank rehearsal on a 1-GPU box; --comm torch, no "
                          "whole-step graph: gloo collectives are not capturable)")
-    ap.add_argument("--comm", choices=["auto", "torch", "native", "native-inline"], default="auto",
+    ap.add_argument("--comm", choices=["auto", "torch", "native", "native-inline", "xgmi"], default="auto",
                     help="collective runtime: torch = ProcessGroupNCCL (RCCL, its own stream: an event "
                          "fork/join per collective); native = grace_amd RCCL runtime on its comm stream; "
                          "native-inline = grace_amd RCCL runtime on the CURRENT stream; auto = native-inline "
                          "under a whole-step graph without overlap (measured 0.44 ms/step less than torch "
-                         "for ResNet-50 Top-K), torch otherwise")
+                         "for ResNet-50 Top-K), torch otherwise; xgmi = native-inline plus the one-shot "
+                         "peer-memory all-gather for payloads <= 8 MB (parallel/xgmi.py, self-checked at start)")
     return ap.parse_args()
 
 
@@ -165,7 +166,11 @@ def main():
             from grace_amd.parallel.native_comm import RcclComm
 
             try:
-                native = RcclComm.from_process_group(inline=comm_kind == "native-inline")
+                native = RcclComm.from_process_group(inline=comm_kind in ("native-inline", "xgmi"))
+                if comm_kind == "xgmi":
+                    from grace_amd.parallel.xgmi import XgmiComm
+
+                    native = XgmiComm(native, capacity_mb=8.0)
                 ok = 1
             except Exception as e:  # every rank must agree before the first GRACE collective
                 print(f"[rank {rank}] native RCCL comm unavailable ({type(e).__name__}: {str(e)[:120]}); "

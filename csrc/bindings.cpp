@@ -760,6 +760,7 @@ std::string build_info() {
 
 void grace_bind_comm(py::module& m);  // csrc/comm/rccl_comm.cpp
 void grace_bind_nn(py::module& m);    // csrc/nn_bindings.cpp
+void grace_bind_xgmi(py::module& m);  // csrc/comm/xgmi_allgather.hip
 
 // ------------------------------------------------------------------------------ Adaq
 void adaq_sample(const Tensor& x, const Tensor& seg_off, const Tensor& samp_off, int64_t seed,
@@ -904,6 +905,7 @@ void inceptionn_decode(const Tensor& base, int64_t rank_stride, int64_t stream_o
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   grace_bind_comm(m);
   grace_bind_nn(m);
+  grace_bind_xgmi(m);
   m.doc() = "grace_amd native CDNA4 kernels and RCCL runtime";
   m.def("build_info", &build_info);
   m.def("topk_select", &topk_select);

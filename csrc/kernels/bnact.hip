@@ -25,8 +25,9 @@
 // In-launch hand-offs follow the gfx950 publish/consume recipe (cdna_hip_programming.md
 // Guideline 16): partial rows are stored WRITE-THROUGH (`sc1`, relaxed agent-scope atomic
 // stores: no L2-writeback release fence), every storing wave drains (`s_waitcnt vmcnt(0)`),
-// workgroup barrier, ONE lane adds to the arrival counter; only the finishing block pays ONE
-// agent-scope acquire before its plain loads.  (Measured on MI355X: a `__threadfence()` in
+// workgroup barrier, ONE lane adds to the arrival counter; the finishing block reads the rows
+// with `sc1` loads only, so it pays no acquire fence either (round 2: the acquire was ~1.7 us
+// per tree level, two levels per reduction kernel, 106 reduction kernels per ResNet-50 step).  (Measured on MI355X: a `__threadfence()` in
 // every thread of every block made these kernels 5-10x slower than their streaming bound; a
 // flat one-block fold of 1024 partial rows, or fp64 atomics from 1024 blocks onto the same
 // 2C addresses, cost 25-130 us per launch.)
@@ -150,10 +151,24 @@ struct Red {
   unsigned* cnt;       // [tiles][kMaxGroups + 1]: group counters, top counter last
 };
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// 16-B `sc1` load (buffer instruction, aux 16 = sc1: L1 bypassed, L2-served) of a row that
+// another workgroup stored `sc1` and drained before its arrival add.  Every load of the
+// published partial rows is one of these, which is what lets the finisher skip the agent-scope
+// acquire (cdna_hip_programming.md §6 Guideline 16; MI355X_MICROARCH.md "Valid forms", first
+// row of the sc1 hand-off table: ≈1.7 us per acquire, two per reduction kernel).
+template <typename V>
+__device__ __forceinline__ V ld16_sc1(const void* base, int64_t bytes, int off) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+  const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);
+  return __builtin_bit_cast(V, w);
+}
+
 // Column fold of `rows` rows (row stride C2 elements, 16-B aligned) into fp64, fixed order.
-// The rows were published by other blocks (possibly on other XCDs), so after the acquire every
-// load misses the local L2: the fold is latency bound and issues ALL of a thread's loads before
-// the first use.  16-B loads: thread t owns vector column g = t % G (G = C2 / VW) and the rows
+// The rows were published by other blocks (possibly on other XCDs) with write-through stores
+// and are read with sc1 loads, so every load misses the local L2: the fold is latency bound and
+// issues ALL of a thread's loads before the first use.  16-B loads: thread t owns vector column g = t % G (G = C2 / VW) and the rows
 // r = t / G (mod P), P = kB / G row phases (unrolled by U, independent); the phases are combined
 // through LDS (lds: kB * VW doubles) in phase order, so the result is run-to-run deterministic.
 // Calls put(col, value) once per column (all threads enter).
@@ -168,13 +183,13 @@ __device__ __forceinline__ void fold_block(const T* src, int rows, int C2, doubl
 #pragma unroll
   for (int j = 0; j < VW; ++j) acc[j] = 0.0;
   if (p < P) {
-    const T* base = src + (size_t)g * VW;
+    const int64_t bytes = (int64_t)rows * C2 * (int64_t)sizeof(T);
     for (int r = p; r < rows; r += U * P) {  // predicated: a short fold is still ONE round trip
       V v[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int rr = r + u * P;
-        if (rr < rows) v[u] = *reinterpret_cast<const V*>(base + (size_t)rr * C2);
+        if (rr < rows) v[u] = ld16_sc1<V>(src, bytes, (int)(((int64_t)rr * C2 + (int64_t)g * VW) * (int64_t)sizeof(T)));
         else v[u] = V{};
       }
 #pragma unroll
@@ -198,8 +213,9 @@ __device__ __forceinline__ void fold_block(const T* src, int rows, int C2, doubl
 }
 
 // Every wave has drained its sc1 stores -> barrier -> one relaxed agent add.  True in every
-// thread of the block whose add completed the count; that block is acquired (one lane's agent
-// acquire + drain, then the barrier) before its plain loads.
+// thread of the block whose add completed the count; its waves load the published rows only
+// after the barrier that follows the add's return, and only with sc1 loads (fold_block), so no
+// acquire fence is needed.
 __device__ __forceinline__ bool arrive(unsigned* counter, unsigned expected_last) {
   __shared__ int flag;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -207,10 +223,6 @@ __device__ __forceinline__ bool arrive(unsigned* counter, unsigned expected_last
   if (threadIdx.x == 0) {
     const unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     flag = (prev == expected_last);
-    if (flag) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
   }
   __syncthreads();
   return flag != 0;
@@ -538,8 +550,6 @@ __device__ __forceinline__ float ld_sc1(const float* p) {
 // one 32-bit VGPR offset, the per-vector part (block base + u * rpi rows) a scalar soffset, so
 // holding V vectors in registers costs no per-vector address registers (flat 64-bit addresses
 // kept live across the reduction for the final stores pushed the V = 16 variant to 255 VGPRs).
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
 struct RowMap {
   int voff;    // bytes: (rs * C + col) * 2
   int sbase;   // bytes: block's first row * C * 2   (wave-uniform)
