@@ -259,6 +259,13 @@ __device__ bool block_reduce_tree(const Red& R, const float* a, const float* b) 
   const int grp = blockIdx.x / R.gsize, g0 = grp * R.gsize;
   const int grows = min(R.nchunks - g0, R.gsize);
   if (!arrive(cnt + grp, (unsigned)grows - 1)) return false;
+  if (R.ngroups == 1) {  // one-level tree: the only group's finisher is the tile's finisher
+    double* total = R.total + (size_t)tile * C2;
+    fold_block(part, grows, C2, lds, [&](int c, double v) { total[c] = v; });
+    __syncthreads();
+    if (threadIdx.x == 0) cnt[0] = 0;  // re-arm (visible at kernel end)
+    return true;
+  }
   double* gpart = R.gpart + (size_t)tile * R.ngroups * C2;
   fold_block(part + (size_t)g0 * C2, grows, C2, lds,
              [&](int c, double v) { store_sc1(gpart + (size_t)grp * C2 + c, v); });
@@ -827,8 +834,30 @@ unsigned* next_slot(hipStream_t stream) {
   return p.counters + (size_t)s * kSlotWords;
 }
 
-// Grid and tree shape.  Target >= ~512 blocks (2 per CU) with 4..16 16-B vectors per thread.
+// Grid and tree shape.  Target ~512 blocks (2 per CU) with 8..32 row vectors per thread (knobs below).
 // `fused_v` > 0: single-launch layout, exactly V row-vectors per thread (rows_per_blk = rpi*V).
+// Grid-shape knobs for experiments (benchmarks/bnact_bench.py sweeps them on the box):
+// GRACE_BN_TARGET_BLOCKS (default 512), GRACE_BN_VPT_MIN / _MAX (default 8 / 32 vectors per
+// thread), GRACE_BN_ONE_LEVEL (fold every partial row in one level up to this many chunks;
+// default 64).  Measured fp32 ResNet-50 (graph-replayed per shape): round-1 shape 4 / 16 / two
+// levels always: fwd 1408 + bwd 1961 us per step; these defaults: 1343 + 1907 us.
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return (e && *e) ? atoi(e) : dflt;
+}
+struct PlanKnobs {
+  int target_blocks, vpt_min, vpt_max, one_level;
+  PlanKnobs()
+      : target_blocks(env_int("GRACE_BN_TARGET_BLOCKS", 512)),
+        vpt_min(env_int("GRACE_BN_VPT_MIN", 8)),
+        vpt_max(env_int("GRACE_BN_VPT_MAX", 32)),
+        one_level(env_int("GRACE_BN_ONE_LEVEL", 64)) {}
+};
+const PlanKnobs& knobs() {
+  static PlanKnobs k;
+  return k;
+}
+
 Red plan(int64_t M, int C, int fused_v = 0) {
   Red R{};
   R.M = M;
@@ -843,9 +872,10 @@ Red plan(int64_t M, int C, int fused_v = 0) {
     rpb = (int64_t)R.rpi * fused_v;
   } else {
     const int64_t n_vec = M * C / 8;
-    int64_t vpt = n_vec / ((int64_t)kB * 512);
-    if (vpt < 4) vpt = 4;
-    if (vpt > 16) vpt = 16;
+    const PlanKnobs& kn = knobs();
+    int64_t vpt = n_vec / ((int64_t)kB * kn.target_blocks);
+    if (vpt < kn.vpt_min) vpt = kn.vpt_min;
+    if (vpt > kn.vpt_max) vpt = kn.vpt_max;
     const int64_t per_blk = R.rpi * vpt;
     int64_t nc = (M + per_blk - 1) / per_blk;
     if (nc * tiles > 2048) nc = (2048 + tiles - 1) / tiles;
@@ -858,6 +888,7 @@ Red plan(int64_t M, int C, int fused_v = 0) {
   R.nchunks = (int)(nc < 1 ? 1 : nc);
   int gs = 1;
   while (gs * gs < R.nchunks) ++gs;
+  if (R.nchunks <= knobs().one_level) gs = R.nchunks;  // one fold of every partial row
   int ng = (R.nchunks + gs - 1) / gs;
   while (ng > kMaxGroups) {
     ++gs;
