@@ -179,9 +179,10 @@ unsigned bn_spin_timeouts();                     // bounded co-residency waits t
 void bn_act_forward(const void* x, const void* res, bool fp32, int64_t M, int C, const float* gamma,
                     const float* beta, float* running_mean, float* running_var, int64_t* nbt, float momentum,
                     float eps, bool relu, float* save, float* ws, void* y, uint8_t* relu_mask, hipStream_t stream);
-void bn_act_backward(const void* dy, const void* x, bool fp32, const uint8_t* relu_mask, int64_t M, int C,
-                     const float* gamma, const float* save, bool relu, float* dgamma, float* dbeta, float* coef,
-                     float* ws, void* dx, void* dres, hipStream_t stream);
+// dy2 (may be nullptr): a second gradient contribution of the same layout, summed into dy
+void bn_act_backward(const void* dy, const void* dy2, const void* x, bool fp32, const uint8_t* relu_mask, int64_t M,
+                     int C, const float* gamma, const float* save, bool relu, float* dgamma, float* dbeta,
+                     float* coef, float* ws, void* dx, void* dres, hipStream_t stream);
 
 // ---------------------------------------------------------------- optim.hip
 constexpr int kSgdSegs = 64;

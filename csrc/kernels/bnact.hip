@@ -395,8 +395,45 @@ struct GradOut {
   float* coef;         // [3C]: a, b, c with dx = a*dz + b*x + c
 };
 
-template <typename T, bool RELU>
-__global__ __launch_bounds__(kB) void bn_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* p, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
+}
+// 8 channels of one row through a buffer descriptor (voff: per-thread bytes, soff: uniform)
+template <typename T>
+__device__ __forceinline__ Bf8 bld8(__amdgpu_buffer_rsrc_t r, int voff, int soff);
+template <>
+__device__ __forceinline__ Bf8 bld8<float>(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+  const u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(r, voff + 16, soff, 0);
+  Bf8 o;
+  o.v[0] = __uint_as_float(a.x); o.v[1] = __uint_as_float(a.y); o.v[2] = __uint_as_float(a.z); o.v[3] = __uint_as_float(a.w);
+  o.v[4] = __uint_as_float(b.x); o.v[5] = __uint_as_float(b.y); o.v[6] = __uint_as_float(b.z); o.v[7] = __uint_as_float(b.w);
+  return o;
+}
+template <>
+__device__ __forceinline__ Bf8 bld8<uint16_t>(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+  Bf8 o;
+  o.v[0] = __uint_as_float(u.x << 16); o.v[1] = __uint_as_float(u.x & 0xffff0000u);
+  o.v[2] = __uint_as_float(u.y << 16); o.v[3] = __uint_as_float(u.y & 0xffff0000u);
+  o.v[4] = __uint_as_float(u.z << 16); o.v[5] = __uint_as_float(u.z & 0xffff0000u);
+  o.v[6] = __uint_as_float(u.w << 16); o.v[7] = __uint_as_float(u.w & 0xffff0000u);
+  return o;
+}
+
+// DY2: the layer's output fed two consumers (a block output -> the next block's conv and its
+// shortcut) and autograd hands the two gradient contributions over separately
+// (ops/bnact.py `dual`): dy = dy + dy2 is summed here instead of in a separate add kernel.
+template <typename T>
+__device__ __forceinline__ void add8(Bf8& d, const T* p) {
+  const Bf8 e = ld8(p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) d.v[j] += e.v[j];
+}
+
+template <typename T, bool RELU, bool DY2>
+__global__ __launch_bounds__(kB) void bn_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ dy2,
+                                                       const T* __restrict__ x,
                                                        const uint8_t* __restrict__ mask, Red R, GradOut o) {
   float s1[8], s2[8], mu[8];
 #pragma unroll
@@ -417,20 +454,42 @@ __global__ __launch_bounds__(kB) void bn_reduce_kernel(const T* __restrict__ dy,
       s2[j] = fmaf(dz, v.v[j] - mu[j], s2[j]);
     }
   };
+  // The 4-row batches address every operand through a buffer descriptor based at the block's
+  // first row: one 32-bit VGPR offset per thread, the row step as a wave-uniform soffset.  With
+  // flat 64-bit addresses each of the (up to) 24 in-flight 16-B loads of the two-gradient fp32
+  // variant held its own VGPR pair and hipcc serialised the loads to stay within 128 VGPRs.
+  const int64_t blk0 = (int64_t)blockIdx.x * R.rows_per_blk * R.C;  // element offset of the chunk
+  const int64_t left = (R.M * (int64_t)R.C - blk0) * (int64_t)sizeof(T);
+  const int nrec = (int)(left < 0x7fffffff ? left : 0x7fffffff);
+  const __amdgpu_buffer_rsrc_t rdy = brsrc(dy + blk0, nrec), rx = brsrc(x + blk0, nrec);
+  const __amdgpu_buffer_rsrc_t rdy2 = brsrc(DY2 ? dy2 + blk0 : dy + blk0, nrec);
   for_rows(R, [&](int64_t e, int64_t step, int n) {
     if (n == 4) {
+      const int vo = (int)((e - blk0) * (int64_t)sizeof(T));
+      const int so = (int)(step * (int64_t)sizeof(T));
       Bf8 d[4], v[4];
       uint32_t w[4] = {0, 0, 0, 0};
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        d[u] = ld8(dy + e + u * step);
-        v[u] = ld8(x + e + u * step);
+        d[u] = bld8<T>(rdy, vo, u * so);
+        v[u] = bld8<T>(rx, vo, u * so);
         if constexpr (RELU) w[u] = mask[(e + u * step) >> 3];
+      }
+      if constexpr (DY2) {
+        Bf8 d2[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) d2[u] = bld8<T>(rdy2, vo, u * so);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) d[u].v[j] += d2[u].v[j];
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc(d[u], v[u], w[u]);
     } else {
-      const Bf8 d = ld8(dy + e), v = ld8(x + e);
+      Bf8 d = ld8(dy + e);
+      const Bf8 v = ld8(x + e);
+      if constexpr (DY2) add8(d, dy2 + e);
       uint32_t w = 0;
       if constexpr (RELU) w = mask[e >> 3];
       acc(d, v, w);
@@ -456,8 +515,9 @@ __global__ __launch_bounds__(kB) void bn_reduce_kernel(const T* __restrict__ dy,
   }
 }
 
-template <typename T, bool RELU, bool RES>
-__global__ __launch_bounds__(kB) void bn_dx_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+template <typename T, bool RELU, bool RES, bool DY2>
+__global__ __launch_bounds__(kB) void bn_dx_kernel(const T* __restrict__ dy, const T* __restrict__ dy2,
+                                                   const T* __restrict__ x,
                                                    const uint8_t* __restrict__ mask, const float* __restrict__ coef,
                                                    T* __restrict__ dx, T* __restrict__ dres,
                                                    int64_t n_vec, int C) {
@@ -473,8 +533,9 @@ __global__ __launch_bounds__(kB) void bn_dx_kernel(const T* __restrict__ dy, con
     cc[j] = coef[2 * C + cg * 8 + j];
   }
   for (; i < n_vec; i += stride) {
-    const Bf8 d = ld8(dy + i * 8);
+    Bf8 d = ld8(dy + i * 8);
     const Bf8 v = ld8(x + i * 8);
+    if constexpr (DY2) add8(d, dy2 + i * 8);
     float dz[8], o[8];
     if constexpr (RELU) {
       const uint32_t mb = mask[i];
@@ -1060,26 +1121,39 @@ void forward_2k(const T* x, const T* res, int64_t M, int C, const StatsOut& o, b
     hipLaunchKernelGGL((bn_apply_kernel<T, false, false>), dim3(gb), dim3(kB), 0, stream, x, res, save, y, mask, n_vec, C);
 }
 
-template <typename T>
-void backward_2k(const T* dy, const T* x, const uint8_t* mask, int64_t M, int C, const GradOut& o, bool relu,
-                 const float* coef, float* ws, T* dx, T* dres, hipStream_t stream) {
+template <typename T, bool DY2>
+void backward_2k_t(const T* dy, const T* dy2, const T* x, const uint8_t* mask, int64_t M, int C, const GradOut& o,
+                   bool relu, const float* coef, float* ws, T* dx, T* dres, hipStream_t stream) {
   Red R = plan(M, C);
   bind_ws(R, ws, stream);
   const dim3 grid(R.nchunks, C / R.CT);
   if (relu)
-    hipLaunchKernelGGL((bn_reduce_kernel<T, true>), grid, dim3(kB), 0, stream, dy, x, mask, R, o);
+    hipLaunchKernelGGL((bn_reduce_kernel<T, true, DY2>), grid, dim3(kB), 0, stream, dy, dy2, x, mask, R, o);
   else
-    hipLaunchKernelGGL((bn_reduce_kernel<T, false>), grid, dim3(kB), 0, stream, dy, x, mask, R, o);
+    hipLaunchKernelGGL((bn_reduce_kernel<T, false, DY2>), grid, dim3(kB), 0, stream, dy, dy2, x, mask, R, o);
   const int64_t n_vec = M * C / 8;
   const int gb = apply_grid(n_vec, C);
   if (relu && dres)
-    hipLaunchKernelGGL((bn_dx_kernel<T, true, true>), dim3(gb), dim3(kB), 0, stream, dy, x, mask, coef, dx, dres, n_vec, C);
+    hipLaunchKernelGGL((bn_dx_kernel<T, true, true, DY2>), dim3(gb), dim3(kB), 0, stream, dy, dy2, x, mask, coef, dx,
+                       dres, n_vec, C);
   else if (relu)
-    hipLaunchKernelGGL((bn_dx_kernel<T, true, false>), dim3(gb), dim3(kB), 0, stream, dy, x, mask, coef, dx, dres, n_vec, C);
+    hipLaunchKernelGGL((bn_dx_kernel<T, true, false, DY2>), dim3(gb), dim3(kB), 0, stream, dy, dy2, x, mask, coef, dx,
+                       dres, n_vec, C);
   else if (dres)
-    hipLaunchKernelGGL((bn_dx_kernel<T, false, true>), dim3(gb), dim3(kB), 0, stream, dy, x, mask, coef, dx, dres, n_vec, C);
+    hipLaunchKernelGGL((bn_dx_kernel<T, false, true, DY2>), dim3(gb), dim3(kB), 0, stream, dy, dy2, x, mask, coef, dx,
+                       dres, n_vec, C);
   else
-    hipLaunchKernelGGL((bn_dx_kernel<T, false, false>), dim3(gb), dim3(kB), 0, stream, dy, x, mask, coef, dx, dres, n_vec, C);
+    hipLaunchKernelGGL((bn_dx_kernel<T, false, false, DY2>), dim3(gb), dim3(kB), 0, stream, dy, dy2, x, mask, coef,
+                       dx, dres, n_vec, C);
+}
+
+template <typename T>
+void backward_2k(const T* dy, const T* dy2, const T* x, const uint8_t* mask, int64_t M, int C, const GradOut& o,
+                 bool relu, const float* coef, float* ws, T* dx, T* dres, hipStream_t stream) {
+  if (dy2)
+    backward_2k_t<T, true>(dy, dy2, x, mask, M, C, o, relu, coef, ws, dx, dres, stream);
+  else
+    backward_2k_t<T, false>(dy, dy2, x, mask, M, C, o, relu, coef, ws, dx, dres, stream);
 }
 
 }  // namespace
@@ -1121,20 +1195,22 @@ void bn_act_forward(const void* xv, const void* resv, bool fp32, int64_t M, int 
   forward_2k(x, res, M, C, o, relu, save, ws, y, mask, stream);
 }
 
-void bn_act_backward(const void* dyv, const void* xv, bool fp32, const uint8_t* mask, int64_t M, int C,
-                     const float* gamma, const float* save, bool relu, float* dgamma, float* dbeta, float* coef,
-                     float* ws, void* dxv, void* dresv, hipStream_t stream) {
+void bn_act_backward(const void* dyv, const void* dy2v, const void* xv, bool fp32, const uint8_t* mask, int64_t M,
+                     int C, const float* gamma, const float* save, bool relu, float* dgamma, float* dbeta,
+                     float* coef, float* ws, void* dxv, void* dresv, hipStream_t stream) {
   GradOut o{gamma, save, dgamma, dbeta, coef};
   if (fp32) {
-    backward_2k(static_cast<const float*>(dyv), static_cast<const float*>(xv), mask, M, C, o, relu, coef, ws,
-                static_cast<float*>(dxv), static_cast<float*>(dresv), stream);
+    backward_2k(static_cast<const float*>(dyv), static_cast<const float*>(dy2v), static_cast<const float*>(xv), mask,
+                M, C, o, relu, coef, ws, static_cast<float*>(dxv), static_cast<float*>(dresv), stream);
     return;
   }
   const uint16_t* dy = static_cast<const uint16_t*>(dyv);
+  const uint16_t* dy2 = static_cast<const uint16_t*>(dy2v);
   const uint16_t* x = static_cast<const uint16_t*>(xv);
   uint16_t* dx = static_cast<uint16_t*>(dxv);
   uint16_t* dres = static_cast<uint16_t*>(dresv);
-  if (const int v = pick_fused_v(M, C, true)) {
+  const int v = dy2 ? 0 : pick_fused_v(M, C, true);  // the single-launch variant reads one dy
+  if (v) {
     Red R = plan(M, C, v);
     bind_ws(R, ws, stream);
     const dim3 grid(R.nchunks, C / R.CT);
@@ -1155,7 +1231,7 @@ void bn_act_backward(const void* dyv, const void* xv, bool fp32, const uint8_t* 
     GRACE_BN_BWD(8)
 #undef GRACE_BN_BWD
   }
-  backward_2k(dy, x, mask, M, C, o, relu, coef, ws, dx, dres, stream);
+  backward_2k(dy, dy2, x, mask, M, C, o, relu, coef, ws, dx, dres, stream);
 }
 
 }  // namespace grace

@@ -75,12 +75,14 @@ std::vector<Tensor> bn_act_fwd(const Tensor& x, const c10::optional<Tensor>& res
 }
 
 // returns (dx, dres (undefined unless want_dres), dweight, dbias)
-std::vector<Tensor> bn_act_bwd(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& mask,
-                               const c10::optional<Tensor>& weight, const Tensor& save, bool relu, bool want_dres,
-                               bool want_dweight) {
+std::vector<Tensor> bn_act_bwd(const Tensor& dy, const c10::optional<Tensor>& dy2, const Tensor& x,
+                               const c10::optional<Tensor>& mask, const c10::optional<Tensor>& weight,
+                               const Tensor& save, bool relu, bool want_dres, bool want_dweight) {
   int64_t M, C;
   check_rows(x, "x", &M, &C);
   same_layout(x, dy, "grad_output");
+  const bool two = dy2.has_value() && dy2->defined();
+  if (two) same_layout(x, *dy2, "second grad_output");
   if (relu) {
     TORCH_CHECK(mask.has_value() && mask->defined() && mask->is_cuda() && mask->scalar_type() == at::kByte &&
                     mask->is_contiguous() && mask->numel() == M * C / 8,
@@ -95,7 +97,7 @@ std::vector<Tensor> bn_act_bwd(const Tensor& dy, const Tensor& x, const c10::opt
   Tensor db = want_dweight ? at::empty({C}, f32) : Tensor();
   Tensor coef = at::empty({3 * C}, f32);
   Tensor ws = at::empty({grace::bn_workspace_floats(M, (int)C)}, f32);
-  grace::bn_act_backward(dy.data_ptr(), x.data_ptr(), x.scalar_type() == at::kFloat,
+  grace::bn_act_backward(dy.data_ptr(), two ? dy2->data_ptr() : nullptr, x.data_ptr(), x.scalar_type() == at::kFloat,
                          relu ? mask->data_ptr<uint8_t>() : nullptr, M, (int)C,
                          opt_f32(weight, C, "weight"), save.data_ptr<float>(), relu,
                          want_dweight ? dg.data_ptr<float>() : nullptr, want_dweight ? db.data_ptr<float>() : nullptr,

@@ -42,9 +42,10 @@ class BasicBlock(nn.Module):
         self.downsample = down
 
     def forward(self, x):
-        idt = x if self.downsample is None else self.downsample(x)
-        y = self.bn1(self.conv1(x))
-        return self.bn2(self.conv2(y), idt)
+        xm, xs = x if isinstance(x, tuple) else (x, x)
+        idt = xs if self.downsample is None else self.downsample(xs)
+        y = self.bn1(self.conv1(xm))
+        return self.bn2(self.conv2(y), idt, dual=True)
 
 
 class Bottleneck(nn.Module):
@@ -62,10 +63,14 @@ class Bottleneck(nn.Module):
         self.downsample = down
 
     def forward(self, x):
-        idt = x if self.downsample is None else self.downsample(x)
-        y = self.bn1(self.conv1(x))
+        # x: the previous block's output as (main, shortcut) aliases (bn_act dual=True: their
+        # two gradients are summed inside the fused BN backward, not by an autograd add), or a
+        # plain tensor for the first block
+        xm, xs = x if isinstance(x, tuple) else (x, x)
+        idt = xs if self.downsample is None else self.downsample(xs)
+        y = self.bn1(self.conv1(xm))
         y = self.bn2(self.conv2(y))
-        return self.bn3(self.conv3(y), idt)
+        return self.bn3(self.conv3(y), idt, dual=True)
 
 
 class ResNet(nn.Module):
@@ -106,6 +111,8 @@ class ResNet(nn.Module):
     def forward(self, x):
         x = self.maxpool(self.bn1(self.conv1(x)))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        if isinstance(x, tuple):
+            x = x[0]
         return self.fc(torch.flatten(self.avgpool(x), 1))
 
 

@@ -42,45 +42,69 @@ def _fusable(x: torch.Tensor, bn: nn.BatchNorm2d, residual: Optional[torch.Tenso
     return True
 
 
+def _kernel_grad(g: Optional[torch.Tensor], like: torch.Tensor) -> Optional[torch.Tensor]:
+    if g is None:
+        return None
+    if g.stride() != like.stride() or g.data_ptr() % 16:
+        g = g.contiguous(memory_format=torch.channels_last)
+        if g.data_ptr() % 16 or g.stride() != like.stride():
+            g = g.clone(memory_format=torch.channels_last)
+    return g
+
+
 class _BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, residual, weight, bias, running_mean, running_var, nbt, momentum, eps, relu):
+    def forward(ctx, x, residual, weight, bias, running_mean, running_var, nbt, momentum, eps, relu, dual):
         y, save, mask = _native.lib().bn_act_fwd(x, residual, weight, bias, running_mean, running_var, nbt,
                                                  float(momentum), float(eps), bool(relu))
         ctx.relu = bool(relu)
         ctx.has_res = residual is not None
         # the backward needs only the ReLU mask (1 bit per element), not the bf16 output
         ctx.save_for_backward(x, mask if relu else None, weight, save)
+        if dual:
+            # two aliases of y for two consumers: autograd then hands their gradients to
+            # backward() separately and the kernels sum them (no add kernel)
+            ctx.set_materialize_grads(False)
+            return y, y.view_as(y)
         return y
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, dy2=None):
         x, mask, weight, save = ctx.saved_tensors
-        dy = dy.contiguous(memory_format=torch.channels_last)
-        if dy.data_ptr() % 16:
-            dy = dy.clone(memory_format=torch.channels_last)
+        if dy is None:
+            dy, dy2 = dy2, None
+        if dy is None:
+            return (None,) * 11
+        dy = _kernel_grad(dy, x)
+        dy2 = _kernel_grad(dy2, x)
         want_w = weight is not None and ctx.needs_input_grad[2]
-        dx, dres, dw, db = _native.lib().bn_act_bwd(dy, x, mask, weight, save, ctx.relu,
+        dx, dres, dw, db = _native.lib().bn_act_bwd(dy, dy2, x, mask, weight, save, ctx.relu,
                                                     ctx.has_res and ctx.needs_input_grad[1], want_w)
         return (dx, dres if ctx.has_res and ctx.needs_input_grad[1] else None,
                 dw if want_w else None, db if want_w and ctx.needs_input_grad[3] else None,
-                None, None, None, None, None, None)
+                None, None, None, None, None, None, None)
 
 
 def bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, residual: Optional[torch.Tensor] = None,
-           relu: bool = False) -> torch.Tensor:
-    """``act(bn(x) + residual)`` with the module's parameters and running statistics."""
+           relu: bool = False, dual: bool = False):
+    """``act(bn(x) + residual)`` with the module's parameters and running statistics.
+
+    ``dual=True`` returns ``(y, y_alias)``: two aliases of the output for two consumers (e.g. a
+    ResNet block output feeding the next block's conv and its shortcut).  Their gradients reach
+    the fused backward separately and are summed inside its kernels instead of by autograd's
+    add kernel (one full read+write pass of the activation saved per block)."""
     training = bn.training or not bn.track_running_stats
     if training and _fusable(x, bn, residual):
         track = bn.training and bn.track_running_stats
         return _BNActFn.apply(x, residual, bn.weight, bn.bias,
                               bn.running_mean if track else None, bn.running_var if track else None,
                               bn.num_batches_tracked if track else None,
-                              bn.momentum if bn.momentum is not None else 0.0, bn.eps, relu)
+                              bn.momentum if bn.momentum is not None else 0.0, bn.eps, relu, bool(dual))
     y = nn.BatchNorm2d.forward(bn, x)
     if residual is not None:
         y = y + residual
-    return F.relu(y) if relu else y
+    y = F.relu(y) if relu else y
+    return (y, y) if dual else y
 
 
 class BatchNormAct2d(nn.BatchNorm2d):
@@ -90,8 +114,8 @@ class BatchNormAct2d(nn.BatchNorm2d):
         super().__init__(num_features, **kw)
         self.relu = relu
 
-    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
-        return bn_act(x, self, residual, self.relu)
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None, dual: bool = False):
+        return bn_act(x, self, residual, self.relu, dual)
 
     def extra_repr(self) -> str:
         return super().extra_repr() + (", relu=True" if self.relu else "")

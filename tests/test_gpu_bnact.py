@@ -217,3 +217,41 @@ def test_resnet_fused_step_as_accurate_as_unfused():
           f"cos(unfused, fp32) {cu:.4f}")
     assert abs(lf - l32) <= abs(lu - l32) + 2e-2
     assert cf >= cu - 0.03, (cf, cu)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(8, 256, 14, 14), (4, 64, 28, 28)])
+def test_bnact_dual_output_grads(dtype, shape):
+    """dual=True: two aliases of the output, their gradients summed inside the fused backward
+    kernels -- same dx / dres / dgamma / dbeta as one output whose gradient is dy1 + dy2."""
+    m, x, res, dy = _case(*shape, relu=True, with_res=True, seed=3, dtype=dtype)
+    g = torch.Generator(device="cpu").manual_seed(9)
+    dy2 = torch.randn(shape, generator=g).to(DEV, dtype).contiguous(memory_format=torch.channels_last)
+    outs = []
+    for dual in (False, True):
+        xg = x.detach().clone().requires_grad_(True)
+        rg = res.detach().clone().requires_grad_(True)
+        m.zero_grad(set_to_none=True)
+        y = m(xg, rg, dual=dual)
+        if dual:
+            y1, y2 = y
+            assert y1.data_ptr() == y2.data_ptr()
+            torch.autograd.backward([y1, y2], [dy, dy2])
+        else:
+            y.backward(dy + dy2)
+        outs.append((xg.grad, rg.grad, m.weight.grad, m.bias.grad))
+    tol = dict(rtol=1e-5, atol=1e-5) if dtype == torch.float32 else dict(rtol=2e-2, atol=2e-2)
+    for i, (a, b) in enumerate(zip(*outs)):
+        t = tol
+        if dtype == torch.bfloat16 and i >= 2:
+            # dgamma / dbeta sum M products: the unfused side rounds dy1 + dy2 to bf16 per element
+            # first (the dual kernels add in fp32), a random-walk difference of ~sqrt(M) ulps
+            t = dict(rtol=2e-2, atol=0.5)
+        torch.testing.assert_close(a.float(), b.float(), **t)
+    # only one alias used: its gradient alone
+    xg = x.detach().clone().requires_grad_(True)
+    y1, _ = m(xg, res, dual=True)
+    y1.backward(dy)
+    xr = x.detach().clone().requires_grad_(True)
+    m(xr, res).backward(dy)
+    torch.testing.assert_close(xg.grad.float(), xr.grad.float(), **tol)
