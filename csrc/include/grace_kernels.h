@@ -184,6 +184,13 @@ void bn_act_backward(const void* dy, const void* dy2, const void* x, bool fp32, 
                      int C, const float* gamma, const float* save, bool relu, float* dgamma, float* dbeta,
                      float* coef, float* ws, void* dx, void* dres, hipStream_t stream);
 
+// conv bias (+ ReLU) over [M, C] channels_last rows (same channel constraints as BN):
+// y = act(x + bias); backward dz = dy * [y > 0] and dbias = Σ_rows dz in ONE pass (ws as BN)
+void bias_act_forward(const void* x, const float* bias, bool fp32, int64_t M, int C, bool relu, void* y,
+                      hipStream_t stream);
+void bias_act_backward(const void* dy, const void* y, bool fp32, int64_t M, int C, bool relu, float* dbias, float* ws,
+                       void* dz, hipStream_t stream);
+
 // ---------------------------------------------------------------- optim.hip
 constexpr int kSgdSegs = 64;
 // buf[i] / w16[i] may be nullptr (no momentum / no bf16 working copy)

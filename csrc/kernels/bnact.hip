@@ -553,6 +553,69 @@ __global__ __launch_bounds__(kB) void bn_dx_kernel(const T* __restrict__ dy, con
 }
 
 
+// ---------------------------------------------------------------- conv bias (+ ReLU)
+// VGG's conv -> bias -> ReLU (MIOpen returns the conv without its bias: PyTorch then runs a
+// broadcast add, a ReLU, and in backward threshold_backward plus a bias-gradient reduction --
+// four full activation passes and three launches around every conv).  Here: forward = one
+// streaming pass y = act(x + b); backward = ONE pass that writes dz = dy * [y > 0] and reduces
+// Σdz per channel into the bias gradient through the same two-level arrival tree as the BN
+// statistics (deterministic fp64 fold).
+template <typename T, bool RELU>
+__global__ __launch_bounds__(kB) void bias_act_fwd_kernel(const T* __restrict__ x, const float* __restrict__ bias,
+                                                          T* __restrict__ y, int64_t n_vec, int C) {
+  const int tpr = C >> 3;
+  const int64_t stride = (int64_t)gridDim.x * kB;
+  int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x;
+  const int cg = (int)(i % tpr);  // stride % tpr == 0 (apply_grid)
+  float b[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) b[j] = bias[cg * 8 + j];
+  for (; i < n_vec; i += stride) {
+    const Bf8 v = ld8(x + i * 8);
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = RELU ? fmaxf(v.v[j] + b[j], 0.f) : v.v[j] + b[j];
+    st8(y + i * 8, o);
+  }
+}
+
+template <typename T, bool RELU>
+__global__ __launch_bounds__(kB) void bias_act_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ y,
+                                                          T* __restrict__ dz, Red R, float* __restrict__ dbias) {
+  float s[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = 0.f;
+  auto one = [&](const Bf8& d, const Bf8& v, T* out) {
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      o[j] = (!RELU || v.v[j] > 0.f) ? d.v[j] : 0.f;
+      s[j] += o[j];
+    }
+    st8(out, o);
+  };
+  for_rows(R, [&](int64_t e, int64_t step, int n) {
+    if (n == 4) {
+      Bf8 d[4], v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        d[u] = ld8(dy + e + u * step);
+        if constexpr (RELU) v[u] = ld8(y + e + u * step);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) one(d[u], v[u], dz + e + u * step);
+    } else {
+      const Bf8 d = ld8(dy + e);
+      Bf8 v{};
+      if constexpr (RELU) v = ld8(y + e);
+      one(d, v, dz + e);
+    }
+  });
+  if (!block_reduce_tree(R, s, s)) return;
+  const double* total = R.total + (size_t)blockIdx.y * 2 * R.CT;
+  for (int cl = threadIdx.x; cl < R.CT; cl += kB) dbias[blockIdx.y * R.CT + cl] = (float)total[cl];
+}
+
 // ---------------------------------------------------------------- single-launch variants
 // For the small/medium layers (ResNet-50 stages 2-4: 0.4-8 M elements) a BN pass is latency
 // bound: two launches, each with a serial reduction tail, for a few MB of data.  The fused
@@ -1232,6 +1295,47 @@ void bn_act_backward(const void* dyv, const void* dy2v, const void* xv, bool fp3
 #undef GRACE_BN_BWD
   }
   backward_2k(dy, dy2, x, mask, M, C, o, relu, coef, ws, dx, dres, stream);
+}
+
+namespace {
+template <typename T>
+void bias_fwd_t(const T* x, const float* bias, int64_t M, int C, bool relu, T* y, hipStream_t stream) {
+  const int64_t n_vec = M * C / 8;
+  const int gb = apply_grid(n_vec, C);
+  if (relu)
+    hipLaunchKernelGGL((bias_act_fwd_kernel<T, true>), dim3(gb), dim3(kB), 0, stream, x, bias, y, n_vec, C);
+  else
+    hipLaunchKernelGGL((bias_act_fwd_kernel<T, false>), dim3(gb), dim3(kB), 0, stream, x, bias, y, n_vec, C);
+}
+template <typename T>
+void bias_bwd_t(const T* dy, const T* y, int64_t M, int C, bool relu, float* dbias, float* ws, T* dz,
+                hipStream_t stream) {
+  Red R = plan(M, C);
+  bind_ws(R, ws, stream);
+  const dim3 grid(R.nchunks, C / R.CT);
+  if (relu)
+    hipLaunchKernelGGL((bias_act_bwd_kernel<T, true>), grid, dim3(kB), 0, stream, dy, y, dz, R, dbias);
+  else
+    hipLaunchKernelGGL((bias_act_bwd_kernel<T, false>), grid, dim3(kB), 0, stream, dy, y, dz, R, dbias);
+}
+}  // namespace
+
+void bias_act_forward(const void* x, const float* bias, bool fp32, int64_t M, int C, bool relu, void* y,
+                      hipStream_t stream) {
+  if (fp32)
+    bias_fwd_t(static_cast<const float*>(x), bias, M, C, relu, static_cast<float*>(y), stream);
+  else
+    bias_fwd_t(static_cast<const uint16_t*>(x), bias, M, C, relu, static_cast<uint16_t*>(y), stream);
+}
+
+void bias_act_backward(const void* dy, const void* y, bool fp32, int64_t M, int C, bool relu, float* dbias, float* ws,
+                       void* dz, hipStream_t stream) {
+  if (fp32)
+    bias_bwd_t(static_cast<const float*>(dy), static_cast<const float*>(y), M, C, relu, dbias, ws,
+               static_cast<float*>(dz), stream);
+  else
+    bias_bwd_t(static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(y), M, C, relu, dbias, ws,
+               static_cast<uint16_t*>(dz), stream);
 }
 
 }  // namespace grace

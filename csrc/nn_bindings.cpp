@@ -147,10 +147,38 @@ void sgd_step(const std::vector<Tensor>& params, const std::vector<Tensor>& grad
   grace::sgd_step(p.data(), g.data(), b.data(), w.data(), len.data(), (int)n, (float)lr, (float)momentum,
                   (float)dampening, (float)wd, nesterov, maximize, first, cur_stream());
 }
+// conv bias (+ ReLU): y = act(x + bias) for channels_last [N, C, H, W] x
+Tensor bias_act_fwd(const Tensor& x, const Tensor& bias, bool relu) {
+  int64_t M, C;
+  check_rows(x, "x", &M, &C);
+  const float* b = opt_f32(bias, C, "bias");
+  TORCH_CHECK(b != nullptr, "bias required");
+  DevGuard guard(x.device());
+  Tensor y = at::empty_like(x);
+  grace::bias_act_forward(x.data_ptr(), b, x.scalar_type() == at::kFloat, M, (int)C, relu, y.data_ptr(), cur_stream());
+  return y;
+}
+
+// returns (dz = dy * [y > 0], dbias = sum over N, H, W of dz) in one pass
+std::vector<Tensor> bias_act_bwd(const Tensor& dy, const Tensor& y, bool relu) {
+  int64_t M, C;
+  check_rows(y, "y", &M, &C);
+  same_layout(y, dy, "grad_output");
+  DevGuard guard(y.device());
+  auto f32 = y.options().dtype(at::kFloat);
+  Tensor dz = at::empty_like(y);
+  Tensor db = at::empty({C}, f32);
+  Tensor ws = at::empty({grace::bn_workspace_floats(M, (int)C)}, f32);
+  grace::bias_act_backward(dy.data_ptr(), y.data_ptr(), y.scalar_type() == at::kFloat, M, (int)C, relu,
+                           db.data_ptr<float>(), ws.data_ptr<float>(), dz.data_ptr(), cur_stream());
+  return {dz, db};
+}
 
 }  // namespace
 
 void grace_bind_nn(py::module& m) {
+  m.def("bias_act_fwd", &bias_act_fwd);
+  m.def("bias_act_bwd", &bias_act_bwd);
   m.def("sgd_step", &sgd_step);
   m.def("bn_supported", &bn_supported);
   m.def("bn_fused_v", [](int64_t M, int64_t C, bool bwd) { return grace::bn_fused_v(M, (int)C, bwd); });

@@ -7,6 +7,8 @@ fc6 (4096 x 25088 = 103M) is the tall-skinny PowerSGD stress case.
 import torch
 import torch.nn as nn
 
+from ..ops.convact import ConvBiasAct2d
+
 _CFG16 = [64, 64, "M", 128, 128, "M", 256, 256, 256, "M", 512, 512, 512, "M", 512, 512, 512, "M"]
 
 
@@ -17,11 +19,13 @@ class VGG(nn.Module):
         for v in cfg:
             if v == "M":
                 layers.append(nn.MaxPool2d(2, 2))
+            elif batch_norm:
+                layers += [nn.Conv2d(c, v, 3, padding=1), nn.BatchNorm2d(v), nn.ReLU(inplace=True)]
+                c = v
             else:
-                layers.append(nn.Conv2d(c, v, 3, padding=1))
-                if batch_norm:
-                    layers.append(nn.BatchNorm2d(v))
-                layers.append(nn.ReLU(inplace=True))
+                # conv + bias + ReLU with the bias add and ReLU as native kernels (ops/convact.py);
+                # the Identity keeps torchvision's features.<i> indices / state_dict keys
+                layers += [ConvBiasAct2d(c, v, 3, padding=1, relu=True), nn.Identity()]
                 c = v
         self.features = nn.Sequential(*layers)
         self.avgpool = nn.AdaptiveAvgPool2d((7, 7))
