@@ -191,6 +191,13 @@ void bias_act_forward(const void* x, const float* bias, bool fp32, int64_t M, in
 void bias_act_backward(const void* dy, const void* y, bool fp32, int64_t M, int C, bool relu, float* dbias, float* ws,
                        void* dz, hipStream_t stream);
 
+// ---------------------------------------------------------------- pool.hip
+// NHWC max pooling (C % 8 == 0, k <= 15) with a 1-byte in-window argmax code per output element
+void maxpool_forward(const void* x, bool fp32, int N, int H, int W, int C, int OH, int OW, int k, int s, int pad,
+                     void* y, uint8_t* code, hipStream_t stream);
+void maxpool_backward(const void* dy, const uint8_t* code, bool fp32, int N, int H, int W, int C, int OH, int OW,
+                      int k, int s, int pad, void* dx, hipStream_t stream);
+
 // ---------------------------------------------------------------- optim.hip
 constexpr int kSgdSegs = 64;
 // buf[i] / w16[i] may be nullptr (no momentum / no bf16 working copy)

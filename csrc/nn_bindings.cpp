@@ -174,9 +174,43 @@ std::vector<Tensor> bias_act_bwd(const Tensor& dy, const Tensor& y, bool relu) {
   return {dz, db};
 }
 
+// NHWC max pooling: returns (y, code) -- code = uint8 in-window argmax per output element
+std::vector<Tensor> maxpool_fwd(const Tensor& x, int64_t k, int64_t s, int64_t pad) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  (x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16),
+              "maxpool: channels_last fp32/bf16 GPU tensor");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(C % 8 == 0 && k >= 1 && k <= 15 && s >= 1 && pad >= 0 && 2 * pad <= k, "maxpool: unsupported shape");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0, "maxpool: 16-B aligned input");
+  const int64_t OH = (H + 2 * pad - k) / s + 1, OW = (W + 2 * pad - k) / s + 1;
+  TORCH_CHECK(OH > 0 && OW > 0, "maxpool: empty output");
+  DevGuard guard(x.device());
+  Tensor y = at::empty({N, C, OH, OW}, x.options(), at::MemoryFormat::ChannelsLast);
+  Tensor code = at::empty({N, C, OH, OW}, x.options().dtype(at::kByte), at::MemoryFormat::ChannelsLast);
+  grace::maxpool_forward(x.data_ptr(), x.scalar_type() == at::kFloat, (int)N, (int)H, (int)W, (int)C, (int)OH,
+                         (int)OW, (int)k, (int)s, (int)pad, y.data_ptr(), code.data_ptr<uint8_t>(), cur_stream());
+  return {y, code};
+}
+
+Tensor maxpool_bwd(const Tensor& dy, const Tensor& code, int64_t H, int64_t W, int64_t k, int64_t s, int64_t pad) {
+  TORCH_CHECK(dy.is_cuda() && dy.dim() == 4 && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  (reinterpret_cast<uintptr_t>(dy.data_ptr()) & 15) == 0,
+              "maxpool backward: channels_last 16-B aligned grad");
+  TORCH_CHECK(code.sizes() == dy.sizes() && code.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  code.scalar_type() == at::kByte, "maxpool backward: code");
+  const int64_t N = dy.size(0), C = dy.size(1), OH = dy.size(2), OW = dy.size(3);
+  DevGuard guard(dy.device());
+  Tensor dx = at::empty({N, C, H, W}, dy.options(), at::MemoryFormat::ChannelsLast);
+  grace::maxpool_backward(dy.data_ptr(), code.data_ptr<uint8_t>(), dy.scalar_type() == at::kFloat, (int)N, (int)H,
+                          (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)pad, dx.data_ptr(), cur_stream());
+  return dx;
+}
+
 }  // namespace
 
 void grace_bind_nn(py::module& m) {
+  m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("maxpool_bwd", &maxpool_bwd);
   m.def("bias_act_fwd", &bias_act_fwd);
   m.def("bias_act_bwd", &bias_act_bwd);
   m.def("sgd_step", &sgd_step);

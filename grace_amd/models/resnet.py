@@ -16,6 +16,7 @@ import torch.nn as nn
 
 from ..ops.bnact import BatchNormAct2d
 from ..ops.conv import Conv1x1F32
+from ..ops.pool import MaxPool2dNHWC
 
 
 def _conv3x3(cin, cout, stride=1):
@@ -83,7 +84,7 @@ class ResNet(nn.Module):
             self.maxpool = nn.Identity()
         else:
             self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
-            self.maxpool = nn.MaxPool2d(3, 2, 1)
+            self.maxpool = MaxPool2dNHWC(3, 2, 1)  # 1-byte window codes, gather backward
         self.bn1 = BatchNormAct2d(64, relu=True)
         self.layer1 = self._make(block, 64, layers[0])
         self.layer2 = self._make(block, 128, layers[1], 2)

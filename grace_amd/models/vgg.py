@@ -8,6 +8,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.convact import ConvBiasAct2d
+from ..ops.pool import MaxPool2dNHWC
 
 _CFG16 = [64, 64, "M", 128, 128, "M", 256, 256, 256, "M", 512, 512, 512, "M", 512, 512, 512, "M"]
 
@@ -18,7 +19,7 @@ class VGG(nn.Module):
         layers, c = [], 3
         for v in cfg:
             if v == "M":
-                layers.append(nn.MaxPool2d(2, 2))
+                layers.append(MaxPool2dNHWC(2, 2))
             elif batch_norm:
                 layers += [nn.Conv2d(c, v, 3, padding=1), nn.BatchNorm2d(v), nn.ReLU(inplace=True)]
                 c = v

@@ -3,7 +3,10 @@
 # Used on the GPU box: bash tools/bench_sweep.sh sweep.txt  (each run under its own timeout)
 while IFS= read -r v; do
   [ -z "$v" ] && continue
-  timeout -k 10 300 python bench.py $v > gpurun_out/sweep_last.log 2>&1
+  # leading VAR=VALUE tokens are environment settings for that run (e.g. GRACE_AMD_FORCE_TORCH=1)
+  envs=(); args=()
+  for t in $v; do if [ ${#args[@]} -eq 0 ] && [[ "$t" == *=* ]]; then envs+=("$t"); else args+=("$t"); fi; done
+  env "${envs[@]}" timeout -k 10 300 python bench.py "${args[@]}" > gpurun_out/sweep_last.log 2>&1
   rc=$?
   if [ $rc -ne 0 ]; then echo "$v FAILED rc=$rc"; tail -5 gpurun_out/sweep_last.log; exit 1; fi
   grep '"metric"' gpurun_out/sweep_last.log | python3 -c "

@@ -10,5 +10,7 @@ printf -- "%s\n" "--steps 30 --warmup 10" "--workload resnet50_none --steps 30 -
   "--workload resnet9_dawn --steps 30 --warmup 10" "--workload resnet18_cifar_none --steps 30 --warmup 10" \
   "--dtype bf16 --steps 30 --warmup 10" "--workload vgg16_powersgd --dtype bf16 --steps 20 --warmup 10" \
   "--workload lstm_efsignsgd --dtype bf16 --steps 40 --warmup 10" "--workload bert_qsgd --dtype bf16 --steps 20 --warmup 10" \
+  "GRACE_AMD_FORCE_TORCH=1 --workload resnet50_none --optimizer torch --steps 30 --warmup 10" \
+  "GRACE_AMD_FORCE_TORCH=1 --workload resnet50_none --optimizer torch --graph off --steps 30 --warmup 10" \
   > gpurun_out/sweep_all_r2.txt
 bash tools/bench_sweep.sh gpurun_out/sweep_all_r2.txt
