@@ -9,6 +9,7 @@ examples/dist/CIFAR10-dawndist/README.md:17, 24-26).
 import torch.nn as nn
 
 from ..ops.bnact import BatchNormAct2d
+from ..ops.pool import MaxPool2dNHWC
 
 
 def conv_bn(cin, cout):
@@ -30,9 +31,9 @@ class ResNet9(nn.Module):
         super().__init__()
         self.net = nn.Sequential(
             conv_bn(3, 64),
-            conv_bn(64, 128), nn.MaxPool2d(2), Residual(128),
-            conv_bn(128, 256), nn.MaxPool2d(2),
-            conv_bn(256, 512), nn.MaxPool2d(2), Residual(512),
+            conv_bn(64, 128), MaxPool2dNHWC(2), Residual(128),
+            conv_bn(128, 256), MaxPool2dNHWC(2),
+            conv_bn(256, 512), MaxPool2dNHWC(2), Residual(512),
             nn.AdaptiveMaxPool2d(1), nn.Flatten(), nn.Linear(512, classes, bias=False))
         self.weight = weight
 
