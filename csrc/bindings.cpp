@@ -331,20 +331,34 @@ void qsgd_aggregate(const Tensor& base, int64_t rank_stride, int64_t codes_off, 
                     int64_t n_ranks, double s, double scale, const Tensor& out, bool accumulate, const Tensor& seg,
                     const Tensor& cb, const Tensor& ce, int64_t n_seg, const c10::optional<Tensor>& shared_norms) {
   CHECK_F32(out);
-  const int64_t code_size = code_bytes == 3 ? 2 : code_bytes;  // 3 = fp16 codes
+  // bytes of the code row: 3 = fp16 codes; kPacked2 / kPacked4 = 2- / 4-bit packed codes
+  const int64_t code_row = code_bytes == grace::kPacked2   ? (out.numel() * 2 + 7) / 8
+                           : code_bytes == grace::kPacked4 ? (out.numel() * 4 + 7) / 8
+                           : out.numel() * (code_bytes == 3 ? 2 : code_bytes);
   const float* sn = nullptr;
   if (shared_norms.has_value()) {
     CHECK_F32((*shared_norms));
     TORCH_CHECK(shared_norms->numel() >= n_seg, "shared_norms too small");
     sn = shared_norms->data_ptr<float>();
-    check_rows(base, rank_stride, n_ranks, codes_off + out.numel() * code_size);
+    check_rows(base, rank_stride, n_ranks, codes_off + code_row);
   } else {
-    check_rows(base, rank_stride, n_ranks, std::max(codes_off + out.numel() * code_size, norms_off + 4 * n_seg));
+    check_rows(base, rank_stride, n_ranks, std::max(codes_off + code_row, norms_off + 4 * n_seg));
   }
   auto ct = make_ct(seg, cb, ce);
   DevGuard guard(out.device());
   grace::qsgd_aggregate(ct, base.data_ptr<uint8_t>(), rank_stride, codes_off, norms_off, sn, (int)code_bytes,
                         (int)n_ranks, (float)s, (float)scale, out.data_ptr<float>(), accumulate, cur_stream());
+}
+
+// int8 codes in [-s, s] -> `bits`-bit fields (code + s) of a uint8 row
+void qsgd_pack(const Tensor& codes, int64_t s, int64_t bits, const Tensor& out) {
+  TORCH_CHECK(codes.is_cuda() && codes.scalar_type() == at::kChar && codes.is_contiguous(), "codes: int8 GPU");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kByte && out.is_contiguous(), "out: uint8 GPU");
+  TORCH_CHECK((bits == 2 && s == 1) || (bits == 4 && s >= 1 && s <= 7), "packing: 2 bits for s = 1, 4 bits for s <= 7");
+  TORCH_CHECK(out.numel() >= (codes.numel() * bits + 7) / 8, "out too small");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(out.data_ptr()) % 8 == 0, "out must be 8-B aligned");
+  DevGuard guard(out.device());
+  grace::qsgd_pack(codes.data_ptr<int8_t>(), codes.numel(), (int)s, (int)bits, out.data_ptr<uint8_t>(), cur_stream());
 }
 
 void tern_quantize(const Tensor& x, const Tensor& clips, const Tensor& scal, int64_t seed,
@@ -921,6 +935,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sign_unpack", &sign_unpack);
   m.def("qsgd_quantize", &qsgd_quantize);
   m.def("qsgd_aggregate", &qsgd_aggregate);
+  m.def("qsgd_pack", &qsgd_pack);
+  m.attr("QSGD_PACKED2") = grace::kPacked2;
+  m.attr("QSGD_PACKED4") = grace::kPacked4;
   m.def("tern_quantize", &tern_quantize);
   m.def("tern_aggregate", &tern_aggregate);
   m.def("natural_encode", &natural_encode);

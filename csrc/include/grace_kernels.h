@@ -68,6 +68,10 @@ void sign_unpack(const ChunkTable& ct, const int64_t* seg_start, const int64_t* 
 // ---------------------------------------------------------------- quant.hip
 void qsgd_quantize(const ChunkTable& ct, const float* x, const float* norms, float s, SeedArg seed, void* codes,
                    int code_bytes, float* resid, hipStream_t stream);
+// qsgd_aggregate code_bytes tags of the bit-packed small-s formats (2-bit: s = 1, 4-bit: s <= 7)
+constexpr int kPacked2 = 0x102;
+constexpr int kPacked4 = 0x104;
+void qsgd_pack(const int8_t* codes, int64_t n, int s, int bits, uint8_t* out, hipStream_t stream);
 void qsgd_aggregate(const ChunkTable& ct, const uint8_t* base, int64_t rank_stride, int64_t codes_off,
                     int64_t norms_off, const float* shared_norms, int code_bytes, int n_ranks, float s, float scale,
                     float* out, bool accumulate, hipStream_t stream);

@@ -63,6 +63,26 @@ __global__ __launch_bounds__(kBlock) void qsgd_quant_kernel(ChunkTable ct, const
   }
 }
 
+// Bit-packed QSGD codes for small s (ceil(log2(2s+1)) bits): code + s stored
+// unsigned in B = 2 (s = 1) or 4 (s <= 7) bits, element i at bit (i * B) of the row.
+template <int B>
+struct PackedCode {};
+
+template <typename CodeT>
+struct CodeIO {  // plain int8 / int16 / fp16 / int32 codes
+  static __device__ __forceinline__ float at(const uint8_t* row, int64_t i, float) {
+    return (float)reinterpret_cast<const CodeT*>(row)[i];
+  }
+};
+template <int B>
+struct CodeIO<PackedCode<B>> {
+  static __device__ __forceinline__ float at(const uint8_t* row, int64_t i, float s) {
+    const int64_t bit = i * B;
+    const uint32_t v = (row[bit >> 3] >> (bit & 7)) & ((1u << B) - 1u);
+    return (float)v - s;
+  }
+};
+
 // 4 codes of one rank as floats (one 4/8/16-B load)
 template <typename CodeT>
 __device__ __forceinline__ float4 load_codes4(const CodeT* p) {
@@ -81,6 +101,50 @@ __device__ __forceinline__ float4 load_codes4(const CodeT* p) {
   }
 }
 
+// 4 codes starting at element i (i % 4 == 0) of one rank's code row
+template <typename CodeT>
+__device__ __forceinline__ float4 load4(const uint8_t* row, int64_t i, float) {
+  return load_codes4(reinterpret_cast<const CodeT*>(row) + i);
+}
+template <>
+__device__ __forceinline__ float4 load4<PackedCode<2>>(const uint8_t* row, int64_t i, float s) {
+  const uint32_t v = row[i >> 2];  // 4 x 2-bit codes in one byte
+  return make_float4((float)(v & 3u) - s, (float)((v >> 2) & 3u) - s, (float)((v >> 4) & 3u) - s,
+                     (float)(v >> 6) - s);
+}
+template <>
+__device__ __forceinline__ float4 load4<PackedCode<4>>(const uint8_t* row, int64_t i, float s) {
+  const uint32_t v = *reinterpret_cast<const uint16_t*>(row + (i >> 1));  // 4 x 4-bit codes
+  return make_float4((float)(v & 15u) - s, (float)((v >> 4) & 15u) - s, (float)((v >> 8) & 15u) - s,
+                     (float)(v >> 12) - s);
+}
+
+// Pack int8 codes in [-s, s] into B-bit fields (code + s); thread t handles codes 16t..16t+15.
+template <int B>
+__global__ __launch_bounds__(kBlock) void qsgd_pack_kernel(const int8_t* __restrict__ codes, int64_t n, int s,
+                                                           uint8_t* __restrict__ out) {
+  for (int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x; t * 16 < n; t += (int64_t)gridDim.x * kBlock) {
+    const int64_t i0 = t * 16;
+    uint64_t word = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int64_t i = i0 + j;
+      const uint64_t v = i < n ? (uint64_t)(codes[i] + s) : 0ull;
+      word |= v << (j * B);
+    }
+    // 16 codes -> 16 * B / 8 bytes (4 or 8), byte-granular tail
+    uint8_t* o = out + i0 * B / 8;
+    const int64_t nbytes_all = (n * B + 7) / 8;
+    const int64_t nb = min<int64_t>(16 * B / 8, nbytes_all - i0 * B / 8);
+    if (nb == 16 * B / 8) {
+      if constexpr (B == 2) *reinterpret_cast<uint32_t*>(o) = (uint32_t)word;
+      else *reinterpret_cast<uint64_t*>(o) = word;
+    } else {
+      for (int64_t k = 0; k < nb; ++k) o[k] = (uint8_t)(word >> (8 * k));
+    }
+  }
+}
+
 // out[i] (+)= scale * sum_r norm_r[seg] / s * code_r[i].  `shared_norms` (shared-scale all-reduced
 // codes: one norm for every rank) replaces the per-rank norms of the payload rows.  VEC: the
 // codes and out are 16-B aligned at element 0 (host-checked), so the chunk body runs 4
@@ -89,7 +153,7 @@ template <typename CodeT, bool VEC>
 __global__ __launch_bounds__(kBlock) void qsgd_aggregate_kernel(ChunkTable ct, const uint8_t* __restrict__ base,
                                                                 int64_t rank_stride, int64_t codes_off,
                                                                 int64_t norms_off, const float* __restrict__ shared_norms,
-                                                                int n_ranks, float inv_s, float scale,
+                                                                int n_ranks, float s, float inv_s, float scale,
                                                                 float* __restrict__ out, int accumulate) {
   const int c = blockIdx.x;
   const int sg = ct.seg[c];
@@ -101,8 +165,8 @@ __global__ __launch_bounds__(kBlock) void qsgd_aggregate_kernel(ChunkTable ct, c
   auto scalar = [&](int64_t i) {
     float acc = 0.f;
     for (int r = 0; r < n_ranks; ++r) {
-      const CodeT q = reinterpret_cast<const CodeT*>(base + (int64_t)r * rank_stride + codes_off)[i];
-      acc += norm(r) * inv_s * (float)q;
+      const float q = CodeIO<CodeT>::at(base + (int64_t)r * rank_stride + codes_off, i, s);
+      acc += norm(r) * inv_s * q;
     }
     acc *= scale;
     out[i] = accumulate ? out[i] + acc : acc;
@@ -118,7 +182,7 @@ __global__ __launch_bounds__(kBlock) void qsgd_aggregate_kernel(ChunkTable ct, c
       float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
       for (int r = 0; r < n_ranks; ++r) {
         const float f = norm(r) * inv_s;
-        const float4 q = load_codes4(reinterpret_cast<const CodeT*>(base + (int64_t)r * rank_stride + codes_off) + i);
+        const float4 q = load4<CodeT>(base + (int64_t)r * rank_stride + codes_off, i, s);
         acc.x += f * q.x;
         acc.y += f * q.y;
         acc.z += f * q.z;
@@ -370,17 +434,27 @@ void qsgd_aggregate(const ChunkTable& ct, const uint8_t* base, int64_t rank_stri
     using T = std::remove_pointer_t<decltype(typed)>;
     if (vec)
       qsgd_aggregate_kernel<T, true><<<ct.n_chunks, kBlock, 0, stream>>>(ct, base, rank_stride, codes_off, norms_off,
-                                                                         shared_norms, n_ranks, inv_s, scale, out,
+                                                                         shared_norms, n_ranks, s, inv_s, scale, out,
                                                                          accumulate);
     else
       qsgd_aggregate_kernel<T, false><<<ct.n_chunks, kBlock, 0, stream>>>(ct, base, rank_stride, codes_off, norms_off,
-                                                                          shared_norms, n_ranks, inv_s, scale, out,
+                                                                          shared_norms, n_ranks, s, inv_s, scale, out,
                                                                           accumulate);
   };
   if (code_bytes == 1) go((int8_t*)nullptr);
   else if (code_bytes == 2) go((int16_t*)nullptr);
   else if (code_bytes == 3) go((_Float16*)nullptr);
+  else if (code_bytes == kPacked2) go((PackedCode<2>*)nullptr);
+  else if (code_bytes == kPacked4) go((PackedCode<4>*)nullptr);
   else go((int32_t*)nullptr);
+}
+
+void qsgd_pack(const int8_t* codes, int64_t n, int s, int bits, uint8_t* out, hipStream_t stream) {
+  if (n == 0) return;
+  const int64_t th = (n + 15) / 16;
+  const int grid = (int)std::min<int64_t>((th + kBlock - 1) / kBlock, 4096);
+  if (bits == 2) qsgd_pack_kernel<2><<<grid, kBlock, 0, stream>>>(codes, n, s, out);
+  else qsgd_pack_kernel<4><<<grid, kBlock, 0, stream>>>(codes, n, s, out);
 }
 
 void tern_quantize(const ChunkTable& ct, const int64_t* seg_start, const int64_t* word_off, const float* x,

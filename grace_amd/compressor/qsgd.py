@@ -4,6 +4,10 @@ Reference: /root/reference/grace_dl/dist/compressor/qsgd.py:6-38 -- norm = ||x||
 l = s/norm*|x|, stochastic rounding, q = sign*level stored int8 (s < 128) else fp16; payload
 (q, norm); decompress norm/s*q.
 
+Small s on the gathered path: codes are bit-packed on the wire -- 2 bits for s = 1, 4 bits for
+s <= 7 (ceil(log2(2s+1)) bits, rounded so no code straddles a byte) -- and the
+aggregate kernel decodes the packed rows directly (4x / 2x fewer bytes than int8).
+
 MI355X (csrc/kernels/quant.hip): norms of every segment of a bucket from one statistics pass
 (fused with the residual compensate when paired with ResidualMemory), then one Philox
 quantize pass that also writes the residual; int16 instead of the reference's lossy fp16 for
@@ -67,6 +71,12 @@ class QSGDCompressor(BucketCompressor):
             return torch.int16
         return torch.int32
 
+    @property
+    def pack_bits(self) -> int:
+        """Bit-packed wire codes for small s (2 bits for s = 1, 4 for s <= 7) on the
+        gathered path.  Shared-scale (all-reduced) codes stay whole bytes: they are summed."""
+        return 0 if self.shared_scale else Q.qsgd_pack_bits(self.quantum_num)
+
     def _encode(self, g, ctx, name, memory=None):
         lay = ctx.layout
         W = self.comm.world_size if (self.shared_scale and self.comm is not None) else 1
@@ -74,7 +84,16 @@ class QSGDCompressor(BucketCompressor):
         cdt = torch.int8 if rs else self.code_dtype(W)
         # reduce-scatter mode: codes padded to W equal 16-B chunks (the pad is never decoded)
         ncode = -(-lay.total // (16 * W)) * 16 * W if rs else lay.total
-        codes, norms = self.payload(g.device, [(cdt, (ncode,)), (torch.float32, (lay.n_seg,))])
+        bits = self.pack_bits
+        if bits:
+            # quantize to int8 in a cached scratch, then pack: ceil(n * bits / 8) bytes on the wire
+            codes8 = lay.cached(g.device, "qsgd_codes8", lambda: torch.empty(lay.total, dtype=torch.int8,
+                                                                           device=g.device))
+            packed, norms = self.payload(g.device, [(torch.uint8, ((lay.total * bits + 7) // 8,)),
+                                                    (torch.float32, (lay.n_seg,))])
+            codes = codes8
+        else:
+            codes, norms = self.payload(g.device, [(cdt, (ncode,)), (torch.float32, (lay.n_seg,))])
         r = None
         if memory is None:
             stats = S.segment_stats(g, lay)
@@ -88,6 +107,9 @@ class QSGDCompressor(BucketCompressor):
             self.comm.all_reduce(norms, op="max")
         seed, step = self.next_rng(name, x.device)
         Q.qsgd_quantize(x, lay, norms, self.quantum_num, seed, codes[:lay.total], resid=r, step=step)
+        if bits:
+            Q.qsgd_pack(codes, self.quantum_num, bits, packed)
+            return [packed, norms]
         if self.shared_scale:
             ctx.extra["norms"] = norms
             return [codes]
@@ -125,7 +147,8 @@ class QSGDCompressor(BucketCompressor):
         out = self.out_buffer(ctx, base.device)
         # shared-scale payloads carry codes only: every row is decoded against the shared norms
         Q.qsgd_aggregate(base, stride, offs[0], offs[1] if norms is None else 0, per_rank[0][0].dtype, n_ranks,
-                         self.quantum_num, ctx.layout, out, scale, shared_norms=norms)
+                         self.quantum_num, ctx.layout, out, scale, shared_norms=norms,
+                         packed_bits=self.pack_bits if per_rank[0][0].dtype == torch.uint8 else 0)
         return self.finish(out, ctx)
 
     def decompress_aggregate_impl(self, per_rank, ctx, n_ranks, scale):

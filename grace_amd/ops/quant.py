@@ -70,13 +70,49 @@ def qsgd_quantize(x: torch.Tensor, layout: SegmentLayout, norms: torch.Tensor, s
         resid.copy_(x - nrm / s * code)
 
 
+def qsgd_pack_bits(s: int) -> int:
+    """Bits per bit-packed code (ceil(log2(2s+1)), rounded to 2 or 4 so codes never
+    straddle a byte): 2 for s = 1, 4 for s <= 7, 0 = no packing (int8 / wider codes)."""
+    return 2 if s == 1 else (4 if 1 < s <= 7 else 0)
+
+
+def qsgd_pack(codes: torch.Tensor, s: int, bits: int, out: torch.Tensor) -> None:
+    """int8 codes in [-s, s] -> ``bits``-bit fields (code + s), element i at bit i*bits of ``out``."""
+    if _native.use_native(codes):
+        _native.lib().qsgd_pack(codes, int(s), int(bits), out)
+        return
+    n = codes.numel()
+    per = 8 // bits
+    v = (codes.to(torch.int32) + s)
+    pad = (-n) % per
+    if pad:
+        v = torch.cat([v, torch.zeros(pad, dtype=torch.int32, device=v.device)])
+    v = v.view(-1, per)
+    shifts = torch.arange(per, device=v.device, dtype=torch.int32) * bits
+    packed = (v << shifts).sum(1).to(torch.uint8)
+    out[:packed.numel()].copy_(packed)
+
+
+def _unpack(row: torch.Tensor, n: int, s: int, bits: int) -> torch.Tensor:
+    per = 8 // bits
+    b = row[: (n * bits + 7) // 8].to(torch.int32)
+    shifts = torch.arange(per, device=row.device, dtype=torch.int32) * bits
+    v = ((b.unsqueeze(1) >> shifts) & ((1 << bits) - 1)).reshape(-1)[:n]
+    return (v - s).float()
+
+
 def qsgd_aggregate(base, rank_stride, codes_off, norms_off, code_dtype, n_ranks, s, layout, out, scale,
-                   accumulate=False, shared_norms=None):
+                   accumulate=False, shared_norms=None, packed_bits: int = 0):
     """Decode-sum of W payload rows.  ``shared_norms``: the shared-scale variant's all-reduced
-    norms, used for every row (the rows then carry codes only; ``norms_off`` is ignored)."""
+    norms, used for every row (the rows then carry codes only; ``norms_off`` is ignored).
+    ``packed_bits`` (2 / 4): the rows carry bit-packed codes (``qsgd_pack``)."""
     if _native.use_native(out):
         t = _tables(layout, out.device)
-        esz = 3 if code_dtype == torch.float16 else torch.empty((), dtype=code_dtype).element_size()
+        if packed_bits:
+            C = _native.lib()
+            esz = C.QSGD_PACKED2 if packed_bits == 2 else C.QSGD_PACKED4
+        else:
+            esz = 3 if code_dtype == torch.float16 else torch.empty((), dtype=code_dtype).element_size()
         _native.lib().qsgd_aggregate(base, rank_stride, codes_off, norms_off, esz, n_ranks, float(s), scale, out,
                                      accumulate, t["seg"], t["begin"], t["end"], layout.n_seg, shared_norms)
         return
@@ -84,7 +120,10 @@ def qsgd_aggregate(base, rank_stride, codes_off, norms_off, code_dtype, n_ranks,
     acc = torch.zeros(layout.total, dtype=torch.float32, device=out.device)
     for r in range(n_ranks):
         row = base[r * rank_stride:]
-        q = row[codes_off:codes_off + esz * layout.total].view(code_dtype).float()
+        if packed_bits:
+            q = _unpack(row[codes_off:], layout.total, s, packed_bits)
+        else:
+            q = row[codes_off:codes_off + esz * layout.total].view(code_dtype).float()
         nrm = shared_norms if shared_norms is not None else row[norms_off:norms_off + 4 * layout.n_seg].view(torch.float32)
         acc += expand(nrm, layout) / s * q
     acc *= scale

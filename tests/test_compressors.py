@@ -327,3 +327,21 @@ def test_qsgd_code_dtypes_are_reducible():
     assert c.code_dtype(2) == torch.float16 and c.code_dtype(8) == torch.float16  # 1016 <= 2048: exact
     assert c.code_dtype(32) == torch.int32
     assert QSGDCompressor(15, shared_scale=True).code_dtype(8) == torch.int8
+
+
+@pytest.mark.parametrize("s,bits", [(1, 2), (3, 4), (7, 4)])
+def test_qsgd_small_s_codes_are_bit_packed(s, bits):
+    """s = 1 -> 2-bit, s <= 7 -> 4-bit codes on the wire; decoding the packed payload gives
+    exactly the int8-code result (same rounding stream)."""
+    class Unpacked(Z.QSGDCompressor):
+        @property
+        def pack_bits(self):
+            return 0
+
+    x = _x(4001)
+    cp, cu = Z.QSGDCompressor(s), Unpacked(s)
+    tp, ctxp = cp.compress(x, "w")
+    tu, ctxu = cu.compress(x, "w")
+    assert tp[0].dtype == torch.uint8 and tp[0].numel() == (x.numel() * bits + 7) // 8
+    assert tu[0].dtype == torch.int8
+    torch.testing.assert_close(cp.decompress(tp, ctxp), cu.decompress(tu, ctxu), rtol=0, atol=0)

@@ -112,6 +112,10 @@ def _body(rank, world, device="cpu"):
         out = run({"compressor": "qsgd", "quantum_num": 15, "communicator": comm}, "q")
         bound = max(t.norm() for t in xs) / 15
         assert (out - mean).abs().max() <= bound * (1 + 1e-4)
+    # small s on the gathered path: 2-bit (s = 1) / 4-bit (s = 3) packed codes on the wire
+    for s_ in (1, 3):
+        out = run({"compressor": "qsgd", "quantum_num": s_, "communicator": "allgather"}, f"qp{s_}")
+        assert (out - mean).abs().max() <= max(t.norm() for t in xs) / s_ * (1 + 1e-4)
     # s = 127 (BASELINE BERT config): int8 codes all-to-all + int16 level sums all-gathered
     # (compressed-domain reduce-scatter), bit-identical to the all-reduce of fp16 integer levels
     out = run({"compressor": "qsgd", "quantum_num": 127, "communicator": "allreduce"}, "q127")

@@ -395,3 +395,29 @@ def test_gram_orthonormalize_ranks_gpu(rank, passes_for):
         got = b[off:off + ln * r].view(ln, r).double()
         assert (got.t() @ got - torch.eye(r, dtype=torch.float64)).abs().max() < 1e-5
         torch.testing.assert_close(got.float(), ref[off:off + ln * r].view(ln, r), rtol=1e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("s,bits", [(1, 2), (3, 4), (7, 4)])
+def test_qsgd_packed_codes_gpu(s, bits):
+    """Native pack + packed-row decode (csrc/kernels/quant.hip qsgd_pack_kernel, PackedCode<B>)
+    equals the int8-code native path bit for bit, and the CPU torch path's packing."""
+    from grace_amd import compressor as Z
+
+    class Unpacked(Z.QSGDCompressor):
+        @property
+        def pack_bits(self):
+            return 0
+
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(100003, generator=g).cuda()
+    cp, cu = Z.QSGDCompressor(s), Unpacked(s)
+    tp, ctxp = cp.compress(x, "w")
+    tu, ctxu = cu.compress(x, "w")
+    assert tp[0].dtype == torch.uint8 and tp[0].numel() == (x.numel() * bits + 7) // 8
+    torch.testing.assert_close(cp.decompress(tp, ctxp), cu.decompress(tu, ctxu), rtol=0, atol=0)
+    # the packed bytes equal the torch reference packing of the same int8 codes
+    from grace_amd.ops import quant as Q
+    codes = tu[0][: x.numel()].cpu()
+    ref_cpu = torch.zeros(tp[0].numel(), dtype=torch.uint8)
+    Q.qsgd_pack(codes, s, bits, ref_cpu)
+    assert torch.equal(tp[0].cpu(), ref_cpu)

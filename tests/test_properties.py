@@ -94,7 +94,7 @@ def test_randomk_properties_cpu(sizes, seed, ratio):
     _check_randomk(x, lay, ratio, "cpu")
 
 
-@given(LAYOUTS, st.integers(0, 10_000), st.sampled_from([4, 64, 127]))
+@given(LAYOUTS, st.integers(0, 10_000), st.sampled_from([1, 4, 7, 64, 127]))
 @settings(**SETTINGS)
 def test_qsgd_error_bound_cpu(sizes, seed, s):
     x, lay = _bucket(sizes, seed)
@@ -127,7 +127,7 @@ def test_randomk_properties_gpu(sizes, seed, ratio):
 
 
 @pytest.mark.gpu
-@given(LAYOUTS, st.integers(0, 10_000), st.sampled_from([4, 64, 127]))
+@given(LAYOUTS, st.integers(0, 10_000), st.sampled_from([1, 4, 7, 64, 127]))
 @settings(**SETTINGS)
 def test_qsgd_error_bound_gpu(sizes, seed, s):
     x, lay = _bucket(sizes, seed)
