@@ -188,6 +188,14 @@ void bn_act_backward(const void* dy, const void* dy2, const void* x, bool fp32, 
                      int C, const float* gamma, const float* save, bool relu, float* dgamma, float* dbeta,
                      float* coef, float* ws, void* dx, void* dres, hipStream_t stream);
 
+// BN + ReLU + max pool (k x k, stride s, padding pad) over NHWC x: stats + one normalise/ReLU/pool
+// pass (pooled y [N, OH, OW, C], 1-byte in-window argmax code per pooled element).  Backward:
+// maxpool_backward, then bn_act_backward with relu_mask == nullptr (mask recomputed from x)
+void bn_act_pool_forward(const void* x, bool fp32, int N, int H, int W, int C, const float* gamma, const float* beta,
+                         float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps, int k,
+                         int s, int pad, int OH, int OW, float* save, float* ws, void* y, uint8_t* code,
+                         hipStream_t stream);
+
 // conv bias (+ ReLU) over [M, C] channels_last rows (same channel constraints as BN):
 // y = act(x + bias); backward dz = dy * [y > 0] and dbias = Σ_rows dz in ONE pass (ws as BN)
 void bias_act_forward(const void* x, const float* bias, bool fp32, int64_t M, int C, bool relu, void* y,

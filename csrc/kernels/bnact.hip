@@ -431,25 +431,35 @@ __device__ __forceinline__ void add8(Bf8& d, const T* p) {
   for (int j = 0; j < 8; ++j) d.v[j] += e.v[j];
 }
 
-template <typename T, bool RELU, bool DY2>
+// RX (with RELU): no saved mask -- the ReLU mask is recomputed from x as fmaf(x, scale, shift)
+// > 0, the exact expression the forward apply thresholds (the fused stem's forward writes no
+// mask: ops/bnact.py bn_relu_maxpool).
+template <typename T, bool RELU, bool DY2, bool RX = false>
 __global__ __launch_bounds__(kB) void bn_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ dy2,
                                                        const T* __restrict__ x,
                                                        const uint8_t* __restrict__ mask, Red R, GradOut o) {
-  float s1[8], s2[8], mu[8];
+  float s1[8], s2[8], mu[8], rsc[8], rsh[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = mu[j] = 0.f;
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = mu[j] = rsc[j] = rsh[j] = 0.f;
   {
     const int cg = threadIdx.x % R.tprp;
     if (cg < R.CT / 8) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) mu[j] = o.save[blockIdx.y * R.CT + cg * 8 + j];
+      for (int j = 0; j < 8; ++j) {
+        mu[j] = o.save[blockIdx.y * R.CT + cg * 8 + j];
+        if constexpr (RX) {
+          rsc[j] = o.save[2 * R.C + blockIdx.y * R.CT + cg * 8 + j];
+          rsh[j] = o.save[3 * R.C + blockIdx.y * R.CT + cg * 8 + j];
+        }
+      }
     }
   }
   auto acc = [&](const Bf8& d, const Bf8& v, uint32_t mb) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float dz = d.v[j];
-      if constexpr (RELU) dz = (mb >> j) & 1u ? dz : 0.f;
+      if constexpr (RELU && RX) dz = fmaf(v.v[j], rsc[j], rsh[j]) > 0.f ? dz : 0.f;
+      else if constexpr (RELU) dz = (mb >> j) & 1u ? dz : 0.f;
       s1[j] += dz;
       s2[j] = fmaf(dz, v.v[j] - mu[j], s2[j]);
     }
@@ -473,7 +483,7 @@ __global__ __launch_bounds__(kB) void bn_reduce_kernel(const T* __restrict__ dy,
       for (int u = 0; u < 4; ++u) {
         d[u] = bld8<T>(rdy, vo, u * so);
         v[u] = bld8<T>(rx, vo, u * so);
-        if constexpr (RELU) w[u] = mask[(e + u * step) >> 3];
+        if constexpr (RELU && !RX) w[u] = mask[(e + u * step) >> 3];
       }
       if constexpr (DY2) {
         Bf8 d2[4];
@@ -491,7 +501,7 @@ __global__ __launch_bounds__(kB) void bn_reduce_kernel(const T* __restrict__ dy,
       const Bf8 v = ld8(x + e);
       if constexpr (DY2) add8(d, dy2 + e);
       uint32_t w = 0;
-      if constexpr (RELU) w = mask[e >> 3];
+      if constexpr (RELU && !RX) w = mask[e >> 3];
       acc(d, v, w);
     }
   });
@@ -515,29 +525,34 @@ __global__ __launch_bounds__(kB) void bn_reduce_kernel(const T* __restrict__ dy,
   }
 }
 
-template <typename T, bool RELU, bool RES, bool DY2>
+template <typename T, bool RELU, bool RES, bool DY2, bool RX = false>
 __global__ __launch_bounds__(kB) void bn_dx_kernel(const T* __restrict__ dy, const T* __restrict__ dy2,
                                                    const T* __restrict__ x,
                                                    const uint8_t* __restrict__ mask, const float* __restrict__ coef,
                                                    T* __restrict__ dx, T* __restrict__ dres,
-                                                   int64_t n_vec, int C) {
+                                                   int64_t n_vec, int C, const float* __restrict__ save = nullptr) {
   const int tpr = C >> 3;
   const int64_t stride = (int64_t)gridDim.x * kB;
   int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x;
   const int cg = (int)(i % tpr);
-  float ca[8], cb[8], cc[8];
+  float ca[8], cb[8], cc[8], rsc[8], rsh[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     ca[j] = coef[cg * 8 + j];
     cb[j] = coef[C + cg * 8 + j];
     cc[j] = coef[2 * C + cg * 8 + j];
+    rsc[j] = RX ? save[2 * C + cg * 8 + j] : 0.f;
+    rsh[j] = RX ? save[3 * C + cg * 8 + j] : 0.f;
   }
   for (; i < n_vec; i += stride) {
     Bf8 d = ld8(dy + i * 8);
     const Bf8 v = ld8(x + i * 8);
     if constexpr (DY2) add8(d, dy2 + i * 8);
     float dz[8], o[8];
-    if constexpr (RELU) {
+    if constexpr (RELU && RX) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dz[j] = fmaf(v.v[j], rsc[j], rsh[j]) > 0.f ? d.v[j] : 0.f;
+    } else if constexpr (RELU) {
       const uint32_t mb = mask[i];
 #pragma unroll
       for (int j = 0; j < 8; ++j) dz[j] = (mb >> j) & 1u ? d.v[j] : 0.f;
@@ -614,6 +629,66 @@ __global__ __launch_bounds__(kB) void bias_act_bwd_kernel(const T* __restrict__ 
   if (!block_reduce_tree(R, s, s)) return;
   const double* total = R.total + (size_t)blockIdx.y * 2 * R.CT;
   for (int cl = threadIdx.x; cl < R.CT; cl += kB) dbias[blockIdx.y * R.CT + cl] = (float)total[cl];
+}
+
+// ---------------------------------------------------------------- BN + ReLU + max pool (stem)
+// The ResNet stem runs conv -> BN -> ReLU -> 3x3/2 max pool: the BN output (the largest
+// activation of the network, 103 MB fp32 at batch 32) is written only to be re-read by the pool,
+// Fused forward = stats + ONE pass that normalises, applies the ReLU and pools straight from x
+// (writes the pooled tensor and a 1-byte in-window argmax per pooled element; no BN output, no
+// ReLU mask).  Backward = the gather max-pool backward (pool.hip) + the two BN passes with the
+// ReLU mask recomputed from x (RX).  (Gathering dz inside the BN passes instead was measured
+// slower: 159 vs 94 us -- per-row dependent code/gradient loads serialise the reduction.)
+// Pool semantics as ops/pool.py.
+struct PoolShape {
+  int H, W, OH, OW, k, s, pad;
+};
+
+template <typename T>
+__global__ __launch_bounds__(kB) void bn_pool_apply_kernel(const T* __restrict__ x, const float* __restrict__ save,
+                                                           T* __restrict__ y, uint8_t* __restrict__ code, PoolShape g,
+                                                           int C, int64_t n_vec) {
+  const int cv = C >> 3;
+  for (int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x; i < n_vec; i += (int64_t)gridDim.x * kB) {
+    const int c8 = (int)(i % cv);
+    const int64_t pix = i / cv;
+    const int ow = (int)(pix % g.OW);
+    const int oh = (int)((pix / g.OW) % g.OH);
+    const int64_t n = pix / ((int64_t)g.OW * g.OH);
+    float sc[8], sh[8], m[8];
+    uint32_t arg[8];
+    const int h0 = oh * g.s - g.pad, w0 = ow * g.s - g.pad;
+    const uint32_t first = (uint32_t)(max(0, -h0) * g.k + max(0, -w0));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sc[j] = save[2 * C + c8 * 8 + j];
+      sh[j] = save[3 * C + c8 * 8 + j];
+      m[j] = -INFINITY;
+      arg[j] = first;
+    }
+    for (int kh = 0; kh < g.k; ++kh) {
+      const int h = h0 + kh;
+      if (h < 0 || h >= g.H) continue;
+      for (int kw = 0; kw < g.k; ++kw) {
+        const int w = w0 + kw;
+        if (w < 0 || w >= g.W) continue;
+        const Bf8 v = ld8(x + (((n * g.H + h) * g.W + w) * C + c8 * 8));
+        const uint32_t pos = (uint32_t)(kh * g.k + kw);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float o = fmaxf(fmaf(v.v[j], sc[j], sh[j]), 0.f);
+          const bool take = (o > m[j]) || (o != o);
+          m[j] = take ? o : m[j];
+          arg[j] = take ? pos : arg[j];
+        }
+      }
+    }
+    st8(y + i * 8, m);
+    uint2 packed;
+    packed.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
+    packed.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24);
+    *reinterpret_cast<uint2*>(code + i * 8) = packed;
+  }
 }
 
 // ---------------------------------------------------------------- single-launch variants
@@ -1210,10 +1285,30 @@ void backward_2k_t(const T* dy, const T* dy2, const T* x, const uint8_t* mask, i
                        dx, dres, n_vec, C);
 }
 
+// ReLU without a saved mask (recomputed from x and the forward's scale / shift in o.save)
+template <typename T>
+void backward_2k_rx(const T* dy, const T* x, int64_t M, int C, const GradOut& o, const float* coef, float* ws, T* dx,
+                    T* dres, hipStream_t stream) {
+  Red R = plan(M, C);
+  bind_ws(R, ws, stream);
+  hipLaunchKernelGGL((bn_reduce_kernel<T, true, false, true>), dim3(R.nchunks, C / R.CT), dim3(kB), 0, stream, dy,
+                     (const T*)nullptr, x, (const uint8_t*)nullptr, R, o);
+  const int64_t n_vec = M * C / 8;
+  const int gb = apply_grid(n_vec, C);
+  if (dres)
+    hipLaunchKernelGGL((bn_dx_kernel<T, true, true, false, true>), dim3(gb), dim3(kB), 0, stream, dy, (const T*)nullptr,
+                       x, (const uint8_t*)nullptr, coef, dx, dres, n_vec, C, o.save);
+  else
+    hipLaunchKernelGGL((bn_dx_kernel<T, true, false, false, true>), dim3(gb), dim3(kB), 0, stream, dy,
+                       (const T*)nullptr, x, (const uint8_t*)nullptr, coef, dx, dres, n_vec, C, o.save);
+}
+
 template <typename T>
 void backward_2k(const T* dy, const T* dy2, const T* x, const uint8_t* mask, int64_t M, int C, const GradOut& o,
                  bool relu, const float* coef, float* ws, T* dx, T* dres, hipStream_t stream) {
-  if (dy2)
+  if (relu && mask == nullptr && dy2 == nullptr)
+    backward_2k_rx<T>(dy, x, M, C, o, coef, ws, dx, dres, stream);
+  else if (dy2)
     backward_2k_t<T, true>(dy, dy2, x, mask, M, C, o, relu, coef, ws, dx, dres, stream);
   else
     backward_2k_t<T, false>(dy, dy2, x, mask, M, C, o, relu, coef, ws, dx, dres, stream);
@@ -1272,7 +1367,8 @@ void bn_act_backward(const void* dyv, const void* dy2v, const void* xv, bool fp3
   const uint16_t* x = static_cast<const uint16_t*>(xv);
   uint16_t* dx = static_cast<uint16_t*>(dxv);
   uint16_t* dres = static_cast<uint16_t*>(dresv);
-  const int v = dy2 ? 0 : pick_fused_v(M, C, true);  // the single-launch variant reads one dy
+  // the single-launch variant reads one dy and a saved mask
+  const int v = (dy2 || (relu && mask == nullptr)) ? 0 : pick_fused_v(M, C, true);
   if (v) {
     Red R = plan(M, C, v);
     bind_ws(R, ws, stream);
@@ -1337,5 +1433,32 @@ void bias_act_backward(const void* dy, const void* y, bool fp32, int64_t M, int 
     bias_bwd_t(static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(y), M, C, relu, dbias, ws,
                static_cast<uint16_t*>(dz), stream);
 }
+
+namespace {
+template <typename T>
+void pool_fwd_t(const T* x, int64_t M, int C, const StatsOut& o, float* save, float* ws, const PoolShape& g, int N,
+                T* y, uint8_t* code, hipStream_t stream) {
+  Red R = plan(M, C);
+  bind_ws(R, ws, stream);
+  hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(R.nchunks, C / R.CT), dim3(kB), 0, stream, x, R, o);
+  const int64_t n_vec = (int64_t)N * g.OH * g.OW * (C / 8);
+  const int gb = (int)std::min<int64_t>((n_vec + kB - 1) / kB, 8192);
+  hipLaunchKernelGGL(bn_pool_apply_kernel<T>, dim3(gb), dim3(kB), 0, stream, x, save, y, code, g, C, n_vec);
+}
+}  // namespace
+
+void bn_act_pool_forward(const void* x, bool fp32, int N, int H, int W, int C, const float* gamma, const float* beta,
+                         float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps, int k,
+                         int s, int pad, int OH, int OW, float* save, float* ws, void* y, uint8_t* code,
+                         hipStream_t stream) {
+  StatsOut o{gamma, beta, running_mean, running_var, nbt, momentum, eps, save};
+  const PoolShape g{H, W, OH, OW, k, s, pad};
+  const int64_t M = (int64_t)N * H * W;
+  if (fp32)
+    pool_fwd_t(static_cast<const float*>(x), M, C, o, save, ws, g, N, static_cast<float*>(y), code, stream);
+  else
+    pool_fwd_t(static_cast<const uint16_t*>(x), M, C, o, save, ws, g, N, static_cast<uint16_t*>(y), code, stream);
+}
+
 
 }  // namespace grace

@@ -83,11 +83,14 @@ std::vector<Tensor> bn_act_bwd(const Tensor& dy, const c10::optional<Tensor>& dy
   same_layout(x, dy, "grad_output");
   const bool two = dy2.has_value() && dy2->defined();
   if (two) same_layout(x, *dy2, "second grad_output");
-  if (relu) {
-    TORCH_CHECK(mask.has_value() && mask->defined() && mask->is_cuda() && mask->scalar_type() == at::kByte &&
-                    mask->is_contiguous() && mask->numel() == M * C / 8,
-                "relu backward needs the forward's [M*C/8] uint8 mask");
+  const bool has_mask = mask.has_value() && mask->defined();
+  if (relu && has_mask) {
+    TORCH_CHECK(mask->is_cuda() && mask->scalar_type() == at::kByte && mask->is_contiguous() &&
+                    mask->numel() == M * C / 8,
+                "relu backward: the forward's mask must be [M*C/8] uint8");
   }
+  // relu without a mask: recomputed from x and save (scale, shift); one dy only
+  TORCH_CHECK(!(relu && !has_mask && dy2.has_value() && dy2->defined()), "maskless relu backward takes one dy");
   TORCH_CHECK(save.is_cuda() && save.scalar_type() == at::kFloat && save.numel() == 4 * C, "save");
   DevGuard guard(x.device());
   auto f32 = x.options().dtype(at::kFloat);
@@ -98,7 +101,7 @@ std::vector<Tensor> bn_act_bwd(const Tensor& dy, const c10::optional<Tensor>& dy
   Tensor coef = at::empty({3 * C}, f32);
   Tensor ws = at::empty({grace::bn_workspace_floats(M, (int)C)}, f32);
   grace::bn_act_backward(dy.data_ptr(), two ? dy2->data_ptr() : nullptr, x.data_ptr(), x.scalar_type() == at::kFloat,
-                         relu ? mask->data_ptr<uint8_t>() : nullptr, M, (int)C,
+                         relu && has_mask ? mask->data_ptr<uint8_t>() : nullptr, M, (int)C,
                          opt_f32(weight, C, "weight"), save.data_ptr<float>(), relu,
                          want_dweight ? dg.data_ptr<float>() : nullptr, want_dweight ? db.data_ptr<float>() : nullptr,
                          coef.data_ptr<float>(), ws.data_ptr<float>(), dx.data_ptr(),
@@ -174,6 +177,39 @@ std::vector<Tensor> bias_act_bwd(const Tensor& dy, const Tensor& y, bool relu) {
   return {dz, db};
 }
 
+// BN (training statistics, running stats) + ReLU + k x k max pool over channels_last x.
+// returns (pooled y, save[4C], code)
+std::vector<Tensor> bn_act_pool_fwd(const Tensor& x, const c10::optional<Tensor>& weight,
+                                    const c10::optional<Tensor>& bias, const c10::optional<Tensor>& running_mean,
+                                    const c10::optional<Tensor>& running_var, const c10::optional<Tensor>& nbt,
+                                    double momentum, double eps, int64_t k, int64_t s, int64_t pad) {
+  int64_t M, C;
+  check_rows(x, "x", &M, &C);
+  TORCH_CHECK(x.dim() == 4 && k >= 1 && k <= 15 && s >= 1 && pad >= 0 && 2 * pad <= k, "bn+pool: NHWC x, k <= 15");
+  const int64_t N = x.size(0), H = x.size(2), W = x.size(3);
+  const int64_t OH = (H + 2 * pad - k) / s + 1, OW = (W + 2 * pad - k) / s + 1;
+  TORCH_CHECK(OH > 0 && OW > 0, "bn+pool: empty output");
+  float* rm = const_cast<float*>(opt_f32(running_mean, C, "running_mean"));
+  float* rv = const_cast<float*>(opt_f32(running_var, C, "running_var"));
+  TORCH_CHECK((rm == nullptr) == (rv == nullptr), "running_mean / running_var: both or neither");
+  int64_t* nb = nullptr;
+  if (nbt.has_value() && nbt->defined()) {
+    TORCH_CHECK(nbt->is_cuda() && nbt->scalar_type() == at::kLong && nbt->numel() == 1, "num_batches_tracked");
+    nb = nbt->data_ptr<int64_t>();
+  }
+  DevGuard guard(x.device());
+  auto f32 = x.options().dtype(at::kFloat);
+  Tensor y = at::empty({N, C, OH, OW}, x.options(), at::MemoryFormat::ChannelsLast);
+  Tensor code = at::empty({N, C, OH, OW}, x.options().dtype(at::kByte), at::MemoryFormat::ChannelsLast);
+  Tensor save = at::empty({4 * C}, f32);
+  Tensor ws = at::empty({grace::bn_workspace_floats(M, (int)C)}, f32);
+  grace::bn_act_pool_forward(x.data_ptr(), x.scalar_type() == at::kFloat, (int)N, (int)H, (int)W, (int)C,
+                             opt_f32(weight, C, "weight"), opt_f32(bias, C, "bias"), rm, rv, nb, (float)momentum,
+                             (float)eps, (int)k, (int)s, (int)pad, (int)OH, (int)OW, save.data_ptr<float>(),
+                             ws.data_ptr<float>(), y.data_ptr(), code.data_ptr<uint8_t>(), cur_stream());
+  return {y, save, code};
+}
+
 // NHWC max pooling: returns (y, code) -- code = uint8 in-window argmax per output element
 std::vector<Tensor> maxpool_fwd(const Tensor& x, int64_t k, int64_t s, int64_t pad) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast) &&
@@ -210,6 +246,7 @@ Tensor maxpool_bwd(const Tensor& dy, const Tensor& code, int64_t H, int64_t W, i
 
 void grace_bind_nn(py::module& m) {
   m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("bn_act_pool_fwd", &bn_act_pool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("bias_act_fwd", &bias_act_fwd);
   m.def("bias_act_bwd", &bias_act_bwd);

@@ -14,7 +14,7 @@ from typing import List, Type, Union
 import torch
 import torch.nn as nn
 
-from ..ops.bnact import BatchNormAct2d
+from ..ops.bnact import BatchNormAct2d, bn_relu_maxpool
 from ..ops.conv import Conv1x1F32
 from ..ops.pool import MaxPool2dNHWC
 
@@ -110,7 +110,8 @@ class ResNet(nn.Module):
         return nn.Sequential(*blocks)
 
     def forward(self, x):
-        x = self.maxpool(self.bn1(self.conv1(x)))
+        # stem: BN + ReLU + max pool fused (the BN output is never written; ops/bnact.py)
+        x = bn_relu_maxpool(self.conv1(x), self.bn1, self.maxpool)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         if isinstance(x, tuple):
             x = x[0]

@@ -119,3 +119,49 @@ class BatchNormAct2d(nn.BatchNorm2d):
 
     def extra_repr(self) -> str:
         return super().extra_repr() + (", relu=True" if self.relu else "")
+
+
+class _BNActPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, nbt, momentum, eps, k, s, pad):
+        y, save, code = _native.lib().bn_act_pool_fwd(x, weight, bias, running_mean, running_var, nbt,
+                                                      float(momentum), float(eps), k, s, pad)
+        ctx.geom = (k, s, pad)
+        ctx.save_for_backward(x, code, weight, save)
+        return y
+
+    @staticmethod
+    def backward(ctx, dp):
+        x, code, weight, save = ctx.saved_tensors
+        k, s, pad = ctx.geom
+        if not dp.is_contiguous(memory_format=torch.channels_last) or dp.data_ptr() % 16:
+            dp = dp.contiguous(memory_format=torch.channels_last)
+            if dp.data_ptr() % 16:
+                dp = dp.clone(memory_format=torch.channels_last)
+        C = _native.lib()
+        dy = C.maxpool_bwd(dp, code, x.shape[2], x.shape[3], k, s, pad)  # gradient of relu(bn(x))
+        want_w = weight is not None and ctx.needs_input_grad[1]
+        # mask None: the ReLU mask is recomputed from x and save's scale / shift
+        dx, _, dw, db = C.bn_act_bwd(dy, None, x, None, weight, save, True, False, want_w)
+        return (dx, dw if want_w else None, db if want_w and ctx.needs_input_grad[2] else None,
+                None, None, None, None, None, None, None, None)
+
+
+def bn_relu_maxpool(x: torch.Tensor, bn: "BatchNormAct2d", pool: nn.MaxPool2d) -> torch.Tensor:
+    """``pool(relu(bn(x)))`` -- the ResNet stem -- as stats + ONE normalise/ReLU/pool pass forward
+    (the 103 MB BN output and its ReLU mask are never written; csrc/kernels/bnact.hip
+    bn_pool_apply_kernel); backward = the gather max-pool backward + the BN backward with the
+    ReLU mask recomputed from x.  Other configurations run ``pool(bn(x))`` through the modules."""
+    from .pool import MaxPool2dNHWC
+
+    training = bn.training or not bn.track_running_stats
+    if (training and bn.relu and isinstance(pool, MaxPool2dNHWC) and pool._native_ok(x)
+            and _fusable(x, bn, None)):
+        k = pool.kernel_size if isinstance(pool.kernel_size, int) else pool.kernel_size[0]
+        st = pool.stride if isinstance(pool.stride, int) else (pool.stride or pool.kernel_size)[0]
+        pd = pool.padding if isinstance(pool.padding, int) else pool.padding[0]
+        track = bn.training and bn.track_running_stats
+        return _BNActPoolFn.apply(x, bn.weight, bn.bias, bn.running_mean if track else None,
+                                  bn.running_var if track else None, bn.num_batches_tracked if track else None,
+                                  bn.momentum if bn.momentum is not None else 0.0, bn.eps, k, st, pd)
+    return pool(bn(x))

@@ -255,3 +255,39 @@ def test_bnact_dual_output_grads(dtype, shape):
     xr = x.detach().clone().requires_grad_(True)
     m(xr, res).backward(dy)
     torch.testing.assert_close(xg.grad.float(), xr.grad.float(), **tol)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape,k,s,p", [((4, 64, 56, 56), 3, 2, 1), ((2, 64, 15, 17), 3, 2, 1),
+                                         ((2, 128, 8, 8), 2, 2, 0)])
+def test_bn_relu_maxpool_fused_matches_reference(shape, k, s, p, dtype):
+    """ResNet stem fusion (ops/bnact.py bn_relu_maxpool): pool(relu(bn(x))) forward and the
+    gathered backward vs the fp32 PyTorch ops; running statistics updated as nn.BatchNorm2d."""
+    from grace_amd.ops.bnact import bn_relu_maxpool
+    from grace_amd.ops.pool import MaxPool2dNHWC
+
+    m, x, _, _ = _case(*shape, relu=True, with_res=False, seed=4, dtype=dtype)
+    pool = MaxPool2dNHWC(k, s, p)
+    xa = x.detach().clone().requires_grad_(True)
+    y = bn_relu_maxpool(xa, m, pool)
+    xr = x.detach().float().requires_grad_(True)
+    w = m.weight.detach().clone().requires_grad_(True)
+    b = m.bias.detach().clone().requires_grad_(True)
+    rm, rv = torch.zeros_like(m.running_mean), torch.ones_like(m.running_var)
+    yr = F.max_pool2d(F.relu(F.batch_norm(xr, rm, rv, w, b, True, m.momentum, m.eps)), k, s, p)
+    tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(y.float(), yr, **tol)
+    torch.testing.assert_close(m.running_mean, rm, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(m.running_var, rv, rtol=1e-4, atol=1e-5)
+    g = torch.Generator(device="cpu").manual_seed(8)
+    dy = torch.randn(yr.shape, generator=g).to(DEV, dtype).contiguous(memory_format=torch.channels_last)
+    y.backward(dy)
+    yr.backward(dy.float())
+    if dtype == torch.float32:
+        torch.testing.assert_close(xa.grad, xr.grad, rtol=1e-3, atol=1e-4)
+        torch.testing.assert_close(m.weight.grad, w.grad, rtol=1e-3, atol=1e-3)
+        torch.testing.assert_close(m.bias.grad, b.grad, rtol=1e-3, atol=1e-3)
+    else:  # bf16 rounding may move an argmax: compare in aggregate
+        rel = (xa.grad.float() - xr.grad).norm() / xr.grad.norm()
+        assert rel < 0.05, rel
+        torch.testing.assert_close(m.bias.grad, b.grad, rtol=5e-2, atol=0.5)
