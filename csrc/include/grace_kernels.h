@@ -209,6 +209,8 @@ void maxpool_forward(const void* x, bool fp32, int N, int H, int W, int C, int O
                      void* y, uint8_t* code, hipStream_t stream);
 void maxpool_backward(const void* dy, const uint8_t* code, bool fp32, int N, int H, int W, int C, int OH, int OW,
                       int k, int s, int pad, void* dx, hipStream_t stream);
+// global average pool backward over channels_last: dx[n, h, w, c] = dy[n, c] / HW (C % 8 == 0)
+void global_avgpool_backward(const void* dy, bool fp32, int N, int HW, int C, void* dx, hipStream_t stream);
 
 // ---------------------------------------------------------------- optim.hip
 constexpr int kSgdSegs = 64;

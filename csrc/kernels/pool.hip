@@ -144,6 +144,22 @@ __global__ __launch_bounds__(kPB) void maxpool_bwd_kernel(const T* __restrict__ 
   }
 }
 
+// global average pool backward: dx[n, h, w, c] = dy[n, c] * inv_hw (channels_last x)
+template <typename T>
+__global__ __launch_bounds__(kPB) void gap_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, int HW, int C,
+                                                      float inv_hw, int64_t n_vec) {
+  const int cv = C >> 3;
+  for (int64_t i = (int64_t)blockIdx.x * kPB + threadIdx.x; i < n_vec; i += (int64_t)gridDim.x * kPB) {
+    const int c8 = (int)(i % cv);
+    const int64_t n = i / ((int64_t)cv * HW);
+    const V8 d = ldv(dy + n * C + c8 * 8);
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = d.v[j] * inv_hw;
+    stv(dx + i * 8, o);
+  }
+}
+
 int pool_grid(int64_t n_vec) {
   int64_t b = (n_vec + kPB - 1) / kPB;
   if (b > 8192) b = 8192;
@@ -163,6 +179,18 @@ void maxpool_forward(const void* x, bool fp32, int N, int H, int W, int C, int O
   else
     hipLaunchKernelGGL(maxpool_fwd_kernel<uint16_t>, dim3(pool_grid(n_vec)), dim3(kPB), 0, stream,
                        static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), code, g, n_vec);
+}
+
+void global_avgpool_backward(const void* dy, bool fp32, int N, int HW, int C, void* dx, hipStream_t stream) {
+  const int64_t n_vec = (int64_t)N * HW * (C / 8);
+  if (n_vec == 0) return;
+  const float inv = 1.f / (float)HW;
+  if (fp32)
+    hipLaunchKernelGGL(gap_bwd_kernel<float>, dim3(pool_grid(n_vec)), dim3(kPB), 0, stream,
+                       static_cast<const float*>(dy), static_cast<float*>(dx), HW, C, inv, n_vec);
+  else
+    hipLaunchKernelGGL(gap_bwd_kernel<uint16_t>, dim3(pool_grid(n_vec)), dim3(kPB), 0, stream,
+                       static_cast<const uint16_t*>(dy), static_cast<uint16_t*>(dx), HW, C, inv, n_vec);
 }
 
 void maxpool_backward(const void* dy, const uint8_t* code, bool fp32, int N, int H, int W, int C, int OH, int OW,

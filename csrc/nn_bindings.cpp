@@ -210,6 +210,19 @@ std::vector<Tensor> bn_act_pool_fwd(const Tensor& x, const c10::optional<Tensor>
   return {y, save, code};
 }
 
+// global average pool backward: dy [N, C] -> dx [N, C, H, W] channels_last
+Tensor gap_bwd(const Tensor& dy, int64_t H, int64_t W) {
+  TORCH_CHECK(dy.is_cuda() && dy.dim() == 2 && dy.is_contiguous() &&
+                  (dy.scalar_type() == at::kFloat || dy.scalar_type() == at::kBFloat16) && dy.size(1) % 8 == 0 &&
+                  (reinterpret_cast<uintptr_t>(dy.data_ptr()) & 15) == 0,
+              "gap backward: contiguous [N, C % 8 == 0] fp32/bf16 GPU grad");
+  DevGuard guard(dy.device());
+  Tensor dx = at::empty({dy.size(0), dy.size(1), H, W}, dy.options(), at::MemoryFormat::ChannelsLast);
+  grace::global_avgpool_backward(dy.data_ptr(), dy.scalar_type() == at::kFloat, (int)dy.size(0), (int)(H * W),
+                                 (int)dy.size(1), dx.data_ptr(), cur_stream());
+  return dx;
+}
+
 // NHWC max pooling: returns (y, code) -- code = uint8 in-window argmax per output element
 std::vector<Tensor> maxpool_fwd(const Tensor& x, int64_t k, int64_t s, int64_t pad) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast) &&
@@ -246,6 +259,7 @@ Tensor maxpool_bwd(const Tensor& dy, const Tensor& code, int64_t H, int64_t W, i
 
 void grace_bind_nn(py::module& m) {
   m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("gap_bwd", &gap_bwd);
   m.def("bn_act_pool_fwd", &bn_act_pool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("bias_act_fwd", &bias_act_fwd);

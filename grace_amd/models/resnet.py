@@ -16,7 +16,7 @@ import torch.nn as nn
 
 from ..ops.bnact import BatchNormAct2d, bn_relu_maxpool
 from ..ops.conv import Conv1x1F32
-from ..ops.pool import MaxPool2dNHWC
+from ..ops.pool import GlobalAvgPoolFlat, MaxPool2dNHWC
 
 
 def _conv3x3(cin, cout, stride=1):
@@ -90,7 +90,7 @@ class ResNet(nn.Module):
         self.layer2 = self._make(block, 128, layers[1], 2)
         self.layer3 = self._make(block, 256, layers[2], 2)
         self.layer4 = self._make(block, 512, layers[3], 2)
-        self.avgpool = nn.AdaptiveAvgPool2d(1)
+        self.avgpool = GlobalAvgPoolFlat()  # mean over H, W + flatten; native broadcast backward
         self.fc = nn.Linear(512 * block.expansion, num_classes)
         for m in self.modules():
             if isinstance(m, nn.Conv2d):
@@ -115,7 +115,7 @@ class ResNet(nn.Module):
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         if isinstance(x, tuple):
             x = x[0]
-        return self.fc(torch.flatten(self.avgpool(x), 1))
+        return self.fc(self.avgpool(x))
 
 
 def resnet18(num_classes=1000):

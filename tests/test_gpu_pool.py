@@ -54,3 +54,21 @@ def test_maxpool_nan_propagates():
     ya.sum().backward()
     yb.sum().backward()
     assert torch.equal(xa.grad, xb.grad)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_global_avgpool_flat_matches_torch(dtype):
+    from grace_amd.ops.pool import GlobalAvgPoolFlat
+
+    g = torch.Generator(device="cpu").manual_seed(3)
+    x = torch.randn(4, 256, 7, 7, generator=g).to(DEV, dtype).contiguous(memory_format=torch.channels_last)
+    xa, xb = x.clone().requires_grad_(True), x.clone().float().requires_grad_(True)
+    ya = GlobalAvgPoolFlat()(xa)
+    yb = torch.flatten(F.adaptive_avg_pool2d(xb, 1), 1)
+    tol = dict(rtol=1e-5, atol=1e-5) if dtype == torch.float32 else dict(rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(ya.float(), yb, **tol)
+    dy = torch.randn(yb.shape, generator=g).to(DEV)
+    ya.backward(dy.to(ya.dtype))
+    yb.backward(dy)
+    assert xa.grad.dtype == dtype and xa.grad.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(xa.grad.float(), xb.grad, **tol)
