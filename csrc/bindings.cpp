@@ -546,7 +546,7 @@ void gram_orthonormalize(const Tensor& buf, const Tensor& mats, int64_t which, i
 }
 
 void powersgd_pqt(const Tensor& P, const Tensor& Q, const Tensor& out, const Tensor& mats, const Tensor& tiles,
-                  const c10::optional<Tensor>& resid, int64_t max_r) {
+                  const c10::optional<Tensor>& resid, int64_t max_r, double scale) {
   CHECK_F32(P);
   CHECK_F32(Q);
   CHECK_F32(out);
@@ -555,8 +555,8 @@ void powersgd_pqt(const Tensor& P, const Tensor& Q, const Tensor& out, const Ten
   if (resid.has_value()) TORCH_CHECK(resid->numel() == out.numel(), "resid size");
   DevGuard guard(out.device());
   grace::powersgd_pqt(P.data_ptr<float>(), Q.data_ptr<float>(), out.data_ptr<float>(), mats.data_ptr<int64_t>(),
-                      tiles.data_ptr<int32_t>(), (int)(tiles.numel() / 3), opt_f32_mut(resid), (int)max_r,
-                      cur_stream());
+                      tiles.data_ptr<int32_t>(), (int)(tiles.numel() / 3), opt_f32_mut(resid), (float)scale,
+                      (int)max_r, cur_stream());
 }
 
 void philox_normal(const Tensor& out, int64_t seed, const c10::optional<Tensor>& step) {
@@ -960,7 +960,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("inceptionn_count", &inceptionn_count);
   m.def("inceptionn_encode", &inceptionn_encode);
   m.def("inceptionn_decode", &inceptionn_decode);
-  m.def("powersgd_pqt", &powersgd_pqt);
+  m.def("powersgd_pqt", &powersgd_pqt, py::arg("P"), py::arg("Q"), py::arg("out"), py::arg("mats"), py::arg("tiles"),
+        py::arg("resid"), py::arg("max_r"), py::arg("scale") = 1.0);
   m.def("philox_normal", &philox_normal);
   m.def("cast16", &cast16);
   m.def("decode16_sum", &decode16_sum);

@@ -108,7 +108,7 @@ void gram_orthonormalize(float* buf, const int64_t* mats, int n_mat, int which, 
                          int n_gtiles, const int32_t* gtile_begin, double* partials, float* T, int passes,
                          int max_r, hipStream_t stream);
 void powersgd_pqt(const float* P, const float* Q, float* out, const int64_t* mats, const int32_t* tiles, int n_tiles,
-                  float* resid, int max_r, hipStream_t stream);
+                  float* resid, float scale, int max_r, hipStream_t stream);
 void philox_normal(float* out, int64_t n, SeedArg seed, hipStream_t stream);
 
 // ---------------------------------------------------------------- cast_sketch.hip

@@ -1,4 +1,5 @@
-// PowerSGD power iteration on CDNA4 matrix cores (fp32-in/fp32-acc MFMA, exact fp32).
+// PowerSGD power iteration on CDNA4: bandwidth-shaped VALU tall-skinny products + an MFMA Gram
+// (fp32-in/fp32-acc v_mfma_f32_16x16x4_f32, exact fp32) for the r > 4 orthonormalisation.
 //
 // Reference per matrix (/root/reference/grace_dl/dist/compressor/powersgd.py:30-65):
 //   P = M Q ; orthogonalize(P) ; Q = M^T P ; decompress P Q^T     (M: n x m, Q: m x r, r <= 4 typ.)
@@ -12,7 +13,8 @@
 //                     metric, in-place A <- A T, twice for CholQR2); r > 4: Gram tiles on MFMA
 //                     (all tiles of all matrices in one launch, v_mfma_f32_16x16x4_f32 on the
 //                     r x r Gram), per-matrix fix, apply -- see below
-//  ps_pqt             out = P Q^T, optionally fused with the residual update r = x - P Q^T
+//  ps_pqt             out = s P Q^T (s = 1/W: the average of the SUM-all-reduced Q folded in),
+//                     optionally fused with the residual update r = x - out
 //  philox_normal      N(0,1) via Philox4x32 + Box-Muller (Q identical on every rank)
 #include "grace_common.h"
 #include "grace_kernels.h"
@@ -47,7 +49,7 @@ __device__ __forceinline__ Mat load_mat(const int64_t* __restrict__ mats, int i)
 //            COMP fuses the PowerSGD error-feedback compensate (M = beta*r + gamma*x -> xout)
 //   ps_mtp   Q[k,:] = sum_i M[i,k] P[i,:]   thread = 4 columns (1 unaligned), block = 256-row strip;
 //            P rows are wave-uniform (scalar loads), one atomic per (column, j) per strip
-//   ps_pqt   out = P Q^T, resid -= out       thread = 4 columns, Q rows in registers, 32-row strip
+//   ps_pqt   out = s P Q^T, resid -= out       thread = 4 columns, Q rows in registers, 32-row strip
 // (The MFMA versions of these -- 64x64 LDS-staged tiles with r padded to the 16-wide MFMA N --
 // ran at 2.6-4.4 TB/s; MFMA utilisation 0.25-1.8 %, profiles/r1_pmc_powersgd.txt.)
 constexpr int kRB0 = 16, kCS0 = 2048;     // ps_mq: rows per block, columns per strip
@@ -242,7 +244,8 @@ __global__ __launch_bounds__(kBlock) void ps_mtp_kernel(const float* __restrict_
 template <int R>
 __global__ __launch_bounds__(kBlock) void ps_pqt_kernel(const float* __restrict__ Pall, const float* __restrict__ Qall,
                                                         float* __restrict__ out, const int64_t* __restrict__ mats,
-                                                        const int32_t* __restrict__ tiles, float* __restrict__ resid) {
+                                                        const int32_t* __restrict__ tiles, float* __restrict__ resid,
+                                                        float scale) {
   const int* tl = tiles + 3 * blockIdx.x;
   const Mat mt = load_mat(mats, tl[0]);
   const int64_t n = mt.n, m = mt.m;
@@ -276,7 +279,7 @@ __global__ __launch_bounds__(kBlock) void ps_pqt_kernel(const float* __restrict_
           float v = 0.f;
 #pragma unroll
           for (int j = 0; j < R; ++j) v = fmaf(p[j], q[t][j], v);
-          o[t] = v;
+          o[t] = v * scale;
         }
         const int64_t gi = mt.x_off + row * m + c;
         *reinterpret_cast<float4*>(out + gi) = make_float4(o[0], o[1], o[2], o[3]);
@@ -296,6 +299,7 @@ __global__ __launch_bounds__(kBlock) void ps_pqt_kernel(const float* __restrict_
       float v = 0.f;
 #pragma unroll
       for (int j = 0; j < R; ++j) v = fmaf(p[j], q[j], v);
+      v *= scale;
       const int64_t gi = mt.x_off + row * m + c;
       out[gi] = v;
       if (resid != nullptr) resid[gi] -= v;
@@ -641,13 +645,13 @@ void gram_orthonormalize(float* buf, const int64_t* mats, int n_mat, int which, 
 }
 
 void powersgd_pqt(const float* P, const float* Q, float* out, const int64_t* mats, const int32_t* tiles, int n_tiles,
-                  float* resid, int max_r, hipStream_t stream) {
+                  float* resid, float scale, int max_r, hipStream_t stream) {
   if (n_tiles <= 0) return;
-  if (max_r <= 1) ps_pqt_kernel<1><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid);
-  else if (max_r <= 2) ps_pqt_kernel<2><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid);
-  else if (max_r <= 4) ps_pqt_kernel<4><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid);
-  else if (max_r <= 8) ps_pqt_kernel<8><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid);
-  else ps_pqt_kernel<16><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid);
+  if (max_r <= 1) ps_pqt_kernel<1><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid, scale);
+  else if (max_r <= 2) ps_pqt_kernel<2><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid, scale);
+  else if (max_r <= 4) ps_pqt_kernel<4><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid, scale);
+  else if (max_r <= 8) ps_pqt_kernel<8><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid, scale);
+  else ps_pqt_kernel<16><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid, scale);
 }
 
 void philox_normal(float* out, int64_t n, SeedArg seed, hipStream_t stream) {

@@ -5,18 +5,29 @@ M (n x m): Q (m x r) ~ N(0,1) orthogonalised, P = M Q, all_reduce(P)/W, orthogon
 Q = M^T P, all_reduce(Q)/W, decompress P Q^T; 1-D tensors are sent uncompressed; the payload of
 matrices is empty (all communication happens inside compress).
 
-Fixes / design (survey 2.14 #4, #5, #7): the real world size divides P and Q (the reference's
-default world_size=1 makes the result W x too large); Q is drawn from a seed shared by all
+Fixes / design (survey 2.14 #4, #5, #7): the real world size divides the result (the
+reference's default world_size=1 makes it W x too large); Q is drawn from a seed shared by all
 ranks (name, step) so every rank multiplies by the SAME Q; warm start (reuse last Q, the
-paper's recipe) is available as ``warm_start=True``.  For a flat bucket all matrices' P live in
-ONE buffer and all Q in another, so a whole bucket costs exactly two all-reduces; the 1-D
-segments travel through the communicator (Allreduce).  PowerSGD is only meaningful with the
-Allreduce communicator (Allgather would silently zero matrices in the reference).
+paper's recipe) is available as ``warm_start=True``.
 
-MI355X kernels (csrc/kernels/powersgd.hip): P = M Q and Q = M^T P as batched tall-skinny
-fp32 MFMA GEMMs (v_mfma_f32_32x32x2_f32 / 16x16x4, all matrices of the bucket in ONE launch
-each), batched LDS-resident Gram-Schmidt (one workgroup per matrix), and decompress
-P Q^T fused with the residual update.
+Collectives: SURVEY 2.11 prescribes "2 allreduces per step for the whole model (flat P, flat Q)".
+Under :class:`~grace_amd.parallel.engine.GraceEngine` (``step_level``) every bucket's P lands in
+its slice of ONE step-level P arena during backward; ``step_flush`` (called by the engine once
+all buckets are compressed) issues ONE P all-reduce, orthonormalises every P, writes every
+Q = M^T P into ONE Q arena and issues ONE Q all-reduce -- two matrix collectives per step however
+many buckets the model has (the reference issues two per matrix,
+/root/reference/grace_dl/dist/compressor/powersgd.py:45-52).  No division kernels: the
+orthonormalisation is scale invariant, so P is orthonormalised as the SUM over ranks, and the
+1/W of Q is folded into the P Q^T decompress pass (``ps_pqt`` ``scale``).  The manual
+``grc.step`` path (one tensor at a time) runs the same exchange immediately.  1-D segments travel
+through the communicator (Allreduce).  PowerSGD is only meaningful with the Allreduce
+communicator (Allgather would silently zero matrices in the reference).
+
+MI355X kernels (csrc/kernels/powersgd.hip): P = M Q and Q = M^T P as bandwidth-shaped VALU
+tall-skinny products (16-B loads, every matrix of the bucket in ONE launch each; MFMA tiles were
+measured at < 2 % matrix-core busy for r <= 4 -- the products are HBM-bound at ~2r FLOP per
+loaded element), the Gram matrix of the orthonormalisation on MFMA (v_mfma_f32_16x16x4_f32) for
+r > 4, register-resident MGS for r <= 4, and decompress P Q^T fused with the residual update.
 """
 from __future__ import annotations
 
@@ -43,6 +54,16 @@ class PowerSGDCompressor(BucketCompressor):
         self.world_size = world_size
         self.q_memory = {}
         self.comm = None
+        # step-level batching (GraceEngine): deferred buckets of the current step and the
+        # P / Q arenas ({"key", "p", "q", "off": name -> (p_off, q_off)})
+        self.step_level = False
+        self._pending = []
+        self._arena = None
+        self.matrix_collectives = 0  # matrix all-reduces issued (tests / monitoring)
+
+    def enable_step_level(self, on: bool = True):
+        """Defer the P/Q exchange of every bucket to :meth:`step_flush` (called by the engine)."""
+        self.step_level = bool(on)
 
     def bind_comm(self, comm):
         super().bind_comm(comm)
@@ -59,7 +80,8 @@ class PowerSGDCompressor(BucketCompressor):
             ctx.extra["plan"] = plan
             return [self.flat(tensor)], ctx
         x = self.flat(tensor)
-        return self._power(x, x, name, ctx, plan), ctx
+        # not deferred: a non-fused memory's update() decompresses right after compress
+        return self._power(x, x, name, ctx, plan, defer=False), ctx
 
     def fused_compress(self, tensor, name, memory):
         """PowerSGDMemory fused into the kernels: the compensate x = r + g is computed while
@@ -85,15 +107,24 @@ class PowerSGDCompressor(BucketCompressor):
             memory.residuals[name] = rs
         r = rs.view(-1)
         # x (matrix segments) lands in r; 1-D segments of x equal g (their residual is zero)
-        vec = self._power(g, r, name, ctx, plan, comp_r=r if valid else None, xout=r)
+        vec = self._power(g, r, name, ctx, plan, comp_r=r if valid else None, xout=r, defer=self.step_level)
         ctx.extra["resid"] = r
         return vec, ctx
 
-    def _power(self, x, x_after, name, ctx, plan, comp_r=None, xout=None):
-        """One power iteration for every matrix of the bucket.  ``x`` feeds the first product
-        (compensated on the fly when ``xout`` is given, which then holds x); ``x_after`` is
-        what the second product reads."""
-        W = self.world_size or 1
+    def _arena_slice(self, name, plan):
+        a = self._arena
+        if a is None or name not in a["off"]:
+            return None
+        po, qo = a["off"][name]
+        if po + plan.p_total > a["p"].numel():
+            return None
+        return a["p"][po:po + plan.p_total]
+
+    def _power(self, x, x_after, name, ctx, plan, comp_r=None, xout=None, defer=False):
+        """P = M Q for every matrix of the bucket (into the step-level P arena when batching);
+        the P/Q collectives run now (manual path) or in :meth:`step_flush`.  ``x`` feeds the
+        first product (compensated on the fly when ``xout`` is given, which then holds x);
+        ``x_after`` is what the second product reads."""
         step, step_t = self.advance(name, x.device)
         q = self.q_memory.get(name) if self.warm_start else None
         if q is None or q.numel() != plan.q_total:
@@ -108,22 +139,72 @@ class PowerSGDCompressor(BucketCompressor):
             # same P-hat, hence the same Q = M^T P-hat and P-hat Q^T (up to rounding; a Gaussian Q is
             # well conditioned).  Skipped: it was a 400 KB single-workgroup pass per step for
             # VGG-16's 25088 x 4 Q.  (A warm-start Q is used as is, as in the reference.)
-        p = PS.mq(x, q, plan, comp_r=comp_r, xout=xout)  # P = M Q for every matrix (one launch)
-        if self.comm is not None and W > 1:
-            self.comm.all_reduce(p)
-        if W > 1:
-            p.div_(W)
-        PS.orthogonalize(p, plan, which="p")
-        q = PS.mtp(x_after, p, plan)  # Q = M^T P
-        if self.comm is not None and W > 1:
-            self.comm.all_reduce(q)
-        if W > 1:
-            q.div_(W)
-        if self.warm_start:
-            self.q_memory[name] = q
-        ctx.extra.update(plan=plan, p=p, q=q)
+        p_out = self._arena_slice(name, plan) if defer else None
+        p = PS.mq(x, q, plan, comp_r=comp_r, xout=xout, out=p_out)  # P = M Q for every matrix (one launch)
+        ctx.extra.update(plan=plan, p=p)
         vec = PS.gather_vectors(x, plan)  # 1-D segments, sent through the communicator
+        entry = (name, x_after, ctx)
+        if defer:
+            self._pending.append(entry)
+        else:
+            self._exchange([entry])
         return [vec] if vec.numel() else []
+
+    def step_flush(self):
+        """The step's P/Q exchange for every deferred bucket: one P all-reduce, one Q
+        all-reduce.  Every rank calls it at the same point (the engine's synchronize)."""
+        pend, self._pending = self._pending, []
+        if pend:
+            self._exchange(pend, arena=True)
+
+    def _build_arena(self, entries):
+        dev = entries[0][2].extra["p"].device
+        off, po, qo = {}, 0, 0
+        for name, _, ctx in entries:
+            plan = ctx.extra["plan"]
+            off[name] = (po, qo)
+            po += plan.p_total
+            qo += plan.q_total
+        key = tuple((name, ctx.extra["plan"].p_total, ctx.extra["plan"].q_total) for name, _, ctx in entries)
+        self._arena = {"key": key, "off": off, "p": torch.empty(po, dtype=torch.float32, device=dev),
+                       "q": torch.empty(qo, dtype=torch.float32, device=dev)}
+
+    def _exchange(self, entries, arena: bool = False):
+        W = self.world_size or 1
+        comm = self.comm if (self.comm is not None and W > 1) else None
+        if arena:
+            key = tuple((name, ctx.extra["plan"].p_total, ctx.extra["plan"].q_total) for name, _, ctx in entries)
+            if self._arena is None or self._arena["key"] != key:
+                self._build_arena(entries)  # first step (or a changed bucket set): re-home P
+            a = self._arena
+            p_all, q_all = a["p"], a["q"]
+            for name, _, ctx in entries:
+                po, qo = a["off"][name]
+                plan = ctx.extra["plan"]
+                pv = p_all[po:po + plan.p_total]
+                if ctx.extra["p"].data_ptr() != pv.data_ptr():
+                    pv.copy_(ctx.extra["p"])
+                    ctx.extra["p"] = pv
+                ctx.extra["q"] = q_all[qo:qo + plan.q_total]
+        else:
+            ((name, _, ctx),) = entries
+            p_all = ctx.extra["p"]
+            q_all = torch.empty(ctx.extra["plan"].q_total, dtype=torch.float32, device=p_all.device)
+            ctx.extra["q"] = q_all
+        if comm is not None:
+            comm.all_reduce(p_all)  # SUM over ranks: the orthonormalisation is scale invariant
+            self.matrix_collectives += 1
+        for _, _, ctx in entries:
+            PS.orthogonalize(ctx.extra["p"], ctx.extra["plan"], which="p")
+        for _, x_after, ctx in entries:
+            PS.mtp(x_after, ctx.extra["p"], ctx.extra["plan"], out=ctx.extra["q"])  # Q = M^T P
+        if comm is not None:
+            comm.all_reduce(q_all)  # SUM; the 1/W is applied inside the P Q^T pass
+            self.matrix_collectives += 1
+        for name, _, ctx in entries:
+            ctx.extra["q_scale"] = 1.0 / W
+            if self.warm_start:
+                self.q_memory[name] = ctx.extra["q"]  # scale is irrelevant: P = M Q is re-orthonormalised
 
     def _decompress(self, tensors, ctx, vec_scale: float):
         plan = ctx.extra["plan"]
@@ -134,7 +215,10 @@ class PowerSGDCompressor(BucketCompressor):
             return self.finish(out.reshape(-1), ctx)
         out = self.out_buffer(ctx, dev)
         # fused path: the residual buffer holds x; this pass also leaves r = x - P Q^T there
-        PS.pqt(ctx.extra["p"], ctx.extra["q"], plan, out, resid=ctx.extra.pop("resid", None))
+        if "q" not in ctx.extra:
+            raise RuntimeError("PowerSGD: decompress before the step's P/Q exchange (call step_flush())")
+        PS.pqt(ctx.extra["p"], ctx.extra["q"], plan, out, resid=ctx.extra.pop("resid", None),
+               scale=ctx.extra.get("q_scale", 1.0))
         if tensors:
             PS.scatter_vectors(tensors[0], plan, out, vec_scale)
         return self.finish(out, ctx)

@@ -88,7 +88,7 @@ _PLANS: Dict[Tuple, Plan] = {}
 
 def plan_for(layout: SegmentLayout, rank: int) -> Plan:
     if not 1 <= rank <= 16:
-        raise ValueError("PowerSGD rank must be in [1, 16] (MFMA N-tile / LDS Gram-Schmidt bound)")
+        raise ValueError("PowerSGD rank must be in [1, 16] (register-resident rows of the tall-skinny kernels / Gram bound)")
     key = (layout.shapes, rank)
     p = _PLANS.get(key)
     if p is not None:
@@ -157,12 +157,13 @@ def orthogonalize(buf: torch.Tensor, plan: Plan, which: str) -> None:
 
 
 def mq(x: torch.Tensor, q: torch.Tensor, plan: Plan, comp_r: Optional[torch.Tensor] = None, beta: float = 1.0,
-       gamma: float = 1.0, xout: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """P_i = M_i Q_i for every matrix (flat P buffer).
+       gamma: float = 1.0, xout: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """P_i = M_i Q_i for every matrix (flat P buffer; ``out``: a caller-owned [p_total] view,
+    e.g. this bucket's slice of the step-level P arena).
 
     With ``xout``: M = beta*comp_r + gamma*x (or M = x without ``comp_r``) is also stored into
     ``xout`` for the matrix segments -- the error-feedback compensate fused into this pass."""
-    p = torch.empty(plan.p_total, dtype=torch.float32, device=x.device)
+    p = out if out is not None else torch.empty(plan.p_total, dtype=torch.float32, device=x.device)
     if _native.use_native(x):
         t = plan.tables(x.device)
         _native.lib().powersgd_mq(x, q, p, t["mat"], t["tiles0"], 0, comp_r, beta, gamma, xout, plan.rank)
@@ -177,9 +178,9 @@ def mq(x: torch.Tensor, q: torch.Tensor, plan: Plan, comp_r: Optional[torch.Tens
     return p
 
 
-def mtp(x: torch.Tensor, p: torch.Tensor, plan: Plan) -> torch.Tensor:
-    """Q_i = M_i^T P_i for every matrix (flat Q buffer)."""
-    q = torch.empty(plan.q_total, dtype=torch.float32, device=x.device)
+def mtp(x: torch.Tensor, p: torch.Tensor, plan: Plan, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Q_i = M_i^T P_i for every matrix (flat Q buffer, or ``out``)."""
+    q = out if out is not None else torch.empty(plan.q_total, dtype=torch.float32, device=x.device)
     if _native.use_native(x):
         t = plan.tables(x.device)
         _native.lib().powersgd_mq(x, p, q, t["mat"], t["tiles1"], 1, None, 1.0, 1.0, None, plan.rank)
@@ -189,16 +190,20 @@ def mtp(x: torch.Tensor, p: torch.Tensor, plan: Plan) -> torch.Tensor:
     return q
 
 
-def pqt(p: torch.Tensor, q: torch.Tensor, plan: Plan, out: torch.Tensor, resid: Optional[torch.Tensor] = None) -> None:
-    """out[matrix i] = P_i Q_i^T (vector segments untouched); with ``resid`` (holding x) also
-    resid[matrix i] -= P_i Q_i^T in the same pass (PowerSGD residual update)."""
+def pqt(p: torch.Tensor, q: torch.Tensor, plan: Plan, out: torch.Tensor, resid: Optional[torch.Tensor] = None,
+        scale: float = 1.0) -> None:
+    """out[matrix i] = scale * P_i Q_i^T (vector segments untouched); with ``resid`` (holding x)
+    also resid[matrix i] -= out in the same pass (PowerSGD residual update).  ``scale`` = 1/W
+    folds the average of the summed Q into this pass (no separate division kernel)."""
     if _native.use_native(out):
         t = plan.tables(out.device)
-        _native.lib().powersgd_pqt(p, q, out, t["mat"], t["tilesp"], resid, plan.rank)
+        _native.lib().powersgd_pqt(p, q, out, t["mat"], t["tilesp"], resid, plan.rank, float(scale))
         return
     for (xo, n, m, r, po, qo) in plan.mats:
         o = out[xo:xo + n * m].view(n, m)
         torch.mm(p[po:po + n * r].view(n, r), q[qo:qo + m * r].view(m, r).t(), out=o)
+        if scale != 1.0:
+            o.mul_(scale)
         if resid is not None:
             resid[xo:xo + n * m].view(n, m).sub_(o)
 

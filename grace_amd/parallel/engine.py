@@ -112,6 +112,11 @@ class GraceEngine:
                 if hasattr(part, "bind_comm"):
                     part.bind_comm(gc)
         self.grouped = isinstance(grc.comm, GroupedComm)
+        # compressors with a step-level exchange (PowerSGD: one P and one Q all-reduce per step
+        # for all buckets) defer it to step_flush(), called once every bucket is compressed
+        self._step_flush = getattr(grc.compressor, "step_flush", None)
+        if self._step_flush is not None and hasattr(grc.compressor, "enable_step_level"):
+            grc.compressor.enable_step_level(True)
         # failure detection (parallel/launch.py Watchdog): every synchronize() tracks the step's
         # collectives and raises in the training thread if an earlier one missed its deadline;
         # RCCL async errors (peer death) are polled on the native comm
@@ -323,6 +328,12 @@ class GraceEngine:
                             b.views[i].copy_(p.grad)
                         p.grad = b.views[i]
                 self._launch(b)
+        if self._step_flush is not None:
+            if self.stream is not None:
+                with torch.cuda.stream(self.stream):
+                    self._step_flush()
+            else:
+                self._step_flush()
         if self.grouped:
             if self.stream is not None:
                 with torch.cuda.stream(self.stream):
@@ -362,6 +373,8 @@ class GraceEngine:
             b.reset()
         self._passes.clear()
         self._sparse_pending.clear()
+        if hasattr(self.grc.compressor, "_pending"):
+            self.grc.compressor._pending = []
         if self.grouped:
             self.grc.comm._pending = []
         self.in_flight = 0

@@ -147,7 +147,7 @@ def test_dgc_gpu_selects_about_ratio():
 
 
 @pytest.mark.parametrize("rank", [1, 2, 4])
-def test_powersgd_mfma_matches_torch(rank):
+def test_powersgd_kernels_match_torch(rank):
     from grace_amd.ops import powersgd as PS
 
     g = torch.Generator().manual_seed(3)
