@@ -250,6 +250,14 @@ def main():
     barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    # a device-side communication fault inside the timed replays (an xGMI peer wait that timed
+    # out: FusedSGD skipped those updates) or an RCCL async error must fail the run loudly
+    from grace_amd.parallel import health as _health
+
+    _health.check()
+    _chk = getattr(opt.engine.grc.comm, "check", None)
+    if callable(_chk):
+        _chk()
     step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:

@@ -775,6 +775,7 @@ std::string build_info() {
 void grace_bind_comm(py::module& m);  // csrc/comm/rccl_comm.cpp
 void grace_bind_nn(py::module& m);    // csrc/nn_bindings.cpp
 void grace_bind_xgmi(py::module& m);  // csrc/comm/xgmi_allgather.hip
+void grace_bind_health(py::module& m);  // csrc/comm/health.cpp
 
 // ------------------------------------------------------------------------------ Adaq
 void adaq_sample(const Tensor& x, const Tensor& seg_off, const Tensor& samp_off, int64_t seed,
@@ -920,6 +921,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   grace_bind_comm(m);
   grace_bind_nn(m);
   grace_bind_xgmi(m);
+  grace_bind_health(m);
   m.doc() = "grace_amd native CDNA4 kernels and RCCL runtime";
   m.def("build_info", &build_info);
   m.def("topk_select", &topk_select);

@@ -25,6 +25,7 @@
 #include <chrono>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <shared_mutex>
 #include <stdexcept>
 #include <string>
@@ -154,49 +155,49 @@ class RcclComm {
   uintptr_t stream_ptr() const { return reinterpret_cast<uintptr_t>(stream_); }
 
   std::shared_ptr<Work> all_gather(const Tensor& out, const Tensor& in) {
-    std::shared_lock<std::shared_timed_mutex> lk(mu_);
+    Issue is(*this);
     check(out);
     check(in);
     TORCH_CHECK(out.numel() == in.numel() * world_, "all_gather: out must be world_size x in");
     TORCH_CHECK(out.scalar_type() == in.scalar_type(), "dtype mismatch");
-    begin();
-    RCCL_CHECK(ncclAllGather(in.data_ptr(), out.data_ptr(), in.numel(), nccl_dtype(in), comm_, s_));
-    return end();
+    is.begin();
+    RCCL_CHECK(ncclAllGather(in.data_ptr(), out.data_ptr(), in.numel(), nccl_dtype(in), comm_, is.s));
+    return is.end();
   }
 
   std::shared_ptr<Work> all_reduce(const Tensor& t, const std::string& op) {
-    std::shared_lock<std::shared_timed_mutex> lk(mu_);
+    Issue is(*this);
     check(t);
     check_bool_op(t, op);
-    begin();
-    RCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t), nccl_op(op), comm_, s_));
-    return end();
+    is.begin();
+    RCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t), nccl_op(op), comm_, is.s));
+    return is.end();
   }
 
   std::shared_ptr<Work> broadcast(const Tensor& t, int root) {
-    std::shared_lock<std::shared_timed_mutex> lk(mu_);
+    Issue is(*this);
     check(t);
-    begin();
-    RCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t), root, comm_, s_));
-    return end();
+    is.begin();
+    RCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t), root, comm_, is.s));
+    return is.end();
   }
 
   std::shared_ptr<Work> reduce_scatter(const Tensor& out, const Tensor& in, const std::string& op) {
-    std::shared_lock<std::shared_timed_mutex> lk(mu_);
+    Issue is(*this);
     check(out);
     check(in);
     check_bool_op(in, op);
     TORCH_CHECK(in.numel() == out.numel() * world_, "reduce_scatter: in must be world_size x out");
-    begin();
+    is.begin();
     RCCL_CHECK(ncclReduceScatter(in.data_ptr(), out.data_ptr(), out.numel(), nccl_dtype(in), nccl_op(op), comm_,
-                                 s_));
-    return end();
+                                 is.s));
+    return is.end();
   }
 
   // out[p] <- chunk `rank` of rank p's in (equal chunks of numel / world): one send and one recv
   // per peer in one group -- on a fully connected xGMI node every pair has its own link
   std::shared_ptr<Work> all_to_all(const Tensor& out, const Tensor& in) {
-    std::shared_lock<std::shared_timed_mutex> lk(mu_);
+    Issue is(*this);
     check(out);
     check(in);
     TORCH_CHECK(out.numel() == in.numel() && in.numel() % world_ == 0, "all_to_all: equal sizes, divisible by W");
@@ -204,20 +205,20 @@ class RcclComm {
     const int64_t chunk = in.numel() / world_;
     const size_t esz = in.element_size();
     auto dt = nccl_dtype(in);
-    begin();
+    is.begin();
     RCCL_CHECK(ncclGroupStart());
     for (int p = 0; p < world_; ++p) {
-      RCCL_CHECK(ncclSend(static_cast<const char*>(in.data_ptr()) + p * chunk * esz, chunk, dt, p, comm_, s_));
-      RCCL_CHECK(ncclRecv(static_cast<char*>(out.data_ptr()) + p * chunk * esz, chunk, dt, p, comm_, s_));
+      RCCL_CHECK(ncclSend(static_cast<const char*>(in.data_ptr()) + p * chunk * esz, chunk, dt, p, comm_, is.s));
+      RCCL_CHECK(ncclRecv(static_cast<char*>(out.data_ptr()) + p * chunk * esz, chunk, dt, p, comm_, is.s));
     }
     RCCL_CHECK(ncclGroupEnd());
-    return end();
+    return is.end();
   }
 
   // Batched: all_gathers of (out_i, in_i) pairs and in-place sum all_reduces in ONE group.
   std::shared_ptr<Work> group(const std::vector<std::pair<Tensor, Tensor>>& gathers,
                               const std::vector<Tensor>& reduces) {
-    std::shared_lock<std::shared_timed_mutex> lk(mu_);
+    Issue is(*this);
     for (auto& g : gathers) {
       check(g.first);
       check(g.second);
@@ -227,15 +228,15 @@ class RcclComm {
       check(t);
       check_bool_op(t, "sum");
     }
-    begin();
+    is.begin();
     RCCL_CHECK(ncclGroupStart());
     for (auto& g : gathers)
       RCCL_CHECK(ncclAllGather(g.second.data_ptr(), g.first.data_ptr(), g.second.numel(), nccl_dtype(g.second),
-                               comm_, s_));
+                               comm_, is.s));
     for (auto& t : reduces)
-      RCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t), ncclSum, comm_, s_));
+      RCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t), ncclSum, comm_, is.s));
     RCCL_CHECK(ncclGroupEnd());
-    return end();
+    return is.end();
   }
 
   std::string check_async_error() {
@@ -248,18 +249,25 @@ class RcclComm {
 
   // Callable from a watchdog thread while the training thread issues collectives: issue paths
   // hold mu_ shared (enqueue only, never a wait), abort takes it exclusively, so comm_ is never
-  // freed under a running ncclXxx call.  An enqueue stuck inside RCCL must not make the abort
-  // hang as well: after a bounded wait the communicator is aborted anyway (ncclCommAbort is the
-  // documented way to unblock it) and later issue calls fail on aborted_.
-  void abort() {
+  // freed under a running ncclXxx call.  If an issuing thread holds the lock for more than 5 s
+  // (an enqueue stuck inside RCCL), abort() only marks the communicator aborted and returns
+  // false: the issuing thread performs the ncclCommAbort itself when its call returns (Issue's
+  // destructor), and every later issue fails on aborted_.  force = true additionally calls
+  // ncclCommAbort concurrently -- the documented way to unblock a hung RCCL call, at the price of
+  // freeing the communicator under that call (use only when the process is going down anyway).
+  bool abort(bool force) {
     aborted_.store(true);
     std::unique_lock<std::shared_timed_mutex> lk(mu_, std::defer_lock);
-    const bool locked = lk.try_lock_for(std::chrono::seconds(5));
-    ncclComm_t c = comm_;
-    if (c != nullptr) {
-      (void)ncclCommAbort(c);
-      if (locked) comm_ = nullptr;
+    if (lk.try_lock_for(std::chrono::seconds(5))) {
+      if (comm_ != nullptr) (void)ncclCommAbort(comm_);
+      comm_ = nullptr;
+      return true;
     }
+    if (force) {
+      ncclComm_t c = comm_;
+      if (c != nullptr && !forced_.exchange(true)) (void)ncclCommAbort(c);
+    }
+    return false;
   }
 
  private:
@@ -268,36 +276,54 @@ class RcclComm {
     TORCH_CHECK(t.get_device() == device_, "tensor on the wrong device");
     TORCH_CHECK(comm_ != nullptr && !aborted_.load(), "communicator aborted");
   }
-  // Forked (default): the comm stream waits on the caller's stream, the collective runs there
-  // and overlaps whatever the caller does next.  Inline: the collective is issued on the
-  // caller's current stream -- inside a whole-step HIP graph that is one more node in a single
-  // chain instead of an event fork + join (a forked capture costs ~0.4 ms/step on MI355X).
-  void begin() {
-    // the caller's current stream is looked up on the COMM's device (a different current device
-    // would record the fork / run an inline collective on another device's stream)
-    guard_.emplace(device_);
-    if (inline_) {
-      s_ = current_stream();
-      return;
+
+  // The issue state of ONE collective call, on the calling thread's stack: the shared lock, the
+  // device guard and the stream it is issued on (two threads issuing at once -- the DDP hook on
+  // the autograd thread and a main-thread all_reduce -- each keep their own).  The fork event
+  // is shared, so the record + wait pair runs under fork_mu_.
+  //   Forked (default): the comm stream waits on the caller's stream, the collective runs there
+  //   and overlaps whatever the caller does next.  Inline: the collective is issued on the
+  //   caller's current stream -- inside a whole-step HIP graph that is one more node in a single
+  //   chain instead of an event fork + join (a forked capture costs ~0.4 ms/step on MI355X).
+  struct Issue {
+    RcclComm& c;
+    std::shared_lock<std::shared_timed_mutex> lk;
+    c10::optional<c10::hip::HIPGuardMasqueradingAsCUDA> guard;
+    hipStream_t s = nullptr;
+    explicit Issue(RcclComm& comm) : c(comm), lk(comm.mu_) {}
+    ~Issue() {
+      const bool deferred_abort = c.aborted_.load() && c.comm_ != nullptr && !g_exiting.load();
+      guard.reset();
+      lk.unlock();
+      if (deferred_abort) c.abort(false);  // an abort() that could not take the lock (see abort)
     }
-    s_ = stream_;
-    HIP_OK(hipEventRecord(fork_, current_stream()));
-    HIP_OK(hipStreamWaitEvent(stream_, fork_, 0));
-  }
-  std::shared_ptr<Work> end() {
-    std::shared_ptr<Work> w;
-    if (inline_) {
-      hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-      HIP_OK(hipStreamIsCapturing(s_, &st));
-      w = std::make_shared<Work>(device_, st == hipStreamCaptureStatusNone);
-      if (w->event() != nullptr) HIP_OK(hipEventRecord(w->event(), s_));
-    } else {
-      w = std::make_shared<Work>(device_);
-      HIP_OK(hipEventRecord(w->event(), stream_));
+    void begin() {
+      // the caller's current stream is looked up on the COMM's device (a different current
+      // device would record the fork / run an inline collective on another device's stream)
+      guard.emplace(c.device_);
+      if (c.inline_) {
+        s = current_stream();
+        return;
+      }
+      s = c.stream_;
+      std::lock_guard<std::mutex> f(c.fork_mu_);
+      HIP_OK(hipEventRecord(c.fork_, current_stream()));
+      HIP_OK(hipStreamWaitEvent(c.stream_, c.fork_, 0));
     }
-    guard_.reset();
-    return w;
-  }
+    std::shared_ptr<Work> end() {
+      std::shared_ptr<Work> w;
+      if (c.inline_) {
+        hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+        HIP_OK(hipStreamIsCapturing(s, &st));
+        w = std::make_shared<Work>(c.device_, st == hipStreamCaptureStatusNone);
+        if (w->event() != nullptr) HIP_OK(hipEventRecord(w->event(), s));
+      } else {
+        w = std::make_shared<Work>(c.device_);
+        HIP_OK(hipEventRecord(w->event(), s));
+      }
+      return w;
+    }
+  };
 
  public:
   void set_inline(bool on) { inline_ = on; }
@@ -307,12 +333,12 @@ class RcclComm {
   int rank_, world_, device_;
   ncclComm_t comm_ = nullptr;
   hipStream_t stream_ = nullptr;
-  hipStream_t s_ = nullptr;  // stream of the collective being issued
-  bool inline_ = false;
+  std::atomic<bool> inline_{false};
   hipEvent_t fork_;
-  c10::optional<c10::hip::HIPGuardMasqueradingAsCUDA> guard_;  // device of the collective in flight
+  std::mutex fork_mu_;
   std::shared_timed_mutex mu_;
   std::atomic<bool> aborted_{false};
+  std::atomic<bool> forced_{false};
 };
 
 void bind(py::module& m) {
@@ -334,7 +360,7 @@ void bind(py::module& m) {
       .def("all_to_all", &RcclComm::all_to_all)
       .def("check_async_error", &RcclComm::check_async_error)
       .def_property("inline", &RcclComm::is_inline, &RcclComm::set_inline)
-      .def("abort", &RcclComm::abort);
+      .def("abort", &RcclComm::abort, py::arg("force") = false);
   m.def("rccl_unique_id", &unique_id);
   m.def("rccl_mark_exiting", &mark_exiting);
 }

@@ -12,28 +12,35 @@
 // Memory: every rank allocates ONE region, exported to the peers as a HIP IPC handle (the
 // handles travel through the torch.distributed Store on the Python side):
 //
-//     [ Ctrl (256 B): ready generation ][ slot 0: cap bytes ][ slot 1: cap bytes ]
+//     [ Ctrl (256 B): ready gen @0, consumed gen @128 ][ slot D: cap ][ slot S: cap ]
 //
-// allocated uncached (hipDeviceMallocUncached: no L2 copy of a peer-visible line, like RCCL's
-// own flag/FIFO buffers) when the IPC export accepts it, plain hipMalloc otherwise; either way
-// the hand-off below uses system-scope release/acquire, so it does not rely on the mapping type.
+// allocated uncached (hipDeviceMallocUncached: stores bypass the XCD L2s, so a payload written
+// by ANY earlier kernel is peer-visible once that kernel is done) when the IPC export accepts
+// it, plain hipMalloc otherwise.  Slot D ("direct", uncached regions only): the payload builder
+// assembles ONE bucket's payload straight into it (XgmiComm.payload_buffer) -- no staging
+// copy; every other payload is staged into slot S.  A call's mode is a property of its input
+// address, the same on every rank.
 //
 // Per all_gather(out, in) call g (every rank issues the same sequence; g = a DEVICE counter,
-// so the two launches are graph-capturable and replay correctly):
-//   1. xg_stage: copy `in` into my slot[g & 1]; every block drains its stores and releases at
-//      system scope before its arrival; the last block publishes ctrl.ready = g (system-scope
-//      store).  Never waits on anything.
-//   2. xg_pull, grid (chunks, W): block (c, q) polls peer q's ctrl.ready >= g (bounded spin,
-//      s_sleep between polls), one system-scope acquire, then copies its chunk of q's slot
-//      into out[q] (own rank: straight from `in`); the launch's last block bumps the counter.
+// so the launches are graph-capturable and replay correctly):
+//   1. xg_stage (only when `in` is not the slot): copy `in` into my slot; every block drains its
+//      stores and releases at system scope before its arrival; the last block publishes
+//      ctrl.ready = g.  Direct mode: xg_pull's first block publishes ready = g instead.
+//   2. xg_pull, grid (chunks, W): block (c, q) polls peer q's ready >= g (bounded spin, s_sleep
+//      between polls), one system-scope acquire, reads the in-band counts of q's payload (when
+//      the caller described its variable-length ranges) and copies only the VALID bytes of
+//      each range of its chunk into out[q] (own rank: from `in`).  The launch's last block
+//      publishes ctrl.consumed = g, waits until every peer's consumed >= g (nobody reads my
+//      slot any more), then bumps the device generation.
+// So the slot is free again when xg_pull completes: the next call (or the payload builder, in
+// direct mode) may rewrite it in stream order.
 //
-// Slot reuse without acknowledgements: rank r rewrites slot[g & 1] only in call g + 2, after
-// its call g + 1 pull saw every peer's ready >= g + 1 -- which each peer publishes only after its
-// call-g pull (stream order), i.e. after it finished reading r's call-g slot.  Peers are never
-// more than one call apart for the same reason, so `ready >= g` (wrap-safe) is exact.
-//
-// A wait that times out (a dead or diverged peer) increments `timeouts` and lets the launch
-// finish (garbage result, no hung device); XgmiComm.check() turns that into an exception.
+// Failure: a wait that exceeds the spin limit (a dead or diverged peer; ~10 s by default) does
+// NOT copy garbage.  The peer's rows of `out` are ZERO-FILLED (every decoder reads a zero
+// payload as "nothing sent": count 0 / zero values), and the process-wide fault flag
+// (csrc/comm/health.cpp) is raised in both its device copy (FusedSGD then skips the update:
+// nothing corrupted reaches the weights) and its host-mapped copy (health_check() / the engine
+// raise on the host without a device sync, also under HIP-graph replay).
 #include <torch/extension.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
@@ -43,6 +50,8 @@
 #include <stdexcept>
 #include <string>
 #include <vector>
+
+#include "grace_kernels.h"
 
 namespace grace_xgmi {
 
@@ -58,21 +67,57 @@ using at::Tensor;
 constexpr int kThreads = 256;
 constexpr int kMaxWorld = 16;
 constexpr int64_t kCtrlBytes = 256;
-constexpr uint32_t kSpinLimit = 1u << 22;  // polls x s_sleep(8) ~ 1-2 s before giving up
+constexpr int kReadyWord = 0;
+constexpr int kConsumedWord = 32;  // own 128-B line
+constexpr int kMaxRanges = 8;
 
 struct Local {        // this rank's bookkeeping (plain device memory, never shared)
   uint32_t gen;       // completed all-gathers
   uint32_t arrive1;   // xg_stage arrival counter (re-armed by the last block)
   uint32_t arrive2;   // xg_pull arrival counter
-  uint32_t timeouts;  // waits that gave up
+  uint32_t pad;
 };
 
 struct Peers {
   char* base[kMaxWorld];  // every rank's region in THIS process's address space (own = local)
 };
 
-__device__ __forceinline__ uint32_t ld_relaxed(uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// The payload as a cover of disjoint 16-B aligned byte ranges.  A variable range's valid bytes
+// are sum_j esz[j] * hdr[j] over up to 4 consecutive int32 words of the payload at byte cnt_off
+// (rounded up to 16 B, clamped to nbytes); cnt_off < 0: fixed (all nbytes valid).
+struct Ranges {
+  int n;
+  int64_t off[kMaxRanges];
+  int64_t nbytes[kMaxRanges];
+  int32_t cnt_off[kMaxRanges];
+  int32_t esz[kMaxRanges][4];
+};
+
+struct Fault {
+  uint32_t* host_dev;  // host-mapped health words (system scope), may be null
+  uint32_t* dev;       // device health words, may be null
+};
+
+__device__ __forceinline__ uint32_t ld_sys(const uint32_t* p) {
+  return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ void raise_fault(const Fault& f) {
+  if (f.host_dev != nullptr) {
+    __hip_atomic_fetch_add(f.host_dev + grace::kHealthXgmiTimeouts, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(f.host_dev + grace::kHealthFault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (f.dev != nullptr) __hip_atomic_store(f.dev + grace::kHealthFault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// bounded wait until (int)(*p - g) >= 0; false on timeout
+__device__ bool wait_ge(const uint32_t* p, uint32_t g, uint32_t spin_limit) {
+  uint32_t spins = 0;
+  while ((int32_t)(ld_sys(p) - g) < 0) {
+    __builtin_amdgcn_s_sleep(8);
+    if (++spins > spin_limit) return false;
+  }
+  return true;
 }
 
 // every wave drained its stores, workgroup barrier, one lane: system-scope release then the
@@ -90,51 +135,95 @@ __device__ __forceinline__ bool arrive_last(uint32_t* counter, uint32_t total) {
 
 __global__ __launch_bounds__(kThreads) void xg_stage(const uint4* __restrict__ in, int64_t nvec, char* my_base,
                                                      int64_t slot_bytes, Local* L) {
-  const uint32_t g = ld_relaxed(&L->gen) + 1u;
-  uint4* dst = reinterpret_cast<uint4*>(my_base + kCtrlBytes + (int64_t)(g & 1u) * slot_bytes);
+  const uint32_t g = __hip_atomic_load(&L->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  uint4* dst = reinterpret_cast<uint4*>(my_base + kCtrlBytes + slot_bytes);  // slot S
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * kThreads)
     dst[i] = in[i];
   if (arrive_last(&L->arrive1, gridDim.x))
-    __hip_atomic_store(reinterpret_cast<uint32_t*>(my_base), g, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(my_base) + kReadyWord, g, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ __launch_bounds__(kThreads) void xg_pull(const uint4* __restrict__ in, int64_t nvec, Peers peers,
-                                                    int rank, int64_t slot_bytes, uint4* __restrict__ out,
-                                                    Local* L) {
+// valid 16-B vectors of range i of the payload starting at p (counts read with system loads)
+__device__ __forceinline__ int64_t range_vecs(const Ranges& R, int i, const char* p) {
+  if (R.cnt_off[i] < 0) return R.nbytes[i] >> 4;
+  const uint32_t* h = reinterpret_cast<const uint32_t*>(p + R.cnt_off[i]);
+  int64_t b = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (R.esz[i][j] != 0) b += (int64_t)R.esz[i][j] * (int64_t)(int32_t)ld_sys(h + j);
+  if (b < 0) b = 0;
+  b = (b + 15) >> 4;
+  const int64_t mx = R.nbytes[i] >> 4;
+  return b < mx ? b : mx;
+}
+
+__global__ __launch_bounds__(kThreads) void xg_pull(const char* __restrict__ in, Ranges R, Peers peers, int rank,
+                                                    int world, int direct, uint32_t spin_limit, int64_t span,
+                                                    int64_t slot_bytes,
+                                                    char* __restrict__ out, Local* L, Fault F) {
+  __shared__ int64_t nv[kMaxRanges];
+  __shared__ int ok;
   const int q = blockIdx.y;
-  const uint32_t g = ld_relaxed(&L->gen) + 1u;
-  const uint4* src = in;
-  if (q != rank) {
-    if (threadIdx.x == 0) {
-      uint32_t* ready = reinterpret_cast<uint32_t*>(peers.base[q]);
-      uint32_t spins = 0;
-      while ((int32_t)(__hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - g) < 0) {
-        __builtin_amdgcn_s_sleep(8);
-        if (++spins > kSpinLimit) {
-          __hip_atomic_fetch_add(&L->timeouts, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
+  const uint32_t g = __hip_atomic_load(&L->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  char* my_base = peers.base[rank];
+  if (direct && blockIdx.x == 0 && q == rank && threadIdx.x == 0) {
+    // the payload builder wrote the (uncached) slot in earlier kernels of this stream
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(my_base) + kReadyWord, g, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  const char* src = in;
+  if (threadIdx.x == 0) {
+    ok = 1;
+    if (q != rank) {
+      if (!wait_ge(reinterpret_cast<const uint32_t*>(peers.base[q]) + kReadyWord, g, spin_limit)) {
+        ok = 0;
+        raise_fault(F);
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: no stale line of q's slot
     }
-    __syncthreads();
-    src = reinterpret_cast<const uint4*>(peers.base[q] + kCtrlBytes + (int64_t)(g & 1u) * slot_bytes);
+    const char* s = q == rank ? in : peers.base[q] + kCtrlBytes + (direct ? 0 : slot_bytes);
+    for (int i = 0; i < R.n; ++i) nv[i] = ok ? range_vecs(R, i, s) : 0;
   }
-  uint4* o = out + (int64_t)q * nvec;
-  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * kThreads)
-    o[i] = src[i];
-  if (arrive_last(&L->arrive2, gridDim.x * gridDim.y)) __hip_atomic_store(&L->gen, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (q != rank) src = peers.base[q] + kCtrlBytes + (direct ? 0 : slot_bytes);
+  char* o = out + (int64_t)q * span;
+  const int64_t tid = (int64_t)blockIdx.x * kThreads + threadIdx.x, stride = (int64_t)gridDim.x * kThreads;
+  if (ok) {
+    for (int i = 0; i < R.n; ++i) {
+      const uint4* s4 = reinterpret_cast<const uint4*>(src + R.off[i]);
+      uint4* o4 = reinterpret_cast<uint4*>(o + R.off[i]);
+      for (int64_t v = tid; v < nv[i]; v += stride) o4[v] = s4[v];
+    }
+  } else {  // timed-out peer: its rows read as an empty payload, never as stale bytes
+    uint4* o4 = reinterpret_cast<uint4*>(o);
+    for (int64_t v = tid; v < (span >> 4); v += stride) o4[v] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  if (arrive_last(&L->arrive2, gridDim.x * gridDim.y)) {
+    // every peer block of this launch has read its peer's slot: tell the peers, then wait until
+    // no peer reads MY slot any more before the generation (and the slot) moves on
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(my_base) + kConsumedWord, g, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    for (int p = 0; p < world; ++p) {
+      if (p == rank) continue;
+      if (!wait_ge(reinterpret_cast<const uint32_t*>(peers.base[p]) + kConsumedWord, g, spin_limit)) raise_fault(F);
+    }
+    __hip_atomic_store(&L->gen, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 inline hipStream_t current_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
 
 class XgmiPeers {
  public:
-  XgmiPeers(int rank, int world, int device, int64_t capacity)
-      : rank_(rank), world_(world), device_(device), cap_((capacity + 255) / 256 * 256) {
+  XgmiPeers(int rank, int world, int device, int64_t capacity, int64_t spin_limit)
+      : rank_(rank), world_(world), device_(device), cap_((capacity + 255) / 256 * 256),
+        spin_((uint32_t)std::max<int64_t>(1, std::min<int64_t>(spin_limit, 0x7fffffff))) {
     if (world < 1 || world > kMaxWorld) throw std::runtime_error("xgmi all-gather: world size must be 1..16");
     if (rank < 0 || rank >= world) throw std::runtime_error("xgmi all-gather: bad rank");
     XG_HIP(hipSetDevice(device));
+    grace::health_init();
     const size_t bytes = (size_t)(kCtrlBytes + 2 * cap_);
     void* p = nullptr;
     uncached_ = hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached) == hipSuccess;
@@ -176,9 +265,22 @@ class XgmiPeers {
     opened_ = true;
   }
 
-  // out = [W, n] bytes, in = [n] bytes; n % 16 == 0 and n <= capacity (checked).  Issued on the
-  // caller's current stream (capturable).
-  void all_gather(const Tensor& out, const Tensor& in) {
+  // Device address of slot D (the payload builder may assemble ONE payload there: direct mode,
+  // uncached regions only -- see the header).
+  uintptr_t slot_ptr() const { return reinterpret_cast<uintptr_t>(mine_ + kCtrlBytes); }
+
+  // uint8 [nbytes] tensor aliasing slot D (no ownership: valid while this object lives)
+  Tensor slot_tensor(int64_t nbytes) const {
+    TORCH_CHECK(uncached_, "xgmi all-gather: slot D needs an uncached region");
+    TORCH_CHECK(nbytes > 0 && nbytes <= cap_, "slot_tensor: size");
+    return torch::from_blob(mine_ + kCtrlBytes, {nbytes},
+                            torch::TensorOptions().dtype(torch::kUInt8).device(torch::kCUDA, device_));
+  }
+
+  // out = [W, n] bytes, in = [n] bytes; n % 16 == 0 and n <= capacity (checked).  `ranges`
+  // (int64 [k, 8]: off, nbytes, cnt_off, esz0..esz3, unused) describes the variable-length
+  // parts (empty = the whole payload fixed).  Issued on the caller's current stream (capturable).
+  void all_gather(const Tensor& out, const Tensor& in, const Tensor& ranges) {
     TORCH_CHECK(opened_ || world_ == 1, "xgmi all-gather: open() the peers first");
     TORCH_CHECK(in.is_cuda() && out.is_cuda() && in.is_contiguous() && out.is_contiguous(), "contiguous GPU tensors");
     TORCH_CHECK(in.get_device() == device_ && out.get_device() == device_, "tensor on the wrong device");
@@ -187,25 +289,51 @@ class XgmiPeers {
     TORCH_CHECK(n % 16 == 0 && n <= cap_, "xgmi all-gather: payload must be 16-B granular and <= capacity");
     TORCH_CHECK(reinterpret_cast<uintptr_t>(in.data_ptr()) % 16 == 0 &&
                     reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0, "16-B aligned buffers");
+    Ranges R{};
+    if (ranges.numel() == 0) {
+      R.n = 1;
+      R.off[0] = 0;
+      R.nbytes[0] = n;
+      R.cnt_off[0] = -1;
+    } else {
+      TORCH_CHECK(!ranges.is_cuda() && ranges.scalar_type() == at::kLong && ranges.dim() == 2 && ranges.size(1) == 8 &&
+                      ranges.size(0) <= kMaxRanges, "ranges: CPU int64 [k <= 8, 8]");
+      auto a = ranges.accessor<int64_t, 2>();
+      R.n = (int)ranges.size(0);
+      int64_t end = 0;
+      for (int i = 0; i < R.n; ++i) {
+        R.off[i] = a[i][0];
+        R.nbytes[i] = a[i][1];
+        R.cnt_off[i] = (int32_t)a[i][2];
+        for (int j = 0; j < 4; ++j) R.esz[i][j] = (int32_t)a[i][3 + j];
+        TORCH_CHECK(R.off[i] == end && R.off[i] % 16 == 0 && R.nbytes[i] % 16 == 0 && R.nbytes[i] >= 0,
+                    "ranges must tile the payload in order, 16-B aligned");
+        TORCH_CHECK(R.cnt_off[i] < 0 || (R.cnt_off[i] % 4 == 0 && R.cnt_off[i] + 16 <= n), "bad count offset");
+        end += R.nbytes[i];
+      }
+      TORCH_CHECK(end == n, "ranges must cover the payload exactly");
+    }
     if (n == 0) return;
     c10::hip::HIPGuardMasqueradingAsCUDA guard(device_);
     hipStream_t s = current_stream();
     const int64_t nvec = n / 16;
     const int64_t per_blk = (int64_t)kThreads * 8;  // 8 x 16 B per thread per block pass
-    int b1 = (int)std::min<int64_t>(std::max<int64_t>((nvec + per_blk - 1) / per_blk, 1), 256);
+    const bool direct = reinterpret_cast<uintptr_t>(in.data_ptr()) == slot_ptr();
+    TORCH_CHECK(!direct || uncached_, "xgmi all-gather: direct slot writes need an uncached slot");
+    if (!direct) {
+      int b1 = (int)std::min<int64_t>(std::max<int64_t>((nvec + per_blk - 1) / per_blk, 1), 256);
+      hipLaunchKernelGGL(xg_stage, dim3(b1), dim3(kThreads), 0, s, static_cast<const uint4*>(in.data_ptr()), nvec,
+                         mine_, cap_, local_);
+    }
     int b2 = (int)std::min<int64_t>(std::max<int64_t>((nvec + per_blk - 1) / per_blk, 1), 64);
-    hipLaunchKernelGGL(xg_stage, dim3(b1), dim3(kThreads), 0, s, static_cast<const uint4*>(in.data_ptr()), nvec,
-                       mine_, cap_, local_);
-    hipLaunchKernelGGL(xg_pull, dim3(b2, world_), dim3(kThreads), 0, s, static_cast<const uint4*>(in.data_ptr()),
-                       nvec, peers_, rank_, cap_, static_cast<uint4*>(out.data_ptr()), local_);
+    const auto& hw = grace::health_words();
+    Fault F{hw.host_dev, hw.dev};
+    hipLaunchKernelGGL(xg_pull, dim3(b2, world_), dim3(kThreads), 0, s, static_cast<const char*>(in.data_ptr()), R,
+                       peers_, rank_, world_, direct ? 1 : 0, spin_, n, cap_, static_cast<char*>(out.data_ptr()),
+                       local_, F);
     XG_HIP(hipGetLastError());
   }
 
-  uint32_t timeouts() {
-    Local h{};
-    XG_HIP(hipMemcpy(&h, local_, sizeof(h), hipMemcpyDeviceToHost));
-    return h.timeouts;
-  }
   int64_t capacity() const { return cap_; }
   bool uncached() const { return uncached_; }
 
@@ -224,6 +352,7 @@ class XgmiPeers {
  private:
   int rank_, world_, device_;
   int64_t cap_;
+  uint32_t spin_;
   bool uncached_ = false, opened_ = false;
   char* mine_ = nullptr;
   Local* local_ = nullptr;
@@ -233,12 +362,13 @@ class XgmiPeers {
 
 void bind(py::module& m) {
   py::class_<XgmiPeers, std::shared_ptr<XgmiPeers>>(m, "XgmiPeers")
-      .def(py::init<int, int, int, int64_t>(), py::arg("rank"), py::arg("world"), py::arg("device"),
-           py::arg("capacity"))
+      .def(py::init<int, int, int, int64_t, int64_t>(), py::arg("rank"), py::arg("world"), py::arg("device"),
+           py::arg("capacity"), py::arg("spin_limit") = (int64_t)1 << 25)
       .def("handle", &XgmiPeers::handle)
       .def("open", &XgmiPeers::open)
       .def("all_gather", &XgmiPeers::all_gather)
-      .def("timeouts", &XgmiPeers::timeouts)
+      .def("slot_ptr", &XgmiPeers::slot_ptr)
+      .def("slot_tensor", &XgmiPeers::slot_tensor)
       .def("close", &XgmiPeers::close)
       .def_property_readonly("capacity", &XgmiPeers::capacity)
       .def_property_readonly("uncached", &XgmiPeers::uncached);

@@ -215,6 +215,20 @@ void global_avgpool_backward(const void* dy, bool fp32, int N, int HW, int C, vo
 // ---------------------------------------------------------------- optim.hip
 constexpr int kSgdSegs = 64;
 // buf[i] / w16[i] may be nullptr (no momentum / no bf16 working copy)
+// Process-wide communication health words (csrc/comm/health.cpp): host-mapped copy (device
+// writes it at system scope, the host reads it without a sync) + a device copy of the fault
+// flag.  Null until health_init() (called before any capture by FusedSGD / XgmiComm).
+constexpr int kHealthWords = 16;
+constexpr int kHealthFault = 0;
+constexpr int kHealthXgmiTimeouts = 1;
+struct HealthWords {
+  uint32_t* host;      // host pointer
+  uint32_t* host_dev;  // device alias of the host words
+  uint32_t* dev;       // device memory
+};
+const HealthWords& health_words();
+void health_init();
+
 void sgd_step(float* const* p, const float* const* g, float* const* buf, uint16_t* const* w16, const int64_t* len,
               int n_seg, float lr, float momentum, float dampening, float wd, bool nesterov, bool maximize,
               bool first, hipStream_t stream);

@@ -12,6 +12,10 @@
 // which is torch.optim.SGD's update (torch/optim/sgd.py, _single_tensor_sgd) element for
 // element in fp32, followed by BF16Weights.refresh()'s cast -- one pass over p/g/buf instead of
 // the foreach kernels (two multi_tensor_apply passes) plus the separate cast pass.
+// Communication fault guard: while the process-wide fault flag (csrc/comm/health.cpp, set e.g.
+// by a timed-out xGMI peer wait in the same step) is raised, every block returns before touching
+// p / buf -- a corrupted exchange inside a replayed HIP graph never reaches the weights, and the
+// host sees the flag through health_check() without a device sync.
 #include "grace_common.h"
 #include "grace_kernels.h"
 
@@ -48,7 +52,8 @@ __device__ __forceinline__ float sgd_elem(float& p, float g, float* bufp, const 
   return p;
 }
 
-__global__ __launch_bounds__(kBlock) void sgd_kernel(SgdTable t, SgdHyper h) {
+__global__ __launch_bounds__(kBlock) void sgd_kernel(SgdTable t, SgdHyper h, const uint32_t* __restrict__ fault) {
+  if (fault != nullptr && __hip_atomic_load(fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
   int lo = 0, hi = t.n - 1;  // last tensor with start <= blockIdx.x
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
@@ -117,7 +122,8 @@ void sgd_step(float* const* p, const float* const* g, float* const* buf, uint16_
     }
     t.start[m] = nb;
     t.n = m;
-    if (nb > 0) hipLaunchKernelGGL(sgd_kernel, dim3((unsigned)nb), dim3(kBlock), 0, stream, t, h);
+    const uint32_t* fault = health_words().dev ? health_words().dev + kHealthFault : nullptr;
+    if (nb > 0) hipLaunchKernelGGL(sgd_kernel, dim3((unsigned)nb), dim3(kBlock), 0, stream, t, h, fault);
   }
 }
 

@@ -30,7 +30,14 @@ def allgather_send(comm, compressor, tensors, world_size):
     if compressor.tensors_size_are_same:
         buf, specs = pack(tensors)
         out = torch.empty(W * buf.numel(), dtype=torch.uint8, device=buf.device)
-        work = comm.all_gather_into(out, buf, async_op=True) if buf.numel() else None
+        kw = {}
+        if getattr(comm, "accepts_ranges", False) and buf.numel():
+            var = compressor.wire_counts(tensors)
+            if var is not None:  # count-aware transport: only the valid bytes of each peer move
+                from ..parallel.xgmi import byte_ranges
+
+                kw["ranges"] = byte_ranges(specs, var, buf.numel())
+        work = comm.all_gather_into(out, buf, async_op=True, **kw) if buf.numel() else None
         return (out, buf.numel(), [specs] * W, work, buf)
     # variable size: exchange element counts, pad every tensor to the max over ranks
     dev = tensors[0].device

@@ -61,6 +61,9 @@ class DgcCompressor(BucketCompressor):
         ctx = self.ctx(tensor, name)
         return self._select(v, ctx, name, vmask=v, umask=u)
 
+    def wire_counts(self, tensors):
+        return [None, (0, [4]), (0, [4])]  # [header(selected, cap), values, indices]
+
     def decompress_aggregate_impl(self, per_rank, ctx, n_ranks, scale):
         out = self.out_buffer(ctx, per_rank[0][1].device, zero=True)
         for hdr, v, i in per_rank:  # rank order: identical on every rank

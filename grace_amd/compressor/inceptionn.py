@@ -73,6 +73,10 @@ class INCEPTIONNCompressor(BucketCompressor):
         C.inceptionn_encode(x, self.e_b, self.mid, ws, hdr, stream, codes)
         return [hdr, stream, codes]
 
+    def wire_counts(self, tensors):
+        # header (0, n8, n16, n32): the value stream holds n8 + 2 n16 + 4 n32 bytes
+        return [None, (0, [0, 1, 2, 4]), None]
+
     def compress(self, tensor, name):
         ctx = self.ctx(tensor, name)
         x = self.flat(tensor)

@@ -76,6 +76,9 @@ class ThresholdCompressor(Compressor):
         ctx = self._ctx(tensor)
         return list(_compact(g, self.threshold, ctx.cap, r, valid, memory.beta, memory.gamma)), ctx
 
+    def wire_counts(self, tensors):
+        return [None, (0, [4]), (0, [4])]  # [header(selected, cap), values, indices]
+
     def decompress(self, tensors, ctx):
         hdr, v, i = tensors
         out = torch.zeros(ctx.numel, dtype=torch.float32, device=v.device)

@@ -57,7 +57,7 @@ class TopKCompressor(Compressor):
 
     def compress(self, tensor, name):
         g, ctx = self._prep(tensor, name)
-        vals, idx = K.topk_ef(g, ctx.layout, ctx.ks)
+        vals, idx = K.topk_ef(g, ctx.layout, ctx.ks, key=name)
         return [vals, idx], ctx
 
     def fused_compress(self, tensor, name, memory):
@@ -66,7 +66,7 @@ class TopKCompressor(Compressor):
         g, ctx = self._prep(tensor, name)
         r, valid = memory.residual_buffer(name, g)
         vals, idx = K.topk_ef(g, ctx.layout, ctx.ks, resid=r, resid_valid=valid, beta=memory.beta,
-                              gamma=memory.gamma)
+                              gamma=memory.gamma, key=name)
         return [vals, idx], ctx
 
     def decompress(self, tensors, ctx):

@@ -120,6 +120,14 @@ class Compressor(Stateful, ABC):
         """compensate + compress + update in one native pass; ``None`` = not supported."""
         return None
 
+    def wire_counts(self, tensors: Sequence[torch.Tensor]):
+        """The variable-length parts of a fixed-capacity payload with in-band counts
+        (ops/cappayload.py): per payload tensor None (fixed) or ``(count_tensor, [esz...])`` --
+        its valid bytes are sum_j esz_j * count_tensor[j] (int32 words).  A count-aware
+        transport (the xGMI one-shot all-gather) then moves only those bytes.  None (default):
+        the whole payload is fixed-size."""
+        return None
+
     def decompress_aggregate(self, per_rank: Sequence[Sequence[torch.Tensor]], ctx: Any,
                              world_size: int) -> torch.Tensor:
         """Decompress every rank's payload, aggregate, and average if ``self.average``.

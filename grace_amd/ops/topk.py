@@ -73,6 +73,7 @@ def topk_ef(
     beta: float = 1.0,
     gamma: float = 1.0,
     out: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+    key: Optional[str] = None,
 ) -> Tuple[torch.Tensor, torch.Tensor]:
     """Compensate + select + (residual update) over a flat bucket.
 
@@ -88,7 +89,7 @@ def topk_ef(
     if out is None:
         from ..parallel.comm import PayloadBuilder
 
-        vals, idx = PayloadBuilder(g.device, [(torch.float32, (K,)), (torch.int32, (K,))]).tensors
+        vals, idx = PayloadBuilder(g.device, [(torch.float32, (K,)), (torch.int32, (K,))], key=key).tensors
     else:
         vals, idx = out
     if _native.use_native(g):

@@ -174,15 +174,20 @@ class GroupedComm(Comm):
             self.flush()
             return self.inner.all_reduce(t, op, async_op)
         lw = _LazyWork()
-        self._pending.append(("ar", t, None, lw))
+        self._pending.append(("ar", t, None, lw, {}))
         return Work([lw])
 
-    def all_gather_into(self, out, inp, async_op=False):
+    @property
+    def accepts_ranges(self) -> bool:
+        return bool(getattr(self.inner, "accepts_ranges", False))
+
+    def all_gather_into(self, out, inp, async_op=False, ranges=None):
+        kw = {"ranges": ranges} if ranges is not None else {}
         if not async_op:
             self.flush()
-            return self.inner.all_gather_into(out, inp, async_op)
+            return self.inner.all_gather_into(out, inp, async_op, **kw)
         lw = _LazyWork()
-        self._pending.append(("ag", out, inp, lw))
+        self._pending.append(("ag", out, inp, lw, kw))
         return Work([lw])
 
     def broadcast(self, t, src, async_op=False):
@@ -207,16 +212,16 @@ class GroupedComm(Comm):
         pend, self._pending = self._pending, []
         native = getattr(self.inner, "_c", None)
         if native is not None and len(pend) > 1 and hasattr(native, "group"):
-            gathers = [(o.view(-1), i.view(-1)) for k, o, i, _ in pend if k == "ag"]
-            reduces = [t for k, t, _, _ in pend if k == "ar"]
-            for k, a, b, _ in pend:
+            gathers = [(o.view(-1), i.view(-1)) for k, o, i, _, _ in pend if k == "ag"]
+            reduces = [t for k, t, _, _, _ in pend if k == "ar"]
+            for k, a, b, _, _ in pend:
                 self.inner._mark(*(x for x in (a, b) if x is not None))
             w = native.group(gathers, reduces)
-            for _, _, _, lw in pend:
+            for _, _, _, lw, _ in pend:
                 lw.bind(w)
             return
-        for k, a, b, lw in pend:
-            w = self.inner.all_reduce(a, "sum", True) if k == "ar" else self.inner.all_gather_into(a, b, True)
+        for k, a, b, lw, kw in pend:
+            w = self.inner.all_reduce(a, "sum", True) if k == "ar" else self.inner.all_gather_into(a, b, True, **kw)
             lw.bind(w)
 
 
@@ -348,11 +353,26 @@ def unpack(buf: torch.Tensor, specs: Sequence[Spec]) -> List[torch.Tensor]:
     return out
 
 
+_PAYLOAD_PROVIDER = None
+
+
+def set_payload_provider(fn) -> None:
+    """``fn(nbytes, key) -> uint8 tensor or None``: where keyed payloads are assembled (the xGMI
+    comm hands out its exported slot so that payload is gathered without a staging copy)."""
+    global _PAYLOAD_PROVIDER
+    _PAYLOAD_PROVIDER = fn
+
+
+def get_payload_provider():
+    return _PAYLOAD_PROVIDER
+
+
 class PayloadBuilder:
     """Allocate a compressor's payload tensors as views of ONE buffer in the packed layout,
-    so that ``pack`` is zero-copy and the whole payload moves in one collective."""
+    so that ``pack`` is zero-copy and the whole payload moves in one collective.  With a ``key``
+    (the bucket name) the registered payload provider may supply the buffer."""
 
-    def __init__(self, device, entries: Sequence[Tuple[torch.dtype, Tuple[int, ...]]]):
+    def __init__(self, device, entries: Sequence[Tuple[torch.dtype, Tuple[int, ...]]], key: Optional[str] = None):
         off, self._specs = 0, []
         for dt, shape in entries:
             n = 1
@@ -361,7 +381,11 @@ class PayloadBuilder:
             nb = n * torch.empty((), dtype=dt).element_size()
             self._specs.append(Spec(dt, tuple(shape), off, nb))
             off = _align(off + nb)
-        self.buffer = torch.empty(max(off, _ALIGN), dtype=torch.uint8, device=device)
+        size = max(off, _ALIGN)
+        buf = None
+        if key is not None and _PAYLOAD_PROVIDER is not None and torch.device(device).type == "cuda":
+            buf = _PAYLOAD_PROVIDER(size, key)
+        self.buffer = buf if buf is not None else torch.empty(size, dtype=torch.uint8, device=device)
         self.tensors = unpack(self.buffer, self._specs)
 
 

@@ -26,6 +26,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 
+from . import health as _health
 from ..core import Communicator, register_layout
 from ..ops import _native
 from ..ops.layout import SegmentLayout
@@ -357,12 +358,15 @@ class GraceEngine:
         if self._sparse:
             self._finish_sparse()
         self.in_flight = 0
+        # device-side communication faults (host-mapped health words: no sync, capture-safe)
+        _health.check()
         if self.watchdog is not None:
             self.watchdog.check()
+            capturing = self.device.type == "cuda" and torch.cuda.is_current_stream_capturing()
             check = getattr(self.grc.comm, "check", None)
-            if callable(check):
+            if callable(check) and not capturing:  # a comm's check may query the device
                 check()
-            if self.device.type == "cuda" and not torch.cuda.is_current_stream_capturing():
+            if self.device.type == "cuda" and not capturing:
                 self.watchdog.track_stream("GRACE exchange")
 
     def abort_step(self):

@@ -45,6 +45,12 @@ class FusedSGD(SGD):
         super().__init__(params, lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay,
                          nesterov=nesterov, maximize=maximize)
         self._working: Dict[int, torch.Tensor] = {}
+        # the kernel honours the process-wide communication fault flag (parallel/health.py):
+        # allocate it now, before any HIP-graph capture of the step
+        if any(p.is_cuda for g in self.param_groups for p in g["params"]):
+            from . import health
+
+            health.init()
 
     def attach_working_copies(self, weights) -> None:
         """Write ``weights``' bf16 working copies in the update kernel (BF16Weights)."""

@@ -25,6 +25,8 @@ from typing import Callable, Optional
 
 import torch
 
+from . import health as _health
+
 #: stochastic codecs whose native kernels read a device step counter
 _DEVICE_STEPPED = ("RandomKCompressor", "QSGDCompressor", "TernGradCompressor", "NaturalCompressor",
                    "PowerSGDCompressor", "DgcCompressor", "AdaqCompressor")
@@ -62,6 +64,10 @@ class GraphedStep:
     step (W > 1) use ``"thread_local"``: RCCL's proxy thread makes HIP calls of its own while
     the training thread captures, and under the default ``"global"`` mode such a call from
     ANY thread invalidates the capture.
+
+    Every replay first checks the process-wide communication health words (a host-mapped read,
+    no device sync): a device-side fault of an earlier replay (an xGMI peer wait that timed out;
+    FusedSGD skipped that update) raises :class:`~grace_amd.parallel.health.CommFault` here.
     """
 
     def __init__(self, fn: Callable[[], torch.Tensor], warmup: int = 3, pool=None,
@@ -80,6 +86,7 @@ class GraphedStep:
         torch.cuda.synchronize()
 
     def __call__(self) -> torch.Tensor:
+        _health.check()
         self.graph.replay()
         return self.loss
 

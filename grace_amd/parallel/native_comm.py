@@ -35,6 +35,17 @@ def _hook_exit():
         _EXIT_HOOKED = True
 
 
+def _agree(ok: bool, group) -> None:
+    """MIN of ``ok`` over the torch process group; every rank raises together on failure."""
+    be = dist.get_backend(group)
+    dev = torch.device("cuda", torch.cuda.current_device()) if be == "nccl" else torch.device("cpu")
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+    if int(flag.item()) != 1:
+        raise RuntimeError("native RCCL runtime failed its cross-rank self-check"
+                           + ("" if not ok else " on a peer rank"))
+
+
 class RcclComm(_comm.Comm):
     def __init__(self, rank: int, world: int, unique_id: bytes, device: int, high_priority: bool = True,
                  inline: bool = False):
@@ -47,7 +58,11 @@ class RcclComm(_comm.Comm):
         self._stream = torch.cuda.ExternalStream(self._c.stream_ptr, device=torch.device("cuda", device))
 
     @classmethod
-    def from_process_group(cls, group=None, high_priority: bool = True, inline: bool = False) -> "RcclComm":
+    def from_process_group(cls, group=None, high_priority: bool = True, inline: bool = False,
+                           verify: bool = True, timeout_s: float = 120.0) -> "RcclComm":
+        """Bootstrap the runtime from the torch.distributed Store; with ``verify`` (default) the
+        new communicator passes :meth:`verify` on every rank before it is returned (all ranks
+        raise together otherwise, so the caller can fall back to ``TorchComm``)."""
         if not dist.is_initialized():
             raise RuntimeError("torch.distributed must be initialised (it provides the Store)")
         rank = dist.get_rank(group)
@@ -59,7 +74,62 @@ class RcclComm(_comm.Comm):
             store.set(key, uid)
         else:
             uid = store.get(key)
-        return cls(rank, world, bytes(uid), torch.cuda.current_device(), high_priority, inline)
+        err = None
+        c = None
+        try:
+            c = cls(rank, world, bytes(uid), torch.cuda.current_device(), high_priority, inline)
+        except Exception as e:  # every rank must learn it (the peers would wait in verify)
+            err = e
+        if verify:
+            ok = err is None and c.verify(timeout_s=timeout_s, agree=False)
+            _agree(ok, group)
+        elif err is not None:
+            raise err
+        if err is not None:
+            raise err
+        return c
+
+    def _wait(self, w, deadline: float) -> None:
+        import time
+
+        while not w.is_completed():
+            if time.monotonic() > deadline:
+                self.abort(force=True)
+                raise TimeoutError("native RCCL self-check: a collective did not complete")
+            time.sleep(1e-3)
+
+    def verify(self, timeout_s: float = 120.0, agree: bool = True) -> bool:
+        """Cross-rank start-up self-check, run BEFORE any HIP-graph capture: an all-reduce, an
+        all-gather and one grouped (all-gather + all-reduce) of rank-dependent data must produce
+        the exact expected values on this rank, each within ``timeout_s`` (a host-side bounded
+        wait: a collective that never completes aborts the communicator instead of hanging).
+        With ``agree`` the verdict is MIN-reduced over the torch process group and every rank
+        raises together on failure; returns this rank's verdict otherwise."""
+        import time
+
+        dev = torch.device("cuda", self.device)
+        W, r = self.world_size, self.rank
+        deadline = time.monotonic() + timeout_s
+        ok = True
+        try:
+            a = torch.arange(4097, device=dev, dtype=torch.float32) + r
+            self._wait(self._c.all_reduce(a, "sum"), deadline)
+            ok &= torch.equal(a, torch.arange(4097, device=dev, dtype=torch.float32) * W + W * (W - 1) / 2)
+            g_in = torch.full((1031,), r + 1, dtype=torch.int32, device=dev)
+            g_out = torch.empty(1031 * W, dtype=torch.int32, device=dev)
+            self._wait(self._c.all_gather(g_out, g_in), deadline)
+            want = (torch.arange(W, device=dev, dtype=torch.int32) + 1).repeat_interleave(1031)
+            ok &= torch.equal(g_out, want)
+            b = torch.full((65,), float(r + 1), device=dev)
+            g_out.zero_()
+            self._wait(self._c.group([(g_out, g_in)], [b]), deadline)
+            ok &= torch.equal(g_out, want) and torch.equal(b, torch.full_like(b, W * (W + 1) / 2))
+            torch.cuda.synchronize(dev)
+        except Exception:
+            ok = False
+        if agree:
+            _agree(ok, None)
+        return bool(ok)
 
     @property
     def stream(self) -> torch.cuda.Stream:
@@ -107,8 +177,11 @@ class RcclComm(_comm.Comm):
         if err:
             raise RuntimeError(f"RCCL async error: {err}")
 
-    def abort(self):
-        self._c.abort()
+    def abort(self, force: bool = False) -> bool:
+        """Abort the communicator (later issues fail).  Returns False when an issuing thread
+        held it for > 5 s: that thread aborts on return (``force`` also aborts concurrently,
+        see csrc/comm/rccl_comm.cpp)."""
+        return bool(self._c.abort(force))
 
     def close(self):
         """Destroy the communicator now (before torch.distributed is torn down)."""

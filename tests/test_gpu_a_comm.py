@@ -63,6 +63,52 @@ def test_native_rccl_comm_single_rank(nccl_group):
     c.check()
 
 
+def test_native_rccl_self_check(nccl_group):
+    """from_process_group runs the cross-rank self-check (all-reduce, all-gather, group) before
+    returning; verify() can be re-run, inline or forked, and agrees over the torch group."""
+    from grace_amd.parallel.native_comm import RcclComm
+
+    for inline in (False, True):
+        c = RcclComm.from_process_group(inline=inline)  # verify=True: raises on a bad runtime
+        assert c.verify(timeout_s=30.0) is True
+
+
+def test_native_rccl_concurrent_issue_threads(nccl_group):
+    """Two threads issuing collectives on one RcclComm at once (the DDP hook on the autograd
+    thread + a main-thread all-reduce): the per-call issue state keeps each call on its own
+    stream and device guard; every result is exact."""
+    import threading
+
+    from grace_amd.parallel.native_comm import RcclComm
+
+    c = RcclComm.from_process_group()
+    errs = []
+
+    def worker(seed):
+        try:
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                for i in range(200):
+                    t = torch.full((257,), float(seed * 1000 + i), device="cuda")
+                    c.all_reduce(t, async_op=True).wait()
+                    o = torch.empty(257, device="cuda")
+                    c.all_gather_into(o, t, async_op=True).wait()
+                    if not torch.equal(o, t):
+                        errs.append((seed, i))
+            s.synchronize()
+        except Exception as e:  # pragma: no cover
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    torch.cuda.synchronize()
+    assert not errs, errs[:4]
+    c.check()
+
+
 def test_native_comm_drives_grace(nccl_group):
     from grace_amd import grace_from_params
     from grace_amd.parallel.native_comm import RcclComm

@@ -115,3 +115,114 @@ def _xgmi_engine_body(rank, world):
     finally:
         set_default_comm(None)
         comm.close()
+
+
+def _xgmi_timeout_body(rank, world):
+    """A peer that arrives later than the spin limit: the waiting rank zero-fills that peer's
+    rows, raises the fault flag (host-mapped: check() raises without a device sync) and its
+    FusedSGD skips the update; the late rank still gets correct data."""
+    import time
+
+    from grace_amd.parallel import FusedSGD, health
+    from grace_amd.parallel.comm import TorchComm
+    from grace_amd.parallel.xgmi import XgmiComm
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    comm = XgmiComm(TorchComm(), capacity_mb=1.0, spin_limit=1 << 18)
+    health.reset()
+    p = torch.nn.Parameter(torch.ones(1024, device=dev))
+    opt = FusedSGD([p], lr=0.5)
+    inp = torch.full((4096,), rank + 1, dtype=torch.int32, device=dev)
+    out = torch.full((world * 4096,), -7, dtype=torch.int32, device=dev)
+    dist.barrier()
+    if rank == 1:
+        time.sleep(4.0)  # far beyond rank 0's spin limit
+    comm.all_gather_into(out, inp)
+    torch.cuda.synchronize()
+    if rank == 0:
+        assert torch.equal(out[:4096], inp)
+        assert torch.equal(out[4096:], torch.zeros(4096, dtype=torch.int32, device=dev)), "late peer not zero-filled"
+        assert health.status()[1] >= 1
+        with pytest.raises(health.CommFault):
+            comm.check()
+        p.grad = torch.ones_like(p)
+        opt.step()  # must be skipped while the fault flag is raised
+        torch.cuda.synchronize()
+        assert torch.equal(p.detach(), torch.ones_like(p))
+    else:
+        want = torch.cat([torch.full((4096,), r + 1, dtype=torch.int32, device=dev) for r in range(world)])
+        assert torch.equal(out, want)
+    dist.barrier()
+    health.reset()
+    p.grad = torch.ones_like(p)
+    opt.step()  # fault cleared: the update runs again
+    torch.cuda.synchronize()
+    assert torch.allclose(p.detach(), torch.full_like(p, 0.5))
+    dist.barrier()
+    comm.close()
+
+
+def test_xgmi_peer_timeout_is_fatal_not_silent():
+    run_distributed(_xgmi_timeout_body, 2, timeout=180)
+
+
+def _xgmi_count_body(rank, world):
+    """Capacity payloads (Threshold): the one-shot pull copies only each peer's VALID entries
+    (count from the peer's in-band header); the decoded result equals the inner comm's."""
+    from grace_amd import grace_from_params
+    from grace_amd.parallel.comm import TorchComm
+    from grace_amd.parallel.xgmi import XgmiComm
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    comm = XgmiComm(TorchComm(), capacity_mb=2.0)
+    params = {"compressor": "threshold", "threshold": 1.5, "memory": "none", "communicator": "allgather",
+              "world_size": world}
+    g = torch.Generator().manual_seed(3 + rank)
+    for step in range(3):
+        x = torch.randn(50000, generator=g).to(dev)
+        a = grace_from_params(params, comm=comm).step(x.clone(), "t")
+        b = grace_from_params(params, comm=TorchComm()).step(x.clone(), "t")
+        torch.cuda.synchronize()
+        assert torch.equal(a, b), f"step {step}"
+    assert comm.one_shot_calls >= 3
+    comm.check()
+    dist.barrier()
+    torch.cuda.synchronize()
+    comm.close()
+
+
+def test_xgmi_count_aware_capacity_payload():
+    run_distributed(_xgmi_count_body, 2, timeout=180)
+
+
+def _xgmi_direct_body(rank, world):
+    """Top-K's payload assembled straight in the exported slot (uncached regions): the gather
+    runs without the staging copy and matches the staged path."""
+    from grace_amd import grace_from_params
+    from grace_amd.parallel.comm import TorchComm
+    from grace_amd.parallel.xgmi import XgmiComm
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    comm = XgmiComm(TorchComm(), capacity_mb=2.0)
+    params = {"compressor": "topk", "compress_ratio": 0.02, "memory": "none", "communicator": "allgather",
+              "world_size": world}
+    g = torch.Generator().manual_seed(11 + rank)
+    for step in range(3):
+        x = torch.randn(60000, generator=g).to(dev)
+        a = grace_from_params(params, comm=comm).step(x.clone(), "bucket")
+        b = grace_from_params(params, comm=TorchComm()).step(x.clone(), "bucket")
+        torch.cuda.synchronize()
+        assert torch.equal(a, b), f"step {step}"
+    if comm._x.uncached:
+        assert comm.direct_calls >= 3
+    comm.check()
+    dist.barrier()
+    torch.cuda.synchronize()
+    comm.close()
+
+
+def test_xgmi_direct_payload_no_staging():
+    run_distributed(_xgmi_direct_body, 2, timeout=180)
