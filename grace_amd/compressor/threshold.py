@@ -7,10 +7,15 @@ writes fp32 values + int32 flat indices into a FIXED-capacity payload with an in
 (grace_amd/ops/cappayload.py), with ResidualMemory fused into the same pass.  No host read of the
 size anywhere, so the exchange is graph-capturable.
 
-``capacity`` (fraction of the tensor, default 1.0 = exact reference semantics, never spills)
-bounds the bytes on the wire: with capacity < 1 at most ceil(capacity * n) of the selected
-entries are sent per step and the rest stay in the residual (ResidualMemory) -- which subset is
-sent is unspecified on the GPU (atomic slot order).
+``capacity`` (fraction of the tensor) bounds the bytes on the wire: at most ceil(capacity * n)
+of the selected entries are sent per step.  ``None`` (default, "auto"):
+  * with ResidualMemory fused (error feedback): 1/32 of the tensor (8n/32 + 16 bytes per rank,
+    ~6 % of the uncompressed 4n), grown lagged and sync-free when a step overflows
+    (ops/cappayload.py AdaptiveCapacity); entries past the capacity stay in the residual and go
+    out in a later step -- spill, not loss;
+  * without error feedback: 1.0 (exact reference semantics, never spills).
+Which subset is sent when a step spills is unspecified on the GPU (atomic slot order).  On the
+xGMI one-shot path only each peer's selected entries move regardless (count-aware pull).
 
 Default threshold 0.01 (the dist helper's 256 selects nothing: survey 2.14 #19).
 """
@@ -32,6 +37,8 @@ class ThresholdCtx:
     shape: torch.Size
     dtype: torch.dtype
     cap: int
+    name: str = ""
+    adapt: bool = False
 
 
 def _compact(g, thr, cap, r=None, r_valid=False, beta=1.0, gamma=1.0):
@@ -55,17 +62,25 @@ def _compact(g, thr, cap, r=None, r_valid=False, beta=1.0, gamma=1.0):
 
 
 class ThresholdCompressor(Compressor):
-    def __init__(self, threshold: float = 0.01, capacity: float = 1.0):
+    AUTO_EF_RATIO = 1.0 / 32
+
+    def __init__(self, threshold: float = 0.01, capacity=None):
         super().__init__(tensors_size_are_same=True)  # fixed-capacity payload
         self.threshold = threshold
         self.capacity = capacity
+        self.adaptive = P.AdaptiveCapacity(self.AUTO_EF_RATIO) if capacity is None else None
 
-    def _ctx(self, tensor):
-        return ThresholdCtx(tensor.numel(), tensor.shape, tensor.dtype, P.capacity(tensor.numel(), self.capacity))
+    def _ctx(self, tensor, name, ef: bool):
+        n = tensor.numel()
+        if self.adaptive is not None and ef:
+            cap = self.adaptive.get(name, n, n)
+        else:
+            cap = P.capacity(n, 1.0 if self.capacity is None else self.capacity)
+        return ThresholdCtx(n, tensor.shape, tensor.dtype, cap, name, self.adaptive is not None and ef)
 
     def compress(self, tensor, name):
         g = tensor.reshape(-1).float().contiguous()
-        ctx = self._ctx(tensor)
+        ctx = self._ctx(tensor, name, ef=False)
         return list(_compact(g, self.threshold, ctx.cap)), ctx
 
     def fused_compress(self, tensor, name, memory):
@@ -73,8 +88,12 @@ class ThresholdCompressor(Compressor):
             return None
         g = tensor.reshape(-1).float().contiguous()
         r, valid = memory.residual_buffer(name, g)
-        ctx = self._ctx(tensor)
+        ctx = self._ctx(tensor, name, ef=True)
         return list(_compact(g, self.threshold, ctx.cap, r, valid, memory.beta, memory.gamma)), ctx
+
+    def _observe(self, per_rank, ctx):
+        if getattr(ctx, "adapt", False):  # every rank's header: the same decision on every rank
+            self.adaptive.observe(ctx.name, [p[0][:1] for p in per_rank], lambda w: w[0])
 
     def wire_counts(self, tensors):
         return [None, (0, [4]), (0, [4])]  # [header(selected, cap), values, indices]
@@ -86,6 +105,7 @@ class ThresholdCompressor(Compressor):
         return out.view(ctx.shape).to(ctx.dtype)
 
     def decompress_aggregate(self, per_rank, ctx, world_size):
+        self._observe(per_rank, ctx)
         out = torch.zeros(ctx.numel, dtype=torch.float32, device=per_rank[0][1].device)
         scale = 1.0 / world_size if self.average else 1.0
         for hdr, v, i in per_rank:  # fixed rank order: identical result on every rank

@@ -27,7 +27,7 @@ COMPRESSORS: Dict[str, Callable[[Dict[str, Any]], Any]] = {
         str(p.get("fp16_dtype", "fp16")), torch.float16)),
     "topk": lambda p: Z.TopKCompressor(p.get("compress_ratio", 0.01)),
     "randomk": lambda p: Z.RandomKCompressor(p.get("compress_ratio", 0.01)),
-    "threshold": lambda p: Z.ThresholdCompressor(p.get("threshold", 0.01), capacity=p.get("capacity", 1.0)),
+    "threshold": lambda p: Z.ThresholdCompressor(p.get("threshold", 0.01), capacity=p.get("capacity")),
     "dgc": lambda p: Z.DgcCompressor(p.get("compress_ratio", 0.01), capacity=p.get("capacity", 2.0)),
     "qsgd": lambda p: Z.QSGDCompressor(p.get("quantum_num", 127), reduce_scatter=p.get("qsgd_reduce_scatter", True)),
     "terngrad": lambda p: Z.TernGradCompressor(),
@@ -40,7 +40,7 @@ COMPRESSORS: Dict[str, Callable[[Dict[str, Any]], Any]] = {
                                                warm_start=p.get("warm_start", False),
                                                world_size=p.get("world_size")),
     "adaq": lambda p: Z.AdaqCompressor(p.get("compress_ratio", 0.01), capacity=p.get("capacity", 2.0)),
-    "inceptionn": lambda p: Z.INCEPTIONNCompressor(p.get("error_bound", 2e-10), capacity=p.get("capacity", 1.0)),
+    "inceptionn": lambda p: Z.INCEPTIONNCompressor(p.get("error_bound", 2e-10), capacity=p.get("capacity")),
     "sketch": lambda p: Z.SketchCompressor(p.get("quantiles", 64)),
     "u8bit": lambda p: Z.U8bitCompressor(),
 }

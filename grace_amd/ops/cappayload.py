@@ -68,3 +68,71 @@ def sent(hdr: torch.Tensor, cap: int) -> int:
 
 def overflow(hdr: torch.Tensor, cap: int) -> bool:
     return int(hdr[0]) > cap
+
+
+class AdaptiveCapacity:
+    """Per-name payload capacity: starts at ``ratio`` of the tensor and GROWS (never shrinks)
+    when a step's in-band count shows the payload overflowed -- with no host synchronisation.
+
+    After each exchange the count words of EVERY rank's header (the gathered payloads: the same
+    bytes on every rank) are reduced to their max on the device and copied to pinned host memory
+    by a non-blocking copy (``observe``); the host reads that at the NEXT compress of the same
+    name, after waiting on the copy's event (recorded a whole step earlier: no real stall).  So
+    every rank takes the same decision at the same step and the payloads stay equal-sized.  When
+    the need exceeded the capacity the capacity becomes ``grow`` x the need (<= the tensor).
+    Nothing adapts while a stream is being captured: a captured HIP graph keeps the capacity it
+    was captured with (its payload buffers are static), and entries past it spill -- into the
+    residual when an error-feedback memory is fused (no loss), or are dropped (counted in
+    ``overflow_steps``).  SURVEY 2.11: the reference pads to the max actual size instead, with a
+    size all-gather and a host read per tensor (grace_dl/dist/communicator/allgather.py:15-38).
+    """
+
+    def __init__(self, ratio: float, grow: float = 1.5):
+        self.ratio = float(ratio)
+        self.grow = float(grow)
+        self.cap = {}        # name -> entries (or bytes, as the codec defines its unit)
+        self._probe = {}     # name -> (pinned int32 words, event, need_fn)
+        self.overflow_steps = 0
+
+    def get(self, name: str, n: int, unit_max: int) -> int:
+        """Current capacity of ``name`` (initially ceil(ratio * n), clamped to [1, unit_max])."""
+        self._poll(name, unit_max)
+        c = self.cap.get(name)
+        if c is None:
+            c = max(1, min(int(unit_max), int(math.ceil(self.ratio * n))))
+            self.cap[name] = c
+        return c
+
+    def _poll(self, name: str, unit_max: int) -> None:
+        pr = self._probe.get(name)
+        if pr is None:
+            return
+        words, ev, need_fn = pr
+        if ev is not None:
+            ev.synchronize()  # recorded one step ago; a deterministic step for every rank
+        del self._probe[name]
+        need = int(need_fn([int(w) for w in words.tolist()]))
+        cur = self.cap.get(name, 0)
+        if need > cur:
+            self.overflow_steps += 1
+            if not _capturing():
+                self.cap[name] = max(cur, min(int(unit_max), int(math.ceil(self.grow * need))))
+
+    def observe(self, name: str, headers, need_fn) -> None:
+        """Queue a lagged read of the element-wise max over ``headers`` (every rank's int32 count
+        words, identical on all ranks); ``need_fn(words) -> units needed``."""
+        if _capturing():
+            return
+        hdr = headers[0] if len(headers) == 1 else torch.stack([h.reshape(-1) for h in headers]).amax(0)
+        if hdr.is_cuda:
+            words = torch.empty(hdr.numel(), dtype=torch.int32, pin_memory=True)
+            words.copy_(hdr, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        else:
+            words, ev = hdr.clone(), None
+        self._probe[name] = (words, ev, need_fn)
+
+
+def _capturing() -> bool:
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
