@@ -80,6 +80,14 @@ def parse():
                     help="process group: nccl = RCCL over xGMI (one GPU per rank); gloo = host transport, lets "
                          "several ranks share one GPU (multi-rank rehearsal on a 1-GPU box; --comm torch, no "
                          "whole-step graph: gloo collectives are not capturable)")
+    ap.add_argument("--grace-split", choices=["on", "off"], default="on",
+                    help="after the timed region, time the SAME whole-step graph with the GRACE exchange replaced "
+                         "by a no-op (None compressor, local comm: a copy) and report the difference as "
+                         "grace_ms_per_step (compress + collective + decode as the measured step pays it)")
+    ap.add_argument("--surface", choices=["engine", "ddp"], default="engine",
+                    help="engine: grace_amd DistributedOptimizer (bucketed GRACE engine, the default); ddp: "
+                         "torch DistributedDataParallel + grace_comm_hook (the DDP comm-hook surface; DDP owns "
+                         "bucketing and backward overlap; eager unless --graph full)")
     ap.add_argument("--comm", choices=["auto", "torch", "native", "native-inline", "xgmi"], default="auto",
                     help="collective runtime: torch = ProcessGroupNCCL (RCCL, its own stream: an event "
                          "fork/join per collective); native = grace_amd RCCL runtime on its comm stream; "
@@ -108,6 +116,8 @@ def main():
         local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if args.surface == "ddp":
+        args.force_dist = True  # DDP needs a process group even for one rank
     if world > 1 or args.force_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
@@ -141,6 +151,8 @@ def main():
     from grace_amd.parallel.graph import GraphedStep, graph_compute, graph_safe
 
     mode = args.graph
+    if args.surface == "ddp" and mode == "auto":
+        mode = "off"  # DDP's reducer is not captured by default (--graph full to try)
     if mode == "auto":
         # measured on MI355X (ResNet-50 Top-K 1%): full 3205 img/s, compute 2640, eager 2520-3240
         # (eager is host-launch bound: ~1100 kernels per step); full without overlap 3525
@@ -183,8 +195,33 @@ def main():
             else:
                 comm_kind = "torch (native comm failed)"
     grc = grace_from_params(dict(w.grace, world_size=world))
-    opt = DistributedOptimizer(base_opt, grc, named_parameters=named,
-                               bucket_cap_mb=args.bucket_mb, overlap=overlap, weights=weights)
+    ddp_state = None
+    if args.surface == "ddp":
+        from grace_amd.parallel import GraceHookState, grace_comm_hook
+
+        if weights is not None:
+            raise SystemExit("--surface ddp trains fp32 masters directly (use --bf16-weights off)")
+        model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], bucket_cap_mb=args.bucket_mb,
+                                                          gradient_as_bucket_view=True)
+        ddp_state = GraceHookState(grc)
+        model.register_comm_hook(ddp_state, grace_comm_hook)
+
+        class _DdpOpt:  # the bench loop's optimizer interface over DDP + a plain optimizer
+            engine = type("E", (), {"grc": grc})()
+
+            def zero_grad(self, set_to_none=True):
+                base_opt.zero_grad(set_to_none=set_to_none)
+
+            def step(self):
+                base_opt.step()
+
+            def abort_step(self):
+                pass
+
+        opt = _DdpOpt()
+    else:
+        opt = DistributedOptimizer(base_opt, grc, named_parameters=named,
+                                   bucket_cap_mb=args.bucket_mb, overlap=overlap, weights=weights)
     data = w.make_batch(batch, dev)
     if w.channels_last and isinstance(data, tuple) and data[0].dim() == 4:
         data = (data[0].contiguous(memory_format=torch.channels_last),) + tuple(data[1:])
@@ -294,6 +331,42 @@ def main():
     if world > 1:
         dist.all_reduce(ex, op=dist.ReduceOp.MAX)
 
+    # GRACE's cost inside the measured path: the same whole-step graph with the exchange replaced by
+    # a no-op (None + local comm = one copy per bucket), timed the same way; the difference is
+    # compress + collective (+ wait) + decode as the graphed step pays it
+    grace_ms = noop_ms = None
+    if args.grace_split == "on" and graph_note == "full" and args.surface == "engine":
+        from grace_amd.parallel.comm import LocalComm
+
+        opt.engine.remove()  # the measured engine's hooks must not fire in the no-op graph
+        noop = DistributedOptimizer(base_opt, grace_from_params({"compressor": "none", "communicator": "allreduce"},
+                                                                comm=LocalComm()),
+                                    named_parameters=named, bucket_cap_mb=args.bucket_mb, overlap=False,
+                                    weights=weights)
+
+        def noop_step():
+            noop.zero_grad(set_to_none=set_to_none)
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp, cache_enabled=False):
+                l3 = w.loss(model, data)
+            l3.backward()
+            noop.step()
+            return l3
+
+        run2 = GraphedStep(noop_step, warmup=3)
+        for _ in range(3):
+            run2()
+        torch.cuda.synchronize()
+        barrier()
+        t2 = time.perf_counter()
+        for _ in range(args.steps):
+            run2()
+        torch.cuda.synchronize()
+        e2 = torch.tensor([time.perf_counter() - t2], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(e2, op=dist.ReduceOp.MAX)
+        noop_ms = float(e2.item()) / args.steps * 1e3
+        grace_ms = elapsed / args.steps * 1e3 - noop_ms
+
     samples = w.samples_per_batch(batch) * world * args.steps
     value = samples / elapsed
     per_gpu = [w.samples_per_batch(batch) / (ms * 1e-3) for ms in step_ms if ms > 0]
@@ -327,6 +400,7 @@ def main():
                 "hip_graph": graph_note,
                 "comm": comm_kind,
                 "grad_mode": args.grad_mode,
+                "surface": args.surface + (f" ({len(ddp_state.layouts)} DDP buckets)" if ddp_state else ""),
                 "bf16_weights": weights is not None,
                 "optimizer": f"{'FusedSGD' if args.optimizer == 'fused' else 'torch.optim.SGD'}(lr={0.01 * world:g}, momentum=0.5)",
             },
@@ -335,7 +409,9 @@ def main():
             "exchange_ms": {k.replace("_ms_per_step", ""): round(v, 4) for k, v in split.items()
                             if k.endswith("_ms_per_step")},
             "bytes_on_wire_per_rank": int(split.get("bytes_per_step", 0)),
-            "exposed_exchange_ms": round(float(ex.item()) * 1e3, 3),
+            "grace_ms_per_step": None if grace_ms is None else round(grace_ms, 3),
+            "noop_exchange_ms_per_step": None if noop_ms is None else round(noop_ms, 3),
+            "exposed_exchange_ms_eager": round(float(ex.item()) * 1e3, 3),
             "final_loss": round(float(loss.float().item()), 4),
         }
         print(json.dumps(out), flush=True)

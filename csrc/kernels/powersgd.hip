@@ -359,8 +359,12 @@ __device__ void mgs_gram_metric(const double (*G)[16], double (*Tm)[16], int r) 
     double nn = 0.0;  // ||A t_i||^2 = t_i^T G t_i
     for (int a = 0; a <= i; ++a)
       for (int b = 0; b <= i; ++b) nn += Tm[a][i] * G[a][b] * Tm[b][i];
-    const double nrm = nn > 0.0 ? sqrt(nn) : 0.0;
-    const double inv = nrm > 1e-30 ? 1.0 / nrm : 0.0;  // zero column stays zero
+    // a column (numerically) inside the span of the previous ones -- residual norm below 1e-5 of
+    // its own original norm (||A e_i||^2 = G[i][i]) -- becomes ZERO instead of normalised noise
+    // (a rank-deficient P, e.g. dead ReLU rows, would otherwise gain a spurious direction and
+    // P-hat P-hat^T would no longer be a projection); zero columns stay zero
+    const double nrm = nn > 1e-10 * G[i][i] && nn > 0.0 ? sqrt(nn) : 0.0;
+    const double inv = nrm > 1e-30 ? 1.0 / nrm : 0.0;
     for (int a = 0; a <= i; ++a) Tm[a][i] *= inv;
     for (int j = i + 1; j < r; ++j) {
       double pr = 0.0;  // <A t_i, A t_j> = t_i^T G t_j
@@ -381,8 +385,8 @@ __device__ __forceinline__ void mgs_gram_metric_reg(const double (&G)[4][4], dou
     for (int a = 0; a <= i; ++a)
 #pragma unroll
       for (int b = 0; b <= i; ++b) nn += Tm[a][i] * G[a][b] * Tm[b][i];
-    const double nrm = nn > 0.0 ? sqrt(nn) : 0.0;
-    const double inv = nrm > 1e-30 ? 1.0 / nrm : 0.0;  // zero column stays zero
+    const double nrm = nn > 1e-10 * G[i][i] && nn > 0.0 ? sqrt(nn) : 0.0;  // as mgs_gram_metric
+    const double inv = nrm > 1e-30 ? 1.0 / nrm : 0.0;
 #pragma unroll
     for (int a = 0; a <= i; ++a) Tm[a][i] *= inv;
 #pragma unroll

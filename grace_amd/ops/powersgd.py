@@ -136,7 +136,10 @@ def _views(buf, plan, which):
 
 def orthogonalize(buf: torch.Tensor, plan: Plan, which: str) -> None:
     """In-place Gram-Schmidt of the columns of every P_i (or Q_i) -- reference
-    dist/compressor/powersgd.py:7-18 (zero columns stay zero instead of becoming NaN)."""
+    dist/compressor/powersgd.py:7-18.  Zero columns stay zero instead of becoming NaN, and a
+    column that is numerically dependent on the previous ones (residual below 1e-5 of its norm:
+    a rank-deficient P) becomes zero instead of normalised rounding noise (the reference's
+    ``col / (norm + 1e-8)`` turns it into an arbitrary non-orthogonal direction)."""
     if _native.use_native(buf):
         # Gram-matrix MGS on MFMA, two passes (CholQR2): csrc/kernels/powersgd.hip
         t = plan.tables(buf.device)
@@ -147,10 +150,16 @@ def orthogonalize(buf: torch.Tensor, plan: Plan, which: str) -> None:
         return
     for a in _views(buf, plan, which):
         r = a.shape[1]
+        n0 = torch.sum(a.double() * a.double(), dim=0)  # original squared column norms
         for i in range(r):
             col = a[:, i:i + 1]
-            nrm = torch.sqrt(torch.sum(col * col))
-            col /= torch.clamp(nrm, min=1e-30)
+            nn = torch.sum(col.double() * col.double())
+            # numerically dependent (residual < 1e-5 of the original norm) or zero -> zero column
+            # (as the native Gram MGS; normalised cancellation noise would add a spurious direction)
+            if nn <= 1e-10 * n0[i] or nn <= 0:
+                col.zero_()
+            else:
+                col /= torch.sqrt(nn).float()
             if i + 1 < r:
                 rest = a[:, i + 1:]
                 rest -= torch.sum(col * rest, dim=0) * col

@@ -1,17 +1,28 @@
 """GRACE as a ``torch.nn.parallel.DistributedDataParallel`` communication hook.
 
-The reference predates DDP comm hooks (survey 2.12); this is the north-star integration:
-``ddp.register_comm_hook(GraceHookState(grc), grace_comm_hook)`` and DDP's own bucketing,
-backward overlap and gradient copy-back drive the GRACE pipeline.
+The reference predates DDP comm hooks (survey 2.12); its torch.distributed surface is the
+per-parameter loop ``grc.step(p.grad, name)`` after backward
+(/root/reference/examples/dist/CIFAR10-dawndist/core.py:203-206).  This is the north-star
+integration: ``ddp.register_comm_hook(GraceHookState(grc), grace_comm_hook)`` and DDP's own
+bucketing, backward overlap and gradient copy-back drive the GRACE pipeline, with the SAME
+per-parameter semantics as that loop (Top-K keeps a per-tensor k, EF-Sign a per-tensor scale ...).
 
 For each DDP bucket the hook (called from the autograd thread as soon as the bucket is ready):
-  1. registers the bucket's parameter layout (per-parameter compression semantics),
-  2. forks a side **compress stream** from the compute stream and on it runs the fused
-     compress kernels, the async RCCL collective and the one-pass decompress/aggregate,
-  3. returns a ``torch.futures.Future`` completed on that side stream -- DDP's finaliser waits
-     on its CUDA event, so backward compute is never blocked by the collective.
+  1. derives the bucket's per-parameter layout from ``bucket.gradients()`` (views into the
+     bucket buffer).  When DDP left gaps between the views (alignment padding), the gradients
+     are first packed into a dense buffer with that layout and unpacked afterwards -- never a
+     silent fall-back to one whole-bucket segment.  The bucket's GRACE name is derived from its
+     parameters, and when DDP re-buckets (it does after the first iteration) the per-element
+     GRACE state of the old buckets -- residuals, momenta -- is re-homed parameter by parameter
+     into the new ones, so error feedback carries over exactly as in the per-parameter loop;
+  2. runs compress + the async collective on a side **compress stream** forked from the
+     compute stream, and the decode/aggregate on a separate **decode stream** that waits for the
+     collective: the next bucket's compress never queues behind this bucket's decode, so
+     compress(i+1) overlaps collective(i) and both overlap the rest of backward;
+  3. returns a ``torch.futures.Future`` carrying the decoded bucket (completed on the decode
+     stream -- DDP's finaliser waits on its CUDA event, backward compute is never blocked).
 """
-from typing import Dict
+from typing import Dict, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -24,45 +35,132 @@ class GraceHookState:
     def __init__(self, grc: Communicator, name: str = "ddp"):
         self.grc = grc
         self.name = name
-        self.layouts: Dict[int, SegmentLayout] = {}
-        self.streams: Dict[int, torch.cuda.Stream] = {}
+        # bucket index -> (layout, packed index or None, buffer numel, GRACE name, param signature)
+        self.layouts: Dict[int, tuple] = {}
+        self.streams: Dict[int, Tuple[torch.cuda.Stream, torch.cuda.Stream]] = {}
+        self.packed_buckets = 0  # buckets that needed the pack/unpack path (padding)
+        self.migrations = 0      # per-element state re-homed after a DDP re-bucketing
+        # id(param) -> (GRACE bucket name, flat offset, numel, layout total) of its current bucket
+        self._loc: Dict[int, Tuple[str, int, int, int]] = {}
 
-    def layout_for(self, bucket) -> str:
+    def layout_for(self, bucket) -> Tuple[str, Optional[torch.Tensor]]:
+        """(registered layout name, None | int64 index of the packed elements in the buffer)."""
         idx = bucket.index()
-        key = f"{self.name}.bucket{idx}"
-        lay = self.layouts.get(idx)
         buf = bucket.buffer()
-        if lay is None or lay.total != buf.numel():
+        params = bucket.parameters()
+        sig = tuple(id(p) for p in params)
+        ent = self.layouts.get(idx)
+        if ent is None or ent[2] != buf.numel() or ent[4] != sig:
+            from ..ops.randomk import fnv1a64
+
             grads = bucket.gradients()
             lay = SegmentLayout.from_tensors(grads)
-            if lay.total != buf.numel():  # padding inside the bucket: single segment
-                lay = SegmentLayout((buf.numel(),), ((buf.numel(),),))
-            self.layouts[idx] = lay
+            es = buf.element_size()
+            offs = [(g.data_ptr() - buf.data_ptr()) // es for g in grads]
+            dense = all(o == lay.offsets[i] for i, o in enumerate(offs)) and lay.total == buf.numel()
+            pidx = None
+            if not dense:  # DDP padding between the views: pack per-parameter segments densely
+                pidx = torch.cat([torch.arange(o, o + g.numel(), dtype=torch.int64) for o, g in zip(offs, grads)])
+                pidx = pidx.to(buf.device)
+                self.packed_buckets += 1
+            shapes = ";".join(f"{tuple(g.shape)}" for g in grads)
+            key = f"{self.name}.b{idx}.{fnv1a64(shapes.encode()) ^ (hash(sig) & 0xFFFFFFFF):016x}"
             register_layout(key, lay)
-        return key
+            self._migrate(key, params, lay)
+            ent = (lay, pidx, buf.numel(), key, sig)
+            self.layouts[idx] = ent
+        return ent[3], ent[1]
+
+    def _containers(self):
+        """The name-keyed per-element state dicts of the memory and the compressor."""
+        for obj in (self.grc.memory, self.grc.compressor):
+            for v in list(vars(obj).values()):
+                if isinstance(v, dict) and v and all(isinstance(k, str) for k in v):
+                    yield v
+
+    def _migrate(self, key: str, params, lay: SegmentLayout) -> None:
+        """Re-home the per-element state of ``params`` from their previous buckets into ``key``."""
+        moves = []
+        for i, p in enumerate(params):
+            old = self._loc.get(id(p))
+            if old is not None and old[0] != key:
+                moves.append((i, old))
+            self._loc[id(p)] = (key, lay.offsets[i], lay.numels[i], lay.total)
+        if not moves:
+            return
+        for d in self._containers():
+            new = None
+            for i, (oname, ooff, on, ototal) in moves:
+                src = d.get(oname)
+                if not isinstance(src, torch.Tensor) or src.numel() != ototal or on != lay.numels[i]:
+                    continue
+                if new is None:
+                    new = d.get(key)
+                    if not isinstance(new, torch.Tensor) or new.numel() != lay.total:
+                        new = torch.zeros(lay.total, dtype=src.dtype, device=src.device)
+                        d[key] = new
+                new.view(-1)[lay.offsets[i]:lay.offsets[i] + on].copy_(src.reshape(-1)[ooff:ooff + on])
+        self.migrations += 1
+
+    def _streams(self, dev):
+        st = self.streams.get(dev.index)
+        if st is None:
+            st = self.streams[dev.index] = (torch.cuda.Stream(dev), torch.cuda.Stream(dev))
+        return st
+
+
+def _record(obj, stream, depth=0):
+    if depth > 6 or obj is None:
+        return
+    if isinstance(obj, torch.Tensor):
+        if obj.is_cuda:
+            obj.record_stream(stream)
+    elif isinstance(obj, (list, tuple)):
+        for o in obj:
+            _record(o, stream, depth + 1)
+    elif isinstance(obj, dict):
+        for o in obj.values():
+            _record(o, stream, depth + 1)
+    elif hasattr(obj, "__dict__") and not isinstance(obj, type):
+        for o in vars(obj).values():
+            _record(o, stream, depth + 1)
 
 
 def grace_comm_hook(state: GraceHookState, bucket: dist.GradBucket) -> torch.futures.Future[torch.Tensor]:
     buf = bucket.buffer()
-    name = state.layout_for(bucket)
+    name, pidx = state.layout_for(bucket)
     grc = state.grc
+
+    def packed(t):
+        g = t if t.dtype == torch.float32 else t.float()
+        return g if pidx is None else g.index_select(0, pidx)
+
+    def unpacked(out):
+        out = out.reshape(-1)
+        if pidx is None:
+            return out.to(buf.dtype).view_as(buf)
+        full = torch.zeros_like(buf)
+        full.index_copy_(0, pidx, out.to(buf.dtype))
+        return full
+
     if not buf.is_cuda:
-        out = grc.step(buf if buf.dtype == torch.float32 else buf.float(), name)
+        out = grc.step(packed(buf), name)
         fut = torch.futures.Future()
-        fut.set_result(out.to(buf.dtype).view_as(buf))
+        fut.set_result(unpacked(out))
         return fut
     dev = buf.device
-    s = state.streams.get(dev.index)
-    if s is None:
-        s = state.streams[dev.index] = torch.cuda.Stream(dev)
+    cs, ds = state._streams(dev)
     cur = torch.cuda.current_stream(dev)
-    s.wait_stream(cur)
+    cs.wait_stream(cur)
+    with torch.cuda.stream(cs):
+        g = packed(buf)
+        handles, ctx = grc.send_step(g, name)  # compress + async collective (comm stream or inline)
+    ds.wait_stream(cs)  # decode after this bucket's compress/issue; the collective is waited on inside
     fut = torch.futures.Future(devices=[dev])
-    with torch.cuda.stream(s):
-        g = buf if buf.dtype == torch.float32 else buf.float()
-        handles, ctx = grc.send_step(g, name)
-        out = grc.receive_step(handles, ctx)
-        out = out.to(buf.dtype).view_as(buf)
-        buf.record_stream(s)
+    with torch.cuda.stream(ds):
+        _record((handles, ctx), ds)
+        out = unpacked(grc.receive_step(handles, ctx))
+        buf.record_stream(ds)
+        g.record_stream(ds)
         fut.set_result(out)
     return fut

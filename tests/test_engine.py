@@ -214,3 +214,103 @@ def test_bf16_working_weights_channels_last_cpu():
     a = _mp_train("cpu", False, channels_last=True)
     b = _mp_train("cpu", True, channels_last=True)
     torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-6)
+
+
+def _ddp_net(seed=0):
+    torch.manual_seed(seed)
+    # every matrix has min(rows, cols) <= 4: PowerSGD rank 4 is then exact (full-rank P Q^T)
+    return nn.Sequential(nn.Conv2d(3, 4, 3, padding=1), nn.ReLU(), nn.AdaptiveAvgPool2d(2), nn.Flatten(),
+                         nn.Linear(16, 4), nn.ReLU(), nn.Linear(4, 3))
+
+
+def _ddp_value_body(rank, world, params, kind):
+    """DDP comm hook == the reference's per-parameter loop ``grc.step(p.grad, name)``
+    (examples/dist/CIFAR10-dawndist/core.py:203-206) on the same gradients, 3 steps with memory."""
+    from grace_amd import grace_from_params
+    from grace_amd.parallel import GraceHookState, grace_comm_hook
+
+    m = _ddp_net()
+    ddp = nn.parallel.DistributedDataParallel(m, bucket_cap_mb=0.0002)  # several buckets
+    st = GraceHookState(grace_from_params(dict(params, world_size=world)))
+    ddp.register_comm_hook(st, grace_comm_hook)
+    ref = _ddp_net()
+    grc_ref = grace_from_params(dict(params, world_size=world))
+    named = list(ref.named_parameters())
+    for s in range(3):
+        g = torch.Generator().manual_seed(100 * s + rank)
+        x, y = torch.randn(8, 3, 6, 6, generator=g), torch.randint(0, 3, (8,), generator=g)
+        for p in ddp.parameters():
+            p.grad = None
+        F.cross_entropy(ddp(x), y).backward()
+        ref.zero_grad()
+        F.cross_entropy(ref(x), y).backward()
+        exp = [grc_ref.step(p.grad.clone(), n) for n, p in named]  # per-parameter loop (reverse not needed)
+        got = [p.grad for p in ddp.module.parameters()]
+        for (n, _), a, b in zip(named, got, exp):
+            if kind == "exact":
+                torch.testing.assert_close(a, b.view_as(a), rtol=1e-5, atol=1e-6, msg=f"{n} step {s}")
+            elif kind == "lowrank":  # full-rank PowerSGD: exact up to the CholQR2 rounding
+                torch.testing.assert_close(a, b.view_as(a), rtol=1e-3, atol=1e-4 * float(b.abs().max()) + 1e-7,
+                                           msg=f"{n} step {s}")
+            else:  # stochastic codec: independent seeds per name; the QSGD error bound holds
+                assert (a - b.view_as(a)).abs().max() <= 2 * float(b.abs().max()) + 1e-6, n
+        # keep both models on the same weights (compare gradients step by step)
+        with torch.no_grad():
+            for p, q in zip(ddp.module.parameters(), ref.parameters()):
+                p.sub_(0.05 * p.grad)
+                q.copy_(p)
+    # the DP invariant
+    for p in ddp.module.parameters():
+        t = p.detach().contiguous()
+        allv = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(allv, t)
+        assert all(torch.equal(a, allv[0]) for a in allv)
+    assert len(st.layouts) > 1
+
+
+@pytest.mark.parametrize("params,kind", [
+    ({"compressor": "topk", "compress_ratio": 0.3, "memory": "residual", "communicator": "allgather"}, "exact"),
+    ({"compressor": "efsignsgd", "lr": 0.1, "memory": "efsignsgd", "communicator": "allreduce"}, "exact"),
+    ({"compressor": "qsgd", "quantum_num": 127, "communicator": "allreduce"}, "bounded"),
+    ({"compressor": "powersgd", "compress_rank": 4, "memory": "powersgd", "communicator": "allreduce"}, "lowrank"),
+])
+@pytest.mark.parametrize("world", [2, 3])
+def test_ddp_hook_matches_per_parameter_loop_gloo(params, kind, world):
+    run_distributed(_ddp_value_body, world, params, kind)
+
+
+def test_ddp_hook_padded_bucket_keeps_per_parameter_layout():
+    """A bucket whose gradient views leave gaps (DDP alignment padding) is packed into the
+    per-parameter layout instead of collapsing to one whole-bucket segment."""
+    from grace_amd import grace_from_params
+    from grace_amd.parallel import GraceHookState, grace_comm_hook
+    from grace_amd.parallel.comm import LocalComm
+
+    buf = torch.zeros(40)
+    g1, g2 = buf[0:10].view(2, 5), buf[16:36].view(4, 5)  # gap at 10..16, tail 36..40
+    p1, p2 = torch.nn.Parameter(torch.zeros(2, 5)), torch.nn.Parameter(torch.zeros(4, 5))
+    torch.manual_seed(0)
+    g1.copy_(torch.randn(2, 5))
+    g2.copy_(torch.randn(4, 5))
+
+    class FakeBucket:
+        def index(self):
+            return 0
+
+        def buffer(self):
+            return buf
+
+        def gradients(self):
+            return [g1, g2]
+
+        def parameters(self):
+            return [p1, p2]
+
+    params = {"compressor": "topk", "compress_ratio": 0.2, "communicator": "allgather"}
+    st = GraceHookState(grace_from_params(params, comm=LocalComm()))
+    out = grace_comm_hook(st, FakeBucket()).wait()
+    assert st.packed_buckets == 1 and st.layouts[0][0].numels == (10, 20)
+    ref = grace_from_params(params, comm=LocalComm())
+    torch.testing.assert_close(out[0:10].view(2, 5), ref.step(g1.clone(), "a"))
+    torch.testing.assert_close(out[16:36].view(4, 5), ref.step(g2.clone(), "b"))
+    assert float(out[10:16].abs().sum()) == 0 and float(out[36:].abs().sum()) == 0

@@ -421,3 +421,21 @@ def test_qsgd_packed_codes_gpu(s, bits):
     ref_cpu = torch.zeros(tp[0].numel(), dtype=torch.uint8)
     Q.qsgd_pack(codes, s, bits, ref_cpu)
     assert torch.equal(tp[0].cpu(), ref_cpu)
+
+
+def test_powersgd_rank_deficient_is_exact_gpu():
+    """A full-rank-capable PowerSGD (rank >= min(n, m)) on a rank-DEFICIENT matrix (a zero row,
+    e.g. dead ReLU units) must reproduce the matrix: the dependent column of P becomes zero in
+    the native Gram MGS instead of normalised rounding noise."""
+    from grace_amd import grace_from_params
+    from grace_amd.parallel.comm import LocalComm
+
+    torch.manual_seed(0)
+    for shape, dead in (((4, 16), 2), ((3, 4), 1), ((8, 300), 5)):
+        m = torch.randn(*shape, device="cuda") * 0.01
+        m[dead, :] = 0
+        g = grace_from_params({"compressor": "powersgd", "compress_rank": min(shape), "communicator": "allreduce"},
+                              comm=LocalComm())
+        out = g.step(m.clone(), "w")
+        torch.cuda.synchronize()
+        assert (out - m).abs().max() <= 1e-5 * m.abs().max(), shape
