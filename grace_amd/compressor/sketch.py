@@ -7,8 +7,10 @@ quantile edges of x (tfp.stats.quantiles), bin of every element (tfp find_bins),
 Here per segment: edges from torch.quantile (linear interpolation, as the reference), bins by
 searchsorted clamped to [0, q-1] (values equal to the last edge go to the last bin), bin means
 by index_add.  Payload [bins uint8/int16 | means fp32 (q per segment)].  On the GPU the edges of
-ALL segments come from one segmented sort, and bucketisation + per-bin sums/counts
-(csrc/kernels/cast_sketch.hip) and the W-rank decode are single passes.
+ALL segments come from the native segmented multi-rank radix select (csrc/kernels/quantile.hip;
+any q up to 1024: q >= 128 runs it in batches of 256 ranks per segment), and bucketisation +
+per-bin sums/counts (csrc/kernels/cast_sketch.hip) and the W-rank decode are single passes --
+no sort on the GPU path, graph-capturable for every q.
 """
 from __future__ import annotations
 
@@ -50,59 +52,104 @@ def segmented_quantile_edges(x: torch.Tensor, lay, q: int) -> torch.Tensor:
     return (a * (1 - w) + b * w).contiguous()
 
 
-_QSEL_CHUNK = 65536  # elements per workgroup of the selection passes (LDS setup amortised)
-_CODEC_CHUNK = 32768  # encode / decode: per-workgroup LDS bin tables amortised over 32K elements
+import os as _os
+
+# elements per workgroup of the selection passes (LDS setup amortised) and of encode / decode
+# (per-workgroup LDS bin tables amortised); env-tunable for sweeps on the GPU box
+_QSEL_CHUNK = int(_os.environ.get("GRACE_QSEL_CHUNK", 65536))
+_CODEC_CHUNK = int(_os.environ.get("GRACE_CODEC_CHUNK", 32768))
 
 
-def _qsel_tables(lay, q: int, dev: torch.device):
-    """Per-layout tables of the native selection: the sorted distinct ranks floor/ceil(j (n-1)/q)
-    of every segment, the positions of each edge's two ranks among them, the interpolation
-    weights (float64 positions rounded to fp32 exactly as ``segmented_quantile_edges``) and the
-    zero-initialised histograms / state the kernels leave clean after every call."""
-    def build():
-        n = torch.tensor(lay.numels, dtype=torch.float64)
-        probs = torch.linspace(0, 1, q + 1, dtype=torch.float64)
-        pos = probs[None, :] * (n[:, None] - 1).clamp_min(0)
-        lo, hi = pos.floor(), pos.ceil()
-        w = (pos - lo).float()
-        per = []
-        for i in range(lay.n_seg):
-            per.append(sorted(set(lo[i].long().tolist()) | set(hi[i].long().tolist())) if lay.numels[i] else [])
-        ms = max(1, max(len(r) for r in per))
-        if ms > 256:
-            return None
-        ranks = torch.zeros(lay.n_seg, ms, dtype=torch.int32)
-        lo_idx = torch.zeros(lay.n_seg, q + 1, dtype=torch.int32)
-        hi_idx = torch.zeros(lay.n_seg, q + 1, dtype=torch.int32)
-        for i, r in enumerate(per):
-            if not r:
-                continue
-            ranks[i, :len(r)] = torch.tensor(r, dtype=torch.int32)
+_QSEL_MAX_RANKS = 256  # distinct target ranks per segment one selection batch resolves
+
+
+def _rank_plan(lay, q: int):
+    """Per segment: the sorted distinct ranks floor/ceil(j (n-1)/q) and each edge's two positions
+    among them, plus the interpolation weights (float64 positions rounded to fp32 exactly as
+    ``segmented_quantile_edges``)."""
+    n = torch.tensor(lay.numels, dtype=torch.float64)
+    probs = torch.linspace(0, 1, q + 1, dtype=torch.float64)
+    pos = probs[None, :] * (n[:, None] - 1).clamp_min(0)
+    lo, hi = pos.floor(), pos.ceil()
+    w = (pos - lo).float()
+    per, lo_idx, hi_idx = [], torch.zeros(lay.n_seg, q + 1, dtype=torch.int32), torch.zeros(lay.n_seg, q + 1,
+                                                                                            dtype=torch.int32)
+    for i in range(lay.n_seg):
+        r = sorted(set(lo[i].long().tolist()) | set(hi[i].long().tolist())) if lay.numels[i] else []
+        per.append(r)
+        if r:
             where = {v: j for j, v in enumerate(r)}
             lo_idx[i] = torch.tensor([where[int(v)] for v in lo[i].tolist()], dtype=torch.int32)
             hi_idx[i] = torch.tensor([where[int(v)] for v in hi[i].tolist()], dtype=torch.int32)
-        z = lambda *shape: torch.zeros(*shape, dtype=torch.int32, device=dev)
-        return {"max_slots": ms, "ranks": ranks.to(dev), "nrank": torch.tensor([len(r) for r in per], dtype=torch.int32,
-                                                                               device=dev),
-                "lo_idx": lo_idx.to(dev), "hi_idx": hi_idx.to(dev), "w": w.contiguous().to(dev),
-                "h0": z(lay.n_seg * 2048), "h": z(lay.n_seg * ms * 128), "st_pfx": z(lay.n_seg * ms),
-                "st_rank": z(lay.n_seg * ms), "slot": z(lay.n_seg * ms), "uniq": z(lay.n_seg * ms),
-                "nuniq": z(lay.n_seg)}
+    return per, lo_idx, hi_idx, w
+
+
+def _batch_tables(lay, per, dev, lo_idx=None, hi_idx=None, w=None, q=None):
+    """Device tables of one selection batch (<= 256 distinct ranks per segment).  Without
+    lo/hi/w the batch emits the VALUES of its ranks (edge j = rank j: lo = hi = j, w = 0)."""
+    ms = max(1, max(len(r) for r in per))
+    ranks = torch.zeros(lay.n_seg, ms, dtype=torch.int32)
+    for i, r in enumerate(per):
+        if r:
+            ranks[i, :len(r)] = torch.tensor(r, dtype=torch.int32)
+    if lo_idx is None:
+        nq = ms - 1
+        ident = torch.stack([torch.clamp(torch.arange(ms), max=max(0, len(r) - 1)) for r in per]).to(torch.int32)
+        lo_idx, hi_idx, w, q = ident, ident, torch.zeros(lay.n_seg, ms), nq
+    z = lambda *shape: torch.zeros(*shape, dtype=torch.int32, device=dev)
+    return {"max_slots": ms, "q": q, "ranks": ranks.to(dev),
+            "nrank": torch.tensor([len(r) for r in per], dtype=torch.int32, device=dev),
+            "lo_idx": lo_idx.contiguous().to(dev), "hi_idx": hi_idx.contiguous().to(dev), "w": w.contiguous().to(dev),
+            "h0": z(lay.n_seg * 2048), "h": z(lay.n_seg * ms * 128), "st_pfx": z(lay.n_seg * ms),
+            "st_rank": z(lay.n_seg * ms), "slot": z(lay.n_seg * ms), "uniq": z(lay.n_seg * ms),
+            "nuniq": z(lay.n_seg)}
+
+
+def _qsel_tables(lay, q: int, dev: torch.device):
+    """Per-layout selection plan.  q <= 127 (<= 256 distinct ranks per segment): ONE batch that
+    emits the interpolated edges directly.  Larger q: the distinct ranks are split into batches
+    of <= 256 per segment; each batch emits the VALUES of its ranks, and the edges are
+    interpolated from them (same unfused fp32 mul/add rounding as the kernel and the sort path).
+    The workspaces are zero-initialised; the kernels leave them clean after every call."""
+    def build():
+        per, lo_idx, hi_idx, w = _rank_plan(lay, q)
+        ms = max(1, max(len(r) for r in per))
+        if ms <= _QSEL_MAX_RANKS:
+            return {"direct": _batch_tables(lay, per, dev, lo_idx, hi_idx, w, q)}
+        nb = -(-ms // _QSEL_MAX_RANKS)
+        batches = [_batch_tables(lay, [r[b * _QSEL_MAX_RANKS:(b + 1) * _QSEL_MAX_RANKS] for r in per], dev)
+                   for b in range(nb)]
+        return {"batches": batches, "ms": ms, "lo_idx": lo_idx.long().to(dev), "hi_idx": hi_idx.long().to(dev),
+                "w": w.to(dev)}
     return lay.cached(dev, f"qsel:{q}", build)
 
 
-def native_quantile_edges(x: torch.Tensor, lay, q: int):
-    """[n_seg, q+1] edges from the HIP multi-rank radix select (csrc/kernels/quantile.hip), or
-    None when the layout needs more than 256 distinct ranks per segment (q > 127)."""
-    tb = _qsel_tables(lay, q, x.device)
-    if tb is None:
-        return None
-    ct = lay.device_tables(x.device, _QSEL_CHUNK)
-    edges = torch.empty(lay.n_seg, q + 1, device=x.device)
+def _run_select(x, lay, ct, tb, out):
     _native.lib().quantile_select(x, ct["seg"], ct["begin"], ct["end"], lay.n_seg, tb["max_slots"], tb["ranks"],
                                   tb["nrank"], tb["h0"], tb["h"], tb["st_pfx"], tb["st_rank"], tb["slot"],
-                                  tb["uniq"], tb["nuniq"], q, tb["lo_idx"], tb["hi_idx"], tb["w"], edges)
-    return edges
+                                  tb["uniq"], tb["nuniq"], tb["q"], tb["lo_idx"], tb["hi_idx"], tb["w"], out)
+
+
+def native_quantile_edges(x: torch.Tensor, lay, q: int):
+    """[n_seg, q+1] edges from the HIP multi-rank radix select (csrc/kernels/quantile.hip), for
+    any q: one batch of <= 256 distinct ranks per segment, or several (q >= 128) whose selected
+    values are then interpolated.  Bit-identical to ``segmented_quantile_edges``; no sort, no
+    host read (graph-capturable)."""
+    tb = _qsel_tables(lay, q, x.device)
+    ct = lay.device_tables(x.device, _QSEL_CHUNK)
+    if "direct" in tb:
+        edges = torch.empty(lay.n_seg, q + 1, device=x.device)
+        _run_select(x, lay, ct, tb["direct"], edges)
+        return edges
+    vals = torch.empty(lay.n_seg, len(tb["batches"]) * _QSEL_MAX_RANKS, device=x.device)
+    for b, bt in enumerate(tb["batches"]):
+        vb = torch.empty(lay.n_seg, bt["max_slots"], device=x.device)
+        _run_select(x, lay, ct, bt, vb)
+        vals[:, b * _QSEL_MAX_RANKS:b * _QSEL_MAX_RANKS + bt["max_slots"]] = vb
+    a = vals.gather(1, tb["lo_idx"])
+    c = vals.gather(1, tb["hi_idx"])
+    w = tb["w"]
+    return a * (1 - w) + c * w
 
 
 class SketchCompressor(BucketCompressor):
@@ -121,8 +168,6 @@ class SketchCompressor(BucketCompressor):
         bins, means = self.payload(x.device, [(bdt, (lay.total,)), (torch.float32, (q * lay.n_seg,))])
         if _native.use_native(x) and q <= 1024:
             edges = native_quantile_edges(x, lay, q)
-            if edges is None:
-                edges = segmented_quantile_edges(x, lay, q)
             sums = torch.zeros(lay.n_seg * q, device=x.device)
             cnts = torch.zeros(lay.n_seg * q, device=x.device)
             t = lay.device_tables(x.device, _CODEC_CHUNK)

@@ -12,11 +12,16 @@ A 1x1 stride-1 convolution over a channels_last activation is a plain GEMM over 
 ResNet bottlenecks; it falls back to ``F.conv2d`` whenever the fast path does not apply (CPU,
 bf16/autocast, non-channels_last input, odd channel counts, stride/padding/groups/bias).
 
-Opt-in (``GRACE_CONV_MFMA=1`` or ``set_enabled(True)``): measured per layer on ResNet-50 b32
-(profiles/r2_conv_fp32_mfma_vs_miopen.txt) the kernel is within ~10 % of MIOpen's tuned
-implicit-GEMM solvers (fwd+bwd of the 1x1 stride-1 layers 4.87 vs 4.47 ms per step), ahead on
-some backward shapes and behind on the memory-bound small-K forwards, so MIOpen stays the
-default conv path.
+Per-direction autotuned dispatch (``GRACE_CONV_AUTO=1``, the default for fp32 channels_last):
+every 1x1 stride-1 layer times, once per (shape, direction) on the device, three backends
+-- MIOpen (``F.conv2d`` / ``aten.convolution_backward``; its time INCLUDES the zero-fill
+``SubTensorOpWithScalar1d`` kernels its implicit-GEMM solvers launch before every call), the
+hipBLASLt GEMM on the [M, C] views (``torch.mm``, no im2col, no fill) and the hand-written f32
+MFMA GEMM -- and keeps the fastest for that direction.  Decisions are taken in eager steps
+(never while a stream is being captured; a captured graph replays them) and are listed by
+``autotune_table()``.  ``GRACE_CONV_MFMA=1`` forces the MFMA GEMM for all three directions
+(measured per layer on ResNet-50 b32 within ~10 % of MIOpen's solvers,
+profiles/r2_conv_fp32_mfma_vs_miopen.txt).
 """
 from __future__ import annotations
 
@@ -79,6 +84,12 @@ class _Conv1x1Fn(torch.autograd.Function):
 
 
 _ENABLED = os.environ.get("GRACE_CONV_MFMA", "0") == "1"
+_AUTO = os.environ.get("GRACE_CONV_AUTO", "1") == "1"
+
+# (direction, M, Cin, Cout) -> backend name; and the measured times (ms) per backend
+_CHOICE = {}
+_TIMES = {}
+BACKENDS = ("miopen", "hipblaslt", "mfma")
 
 
 def set_enabled(on: bool) -> None:
@@ -86,8 +97,115 @@ def set_enabled(on: bool) -> None:
     _ENABLED = bool(on)
 
 
+def set_autotune(on: bool) -> None:
+    global _AUTO
+    _AUTO = bool(on)
+
+
+def autotune_table():
+    """[(direction, M, Cin, Cout, chosen, {backend: ms})] of every tuned layer direction."""
+    return [(k[0], k[1], k[2], k[3], v, dict(_TIMES.get(k, {}))) for k, v in sorted(_CHOICE.items())]
+
+
+def _x2d(t: torch.Tensor) -> torch.Tensor:
+    """[M, C] view of a channels_last NCHW tensor."""
+    return t.permute(0, 2, 3, 1).reshape(-1, t.shape[1])
+
+
+def _cl_from_2d(y2d: torch.Tensor, nb: int, h: int, w: int) -> torch.Tensor:
+    return y2d.view(nb, h, w, -1).permute(0, 3, 1, 2)
+
+
+def _run(direction: str, backend: str, x, wt, dy, wshape):
+    """One direction on one backend.  x: [N, Cin, H, W] channels_last; wt: [Cout, Cin]; dy:
+    [N, Cout, H, W] channels_last (backward) -- returns y / dx (channels_last) / dw [Cout, Cin]."""
+    nb, cin, h, w = x.shape
+    cout = wt.shape[0]
+    m = nb * h * w
+    if backend == "miopen":
+        w4 = wt.view(wshape)
+        if direction == "fwd":
+            return F.conv2d(x, w4)
+        mask = [direction == "dgrad", direction == "wgrad", False]
+        gi, gw, _ = torch.ops.aten.convolution_backward(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
+                                                        mask)
+        return gi if direction == "dgrad" else gw.reshape(cout, cin)
+    if backend == "hipblaslt":
+        if direction == "fwd":
+            return _cl_from_2d(torch.mm(_x2d(x), wt.t()), nb, h, w)
+        if direction == "dgrad":
+            return _cl_from_2d(torch.mm(_x2d(dy), wt), nb, h, w)
+        return torch.mm(_x2d(dy).t(), _x2d(x))
+    # mfma: csrc/kernels/gemm_f32.hip
+    if direction == "fwd":
+        y = torch.empty((nb, cout, h, w), device=x.device, dtype=torch.float32, memory_format=torch.channels_last)
+        gemm(x, True, cin, wt, True, cin, y, cout, m, cout, cin, 0)
+        return y
+    if direction == "dgrad":
+        dx = torch.empty_like(x, memory_format=torch.channels_last)
+        gemm(dy, True, cout, wt, False, cin, dx, cin, m, cin, cout, 0)
+        return dx
+    dw = torch.empty((cout, cin), device=x.device, dtype=torch.float32)
+    gemm(dy, False, cout, x, False, cin, dw, cin, cout, cin, m, _splits(cout, cin, m))
+    return dw
+
+
+def _pick(direction: str, x, wt, dy, wshape) -> str:
+    if _ENABLED:
+        return "mfma"
+    nb, cin, h, w = x.shape
+    key = (direction, nb * h * w, cin, wt.shape[0])
+    c = _CHOICE.get(key)
+    if c is not None:
+        return c
+    if torch.cuda.is_current_stream_capturing():
+        return "miopen"  # never time inside a capture
+    times = {}
+    for be in BACKENDS:
+        try:
+            for _ in range(2):
+                _run(direction, be, x, wt, dy, wshape)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(5):
+                _run(direction, be, x, wt, dy, wshape)
+            e.record()
+            e.synchronize()
+            times[be] = s.elapsed_time(e) / 5
+        except Exception:  # a backend that rejects the shape is simply not a candidate
+            continue
+    c = min(times, key=times.get) if times else "miopen"
+    _CHOICE[key] = c
+    _TIMES[key] = times
+    return c
+
+
+class _Conv1x1AutoFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight):
+        cout, cin = weight.shape[0], weight.shape[1]
+        wt = weight.reshape(cout, cin)
+        if not wt.is_contiguous():
+            wt = wt.contiguous()
+        y = _run("fwd", _pick("fwd", x, wt, None, weight.shape), x, wt, None, weight.shape)
+        ctx.save_for_backward(x, wt)
+        ctx.wshape = weight.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wt = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = _run("dgrad", _pick("dgrad", x, wt, dy, ctx.wshape), x, wt, dy, ctx.wshape)
+        if ctx.needs_input_grad[1]:
+            dw = _run("wgrad", _pick("wgrad", x, wt, dy, ctx.wshape), x, wt, dy, ctx.wshape).view(ctx.wshape)
+        return dx, dw
+
+
 def fast_ok(x: torch.Tensor, conv: nn.Conv2d, force: bool = False) -> bool:
-    if not (_ENABLED or force):
+    if not (_ENABLED or _AUTO or force):
         return False
     if not (x.is_cuda and x.dtype == torch.float32 and conv.weight.dtype == torch.float32):
         return False
@@ -110,5 +228,5 @@ class Conv1x1F32(nn.Conv2d):
 
     def forward(self, x):
         if fast_ok(x, self):
-            return _Conv1x1Fn.apply(x, self.weight)
+            return (_Conv1x1Fn if _ENABLED else _Conv1x1AutoFn).apply(x, self.weight)
         return super().forward(x)

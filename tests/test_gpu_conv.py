@@ -63,3 +63,31 @@ def test_conv1x1_f32_fwd_bwd(nb, cin, cout, hw):
     torch.testing.assert_close(x.grad.double().cpu(), xr.grad, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(conv.weight.grad.double().cpu(), wr.grad, rtol=1e-5, atol=1e-4)
     conv_mod.set_enabled(False)
+
+
+@pytest.mark.parametrize("nb,cin,cout,hw", [(4, 64, 256, 14), (2, 512, 128, 9), (8, 1024, 256, 14)])
+def test_conv1x1_autotuned_dispatch(nb, cin, cout, hw):
+    """The per-direction autotuned 1x1 path (MIOpen / hipBLASLt / MFMA GEMM, the fastest per
+    direction) computes the same convolution as the fp64 reference, and records its choices."""
+    torch.manual_seed(1)
+    conv_mod.set_enabled(False)
+    conv_mod.set_autotune(True)
+    conv = Conv1x1F32(cin, cout).cuda()
+    x = torch.randn(nb, cin, hw, hw, device="cuda").contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    for _ in range(2):  # first call tunes, second replays the choice
+        x.grad = None
+        conv.weight.grad = None
+        y = conv(x)
+        dy = torch.randn_like(y)
+        y.backward(dy)
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    xr = x.detach().double().cpu().requires_grad_(True)
+    wr = conv.weight.detach().double().cpu().requires_grad_(True)
+    yr = F.conv2d(xr, wr)
+    yr.backward(dy.double().cpu())
+    torch.testing.assert_close(y.detach().double().cpu(), yr, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(x.grad.double().cpu(), xr.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(conv.weight.grad.double().cpu(), wr.grad, rtol=1e-4, atol=1e-3)
+    m = nb * hw * hw
+    got = {d for d, mm, ci, co, _, _ in conv_mod.autotune_table() if (mm, ci, co) == (m, cin, cout)}
+    assert got == {"fwd", "dgrad", "wgrad"}

@@ -32,7 +32,7 @@ def _segments(seed=0):
     ]
 
 
-@pytest.mark.parametrize("q", [64, 16, 127])
+@pytest.mark.parametrize("q", [64, 16, 127, 255, 512])
 def test_native_edges_equal_sort_edges(q):
     assert _native.available()
     segs = _segments()
@@ -82,3 +82,37 @@ def test_sketch_graph_replay_equals_eager():
     ref = comp.decompress(*comp.compress(x.clone(), "sk_graph")).clone()
     torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6)
     assert not torch.equal(got, eager)
+
+
+@pytest.mark.parametrize("q", [255, 512])
+def test_sketch_large_q_codec_and_graph(q):
+    """q >= 128 (uint16/int16 bins, batched native select): CPU parity and graph capture."""
+    from grace_amd.parallel.graph import graph_safe
+    from grace_amd import grace_from_params
+    from grace_amd.parallel.comm import LocalComm
+
+    assert graph_safe(grace_from_params({"compressor": "sketch", "quantiles": q}, comm=LocalComm())) is None
+    segs = _segments(3)
+    flat = torch.cat(segs)
+    lay = SegmentLayout.from_tensors(segs)
+    register_layout(f"skq{q}", lay)
+    comp_c, comp_g = Z.SketchCompressor(q), Z.SketchCompressor(q)
+    pc, cc = comp_c.compress(flat, f"skq{q}")
+    pg, cg = comp_g.compress(flat.cuda(), f"skq{q}")
+    assert pg[0].dtype == torch.int16 and torch.equal(pg[0].cpu(), pc[0])
+    torch.testing.assert_close(comp_g.decompress(pg, cg).cpu(), comp_c.decompress(pc, cc), rtol=1e-5, atol=1e-6)
+    x = flat.cuda()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        comp_g.decompress(*comp_g.compress(x, f"skq{q}"))
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = comp_g.decompress(*comp_g.compress(x, f"skq{q}"))
+    x.mul_(0.5)
+    g.replay()
+    torch.cuda.synchronize()
+    got = out.clone()
+    ref = comp_g.decompress(*comp_g.compress(x.clone(), f"skq{q}")).clone()
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6)
