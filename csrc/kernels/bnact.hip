@@ -34,6 +34,7 @@
 //
 // Constraints (host-checked, other shapes use the PyTorch path): C % 8 == 0, C <= 2048, and
 // C % 256 == 0 when C > 256.
+#include <cstdlib>
 #include <type_traits>
 
 #include "grace_common.h"
@@ -434,10 +435,14 @@ __device__ __forceinline__ void add8(Bf8& d, const T* p) {
 // RX (with RELU): no saved mask -- the ReLU mask is recomputed from x as fmaf(x, scale, shift)
 // > 0, the exact expression the forward apply thresholds (the fused stem's forward writes no
 // mask: ops/bnact.py bn_relu_maxpool).
-template <typename T, bool RELU, bool DY2, bool RX = false>
+// WDZ: also store dz = [y > 0] (dy + dy2) (the residual input's gradient of a block-output BN):
+// the dx pass then reads dz and x only (bn_dx_dz_kernel) and dz IS d(residual) -- 7 activation
+// passes per layer instead of 8 (dy, dy2 and the mask read once, d(residual) not rewritten).
+template <typename T, bool RELU, bool DY2, bool RX = false, bool WDZ = false>
 __global__ __launch_bounds__(kB) void bn_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ dy2,
                                                        const T* __restrict__ x,
-                                                       const uint8_t* __restrict__ mask, Red R, GradOut o) {
+                                                       const uint8_t* __restrict__ mask, Red R, GradOut o,
+                                                       T* __restrict__ dzout = nullptr) {
   float s1[8], s2[8], mu[8], rsc[8], rsh[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) s1[j] = s2[j] = mu[j] = rsc[j] = rsh[j] = 0.f;
@@ -454,15 +459,18 @@ __global__ __launch_bounds__(kB) void bn_reduce_kernel(const T* __restrict__ dy,
       }
     }
   }
-  auto acc = [&](const Bf8& d, const Bf8& v, uint32_t mb) {
+  auto acc = [&](const Bf8& d, const Bf8& v, uint32_t mb, T* dzp) {
+    float z[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float dz = d.v[j];
       if constexpr (RELU && RX) dz = fmaf(v.v[j], rsc[j], rsh[j]) > 0.f ? dz : 0.f;
       else if constexpr (RELU) dz = (mb >> j) & 1u ? dz : 0.f;
+      z[j] = dz;
       s1[j] += dz;
       s2[j] = fmaf(dz, v.v[j] - mu[j], s2[j]);
     }
+    if constexpr (WDZ) st8(dzp, z);
   };
   // The 4-row batches address every operand through a buffer descriptor based at the block's
   // first row: one 32-bit VGPR offset per thread, the row step as a wave-uniform soffset.  With
@@ -495,14 +503,14 @@ __global__ __launch_bounds__(kB) void bn_reduce_kernel(const T* __restrict__ dy,
           for (int j = 0; j < 8; ++j) d[u].v[j] += d2[u].v[j];
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) acc(d[u], v[u], w[u]);
+      for (int u = 0; u < 4; ++u) acc(d[u], v[u], w[u], WDZ ? dzout + e + u * step : nullptr);
     } else {
       Bf8 d = ld8(dy + e);
       const Bf8 v = ld8(x + e);
       if constexpr (DY2) add8(d, dy2 + e);
       uint32_t w = 0;
       if constexpr (RELU && !RX) w = mask[e >> 3];
-      acc(d, v, w);
+      acc(d, v, w, WDZ ? dzout + e : nullptr);
     }
   });
   if (!block_reduce_tree(R, s1, s2)) return;
@@ -567,6 +575,32 @@ __global__ __launch_bounds__(kB) void bn_dx_kernel(const T* __restrict__ dy, con
   }
 }
 
+
+// dx = a*dz + b*x + c with dz already masked and summed (written by bn_reduce_kernel<WDZ>)
+template <typename T>
+__global__ __launch_bounds__(kB) void bn_dx_dz_kernel(const T* __restrict__ dz, const T* __restrict__ x,
+                                                      const float* __restrict__ coef, T* __restrict__ dx, int64_t n_vec,
+                                                      int C) {
+  const int tpr = C >> 3;
+  const int64_t stride = (int64_t)gridDim.x * kB;
+  int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x;
+  const int cg = (int)(i % tpr);
+  float ca[8], cb[8], cc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    ca[j] = coef[cg * 8 + j];
+    cb[j] = coef[C + cg * 8 + j];
+    cc[j] = coef[2 * C + cg * 8 + j];
+  }
+  for (; i < n_vec; i += stride) {
+    const Bf8 d = ld8(dz + i * 8);
+    const Bf8 v = ld8(x + i * 8);
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = fmaf(ca[j], d.v[j], fmaf(cb[j], v.v[j], cc[j]));
+    st8(dx + i * 8, o);
+  }
+}
 
 // ---------------------------------------------------------------- conv bias (+ ReLU)
 // VGG's conv -> bias -> ReLU (MIOpen returns the conv without its bias: PyTorch then runs a
@@ -1057,6 +1091,15 @@ const PlanKnobs& knobs() {
   return k;
 }
 
+// GRACE_BN_DZ=0 restores the 8-pass backward of the dual-gradient residual layers (A/B knob)
+bool bn_dz_mode() {
+  static const bool on = [] {
+    const char* e = std::getenv("GRACE_BN_DZ");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
+
 Red plan(int64_t M, int C, int fused_v = 0) {
   Red R{};
   R.M = M;
@@ -1303,11 +1346,32 @@ void backward_2k_rx(const T* dy, const T* x, int64_t M, int C, const GradOut& o,
                        (const T*)nullptr, x, (const uint8_t*)nullptr, coef, dx, dres, n_vec, C, o.save);
 }
 
+// Two gradients (dual output) AND a residual gradient wanted: the reduce pass stores dz (it is
+// d(residual)) and the dx pass reads dz + x -- see bn_reduce_kernel WDZ.
+template <typename T>
+void backward_2k_dz(const T* dy, const T* dy2, const T* x, const uint8_t* mask, int64_t M, int C, const GradOut& o,
+                    bool relu, const float* coef, float* ws, T* dx, T* dres, hipStream_t stream) {
+  Red R = plan(M, C);
+  bind_ws(R, ws, stream);
+  const dim3 grid(R.nchunks, C / R.CT);
+  if (relu)
+    hipLaunchKernelGGL((bn_reduce_kernel<T, true, true, false, true>), grid, dim3(kB), 0, stream, dy, dy2, x, mask,
+                       R, o, dres);
+  else
+    hipLaunchKernelGGL((bn_reduce_kernel<T, false, true, false, true>), grid, dim3(kB), 0, stream, dy, dy2, x, mask,
+                       R, o, dres);
+  const int64_t n_vec = M * C / 8;
+  hipLaunchKernelGGL(bn_dx_dz_kernel<T>, dim3(apply_grid(n_vec, C)), dim3(kB), 0, stream, (const T*)dres, x, coef, dx,
+                     n_vec, C);
+}
+
 template <typename T>
 void backward_2k(const T* dy, const T* dy2, const T* x, const uint8_t* mask, int64_t M, int C, const GradOut& o,
                  bool relu, const float* coef, float* ws, T* dx, T* dres, hipStream_t stream) {
   if (relu && mask == nullptr && dy2 == nullptr)
     backward_2k_rx<T>(dy, x, M, C, o, coef, ws, dx, dres, stream);
+  else if (std::is_same<T, float>::value && dy2 && dres && bn_dz_mode())  // fp32: dz stored exactly
+    backward_2k_dz<T>(dy, dy2, x, mask, M, C, o, relu, coef, ws, dx, dres, stream);
   else if (dy2)
     backward_2k_t<T, true>(dy, dy2, x, mask, M, C, o, relu, coef, ws, dx, dres, stream);
   else
