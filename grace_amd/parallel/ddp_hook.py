@@ -42,6 +42,7 @@ class GraceHookState:
         self.migrations = 0      # per-element state re-homed after a DDP re-bucketing
         # id(param) -> (GRACE bucket name, flat offset, numel, layout total) of its current bucket
         self._loc: Dict[int, Tuple[str, int, int, int]] = {}
+        self._gen: Dict[int, int] = {}
 
     def layout_for(self, bucket) -> Tuple[str, Optional[torch.Tensor]]:
         """(registered layout name, None | int64 index of the packed elements in the buffer)."""
@@ -63,8 +64,11 @@ class GraceHookState:
                 pidx = torch.cat([torch.arange(o, o + g.numel(), dtype=torch.int64) for o, g in zip(offs, grads)])
                 pidx = pidx.to(buf.device)
                 self.packed_buckets += 1
+            # rank-invariant name (seeds of RandomK & co. must agree across ranks): bucket index,
+            # shapes and the layout generation of that index (DDP re-buckets identically everywhere)
+            self._gen[idx] = self._gen.get(idx, -1) + 1
             shapes = ";".join(f"{tuple(g.shape)}" for g in grads)
-            key = f"{self.name}.b{idx}.{fnv1a64(shapes.encode()) ^ (hash(sig) & 0xFFFFFFFF):016x}"
+            key = f"{self.name}.b{idx}.{fnv1a64(shapes.encode()):016x}.g{self._gen[idx]}"
             register_layout(key, lay)
             self._migrate(key, params, lay)
             ent = (lay, pidx, buf.numel(), key, sig)

@@ -314,3 +314,29 @@ def test_ddp_hook_padded_bucket_keeps_per_parameter_layout():
     torch.testing.assert_close(out[0:10].view(2, 5), ref.step(g1.clone(), "a"))
     torch.testing.assert_close(out[16:36].view(4, 5), ref.step(g2.clone(), "b"))
     assert float(out[10:16].abs().sum()) == 0 and float(out[36:].abs().sum()) == 0
+
+
+def _ddp_randomk_body(rank, world):
+    """Random-K through the DDP hook: every rank must draw the SAME indices (rank-invariant bucket
+    names feed the shared seed), so each tensor's averaged gradient has exactly k non-zeros."""
+    from grace_amd import grace_from_params
+    from grace_amd.parallel import GraceHookState, grace_comm_hook
+
+    m = _ddp_net()
+    ddp = nn.parallel.DistributedDataParallel(m, bucket_cap_mb=0.0002)
+    ddp.register_comm_hook(GraceHookState(grace_from_params({"compressor": "randomk", "compress_ratio": 0.25,
+                                                             "communicator": "allreduce", "world_size": world})),
+                           grace_comm_hook)
+    for s in range(3):
+        g = torch.Generator().manual_seed(100 * s + rank)
+        x, y = torch.randn(8, 3, 6, 6, generator=g), torch.randint(0, 3, (8,), generator=g)
+        for p in ddp.parameters():
+            p.grad = None
+        F.cross_entropy(ddp(x), y).backward()
+        for p in ddp.module.parameters():
+            k = max(1, int(p.numel() * 0.25))
+            assert int((p.grad != 0).sum()) <= k, (tuple(p.shape), int((p.grad != 0).sum()), k)
+
+
+def test_ddp_hook_randomk_shared_indices_gloo():
+    run_distributed(_ddp_randomk_body, 2)
