@@ -656,7 +656,7 @@ static void check_operand(const Tensor& x, bool kc, int64_t ld, int64_t rows, in
 }
 
 void gemm_f32(const Tensor& A, bool a_kc, int64_t lda, const Tensor& B, bool b_kc, int64_t ldb, const Tensor& C,
-              int64_t ldc, int64_t M, int64_t N, int64_t K, int64_t splits) {
+              int64_t ldc, int64_t M, int64_t N, int64_t K, int64_t splits, int64_t tile) {
   check_operand(A, a_kc, lda, M, K, "A");
   check_operand(B, b_kc, ldb, N, K, "B");
   CHECK_DEV(C);
@@ -666,7 +666,7 @@ void gemm_f32(const Tensor& A, bool a_kc, int64_t lda, const Tensor& B, bool b_k
   TORCH_CHECK(M < (1LL << 31) && N < (1LL << 31) && K < (1LL << 31), "GEMM dims must fit int32");
   DevGuard guard(C.device());
   grace::gemm_f32(A.data_ptr<float>(), a_kc, lda, B.data_ptr<float>(), b_kc, ldb, C.data_ptr<float>(), ldc, (int)M,
-                  (int)N, (int)K, (int)splits, cur_stream());
+                  (int)N, (int)K, (int)splits, cur_stream(), (int)tile);
 }
 
 // ------------------------------------------------------------------------------ segment stats
@@ -970,7 +970,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sketch_encode", &sketch_encode);
   m.def("sketch_decode", &sketch_decode);
   m.def("quantile_select", &quantile_select);
-  m.def("gemm_f32", &gemm_f32);
+  m.def("gemm_f32", &gemm_f32, py::arg("A"), py::arg("a_kc"), py::arg("lda"), py::arg("B"), py::arg("b_kc"),
+        py::arg("ldb"), py::arg("C"), py::arg("ldc"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("splits"),
+        py::arg("tile") = 0);
   m.def("axpby", &axpby);
   m.def("scale_", &scale_);
   m.def("gather_segments", &gather_segments);

@@ -131,7 +131,7 @@ void quantile_select(const ChunkTable& ct, int n_seg, const float* x, int max_sl
 // C[m][n] (+)= sum_k A(m,k) B(n,k) on the f32 MFMA; X(r,k) = x[r*ld+k] (kcontig) or x[k*ld+r];
 // splits > 1: split-K with f32 atomics into C (zeroed here; needs ldc == N)
 void gemm_f32(const float* A, bool a_kcontig, int64_t lda, const float* B, bool b_kcontig, int64_t ldb, float* C,
-              int64_t ldc, int M, int N, int K, int splits, hipStream_t stream);
+              int64_t ldc, int M, int N, int K, int splits, hipStream_t stream, int tile = 0);
 
 // ---------------------------------------------------------------- ef.hip (elementwise)
 void axpby(const float* x, const float* y, float* out, int64_t n, float a, float b, hipStream_t stream);

@@ -261,8 +261,22 @@ void launch_layout(GemmParams p, hipStream_t stream) {
 
 }  // namespace
 
+namespace {
+// tile: 0 = by the launcher's rule, 1 = 128x128, 2 = 128x64, 3 = 64x128, 4 = 64x64
+template <bool AKC, bool BKC>
+void launch_tile(GemmParams p, int tile, hipStream_t stream) {
+  switch (tile) {
+    case 1: launch_cfg<128, 128, AKC, BKC>(p, stream); return;
+    case 2: launch_cfg<128, 64, AKC, BKC>(p, stream); return;
+    case 3: launch_cfg<64, 128, AKC, BKC>(p, stream); return;
+    case 4: launch_cfg<64, 64, AKC, BKC>(p, stream); return;
+    default: launch_layout<AKC, BKC>(p, stream);
+  }
+}
+}  // namespace
+
 void gemm_f32(const float* A, bool a_kcontig, int64_t lda, const float* B, bool b_kcontig, int64_t ldb, float* C,
-              int64_t ldc, int M, int N, int K, int splits, hipStream_t stream) {
+              int64_t ldc, int M, int N, int K, int splits, hipStream_t stream, int tile) {
   if (M <= 0 || N <= 0) return;
   GemmParams p{};
   p.A = A;
@@ -289,13 +303,13 @@ void gemm_f32(const float* A, bool a_kcontig, int64_t lda, const float* B, bool 
   p.c_vec = (reinterpret_cast<uintptr_t>(C) % 16 == 0) && (ldc % 4 == 0);
   if (p.atomic) GRACE_HIP_CHECK(hipMemsetAsync(C, 0, sizeof(float) * (size_t)M * ldc, stream));  // ldc == N (host-checked)
   if (a_kcontig && b_kcontig)
-    launch_layout<true, true>(p, stream);
+    launch_tile<true, true>(p, tile, stream);
   else if (a_kcontig && !b_kcontig)
-    launch_layout<true, false>(p, stream);
+    launch_tile<true, false>(p, tile, stream);
   else if (!a_kcontig && !b_kcontig)
-    launch_layout<false, false>(p, stream);
+    launch_tile<false, false>(p, tile, stream);
   else
-    launch_layout<false, true>(p, stream);
+    launch_tile<false, true>(p, tile, stream);
 }
 
 }  // namespace grace

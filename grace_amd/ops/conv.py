@@ -44,10 +44,11 @@ def _splits(m: int, n: int, k: int) -> int:
     return max(1, min(math.ceil(_TARGET_BLOCKS / tiles), k // 256))
 
 
-def gemm(a, a_kc, lda, b, b_kc, ldb, c, ldc, m, n, k, splits=1):
+def gemm(a, a_kc, lda, b, b_kc, ldb, c, ldc, m, n, k, splits=1, tile=0):
     """C[m, n] = sum_k A(m, k) B(n, k) (see csrc/kernels/gemm_f32.hip); splits=0: split-K chosen by
-    the launcher when the output has too few tiles to fill the chip (needs a dense C)."""
-    _native.lib().gemm_f32(a, a_kc, lda, b, b_kc, ldb, c, ldc, m, n, k, splits)
+    the launcher when the output has too few tiles to fill the chip (needs a dense C); tile:
+    0 = launcher's rule, 1 = 128x128, 2 = 128x64, 3 = 64x128, 4 = 64x64."""
+    _native.lib().gemm_f32(a, a_kc, lda, b, b_kc, ldb, c, ldc, m, n, k, splits, tile)
 
 
 class _Conv1x1Fn(torch.autograd.Function):
@@ -89,7 +90,7 @@ _AUTO = os.environ.get("GRACE_CONV_AUTO", "1") == "1"
 # (direction, M, Cin, Cout) -> backend name; and the measured times (ms) per backend
 _CHOICE = {}
 _TIMES = {}
-BACKENDS = ("miopen", "hipblaslt", "mfma")
+BACKENDS = ("miopen", "hipblaslt", "mfma", "mfma_t1", "mfma_t2", "mfma_t3", "mfma_t4")
 
 
 def set_enabled(on: bool) -> None:
@@ -136,17 +137,18 @@ def _run(direction: str, backend: str, x, wt, dy, wshape):
         if direction == "dgrad":
             return _cl_from_2d(torch.mm(_x2d(dy), wt), nb, h, w)
         return torch.mm(_x2d(dy).t(), _x2d(x))
-    # mfma: csrc/kernels/gemm_f32.hip
+    # mfma[_tN]: csrc/kernels/gemm_f32.hip with the launcher's tile rule or a forced tile
+    tile = int(backend[6:]) if backend.startswith("mfma_t") else 0
     if direction == "fwd":
         y = torch.empty((nb, cout, h, w), device=x.device, dtype=torch.float32, memory_format=torch.channels_last)
-        gemm(x, True, cin, wt, True, cin, y, cout, m, cout, cin, 0)
+        gemm(x, True, cin, wt, True, cin, y, cout, m, cout, cin, 0, tile)
         return y
     if direction == "dgrad":
         dx = torch.empty_like(x, memory_format=torch.channels_last)
-        gemm(dy, True, cout, wt, False, cin, dx, cin, m, cin, cout, 0)
+        gemm(dy, True, cout, wt, False, cin, dx, cin, m, cin, cout, 0, tile)
         return dx
     dw = torch.empty((cout, cin), device=x.device, dtype=torch.float32)
-    gemm(dy, False, cout, x, False, cin, dw, cin, cout, cin, m, _splits(cout, cin, m))
+    gemm(dy, False, cout, x, False, cin, dw, cin, cout, cin, m, _splits(cout, cin, m), tile)
     return dw
 
 
