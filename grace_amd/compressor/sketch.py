@@ -174,10 +174,12 @@ class SketchCompressor(BucketCompressor):
             _native.lib().sketch_encode(x, edges, q, bins, sums, cnts, t["seg"], t["begin"], t["end"])
             torch.where(cnts > 0, sums / cnts.clamp_min(1), torch.zeros_like(sums), out=means)
             return [bins, means], ctx
-        probs = torch.linspace(0, 1, q + 1, device=x.device)
+        # edges at float64 quantile positions j (n-1) / q (the native select's exact ranks and
+        # weights: fp32 positions mis-round for q not a power of two)
+        all_edges = segmented_quantile_edges(x, lay, q) if lay.total else None
         for i, o, n in lay.segments():
             seg = x[o:o + n]
-            edges = _quantiles(seg, probs) if n > 1 else seg.repeat(q + 1)
+            edges = all_edges[i].contiguous()
             b = (torch.searchsorted(edges, seg.contiguous(), right=True) - 1).clamp(0, q - 1)
             s = torch.zeros(q, device=x.device).index_add_(0, b, seg)
             c = torch.zeros(q, device=x.device).index_add_(0, b, torch.ones_like(seg))
