@@ -65,7 +65,7 @@ def test_conv1x1_f32_fwd_bwd(nb, cin, cout, hw):
     conv_mod.set_enabled(False)
 
 
-@pytest.mark.parametrize("nb,cin,cout,hw", [(4, 64, 256, 14), (2, 512, 128, 9), (8, 1024, 256, 14)])
+@pytest.mark.parametrize("nb,cin,cout,hw", [(4, 64, 256, 14), (2, 512, 128, 8), (8, 1024, 256, 14)])
 def test_conv1x1_autotuned_dispatch(nb, cin, cout, hw):
     """The per-direction autotuned 1x1 path (MIOpen / hipBLASLt / MFMA GEMM, the fastest per
     direction) computes the same convolution as the fp64 reference, and records its choices."""
