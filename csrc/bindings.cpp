@@ -655,8 +655,9 @@ static void check_operand(const Tensor& x, bool kc, int64_t ld, int64_t rows, in
   TORCH_CHECK(x.numel() >= need && ld >= (kc ? K : rows), what, ": view exceeds the tensor");
 }
 
-void gemm_f32(const Tensor& A, bool a_kc, int64_t lda, const Tensor& B, bool b_kc, int64_t ldb, const Tensor& C,
-              int64_t ldc, int64_t M, int64_t N, int64_t K, int64_t splits, int64_t tile) {
+int64_t gemm_f32(const Tensor& A, bool a_kc, int64_t lda, const Tensor& B, bool b_kc, int64_t ldb, const Tensor& C,
+                 int64_t ldc, int64_t M, int64_t N, int64_t K, int64_t splits, int64_t tile,
+                 const c10::optional<Tensor>& stats) {
   check_operand(A, a_kc, lda, M, K, "A");
   check_operand(B, b_kc, ldb, N, K, "B");
   CHECK_DEV(C);
@@ -664,9 +665,17 @@ void gemm_f32(const Tensor& A, bool a_kc, int64_t lda, const Tensor& B, bool b_k
   TORCH_CHECK(C.numel() >= (M - 1) * ldc + N && ldc >= N, "C too small");
   TORCH_CHECK(splits == 0 || splits == 1 || ldc == N, "split-K needs a dense C");
   TORCH_CHECK(M < (1LL << 31) && N < (1LL << 31) && K < (1LL << 31), "GEMM dims must fit int32");
+  float* st = nullptr;
+  if (stats.has_value() && stats->defined()) {
+    CHECK_DEV((*stats));
+    CHECK_DT((*stats), at::kFloat);
+    TORCH_CHECK(splits == 1, "GEMM statistics need whole-K tiles (splits = 1)");
+    TORCH_CHECK(stats->is_contiguous() && stats->numel() >= ((M + 63) / 64) * 2 * N, "stats: [ceil(M/64)][2][N]");
+    st = stats->data_ptr<float>();
+  }
   DevGuard guard(C.device());
-  grace::gemm_f32(A.data_ptr<float>(), a_kc, lda, B.data_ptr<float>(), b_kc, ldb, C.data_ptr<float>(), ldc, (int)M,
-                  (int)N, (int)K, (int)splits, cur_stream(), (int)tile);
+  return grace::gemm_f32(A.data_ptr<float>(), a_kc, lda, B.data_ptr<float>(), b_kc, ldb, C.data_ptr<float>(), ldc,
+                         (int)M, (int)N, (int)K, (int)splits, cur_stream(), (int)tile, st);
 }
 
 // ------------------------------------------------------------------------------ segment stats
@@ -972,7 +981,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("quantile_select", &quantile_select);
   m.def("gemm_f32", &gemm_f32, py::arg("A"), py::arg("a_kc"), py::arg("lda"), py::arg("B"), py::arg("b_kc"),
         py::arg("ldb"), py::arg("C"), py::arg("ldc"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("splits"),
-        py::arg("tile") = 0);
+        py::arg("tile") = 0, py::arg("stats") = py::none());
   m.def("axpby", &axpby);
   m.def("scale_", &scale_);
   m.def("gather_segments", &gather_segments);

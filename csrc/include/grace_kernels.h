@@ -130,8 +130,9 @@ void quantile_select(const ChunkTable& ct, int n_seg, const float* x, int max_sl
 // ---------------------------------------------------------------- gemm_f32.hip
 // C[m][n] (+)= sum_k A(m,k) B(n,k) on the f32 MFMA; X(r,k) = x[r*ld+k] (kcontig) or x[k*ld+r];
 // splits > 1: split-K with f32 atomics into C (zeroed here; needs ldc == N)
-void gemm_f32(const float* A, bool a_kcontig, int64_t lda, const float* B, bool b_kcontig, int64_t ldb, float* C,
-              int64_t ldc, int M, int N, int K, int splits, hipStream_t stream, int tile = 0);
+int gemm_f32(const float* A, bool a_kcontig, int64_t lda, const float* B, bool b_kcontig, int64_t ldb, float* C,
+              int64_t ldc, int M, int N, int K, int splits, hipStream_t stream, int tile = 0,
+             float* stats = nullptr);
 
 // ---------------------------------------------------------------- ef.hip (elementwise)
 void axpby(const float* x, const float* y, float* out, int64_t n, float a, float b, hipStream_t stream);
@@ -184,6 +185,10 @@ void bn_act_forward(const void* x, const void* res, bool fp32, int64_t M, int C,
                     const float* beta, float* running_mean, float* running_var, int64_t* nbt, float momentum,
                     float eps, bool relu, float* save, float* ws, void* y, uint8_t* relu_mask, hipStream_t stream);
 // dy2 (may be nullptr): a second gradient contribution of the same layout, summed into dy
+void bn_act_forward_from_partials(const float* x, const float* res, const float* part, int tiles, int64_t M, int C,
+                                  const float* gamma, const float* beta, float* running_mean, float* running_var,
+                                  int64_t* nbt, float momentum, float eps, bool relu, float* save, float* y,
+                                  uint8_t* mask, hipStream_t stream);
 void bn_act_backward(const void* dy, const void* dy2, const void* x, bool fp32, const uint8_t* relu_mask, int64_t M,
                      int C, const float* gamma, const float* save, bool relu, float* dgamma, float* dbeta,
                      float* coef, float* ws, void* dx, void* dres, hipStream_t stream);

@@ -1302,6 +1302,51 @@ void forward_2k(const T* x, const T* res, int64_t M, int C, const StatsOut& o, b
     hipLaunchKernelGGL((bn_apply_kernel<T, false, false>), dim3(gb), dim3(kB), 0, stream, x, res, save, y, mask, n_vec, C);
 }
 
+// BN statistics from the producing GEMM's epilogue partials (csrc/kernels/gemm_f32.hip p.stats:
+// per (row tile, channel) [sum | sum of squares] of the output as stored): the statistics pass
+// over the activation disappears; this fold reads tiles x 2C floats.  Block = 32 channels x 8
+// tile phases, fp64 accumulation in fixed order (deterministic), finish as bn_stats_kernel.
+__global__ __launch_bounds__(kB) void bn_stats_fold_kernel(const float* __restrict__ part, int tiles, int64_t M,
+                                                           int C, StatsOut o) {
+  const int cl = threadIdx.x & 31, ph = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
+  double sx = 0.0, sq = 0.0;
+  if (c < C)
+    for (int t = ph; t < tiles; t += 8) {
+      sx += (double)part[(int64_t)t * 2 * C + c];
+      sq += (double)part[(int64_t)t * 2 * C + C + c];
+    }
+  __shared__ double ls[8][32], lq[8][32];
+  ls[ph][cl] = sx;
+  lq[ph][cl] = sq;
+  __syncthreads();
+  if (ph == 0 && c < C) {
+    double S = 0.0, Q = 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      S += ls[i][cl];
+      Q += lq[i][cl];
+    }
+    const double inv_m = 1.0 / (double)M;
+    const double unbias = M > 1 ? (double)M / (double)(M - 1) : 1.0;
+    const double mean = S * inv_m;
+    const double var = fmax(Q * inv_m - mean * mean, 0.0);
+    const float invstd = (float)(1.0 / sqrt(var + (double)o.eps));
+    const float ga = o.gamma ? o.gamma[c] : 1.f;
+    const float be = o.beta ? o.beta[c] : 0.f;
+    const float scale = ga * invstd;
+    o.save[c] = (float)mean;
+    o.save[C + c] = invstd;
+    o.save[2 * C + c] = scale;
+    o.save[3 * C + c] = be - (float)mean * scale;
+    if (o.running_mean) {
+      o.running_mean[c] = (1.f - o.momentum) * o.running_mean[c] + o.momentum * (float)mean;
+      o.running_var[c] = (1.f - o.momentum) * o.running_var[c] + o.momentum * (float)(var * unbias);
+    }
+  }
+  if (threadIdx.x == 0 && blockIdx.x == 0 && o.nbt) *o.nbt += 1;
+}
+
 template <typename T, bool DY2>
 void backward_2k_t(const T* dy, const T* dy2, const T* x, const uint8_t* mask, int64_t M, int C, const GradOut& o,
                    bool relu, const float* coef, float* ws, T* dx, T* dres, hipStream_t stream) {
@@ -1415,6 +1460,25 @@ void bn_act_forward(const void* xv, const void* resv, bool fp32, int64_t M, int 
 #undef GRACE_BN_FWD
   }
   forward_2k(x, res, M, C, o, relu, save, ws, y, mask, stream);
+}
+
+// Forward from GEMM-epilogue statistics (fp32): fold + apply, no statistics pass over x.
+void bn_act_forward_from_partials(const float* x, const float* res, const float* part, int tiles, int64_t M, int C,
+                                  const float* gamma, const float* beta, float* running_mean, float* running_var,
+                                  int64_t* nbt, float momentum, float eps, bool relu, float* save, float* y,
+                                  uint8_t* mask, hipStream_t stream) {
+  StatsOut o{gamma, beta, running_mean, running_var, nbt, momentum, eps, save};
+  hipLaunchKernelGGL(bn_stats_fold_kernel, dim3((C + 31) / 32), dim3(kB), 0, stream, part, tiles, M, C, o);
+  const int64_t n_vec = M * C / 8;
+  const int gb = apply_grid(n_vec, C);
+  if (relu && res)
+    hipLaunchKernelGGL((bn_apply_kernel<float, true, true>), dim3(gb), dim3(kB), 0, stream, x, res, save, y, mask, n_vec, C);
+  else if (relu)
+    hipLaunchKernelGGL((bn_apply_kernel<float, true, false>), dim3(gb), dim3(kB), 0, stream, x, res, save, y, mask, n_vec, C);
+  else if (res)
+    hipLaunchKernelGGL((bn_apply_kernel<float, false, true>), dim3(gb), dim3(kB), 0, stream, x, res, save, y, mask, n_vec, C);
+  else
+    hipLaunchKernelGGL((bn_apply_kernel<float, false, false>), dim3(gb), dim3(kB), 0, stream, x, res, save, y, mask, n_vec, C);
 }
 
 void bn_act_backward(const void* dyv, const void* dy2v, const void* xv, bool fp32, const uint8_t* mask, int64_t M,

@@ -50,6 +50,8 @@ struct GemmParams {
   int tiles_m, tiles_n, splits, k_per_split;
   int atomic;
   int c_vec;  // C rows 16-B aligned (ldc % 4 == 0, C 16-B aligned): float4 stores
+  float* stats;  // optional (non-split GEMMs): per (row tile, column) [sum | sum of squares] of C,
+                 // [tiles_m][2][N] -- the BatchNorm statistics of a conv output, fused
 };
 
 template <int R, bool KC>
@@ -178,7 +180,11 @@ __global__ __launch_bounds__(kGB, 2) void gemm_f32_kernel(GemmParams p) {
   // C/D map of the 32x32 f32 MFMA: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
   if (!p.atomic) {
     // each wave stages its 32-row slabs through its own LDS region (the k-loop's stages are free
-    // after the last barrier) and stores 16 B per lane: WN/4 lanes cover a row segment
+    // after the last barrier) and stores 16 B per lane: WN/4 lanes cover a row segment.
+    // With p.stats every lane also accumulates its 4 columns' sum / sum of squares over the rows
+    // it stores (the BN statistics of the output, from the values as stored), reduced across the
+    // lanes sharing those columns and across the two waves of the column band below.
+    float st_s[4] = {0.f, 0.f, 0.f, 0.f}, st_q[4] = {0.f, 0.f, 0.f, 0.f};
     float* slab = lds + w * 32 * CP;
     constexpr int LPR = WN / 4;          // lanes per staged row
     constexpr int RPI = kWave / LPR;     // rows per wave instruction
@@ -199,6 +205,11 @@ __global__ __launch_bounds__(kGB, 2) void gemm_f32_kernel(GemmParams p) {
         if (row < p.M) {
           const float4 v = *reinterpret_cast<const float4*>(slab + rr * CP + 4 * cq);
           float* dst = p.C + (int64_t)row * p.ldc + col;
+          if (p.stats != nullptr) {
+            st_s[0] += v.x; st_s[1] += v.y; st_s[2] += v.z; st_s[3] += v.w;
+            st_q[0] = fmaf(v.x, v.x, st_q[0]); st_q[1] = fmaf(v.y, v.y, st_q[1]);
+            st_q[2] = fmaf(v.z, v.z, st_q[2]); st_q[3] = fmaf(v.w, v.w, st_q[3]);
+          }
           if (p.c_vec && col + 3 < p.N) {
             *reinterpret_cast<float4*>(dst) = v;
           } else {
@@ -212,6 +223,37 @@ __global__ __launch_bounds__(kGB, 2) void gemm_f32_kernel(GemmParams p) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (p.stats != nullptr) {
+      // lanes l, l + LPR, l + 2 LPR ... hold the same 4 columns: butterfly over the row phases
+#pragma unroll
+      for (int off = LPR; off < kWave; off <<= 1)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          st_s[j] += __shfl_xor(st_s[j], off, kWave);
+          st_q[j] += __shfl_xor(st_q[j], off, kWave);
+        }
+      __syncthreads();  // every wave is done with its slab: reuse the LDS for the wm-pair fold
+      float* red = lds;  // [2 (wn)][2 (s, q)][WN]
+      if (wm == 1 && lane < LPR) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          red[(wn * 2 + 0) * WN + 4 * cq + j] = st_s[j];
+          red[(wn * 2 + 1) * WN + 4 * cq + j] = st_q[j];
+        }
+      }
+      __syncthreads();
+      if (wm == 0 && lane < LPR) {
+        float* out = p.stats + (int64_t)tm * 2 * p.N;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int c = col + j;
+          if (c < p.N) {
+            out[c] = st_s[j] + red[(wn * 2 + 0) * WN + 4 * cq + j];
+            out[p.N + c] = st_q[j] + red[(wn * 2 + 1) * WN + 4 * cq + j];
+          }
+        }
+      }
     }
     return;
   }
@@ -233,11 +275,12 @@ __global__ __launch_bounds__(kGB, 2) void gemm_f32_kernel(GemmParams p) {
 }
 
 template <int BM, int BN, bool AKC, bool BKC>
-void launch_cfg(GemmParams p, hipStream_t stream) {
+int launch_cfg(GemmParams p, hipStream_t stream) {
   p.tiles_m = (p.M + BM - 1) / BM;
   p.tiles_n = (p.N + BN - 1) / BN;
   const int64_t blocks = (int64_t)p.tiles_m * p.tiles_n * p.splits;
   gemm_f32_kernel<BM, BN, AKC, BKC><<<(unsigned)blocks, kGB, 0, stream>>>(p);
+  return p.tiles_m;
 }
 
 inline int64_t ntiles(int M, int N, int bm, int bn) { return (int64_t)((M + bm - 1) / bm) * ((N + bn - 1) / bn); }
@@ -245,18 +288,14 @@ inline int64_t ntiles(int M, int N, int bm, int bn) { return (int64_t)((M + bm -
 // tile shape: the largest of 128x128 / 128x64 / 64x128 / 64x64 that still gives >= 1.5 workgroups
 // per CU (small-M layers, e.g. the 7x7 stage at M = 1568, otherwise leave most of the chip idle)
 template <bool AKC, bool BKC>
-void launch_layout(GemmParams p, hipStream_t stream) {
+int launch_layout(GemmParams p, hipStream_t stream) {
   const int64_t want = 384;
   const int64_t t128 = ntiles(p.M, p.N, 128, 128) * p.splits;
   const int64_t tm = ntiles(p.M, p.N, 128, 64) * p.splits, tn = ntiles(p.M, p.N, 64, 128) * p.splits;
-  if (p.M > 64 && p.N > 64 && t128 >= want)
-    launch_cfg<128, 128, AKC, BKC>(p, stream);
-  else if (p.M > 64 && tm >= want && (p.N <= 64 || tm >= tn))
-    launch_cfg<128, 64, AKC, BKC>(p, stream);
-  else if (p.N > 64 && tn >= want)
-    launch_cfg<64, 128, AKC, BKC>(p, stream);
-  else
-    launch_cfg<64, 64, AKC, BKC>(p, stream);
+  if (p.M > 64 && p.N > 64 && t128 >= want) return launch_cfg<128, 128, AKC, BKC>(p, stream);
+  if (p.M > 64 && tm >= want && (p.N <= 64 || tm >= tn)) return launch_cfg<128, 64, AKC, BKC>(p, stream);
+  if (p.N > 64 && tn >= want) return launch_cfg<64, 128, AKC, BKC>(p, stream);
+  return launch_cfg<64, 64, AKC, BKC>(p, stream);
 }
 
 }  // namespace
@@ -264,20 +303,20 @@ void launch_layout(GemmParams p, hipStream_t stream) {
 namespace {
 // tile: 0 = by the launcher's rule, 1 = 128x128, 2 = 128x64, 3 = 64x128, 4 = 64x64
 template <bool AKC, bool BKC>
-void launch_tile(GemmParams p, int tile, hipStream_t stream) {
+int launch_tile(GemmParams p, int tile, hipStream_t stream) {
   switch (tile) {
-    case 1: launch_cfg<128, 128, AKC, BKC>(p, stream); return;
-    case 2: launch_cfg<128, 64, AKC, BKC>(p, stream); return;
-    case 3: launch_cfg<64, 128, AKC, BKC>(p, stream); return;
-    case 4: launch_cfg<64, 64, AKC, BKC>(p, stream); return;
-    default: launch_layout<AKC, BKC>(p, stream);
+    case 1: return launch_cfg<128, 128, AKC, BKC>(p, stream);
+    case 2: return launch_cfg<128, 64, AKC, BKC>(p, stream);
+    case 3: return launch_cfg<64, 128, AKC, BKC>(p, stream);
+    case 4: return launch_cfg<64, 64, AKC, BKC>(p, stream);
+    default: return launch_layout<AKC, BKC>(p, stream);
   }
 }
 }  // namespace
 
-void gemm_f32(const float* A, bool a_kcontig, int64_t lda, const float* B, bool b_kcontig, int64_t ldb, float* C,
-              int64_t ldc, int M, int N, int K, int splits, hipStream_t stream, int tile) {
-  if (M <= 0 || N <= 0) return;
+int gemm_f32(const float* A, bool a_kcontig, int64_t lda, const float* B, bool b_kcontig, int64_t ldb, float* C,
+             int64_t ldc, int M, int N, int K, int splits, hipStream_t stream, int tile, float* stats) {
+  if (M <= 0 || N <= 0) return 0;
   GemmParams p{};
   p.A = A;
   p.B = B;
@@ -301,15 +340,12 @@ void gemm_f32(const float* A, bool a_kcontig, int64_t lda, const float* B, bool 
   p.k_per_split = kps;
   p.atomic = splits > 1;
   p.c_vec = (reinterpret_cast<uintptr_t>(C) % 16 == 0) && (ldc % 4 == 0);
+  p.stats = p.atomic ? nullptr : stats;  // statistics need whole-K tiles (the binding checks)
   if (p.atomic) GRACE_HIP_CHECK(hipMemsetAsync(C, 0, sizeof(float) * (size_t)M * ldc, stream));  // ldc == N (host-checked)
-  if (a_kcontig && b_kcontig)
-    launch_tile<true, true>(p, tile, stream);
-  else if (a_kcontig && !b_kcontig)
-    launch_tile<true, false>(p, tile, stream);
-  else if (!a_kcontig && !b_kcontig)
-    launch_tile<false, false>(p, tile, stream);
-  else
-    launch_tile<false, true>(p, tile, stream);
+  if (a_kcontig && b_kcontig) return launch_tile<true, true>(p, tile, stream);
+  if (a_kcontig && !b_kcontig) return launch_tile<true, false>(p, tile, stream);
+  if (!a_kcontig && !b_kcontig) return launch_tile<false, false>(p, tile, stream);
+  return launch_tile<false, true>(p, tile, stream);
 }
 
 }  // namespace grace

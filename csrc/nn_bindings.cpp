@@ -74,6 +74,39 @@ std::vector<Tensor> bn_act_fwd(const Tensor& x, const c10::optional<Tensor>& res
   return {y, save, mask};
 }
 
+// fp32 forward from the conv GEMM's epilogue statistics ([tiles][2][C] partial sums)
+std::vector<Tensor> bn_act_fwd_partials(const Tensor& x, const c10::optional<Tensor>& res, const Tensor& part,
+                                        int64_t tiles, const c10::optional<Tensor>& weight,
+                                        const c10::optional<Tensor>& bias, const c10::optional<Tensor>& running_mean,
+                                        const c10::optional<Tensor>& running_var, const c10::optional<Tensor>& nbt,
+                                        double momentum, double eps, bool relu) {
+  int64_t M, C;
+  check_rows(x, "x", &M, &C);
+  TORCH_CHECK(x.scalar_type() == at::kFloat, "bn_act_fwd_partials: fp32 activations");
+  const bool has_res = res.has_value() && res->defined();
+  if (has_res) same_layout(x, *res, "residual");
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() &&
+                  tiles >= 1 && part.numel() >= tiles * 2 * C, "partials: fp32 [tiles][2][C]");
+  float* rm = const_cast<float*>(opt_f32(running_mean, C, "running_mean"));
+  float* rv = const_cast<float*>(opt_f32(running_var, C, "running_var"));
+  TORCH_CHECK((rm == nullptr) == (rv == nullptr), "running_mean / running_var: both or neither");
+  int64_t* nb = nullptr;
+  if (nbt.has_value() && nbt->defined()) {
+    TORCH_CHECK(nbt->is_cuda() && nbt->scalar_type() == at::kLong && nbt->numel() == 1, "num_batches_tracked");
+    nb = nbt->data_ptr<int64_t>();
+  }
+  DevGuard guard(x.device());
+  Tensor y = at::empty_like(x);
+  Tensor save = at::empty({4 * C}, x.options());
+  Tensor mask = relu ? at::empty({M * C / 8}, x.options().dtype(at::kByte)) : Tensor();
+  grace::bn_act_forward_from_partials(x.data_ptr<float>(), has_res ? res->data_ptr<float>() : nullptr,
+                                      part.data_ptr<float>(), (int)tiles, M, (int)C, opt_f32(weight, C, "weight"),
+                                      opt_f32(bias, C, "bias"), rm, rv, nb, (float)momentum, (float)eps, relu,
+                                      save.data_ptr<float>(), y.data_ptr<float>(),
+                                      relu ? mask.data_ptr<uint8_t>() : nullptr, cur_stream());
+  return {y, save, mask};
+}
+
 // returns (dx, dres (undefined unless want_dres), dweight, dbias)
 std::vector<Tensor> bn_act_bwd(const Tensor& dy, const c10::optional<Tensor>& dy2, const Tensor& x,
                                const c10::optional<Tensor>& mask, const c10::optional<Tensor>& weight,
@@ -271,4 +304,5 @@ void grace_bind_nn(py::module& m) {
   m.def("bn_spin_timeouts", []() { return (int64_t)grace::bn_spin_timeouts(); });
   m.def("bn_act_fwd", &bn_act_fwd);
   m.def("bn_act_bwd", &bn_act_bwd);
+  m.def("bn_act_fwd_partials", &bn_act_fwd_partials);
 }

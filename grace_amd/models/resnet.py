@@ -15,7 +15,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.bnact import BatchNormAct2d, bn_relu_maxpool
-from ..ops.conv import Conv1x1F32
+from ..ops.conv import Conv1x1F32, conv_bn_act
 from ..ops.pool import GlobalAvgPoolFlat, MaxPool2dNHWC
 
 
@@ -69,9 +69,11 @@ class Bottleneck(nn.Module):
         # plain tensor for the first block
         xm, xs = x if isinstance(x, tuple) else (x, x)
         idt = xs if self.downsample is None else self.downsample(xs)
-        y = self.bn1(self.conv1(xm))
+        # 1x1 conv -> BN pairs: the BN statistics may come from the conv GEMM's epilogue
+        # (ops/conv.py conv_bn_act, autotuned; otherwise exactly bn(conv(x)))
+        y = conv_bn_act(self.conv1, self.bn1, xm)
         y = self.bn2(self.conv2(y))
-        return self.bn3(self.conv3(y), idt, dual=True)
+        return conv_bn_act(self.conv3, self.bn3, y, idt, dual=True)
 
 
 class ResNet(nn.Module):

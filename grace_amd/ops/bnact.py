@@ -54,9 +54,15 @@ def _kernel_grad(g: Optional[torch.Tensor], like: torch.Tensor) -> Optional[torc
 
 class _BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, residual, weight, bias, running_mean, running_var, nbt, momentum, eps, relu, dual):
-        y, save, mask = _native.lib().bn_act_fwd(x, residual, weight, bias, running_mean, running_var, nbt,
-                                                 float(momentum), float(eps), bool(relu))
+    def forward(ctx, x, residual, weight, bias, running_mean, running_var, nbt, momentum, eps, relu, dual,
+                partials=None, tiles=0):
+        if partials is not None:  # statistics from the producing conv GEMM's epilogue (ops/conv.py)
+            y, save, mask = _native.lib().bn_act_fwd_partials(x, residual, partials, int(tiles), weight, bias,
+                                                              running_mean, running_var, nbt, float(momentum),
+                                                              float(eps), bool(relu))
+        else:
+            y, save, mask = _native.lib().bn_act_fwd(x, residual, weight, bias, running_mean, running_var, nbt,
+                                                     float(momentum), float(eps), bool(relu))
         ctx.relu = bool(relu)
         ctx.has_res = residual is not None
         # the backward needs only the ReLU mask (1 bit per element), not the bf16 output
@@ -74,7 +80,7 @@ class _BNActFn(torch.autograd.Function):
         if dy is None:
             dy, dy2 = dy2, None
         if dy is None:
-            return (None,) * 11
+            return (None,) * 13
         dy = _kernel_grad(dy, x)
         dy2 = _kernel_grad(dy2, x)
         want_w = weight is not None and ctx.needs_input_grad[2]
@@ -82,11 +88,11 @@ class _BNActFn(torch.autograd.Function):
                                                     ctx.has_res and ctx.needs_input_grad[1], want_w)
         return (dx, dres if ctx.has_res and ctx.needs_input_grad[1] else None,
                 dw if want_w else None, db if want_w and ctx.needs_input_grad[3] else None,
-                None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None)
 
 
 def bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, residual: Optional[torch.Tensor] = None,
-           relu: bool = False, dual: bool = False):
+           relu: bool = False, dual: bool = False, partials: Optional[torch.Tensor] = None, tiles: int = 0):
     """``act(bn(x) + residual)`` with the module's parameters and running statistics.
 
     ``dual=True`` returns ``(y, y_alias)``: two aliases of the output for two consumers (e.g. a
@@ -99,7 +105,8 @@ def bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, residual: Optional[torch.Tensor]
         return _BNActFn.apply(x, residual, bn.weight, bn.bias,
                               bn.running_mean if track else None, bn.running_var if track else None,
                               bn.num_batches_tracked if track else None,
-                              bn.momentum if bn.momentum is not None else 0.0, bn.eps, relu, bool(dual))
+                              bn.momentum if bn.momentum is not None else 0.0, bn.eps, relu, bool(dual),
+                              partials, tiles)
     y = nn.BatchNorm2d.forward(bn, x)
     if residual is not None:
         y = y + residual

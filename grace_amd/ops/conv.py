@@ -206,6 +206,124 @@ class _Conv1x1AutoFn(torch.autograd.Function):
         return dx, dw
 
 
+class _Conv1x1StatsFn(torch.autograd.Function):
+    """Forward on the MFMA GEMM whose epilogue also emits the per-(row tile, channel) sum / sum of
+    squares of the output (the following BatchNorm's statistics: its statistics pass over the
+    activation disappears); backward = the autotuned dgrad / wgrad of _Conv1x1AutoFn."""
+
+    @staticmethod
+    def forward(ctx, x, weight, tile):
+        nb, cin, h, w = x.shape
+        cout = weight.shape[0]
+        m = nb * h * w
+        wt = weight.reshape(cout, cin)
+        if not wt.is_contiguous():
+            wt = wt.contiguous()
+        y = torch.empty((nb, cout, h, w), device=x.device, dtype=torch.float32, memory_format=torch.channels_last)
+        part = torch.empty(((m + 63) // 64) * 2 * cout, device=x.device, dtype=torch.float32)
+        _native.lib().gemm_f32(x, True, cin, wt, True, cin, y, cout, m, cout, cin, 1, int(tile), part)
+        ctx.save_for_backward(x, wt)
+        ctx.wshape = weight.shape
+        ctx.mark_non_differentiable(part)
+        return y, part
+
+    @staticmethod
+    def backward(ctx, dy, _dpart=None):
+        dx, dw = _Conv1x1AutoFn.backward(ctx, dy)
+        return dx, dw, None
+
+
+def _tiles_m(m: int, tile: int) -> int:
+    return (m + 127) // 128 if tile in (1, 2) else (m + 63) // 64
+
+
+# (M, Cin, Cout, relu, residual) -> "unfused" | "stats_t<tile>" ; measured ms per candidate
+_BN_CHOICE = {}
+_BN_TIMES = {}
+_BN_FUSE = os.environ.get("GRACE_CONV_BN_STATS", "1") == "1"
+
+
+def _time(fn, reps=5):
+    for _ in range(2):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def _pick_bn(conv, bn, x, residual, relu) -> str:
+    nb, cin, h, w = x.shape
+    key = (nb * h * w, cin, conv.out_channels, bool(relu), residual is not None)
+    c = _BN_CHOICE.get(key)
+    if c is not None:
+        return c
+    if torch.cuda.is_current_stream_capturing():
+        return "unfused"
+    C = _native.lib()
+    cout = conv.out_channels
+    wt = conv.weight.detach().reshape(cout, cin).contiguous()
+    w4 = conv.weight.detach()
+    rm, rv = torch.zeros(cout, device=x.device), torch.ones(cout, device=x.device)
+    nbt = torch.zeros((), dtype=torch.int64, device=x.device)
+    g, b = bn.weight.detach(), bn.bias.detach()
+    res = residual.detach() if residual is not None else None
+    xd = x.detach()
+    m = nb * h * w
+    times = {}
+
+    def unfused():
+        y = _run("fwd", _pick("fwd", xd, wt, None, w4.shape), xd, wt, None, w4.shape)
+        C.bn_act_fwd(y, res, g, b, rm, rv, nbt, 0.1, 1e-5, bool(relu))
+
+    times["unfused"] = _time(unfused)
+    part = torch.empty(((m + 63) // 64) * 2 * cout, device=x.device)
+    for tile in (1, 2, 3, 4):
+        def fused(tile=tile):
+            y = torch.empty((nb, cout, h, w), device=x.device, memory_format=torch.channels_last)
+            t = C.gemm_f32(xd, True, cin, wt, True, cin, y, cout, m, cout, cin, 1, tile, part)
+            C.bn_act_fwd_partials(y, res, part, t, g, b, rm, rv, nbt, 0.1, 1e-5, bool(relu))
+        try:
+            times[f"stats_t{tile}"] = _time(fused)
+        except Exception:
+            continue
+    c = min(times, key=times.get)
+    _BN_CHOICE[key] = c
+    _BN_TIMES[key] = times
+    return c
+
+
+def bn_autotune_table():
+    """[(M, Cin, Cout, relu, residual, chosen, {candidate: ms})] of the conv -> BN forward pairs."""
+    return [k + (v, dict(_BN_TIMES.get(k, {}))) for k, v in sorted(_BN_CHOICE.items())]
+
+
+def conv_bn_act(conv: nn.Module, bn: nn.Module, x: torch.Tensor, residual=None, dual: bool = False):
+    """``bn(conv(x), residual, dual)`` for a 1x1 stride-1 ``Conv1x1F32`` followed by a fused
+    ``BatchNormAct2d``: when the autotuner measured it faster (GEMM + statistics epilogue + fold +
+    apply vs the best conv backend + the BN statistics and apply passes, each timed whole), the
+    conv runs on the MFMA GEMM that also emits the BN statistics, and the BN skips its
+    statistics pass over the activation.  Otherwise exactly ``bn(conv(x), residual, dual=dual)``."""
+    from .bnact import _fusable, bn_act
+
+    relu = getattr(bn, "relu", False)
+    if (_BN_FUSE and not _ENABLED and isinstance(conv, Conv1x1F32) and fast_ok(x, conv)
+            and bn.training and bn.track_running_stats and bn.momentum is not None
+            and x.shape[0] * x.shape[2] * x.shape[3] < (1 << 31)):
+        choice = _pick_bn(conv, bn, x, residual, relu)
+        if choice.startswith("stats_t"):
+            tile = int(choice[7:])
+            y, part = _Conv1x1StatsFn.apply(x, conv.weight, tile)
+            if _fusable(y, bn, residual):
+                m = x.shape[0] * x.shape[2] * x.shape[3]
+                return bn_act(y, bn, residual, relu, dual, partials=part, tiles=_tiles_m(m, tile))
+            return bn(y, residual, dual=dual)
+    return bn(conv(x), residual, dual=dual)
+
+
 def fast_ok(x: torch.Tensor, conv: nn.Conv2d, force: bool = False) -> bool:
     if not (_ENABLED or _AUTO or force):
         return False

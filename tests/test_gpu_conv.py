@@ -91,3 +91,41 @@ def test_conv1x1_autotuned_dispatch(nb, cin, cout, hw):
     m = nb * hw * hw
     got = {d for d, mm, ci, co, _, _ in conv_mod.autotune_table() if (mm, ci, co) == (m, cin, cout)}
     assert got == {"fwd", "dgrad", "wgrad"}
+
+
+@pytest.mark.parametrize("nb,cin,cout,hw,relu,res", [(4, 64, 256, 14, True, True), (2, 512, 128, 8, True, False),
+                                                     (8, 256, 64, 16, False, False)])
+def test_conv_bn_stats_epilogue_matches_unfused(nb, cin, cout, hw, relu, res):
+    """GEMM with the BN-statistics epilogue + fold + apply == conv + the fused BN's own
+    statistics pass: same outputs, running statistics and gradients (fp32)."""
+    from grace_amd.ops.bnact import BatchNormAct2d
+
+    torch.manual_seed(2)
+    conv_mod.set_enabled(False)
+    conv_a = Conv1x1F32(cin, cout).cuda()
+    bn_a = BatchNormAct2d(cout, relu=relu).cuda()
+    conv_b = Conv1x1F32(cin, cout).cuda()
+    bn_b = BatchNormAct2d(cout, relu=relu).cuda()
+    conv_b.load_state_dict(conv_a.state_dict())
+    with torch.no_grad():
+        bn_a.weight.uniform_(0.5, 1.5)
+        bn_a.bias.uniform_(-0.2, 0.2)
+    bn_b.load_state_dict(bn_a.state_dict())
+    x = torch.randn(nb, cin, hw, hw, device="cuda").contiguous(memory_format=torch.channels_last)
+    r = torch.randn(nb, cout, hw, hw, device="cuda").contiguous(memory_format=torch.channels_last) if res else None
+    xa, xb = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    key = (nb * hw * hw, cin, cout, relu, res)
+    conv_mod._BN_CHOICE[key] = "stats_t2"  # force the fused path for this shape
+    ya = conv_mod.conv_bn_act(conv_a, bn_a, xa, r)
+    yb = bn_b(conv_b(xb), r)
+    dy = torch.randn_like(ya)
+    ya.backward(dy)
+    yb.backward(dy)
+    torch.testing.assert_close(ya, yb, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(bn_a.running_mean, bn_b.running_mean, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(bn_a.running_var, bn_b.running_var, rtol=1e-4, atol=1e-5)
+    assert int(bn_a.num_batches_tracked) == int(bn_b.num_batches_tracked) == 1
+    torch.testing.assert_close(xa.grad, xb.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(conv_a.weight.grad, conv_b.weight.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(bn_a.weight.grad, bn_b.weight.grad, rtol=1e-4, atol=1e-3)
+    del conv_mod._BN_CHOICE[key]

@@ -15,7 +15,10 @@ finally:
     from grace_amd.ops import conv
     for r in conv.autotune_table():
         print('AUTOTUNE', r, flush=True)
-" > gpurun_out/r3_ab2.log 2>&1 && grep -o "$B" gpurun_out/r3_ab2.log && grep AUTOTUNE gpurun_out/r3_ab2.log | cut -c1-170 || exit 1
+    for r in conv.bn_autotune_table():
+        print('BNTUNE', r, flush=True)
+" > gpurun_out/r3_ab2.log 2>&1 && grep -o "$B" gpurun_out/r3_ab2.log && grep -E "AUTOTUNE|BNTUNE" gpurun_out/r3_ab2.log | cut -c1-220 || exit 1
+timeout -k 10 200 python benchmarks/gemm_bench.py --iters 20 2>/dev/null | tee gpurun_out/r3_gemm_bench.txt || exit 1
 for cfg in "65536 32768" "32768 8192" "16384 8192" "16384 4096"; do set -- $cfg
   echo "sketch qsel $1 codec $2: $(GRACE_QSEL_CHUNK=$1 GRACE_CODEC_CHUNK=$2 timeout -k 10 120 python benchmarks/grace_kernels.py --pipeline sketch --model resnet50 --iters 20 --bucket-mb 128 2>/dev/null | tail -1)" || exit 1
 done
