@@ -56,8 +56,8 @@ import os as _os
 
 # elements per workgroup of the selection passes (LDS setup amortised) and of encode / decode
 # (per-workgroup LDS bin tables amortised); env-tunable for sweeps on the GPU box
-_QSEL_CHUNK = int(_os.environ.get("GRACE_QSEL_CHUNK", 65536))
-_CODEC_CHUNK = int(_os.environ.get("GRACE_CODEC_CHUNK", 32768))
+_QSEL_CHUNK = int(_os.environ.get("GRACE_QSEL_CHUNK", 32768))
+_CODEC_CHUNK = int(_os.environ.get("GRACE_CODEC_CHUNK", 8192))
 
 
 _QSEL_MAX_RANKS = 256  # distinct target ranks per segment one selection batch resolves
