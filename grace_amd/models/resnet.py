@@ -17,10 +17,12 @@ import torch.nn as nn
 from ..ops.bnact import BatchNormAct2d, bn_relu_maxpool
 from ..ops.conv import Conv1x1F32, conv_bn_act
 from ..ops.pool import GlobalAvgPoolFlat, MaxPool2dNHWC
+from ..ops.wgrad import Conv2dSplitGrad
 
 
 def _conv3x3(cin, cout, stride=1):
-    return nn.Conv2d(cin, cout, 3, stride=stride, padding=1, bias=False)
+    # weight gradient on the side stream (ops/wgrad.py), nn.Conv2d state_dict
+    return Conv2dSplitGrad(cin, cout, 3, stride=stride, padding=1, bias=False)
 
 
 def _conv1x1(cin, cout, stride=1):
@@ -28,7 +30,7 @@ def _conv1x1(cin, cout, stride=1):
     # the hand-written f32 MFMA GEMM (opt-in, GRACE_CONV_MFMA=1; nn.Conv2d state_dict either way)
     if stride == 1:
         return Conv1x1F32(cin, cout)
-    return nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
+    return Conv2dSplitGrad(cin, cout, 1, stride=stride, bias=False)
 
 
 class BasicBlock(nn.Module):
@@ -82,10 +84,10 @@ class ResNet(nn.Module):
         super().__init__()
         self.inplanes = 64
         if cifar_stem:
-            self.conv1 = nn.Conv2d(3, 64, 3, 1, 1, bias=False)
+            self.conv1 = Conv2dSplitGrad(3, 64, 3, 1, 1, bias=False)
             self.maxpool = nn.Identity()
         else:
-            self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
+            self.conv1 = Conv2dSplitGrad(3, 64, 7, 2, 3, bias=False)
             self.maxpool = MaxPool2dNHWC(3, 2, 1)  # 1-byte window codes, gather backward
         self.bn1 = BatchNormAct2d(64, relu=True)
         self.layer1 = self._make(block, 64, layers[0])

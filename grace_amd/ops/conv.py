@@ -33,6 +33,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _native
+from . import wgrad as _wg
 
 _TARGET_BLOCKS = 512  # >> 256 CUs
 
@@ -64,6 +65,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         gemm(x, True, cin, wt, True, cin, y, cout, m, cout, cin, 0)
         ctx.save_for_backward(x, wt)
         ctx.wshape = weight.shape
+        ctx.weight = weight
         return y
 
     @staticmethod
@@ -78,9 +80,16 @@ class _Conv1x1Fn(torch.autograd.Function):
             dx = torch.empty_like(x, memory_format=torch.channels_last)
             gemm(dy, True, cout, wt, False, cin, dx, cin, m, cin, cout, 0)
         if ctx.needs_input_grad[1]:
-            dw = torch.empty((cout, cin), device=x.device, dtype=torch.float32)
-            gemm(dy, False, cout, x, False, cin, dw, cin, cout, cin, m, _splits(cout, cin, m))
-            dw = dw.view(ctx.wshape)
+            f = _wg.fork(dy, ctx.weight)
+            with f as side:
+                dw = torch.empty((cout, cin), device=x.device, dtype=torch.float32)
+                gemm(dy, False, cout, x, False, cin, dw, cin, cout, cin, m, _splits(cout, cin, m))
+                dw = dw.view(ctx.wshape)
+                if side:
+                    s = torch.cuda.current_stream(dy.device)
+                    _wg.tag(dy, s)
+                    _wg.tag(x, s)
+                    _wg.tag(dw, f.main)
         return dx, dw
 
 
@@ -192,6 +201,7 @@ class _Conv1x1AutoFn(torch.autograd.Function):
         y = _run("fwd", _pick("fwd", x, wt, None, weight.shape), x, wt, None, weight.shape)
         ctx.save_for_backward(x, wt)
         ctx.wshape = weight.shape
+        ctx.weight = weight
         return y
 
     @staticmethod
@@ -199,10 +209,18 @@ class _Conv1x1AutoFn(torch.autograd.Function):
         x, wt = ctx.saved_tensors
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = None
+        f = _wg.fork(dy, ctx.weight) if ctx.needs_input_grad[1] else None
         if ctx.needs_input_grad[0]:
             dx = _run("dgrad", _pick("dgrad", x, wt, dy, ctx.wshape), x, wt, dy, ctx.wshape)
-        if ctx.needs_input_grad[1]:
-            dw = _run("wgrad", _pick("wgrad", x, wt, dy, ctx.wshape), x, wt, dy, ctx.wshape).view(ctx.wshape)
+        if f is not None:
+            be = _pick("wgrad", x, wt, dy, ctx.wshape)  # autotuned on the current stream, never on the side one
+            with f as side:  # wgrad off the critical path (ops/wgrad.py)
+                dw = _run("wgrad", be, x, wt, dy, ctx.wshape).view(ctx.wshape)
+                if side:
+                    s = torch.cuda.current_stream(dy.device)
+                    _wg.tag(dy, s)
+                    _wg.tag(x, s)
+                    _wg.tag(dw, f.main)
         return dx, dw
 
 
@@ -224,6 +242,7 @@ class _Conv1x1StatsFn(torch.autograd.Function):
         _native.lib().gemm_f32(x, True, cin, wt, True, cin, y, cout, m, cout, cin, 1, int(tile), part)
         ctx.save_for_backward(x, wt)
         ctx.wshape = weight.shape
+        ctx.weight = weight
         ctx.mark_non_differentiable(part)
         return y, part
 
@@ -340,7 +359,7 @@ def fast_ok(x: torch.Tensor, conv: nn.Conv2d, force: bool = False) -> bool:
     return cin % 4 == 0 and cout % 4 == 0 and x.shape[0] * x.shape[2] * x.shape[3] % 4 == 0
 
 
-class Conv1x1F32(nn.Conv2d):
+class Conv1x1F32(_wg.Conv2dSplitGrad):
     """``nn.Conv2d(cin, cout, 1, bias=False)`` whose fp32 channels_last path runs on the f32 MFMA GEMM."""
 
     def __init__(self, cin: int, cout: int, **kw):

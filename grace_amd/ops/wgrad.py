@@ -1,0 +1,181 @@
+"""Weight gradients on a side stream: the backward critical path is dgrad -> BN backward ->
+dgrad -> ...; every weight gradient (wgrad) hangs off it and is consumed only by the GRACE
+exchange / optimizer after backward.
+
+In a ResNet-50 backward the fused-BN passes are latency bound (a few MB per launch, a serial
+fold tail) and the wgrad GEMMs are MFMA bound, yet on one stream every kernel waits for the
+one before it.  Here each conv's backward issues its dgrad on the current (critical) stream and
+its wgrad on a per-device side stream that first waits for the conv's output gradient: the
+wgrad of layer L runs while the BN backward and dgrad of layer L-1 run, so latency-bound
+launches share the chip with MFMA work instead of leaving it idle.  In a whole-step HIP graph
+the fork becomes a parallel branch of the graph (no host involvement at replay).
+
+Joins: (1) the GRACE engine's bucket launch (parallel/engine.py ``_launch`` / ``synchronize``)
+makes its consuming stream wait for every wgrad issued so far; (2) a final-callback of every
+backward that forked joins the side stream into the caller's current stream, so a user reading
+``p.grad`` after ``loss.backward()`` sees finished gradients.  Tensors crossing streams are
+tagged with ``record_stream`` so the caching allocator never recycles them early (inside a
+capture their reuse is deferred to the end of the capture).
+
+The gradient tensors are handed to autograd without extra references, so AccumulateGrad steals
+them (no copy kernel on the critical stream before the join).
+
+``GRACE_WGRAD_STREAM=0`` runs every wgrad in line (A/B knob).  The horovod-style ordering the
+reference relies on -- gradients exchanged as they become ready, after their producing kernels
+(/root/reference/patch_files/horovod/torch/__init__.py:107-141) -- is kept by join (1).
+"""
+from __future__ import annotations
+
+import os
+import threading
+from typing import Dict, Optional
+
+import torch
+
+_ENABLED = os.environ.get("GRACE_WGRAD_STREAM", "1") == "1"
+_streams: Dict[int, "torch.cuda.Stream"] = {}
+_pending: Dict[int, bool] = {}  # device -> side work issued since the last join
+_lock = threading.Lock()
+
+
+def set_enabled(on: bool) -> None:
+    global _ENABLED
+    _ENABLED = bool(on)
+
+
+def enabled() -> bool:
+    return _ENABLED
+
+
+def _side(device: torch.device) -> "torch.cuda.Stream":
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    s = _streams.get(idx)
+    if s is None:
+        with _lock:
+            s = _streams.get(idx)
+            if s is None:
+                with torch.cuda.device(idx):
+                    s = torch.cuda.Stream()
+                _streams[idx] = s
+    return s
+
+
+def _final_join():
+    join()
+
+
+class fork:
+    """``f = fork(t)`` marks the current stream's position NOW (before the caller issues its
+    critical-path kernels); ``with f as go:`` then runs the body on the side stream of ``t``'s
+    device, ordered after that mark only.  ``go`` is False (body runs in line, on the current
+    stream) for CPU tensors or when disabled."""
+
+    def __init__(self, t: torch.Tensor, param: Optional[torch.Tensor] = None):
+        self.t = t
+        self.ctx = None
+        self.main = None
+        self.ev = None
+        # a parameter that already holds a .grad gets the new one ADDED by AccumulateGrad on the
+        # current stream right after this backward returns (before any join): stay in line
+        if _ENABLED and t.is_cuda and (param is None or param.grad is None):
+            self.main = torch.cuda.current_stream(t.device)
+            self.ev = torch.cuda.Event()
+            self.ev.record(self.main)
+
+    def __enter__(self) -> bool:
+        if self.ev is None:
+            return False
+        t = self.t
+        side = _side(t.device)
+        side.wait_event(self.ev)
+        self.ctx = torch.cuda.stream(side)
+        self.ctx.__enter__()
+        idx = t.device.index
+        if not _pending.get(idx):
+            _pending[idx] = True
+            # one final callback per backward pass: join before backward() returns
+            try:
+                torch.autograd.Variable._execution_engine.queue_callback(_final_join)
+            except RuntimeError:  # not inside a backward pass
+                pass
+        return True
+
+    def __exit__(self, *exc):
+        if self.ctx is not None:
+            self.ctx.__exit__(*exc)
+        return False
+
+
+def tag(t: Optional[torch.Tensor], stream: "torch.cuda.Stream") -> None:
+    """The caching allocator must not recycle ``t`` before ``stream``'s work on it ran."""
+    if t is not None and t.is_cuda:
+        t.record_stream(stream)
+
+
+def join(stream: Optional["torch.cuda.Stream"] = None, device=None) -> None:
+    """Make ``stream`` (default: the current stream) wait for every side-stream wgrad issued so far."""
+    if not _pending:
+        return
+    if stream is not None:
+        devs = [stream.device.index]
+    elif device is not None:
+        devs = [torch.device(device).index if not isinstance(device, int) else device]
+    else:
+        devs = [torch.cuda.current_device()]
+    for idx in devs:
+        if _pending.get(idx):
+            tgt = stream if stream is not None else torch.cuda.current_stream(idx)
+            tgt.wait_stream(_streams[idx])
+            _pending[idx] = False
+
+
+# ---------------------------------------------------------------- convolution with a forked wgrad
+import torch.nn as nn  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+
+class _ConvSplitFn(torch.autograd.Function):
+    """conv2d (no bias) whose backward issues dgrad in line and wgrad on the side stream
+    (``aten.convolution_backward`` once per direction: MIOpen runs them as two solvers anyway)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride, padding, dilation, groups):
+        ctx.save_for_backward(x, weight)
+        ctx.conf = (stride, padding, dilation, groups)
+        return F.conv2d(x, weight, None, stride, padding, dilation, groups)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        stride, padding, dilation, groups = ctx.conf
+        cb = torch.ops.aten.convolution_backward
+        dx = dw = None
+        f = fork(dy, w) if ctx.needs_input_grad[1] else None
+        if ctx.needs_input_grad[0]:
+            dx = cb(dy, x, w, None, stride, padding, dilation, False, [0, 0], groups, [True, False, False])[0]
+        if f is not None:
+            with f as side:
+                dw = cb(dy, x, w, None, stride, padding, dilation, False, [0, 0], groups, [False, True, False])[1]
+                if side:
+                    s = torch.cuda.current_stream(dy.device)
+                    tag(dy, s)
+                    tag(x, s)
+                    tag(dw, f.main)
+        return dx, dw, None, None, None, None
+
+
+def _as2(v):
+    return list(v) if isinstance(v, (tuple, list)) else [v, v]
+
+
+class Conv2dSplitGrad(nn.Conv2d):
+    """``nn.Conv2d`` (same parameters / state_dict) whose weight gradient runs on the side stream
+    on GPU; bias / string padding / non-zero padding modes / CPU fall back to ``nn.Conv2d``."""
+
+    def forward(self, x):
+        if (_ENABLED and x.is_cuda and self.bias is None and self.padding_mode == "zeros"
+                and not isinstance(self.padding, str) and torch.is_grad_enabled() and self.weight.requires_grad
+                and not torch.is_autocast_enabled() and x.dtype == self.weight.dtype):
+            return _ConvSplitFn.apply(x, self.weight, _as2(self.stride), _as2(self.padding), _as2(self.dilation),
+                                      self.groups)
+        return super().forward(x)

@@ -29,6 +29,7 @@ import torch
 from . import health as _health
 from ..core import Communicator, register_layout
 from ..ops import _native
+from ..ops import wgrad as _wgrad
 from ..ops.layout import SegmentLayout
 from ..ops.randomk import fnv1a64
 
@@ -219,6 +220,8 @@ class GraceEngine:
             if self._gatherable(p.grad, view):
                 b.stolen[idx] = p.grad
             else:
+                if p.grad.is_cuda:
+                    _wgrad.join(torch.cuda.current_stream(p.grad.device))
                 view.copy_(p.grad)
                 if p is not b.params[idx]:
                     p.grad = None
@@ -307,10 +310,13 @@ class GraceEngine:
                                "backward_passes_per_step or call synchronize()")
         if self.stream is not None:
             self.stream.wait_stream(torch.cuda.current_stream(self.device))
+            _wgrad.join(self.stream)  # weight gradients issued on the side stream (ops/wgrad.py)
             with torch.cuda.stream(self.stream):
                 self._gather(b)
                 b.handles, b.ctx = self.grc.send_step(b.flat, b.name)
         else:
+            if self.device.type == "cuda":
+                _wgrad.join(torch.cuda.current_stream(self.device))
             self._gather(b)
             b.handles, b.ctx = self.grc.send_step(b.flat, b.name)
         self.in_flight += 1
@@ -326,6 +332,8 @@ class GraceEngine:
                         if self._grads_none:
                             b.views[i].zero_()
                         elif p.grad is not None and p.grad.data_ptr() != b.views[i].data_ptr():
+                            if p.grad.is_cuda:
+                                _wgrad.join(torch.cuda.current_stream(p.grad.device))
                             b.views[i].copy_(p.grad)
                         p.grad = b.views[i]
                 self._launch(b)
