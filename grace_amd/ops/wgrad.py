@@ -31,6 +31,8 @@ import threading
 from typing import Dict, Optional
 
 import torch
+import torch.nn as nn
+import torch.nn.functional as F
 
 _ENABLED = os.environ.get("GRACE_WGRAD_STREAM", "1") == "1"
 _streams: Dict[int, "torch.cuda.Stream"] = {}
@@ -129,11 +131,67 @@ def join(stream: Optional["torch.cuda.Stream"] = None, device=None) -> None:
             _pending[idx] = False
 
 
+# ---------------------------------------------------------------- dgrad as a forward convolution
+# A stride-1 convolution's data gradient is itself a stride-1 convolution of dy with the
+# spatially flipped, in/out-transposed filter (padding k-1-p).  MIOpen's backward-data solvers
+# for the fp32 NHWC 3x3 layers are implicit GEMMs that zero-fill their output first
+# (SubTensorOpWithScalar1d) and trail its forward solvers; the per-shape autotune below times
+# both forms on the device (the flipped filter's two small transform kernels charged to the
+# forward form) and keeps the faster one.  Decisions are taken in eager steps only.
+_DG_CHOICE = {}
+_DG_TIMES = {}
+_DG_AUTO = os.environ.get("GRACE_DGRAD_AUTO", "1") == "1"
+
+
+def dgrad_table():
+    """[(key, chosen, {form: ms})] of the autotuned data-gradient forms."""
+    return [(k, v, dict(_DG_TIMES.get(k, {}))) for k, v in sorted(_DG_CHOICE.items())]
+
+
+def _flipped(w):
+    return w.permute(1, 0, 2, 3).flip(2, 3).contiguous(memory_format=torch.channels_last)
+
+
+def _dgrad(dy, x, w, stride, padding, dilation, groups):
+    cb = torch.ops.aten.convolution_backward
+    kh, kw = w.shape[2], w.shape[3]
+    eligible = (_DG_AUTO and dy.is_cuda and groups == 1 and list(stride) == [1, 1] and list(dilation) == [1, 1]
+                and (kh > 1 or kw > 1) and padding[0] <= kh - 1 and padding[1] <= kw - 1
+                and x.is_contiguous(memory_format=torch.channels_last))
+
+    def bwd():
+        return cb(dy, x, w, None, stride, padding, dilation, False, [0, 0], groups, [True, False, False])[0]
+
+    if not eligible:
+        return bwd()
+    pad = [kh - 1 - padding[0], kw - 1 - padding[1]]
+
+    def fwd():
+        return F.conv2d(dy, _flipped(w), None, 1, pad)
+
+    key = (tuple(x.shape), tuple(w.shape), tuple(padding), x.dtype)
+    c = _DG_CHOICE.get(key)
+    if c is None:
+        if torch.cuda.is_current_stream_capturing():
+            return bwd()
+        times = {}
+        for name, fn in (("bwd", bwd), ("fwd_flipped", fwd)):
+            for _ in range(2):
+                fn()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(5):
+                fn()
+            e.record()
+            e.synchronize()
+            times[name] = s.elapsed_time(e) / 5
+        c = min(times, key=times.get)
+        _DG_CHOICE[key] = c
+        _DG_TIMES[key] = times
+    return fwd() if c == "fwd_flipped" else bwd()
+
+
 # ---------------------------------------------------------------- convolution with a forked wgrad
-import torch.nn as nn  # noqa: E402
-import torch.nn.functional as F  # noqa: E402
-
-
 class _ConvSplitFn(torch.autograd.Function):
     """conv2d (no bias) whose backward issues dgrad in line and wgrad on the side stream
     (``aten.convolution_backward`` once per direction: MIOpen runs them as two solvers anyway)."""
@@ -152,7 +210,7 @@ class _ConvSplitFn(torch.autograd.Function):
         dx = dw = None
         f = fork(dy, w) if ctx.needs_input_grad[1] else None
         if ctx.needs_input_grad[0]:
-            dx = cb(dy, x, w, None, stride, padding, dilation, False, [0, 0], groups, [True, False, False])[0]
+            dx = _dgrad(dy, x, w, stride, padding, dilation, groups)
         if f is not None:
             with f as side:
                 dw = cb(dy, x, w, None, stride, padding, dilation, False, [0, 0], groups, [False, True, False])[1]

