@@ -133,14 +133,16 @@ def join(stream: Optional["torch.cuda.Stream"] = None, device=None) -> None:
 
 # ---------------------------------------------------------------- dgrad as a forward convolution
 # A stride-1 convolution's data gradient is itself a stride-1 convolution of dy with the
-# spatially flipped, in/out-transposed filter (padding k-1-p).  MIOpen's backward-data solvers
-# for the fp32 NHWC 3x3 layers are implicit GEMMs that zero-fill their output first
-# (SubTensorOpWithScalar1d) and trail its forward solvers; the per-shape autotune below times
-# both forms on the device (the flipped filter's two small transform kernels charged to the
-# forward form) and keeps the faster one.  Decisions are taken in eager steps only.
+# spatially flipped, in/out-transposed filter (padding k-1-p), so MIOpen's forward solvers are
+# an alternative to its backward-data solvers (which zero-fill their output first,
+# SubTensorOpWithScalar1d).  The per-shape autotune below times both forms on the device (the
+# flipped filter's two small transform kernels charged to the forward form) and keeps the
+# faster one; decisions are taken in eager steps only.  Measured on the fp32 ResNet-50 b32 3x3
+# layers (profiles/r3_wgrad_side_stream_ab.txt) the backward-data solver wins every shape
+# (80-83 us vs 93-110 us per call), so the autotune is opt-in (GRACE_DGRAD_AUTO=1).
 _DG_CHOICE = {}
 _DG_TIMES = {}
-_DG_AUTO = os.environ.get("GRACE_DGRAD_AUTO", "1") == "1"
+_DG_AUTO = os.environ.get("GRACE_DGRAD_AUTO", "0") == "1"
 
 
 def dgrad_table():
