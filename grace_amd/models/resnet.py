@@ -17,7 +17,7 @@ import torch.nn as nn
 from ..ops.bnact import BatchNormAct2d, bn_relu_maxpool
 from ..ops.conv import Conv1x1F32, conv_bn_act
 from ..ops.pool import GlobalAvgPoolFlat, MaxPool2dNHWC
-from ..ops.wgrad import Conv2dSplitGrad
+from ..ops.wgrad import Conv2dSplitGrad, branch
 
 
 def _conv3x3(cin, cout, stride=1):
@@ -70,11 +70,17 @@ class Bottleneck(nn.Module):
         # two gradients are summed inside the fused BN backward, not by an autograd add), or a
         # plain tensor for the first block
         xm, xs = x if isinstance(x, tuple) else (x, x)
-        idt = xs if self.downsample is None else self.downsample(xs)
+        if self.downsample is None:
+            idt, br = xs, None
+        else:  # projection shortcut on a second stream, beside the main path (ops/wgrad.py branch)
+            with branch(xs) as br:
+                idt = self.downsample(xs)
         # 1x1 conv -> BN pairs: the BN statistics may come from the conv GEMM's epilogue
         # (ops/conv.py conv_bn_act, autotuned; otherwise exactly bn(conv(x)))
         y = conv_bn_act(self.conv1, self.bn1, xm)
         y = self.bn2(self.conv2(y))
+        if br is not None:
+            idt = br.merge(idt)
         return conv_bn_act(self.conv3, self.bn3, y, idt, dual=True)
 
 

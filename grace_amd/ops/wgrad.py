@@ -239,3 +239,61 @@ class Conv2dSplitGrad(nn.Conv2d):
             return _ConvSplitFn.apply(x, self.weight, _as2(self.stride), _as2(self.padding), _as2(self.dilation),
                                       self.groups)
         return super().forward(x)
+
+
+# ---------------------------------------------------------------- forward branches
+# A ResNet stage's first block has two independent branches from its input: the main path
+# (1x1 -> BN -> 3x3 -> BN -> 1x1) and the projection shortcut (strided 1x1 -> BN).  ``branch``
+# runs the shortcut on a second per-device stream that waits for the block input; ``merge``
+# makes the current stream wait for it before the residual add consumes it.  Autograd runs each
+# backward op on its forward op's stream and syncs the two where gradients cross, so the
+# shortcut's backward also runs beside the main path's.
+_bstreams: Dict[int, "torch.cuda.Stream"] = {}
+
+
+def _branch_stream(device: torch.device) -> "torch.cuda.Stream":
+    idx = device.index
+    s = _bstreams.get(idx)
+    if s is None:
+        with _lock:
+            s = _bstreams.get(idx)
+            if s is None:
+                with torch.cuda.device(idx):
+                    s = torch.cuda.Stream()
+                _bstreams[idx] = s
+    return s
+
+
+_BRANCH = os.environ.get("GRACE_BRANCH_STREAM", "1") == "1"
+
+
+class branch:
+    """``with branch(x) as b: y = f(x)`` then ``y = b.merge(y)`` before the current stream uses y."""
+
+    def __init__(self, x: torch.Tensor):
+        self.x = x
+        self.on = _ENABLED and _BRANCH and x.is_cuda and not torch.is_autocast_enabled()
+        self.main = self.ctx = None
+
+    def __enter__(self):
+        if self.on:
+            self.main = torch.cuda.current_stream(self.x.device)
+            s = _branch_stream(self.x.device)
+            s.wait_stream(self.main)
+            self.ctx = torch.cuda.stream(s)
+            self.ctx.__enter__()
+            tag(self.x, s)
+        return self
+
+    def __exit__(self, *exc):
+        if self.ctx is not None:
+            self.ctx.__exit__(*exc)
+        return False
+
+    def merge(self, y):
+        if not self.on:
+            return y
+        self.main.wait_stream(_branch_stream(self.x.device))
+        for t in (y if isinstance(y, (tuple, list)) else (y,)):
+            tag(t, self.main)
+        return y

@@ -170,3 +170,35 @@ def test_dgrad_forms_agree(k, pad):
     finally:
         wgrad._DG_AUTO = auto
     _close(got.double(), ref)
+
+
+def test_projection_branch_stream_matches_inline():
+    """a ResNet first block (projection shortcut on the branch stream) gives the in-line outputs,
+    input gradient and parameter gradients"""
+    import torch.nn as nn
+
+    from grace_amd.models.resnet import Bottleneck, _conv1x1
+    from grace_amd.ops.bnact import BatchNormAct2d
+
+    torch.manual_seed(0)
+    down = nn.Sequential(_conv1x1(32, 64, 2), BatchNormAct2d(64))
+    blk = Bottleneck(32, 16, 2, down).cuda().to(memory_format=torch.channels_last)
+    x = torch.randn(8, 32, 20, 20, device="cuda").contiguous(memory_format=torch.channels_last)
+
+    def run():
+        for p in blk.parameters():
+            p.grad = None
+        xi = x.clone().requires_grad_(True)
+        y = blk(xi)[0]
+        (y * y).sum().backward()
+        return [y.detach().clone(), xi.grad.clone()] + [p.grad.clone() for p in blk.parameters()]
+
+    wgrad._BRANCH = False
+    try:
+        run()
+        ref = run()
+    finally:
+        wgrad._BRANCH = True
+    for _ in range(2):
+        for a, b in zip(run(), ref):
+            _close(a, b)
