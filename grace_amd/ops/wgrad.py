@@ -247,7 +247,10 @@ class Conv2dSplitGrad(nn.Conv2d):
 # runs the shortcut on a second per-device stream that waits for the block input; ``merge``
 # makes the current stream wait for it before the residual add consumes it.  Autograd runs each
 # backward op on its forward op's stream and syncs the two where gradients cross, so the
-# shortcut's backward also runs beside the main path's.
+# shortcut's backward also runs beside the main path's.  Measured on the fp32 ResNet-50 headline
+# (profiles/r3_wgrad_side_stream_ab.txt): 2647 -> 2590 img/s with the branch -- the autograd
+# cross-stream event pairs around every shortcut gradient cost more than the overlap hides --
+# so it is opt-in (GRACE_BRANCH_STREAM=1).
 _bstreams: Dict[int, "torch.cuda.Stream"] = {}
 
 
@@ -264,7 +267,7 @@ def _branch_stream(device: torch.device) -> "torch.cuda.Stream":
     return s
 
 
-_BRANCH = os.environ.get("GRACE_BRANCH_STREAM", "1") == "1"
+_BRANCH = os.environ.get("GRACE_BRANCH_STREAM", "0") == "1"
 
 
 class branch:

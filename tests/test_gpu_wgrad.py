@@ -197,8 +197,9 @@ def test_projection_branch_stream_matches_inline():
     try:
         run()
         ref = run()
-    finally:
         wgrad._BRANCH = True
-    for _ in range(2):
-        for a, b in zip(run(), ref):
-            _close(a, b)
+        for _ in range(2):
+            for a, b in zip(run(), ref):
+                _close(a, b)
+    finally:
+        wgrad._BRANCH = False
