@@ -191,7 +191,7 @@ void bn_act_forward_from_partials(const float* x, const float* res, const float*
                                   uint8_t* mask, hipStream_t stream);
 void bn_act_backward(const void* dy, const void* dy2, const void* x, bool fp32, const uint8_t* relu_mask, int64_t M,
                      int C, const float* gamma, const float* save, bool relu, float* dgamma, float* dbeta,
-                     float* coef, float* ws, void* dx, void* dres, hipStream_t stream);
+                     float* coef, float* ws, void* dx, void* dres, bool deterministic, hipStream_t stream);
 
 // BN + ReLU + max pool (k x k, stride s, padding pad) over NHWC x: stats + one normalise/ReLU/pool
 // pass (pooled y [N, OH, OW, C], 1-byte in-window argmax code per pooled element).  Backward:

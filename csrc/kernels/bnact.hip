@@ -231,7 +231,10 @@ __device__ __forceinline__ bool arrive(unsigned* counter, unsigned expected_last
 
 // Per-thread 8-channel accumulators -> this block's partial row -> the tile's arrival tree.
 // True in every thread of the tile's final block; totals then in total[tile][0..2CT).
-__device__ bool block_reduce_tree(const Red& R, const float* a, const float* b) {
+// atot != nullptr (the backward's ATOMIC mode, see bn_reduce_kernel): the block's partial row is
+// added into atot[0..2C) with fp32 no-return atomics instead (no arrival, no finisher); returns
+// false everywhere.
+__device__ bool block_reduce_tree(const Red& R, const float* a, const float* b, float* atot = nullptr) {
   __shared__ __align__(16) float sa[kB * 8];
   __shared__ float sb[kB * 8];
   double* lds = reinterpret_cast<double*>(sa);  // fold scratch (kB * 4 doubles), after sa is consumed
@@ -245,6 +248,19 @@ __device__ bool block_reduce_tree(const Red& R, const float* a, const float* b) 
     }
   }
   __syncthreads();
+  if (atot != nullptr) {
+    for (int c = threadIdx.x; c < CT; c += kB) {
+      float x = 0.f, y = 0.f;
+      for (int i = 0; i < R.rpi; ++i) {
+        x += sa[i * CT + c];
+        y += sb[i * CT + c];
+      }
+      const int cc = tile * CT + c;
+      __hip_atomic_fetch_add(atot + cc, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(atot + R.C + cc, y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return false;
+  }
   float* part = R.part + (size_t)tile * R.nchunks * C2;
   float* pb = part + (size_t)blockIdx.x * C2;
   for (int c = threadIdx.x; c < CT; c += kB) {
@@ -345,6 +361,8 @@ __global__ __launch_bounds__(kB) void bn_stats_kernel(const T* __restrict__ x, R
     o.save[C + c] = invstd;
     o.save[2 * C + c] = scale;
     o.save[3 * C + c] = be - (float)mean * scale;
+    o.save[4 * C + c] = 0.f;  // the backward's atomic totals (bn_reduce_kernel ATOMIC mode)
+    o.save[5 * C + c] = 0.f;
     if (o.running_mean) {
       o.running_mean[c] = (1.f - o.momentum) * o.running_mean[c] + o.momentum * (float)mean;
       o.running_var[c] = (1.f - o.momentum) * o.running_var[c] + o.momentum * (float)(var * unbias);
@@ -442,7 +460,7 @@ template <typename T, bool RELU, bool DY2, bool RX = false, bool WDZ = false>
 __global__ __launch_bounds__(kB) void bn_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ dy2,
                                                        const T* __restrict__ x,
                                                        const uint8_t* __restrict__ mask, Red R, GradOut o,
-                                                       T* __restrict__ dzout = nullptr) {
+                                                       T* __restrict__ dzout = nullptr, float* atot = nullptr) {
   float s1[8], s2[8], mu[8], rsc[8], rsh[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) s1[j] = s2[j] = mu[j] = rsc[j] = rsh[j] = 0.f;
@@ -513,7 +531,7 @@ __global__ __launch_bounds__(kB) void bn_reduce_kernel(const T* __restrict__ dy,
       acc(d, v, w, WDZ ? dzout + e : nullptr);
     }
   });
-  if (!block_reduce_tree(R, s1, s2)) return;
+  if (!block_reduce_tree(R, s1, s2, atot)) return;
   const int CT = R.CT, C = R.C;
   const double* total = R.total + (size_t)blockIdx.y * 2 * CT;
   const double inv_m = 1.0 / (double)R.M;
@@ -533,24 +551,70 @@ __global__ __launch_bounds__(kB) void bn_reduce_kernel(const T* __restrict__ dy,
   }
 }
 
+// Where a dx pass gets its per-channel coefficients (dx = a*dz + b*x + c): the reduce kernel's
+// finisher wrote them to coef[3C] (deterministic tree), or -- ATOMIC mode -- every thread derives
+// its 8 channels' coefficients from the atomic totals tot = save + 4C ([sum dz | sum dz (x-mean)])
+// and the forward's mean / invstd, and block 0 writes dgamma / dbeta.  The atomic mode removes
+// the reduce kernel's arrival round trip and serial fold: on the small ResNet layers that tail
+// is most of the reduce kernel's time.
+struct CoefSrc {
+  const float* coef;   // [3C] (tree mode) or nullptr
+  const float* save;   // [6C] forward save: mean, invstd, scale, shift, tot[2C]
+  const float* gamma;  // may be null
+  float* dgamma;       // may be null
+  float* dbeta;        // may be null
+  double inv_m;
+};
+
+__device__ __forceinline__ void get_coef(const CoefSrc& s, int C, int c0, float* ca, float* cb, float* cc) {
+  if (s.coef != nullptr) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ca[j] = s.coef[c0 + j];
+      cb[j] = s.coef[C + c0 + j];
+      cc[j] = s.coef[2 * C + c0 + j];
+    }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = c0 + j;
+    const double S1 = s.save[4 * C + c], S2 = s.save[5 * C + c];
+    const double mean = s.save[c], invstd = s.save[C + c];
+    const double a = (double)(s.gamma ? s.gamma[c] : 1.f) * invstd;
+    const double b = -a * invstd * (S2 * invstd) * s.inv_m;
+    ca[j] = (float)a;
+    cb[j] = (float)b;
+    cc[j] = (float)(-a * S1 * s.inv_m - b * mean);
+  }
+}
+
+__device__ __forceinline__ void put_dgamma(const CoefSrc& s, int C) {
+  if (s.coef != nullptr || blockIdx.x != 0) return;
+  for (int c = threadIdx.x; c < C; c += kB) {
+    const float S1 = s.save[4 * C + c], S2 = s.save[5 * C + c];
+    if (s.dgamma) s.dgamma[c] = (float)((double)S2 * (double)s.save[C + c]);  // sum dz * xhat
+    if (s.dbeta) s.dbeta[c] = S1;
+  }
+}
+
 template <typename T, bool RELU, bool RES, bool DY2, bool RX = false>
 __global__ __launch_bounds__(kB) void bn_dx_kernel(const T* __restrict__ dy, const T* __restrict__ dy2,
                                                    const T* __restrict__ x,
-                                                   const uint8_t* __restrict__ mask, const float* __restrict__ coef,
+                                                   const uint8_t* __restrict__ mask, CoefSrc cs,
                                                    T* __restrict__ dx, T* __restrict__ dres,
-                                                   int64_t n_vec, int C, const float* __restrict__ save = nullptr) {
+                                                   int64_t n_vec, int C) {
   const int tpr = C >> 3;
   const int64_t stride = (int64_t)gridDim.x * kB;
   int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x;
   const int cg = (int)(i % tpr);
+  put_dgamma(cs, C);
   float ca[8], cb[8], cc[8], rsc[8], rsh[8];
+  get_coef(cs, C, cg * 8, ca, cb, cc);
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    ca[j] = coef[cg * 8 + j];
-    cb[j] = coef[C + cg * 8 + j];
-    cc[j] = coef[2 * C + cg * 8 + j];
-    rsc[j] = RX ? save[2 * C + cg * 8 + j] : 0.f;
-    rsh[j] = RX ? save[3 * C + cg * 8 + j] : 0.f;
+    rsc[j] = RX ? cs.save[2 * C + cg * 8 + j] : 0.f;
+    rsh[j] = RX ? cs.save[3 * C + cg * 8 + j] : 0.f;
   }
   for (; i < n_vec; i += stride) {
     Bf8 d = ld8(dy + i * 8);
@@ -579,19 +643,14 @@ __global__ __launch_bounds__(kB) void bn_dx_kernel(const T* __restrict__ dy, con
 // dx = a*dz + b*x + c with dz already masked and summed (written by bn_reduce_kernel<WDZ>)
 template <typename T>
 __global__ __launch_bounds__(kB) void bn_dx_dz_kernel(const T* __restrict__ dz, const T* __restrict__ x,
-                                                      const float* __restrict__ coef, T* __restrict__ dx, int64_t n_vec,
-                                                      int C) {
+                                                      CoefSrc cs, T* __restrict__ dx, int64_t n_vec, int C) {
   const int tpr = C >> 3;
   const int64_t stride = (int64_t)gridDim.x * kB;
   int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x;
   const int cg = (int)(i % tpr);
+  put_dgamma(cs, C);
   float ca[8], cb[8], cc[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    ca[j] = coef[cg * 8 + j];
-    cb[j] = coef[C + cg * 8 + j];
-    cc[j] = coef[2 * C + cg * 8 + j];
-  }
+  get_coef(cs, C, cg * 8, ca, cb, cc);
   for (; i < n_vec; i += stride) {
     const Bf8 d = ld8(dz + i * 8);
     const Bf8 v = ld8(x + i * 8);
@@ -892,6 +951,8 @@ __device__ __forceinline__ void finish_stats(const Red& R, const StatsOut& o, St
     store(o.save + C + c, invstd);
     store(o.save + 2 * C + c, scale);
     store(o.save + 3 * C + c, be - (float)mean * scale);
+    store(o.save + 4 * C + c, 0.f);  // the backward's atomic totals
+    store(o.save + 5 * C + c, 0.f);
     if (o.running_mean) {
       o.running_mean[c] = (1.f - o.momentum) * o.running_mean[c] + o.momentum * (float)mean;
       o.running_var[c] = (1.f - o.momentum) * o.running_var[c] + o.momentum * (float)(var * unbias);
@@ -1339,6 +1400,8 @@ __global__ __launch_bounds__(kB) void bn_stats_fold_kernel(const float* __restri
     o.save[C + c] = invstd;
     o.save[2 * C + c] = scale;
     o.save[3 * C + c] = be - (float)mean * scale;
+    o.save[4 * C + c] = 0.f;  // the backward's atomic totals
+    o.save[5 * C + c] = 0.f;
     if (o.running_mean) {
       o.running_mean[c] = (1.f - o.momentum) * o.running_mean[c] + o.momentum * (float)mean;
       o.running_var[c] = (1.f - o.momentum) * o.running_var[c] + o.momentum * (float)(var * unbias);
@@ -1347,80 +1410,103 @@ __global__ __launch_bounds__(kB) void bn_stats_fold_kernel(const float* __restri
   if (threadIdx.x == 0 && blockIdx.x == 0 && o.nbt) *o.nbt += 1;
 }
 
+// ATOMIC mode (default; GRACE_BN_DETERMINISTIC=1 or a repeated backward of one forward selects the
+// fixed-order tree): the reduce kernel adds its blocks' partial rows into save[4C..6C) (zeroed by
+// the forward's statistics finisher) and the dx kernel derives the coefficients (CoefSrc).
+bool bn_deterministic_env() {
+  static const bool on = [] {
+    const char* e = std::getenv("GRACE_BN_DETERMINISTIC");
+    return e != nullptr && e[0] == '1';
+  }();
+  return on;
+}
+
+CoefSrc coef_src(const GradOut& o, int64_t M, bool atomic) {
+  return CoefSrc{atomic ? nullptr : o.coef, o.save, o.gamma, o.dgamma, o.dbeta, 1.0 / (double)M};
+}
+
+float* atot_of(const GradOut& o, int C, bool atomic) {
+  return atomic ? const_cast<float*>(o.save) + 4 * (int64_t)C : nullptr;
+}
+
 template <typename T, bool DY2>
 void backward_2k_t(const T* dy, const T* dy2, const T* x, const uint8_t* mask, int64_t M, int C, const GradOut& o,
-                   bool relu, const float* coef, float* ws, T* dx, T* dres, hipStream_t stream) {
+                   bool relu, bool atomic, float* ws, T* dx, T* dres, hipStream_t stream) {
   Red R = plan(M, C);
   bind_ws(R, ws, stream);
   const dim3 grid(R.nchunks, C / R.CT);
+  float* at = atot_of(o, C, atomic);
   if (relu)
-    hipLaunchKernelGGL((bn_reduce_kernel<T, true, DY2>), grid, dim3(kB), 0, stream, dy, dy2, x, mask, R, o);
+    hipLaunchKernelGGL((bn_reduce_kernel<T, true, DY2>), grid, dim3(kB), 0, stream, dy, dy2, x, mask, R, o, nullptr, at);
   else
-    hipLaunchKernelGGL((bn_reduce_kernel<T, false, DY2>), grid, dim3(kB), 0, stream, dy, dy2, x, mask, R, o);
+    hipLaunchKernelGGL((bn_reduce_kernel<T, false, DY2>), grid, dim3(kB), 0, stream, dy, dy2, x, mask, R, o, nullptr, at);
   const int64_t n_vec = M * C / 8;
   const int gb = apply_grid(n_vec, C);
+  const CoefSrc cs = coef_src(o, M, atomic);
   if (relu && dres)
-    hipLaunchKernelGGL((bn_dx_kernel<T, true, true, DY2>), dim3(gb), dim3(kB), 0, stream, dy, dy2, x, mask, coef, dx,
+    hipLaunchKernelGGL((bn_dx_kernel<T, true, true, DY2>), dim3(gb), dim3(kB), 0, stream, dy, dy2, x, mask, cs, dx,
                        dres, n_vec, C);
   else if (relu)
-    hipLaunchKernelGGL((bn_dx_kernel<T, true, false, DY2>), dim3(gb), dim3(kB), 0, stream, dy, dy2, x, mask, coef, dx,
+    hipLaunchKernelGGL((bn_dx_kernel<T, true, false, DY2>), dim3(gb), dim3(kB), 0, stream, dy, dy2, x, mask, cs, dx,
                        dres, n_vec, C);
   else if (dres)
-    hipLaunchKernelGGL((bn_dx_kernel<T, false, true, DY2>), dim3(gb), dim3(kB), 0, stream, dy, dy2, x, mask, coef, dx,
+    hipLaunchKernelGGL((bn_dx_kernel<T, false, true, DY2>), dim3(gb), dim3(kB), 0, stream, dy, dy2, x, mask, cs, dx,
                        dres, n_vec, C);
   else
-    hipLaunchKernelGGL((bn_dx_kernel<T, false, false, DY2>), dim3(gb), dim3(kB), 0, stream, dy, dy2, x, mask, coef,
+    hipLaunchKernelGGL((bn_dx_kernel<T, false, false, DY2>), dim3(gb), dim3(kB), 0, stream, dy, dy2, x, mask, cs,
                        dx, dres, n_vec, C);
 }
 
 // ReLU without a saved mask (recomputed from x and the forward's scale / shift in o.save)
 template <typename T>
-void backward_2k_rx(const T* dy, const T* x, int64_t M, int C, const GradOut& o, const float* coef, float* ws, T* dx,
+void backward_2k_rx(const T* dy, const T* x, int64_t M, int C, const GradOut& o, bool atomic, float* ws, T* dx,
                     T* dres, hipStream_t stream) {
   Red R = plan(M, C);
   bind_ws(R, ws, stream);
   hipLaunchKernelGGL((bn_reduce_kernel<T, true, false, true>), dim3(R.nchunks, C / R.CT), dim3(kB), 0, stream, dy,
-                     (const T*)nullptr, x, (const uint8_t*)nullptr, R, o);
+                     (const T*)nullptr, x, (const uint8_t*)nullptr, R, o, nullptr, atot_of(o, C, atomic));
   const int64_t n_vec = M * C / 8;
   const int gb = apply_grid(n_vec, C);
+  const CoefSrc cs = coef_src(o, M, atomic);
   if (dres)
     hipLaunchKernelGGL((bn_dx_kernel<T, true, true, false, true>), dim3(gb), dim3(kB), 0, stream, dy, (const T*)nullptr,
-                       x, (const uint8_t*)nullptr, coef, dx, dres, n_vec, C, o.save);
+                       x, (const uint8_t*)nullptr, cs, dx, dres, n_vec, C);
   else
     hipLaunchKernelGGL((bn_dx_kernel<T, true, false, false, true>), dim3(gb), dim3(kB), 0, stream, dy,
-                       (const T*)nullptr, x, (const uint8_t*)nullptr, coef, dx, dres, n_vec, C, o.save);
+                       (const T*)nullptr, x, (const uint8_t*)nullptr, cs, dx, dres, n_vec, C);
 }
 
 // Two gradients (dual output) AND a residual gradient wanted: the reduce pass stores dz (it is
 // d(residual)) and the dx pass reads dz + x -- see bn_reduce_kernel WDZ.
 template <typename T>
 void backward_2k_dz(const T* dy, const T* dy2, const T* x, const uint8_t* mask, int64_t M, int C, const GradOut& o,
-                    bool relu, const float* coef, float* ws, T* dx, T* dres, hipStream_t stream) {
+                    bool relu, bool atomic, float* ws, T* dx, T* dres, hipStream_t stream) {
   Red R = plan(M, C);
   bind_ws(R, ws, stream);
   const dim3 grid(R.nchunks, C / R.CT);
+  float* at = atot_of(o, C, atomic);
   if (relu)
     hipLaunchKernelGGL((bn_reduce_kernel<T, true, true, false, true>), grid, dim3(kB), 0, stream, dy, dy2, x, mask,
-                       R, o, dres);
+                       R, o, dres, at);
   else
     hipLaunchKernelGGL((bn_reduce_kernel<T, false, true, false, true>), grid, dim3(kB), 0, stream, dy, dy2, x, mask,
-                       R, o, dres);
+                       R, o, dres, at);
   const int64_t n_vec = M * C / 8;
-  hipLaunchKernelGGL(bn_dx_dz_kernel<T>, dim3(apply_grid(n_vec, C)), dim3(kB), 0, stream, (const T*)dres, x, coef, dx,
-                     n_vec, C);
+  hipLaunchKernelGGL(bn_dx_dz_kernel<T>, dim3(apply_grid(n_vec, C)), dim3(kB), 0, stream, (const T*)dres, x,
+                     coef_src(o, M, atomic), dx, n_vec, C);
 }
 
 template <typename T>
 void backward_2k(const T* dy, const T* dy2, const T* x, const uint8_t* mask, int64_t M, int C, const GradOut& o,
-                 bool relu, const float* coef, float* ws, T* dx, T* dres, hipStream_t stream) {
+                 bool relu, bool atomic, float* ws, T* dx, T* dres, hipStream_t stream) {
   if (relu && mask == nullptr && dy2 == nullptr)
-    backward_2k_rx<T>(dy, x, M, C, o, coef, ws, dx, dres, stream);
+    backward_2k_rx<T>(dy, x, M, C, o, atomic, ws, dx, dres, stream);
   else if (std::is_same<T, float>::value && dy2 && dres && bn_dz_mode())  // fp32: dz stored exactly
-    backward_2k_dz<T>(dy, dy2, x, mask, M, C, o, relu, coef, ws, dx, dres, stream);
+    backward_2k_dz<T>(dy, dy2, x, mask, M, C, o, relu, atomic, ws, dx, dres, stream);
   else if (dy2)
-    backward_2k_t<T, true>(dy, dy2, x, mask, M, C, o, relu, coef, ws, dx, dres, stream);
+    backward_2k_t<T, true>(dy, dy2, x, mask, M, C, o, relu, atomic, ws, dx, dres, stream);
   else
-    backward_2k_t<T, false>(dy, dy2, x, mask, M, C, o, relu, coef, ws, dx, dres, stream);
+    backward_2k_t<T, false>(dy, dy2, x, mask, M, C, o, relu, atomic, ws, dx, dres, stream);
 }
 
 }  // namespace
@@ -1483,11 +1569,12 @@ void bn_act_forward_from_partials(const float* x, const float* res, const float*
 
 void bn_act_backward(const void* dyv, const void* dy2v, const void* xv, bool fp32, const uint8_t* mask, int64_t M,
                      int C, const float* gamma, const float* save, bool relu, float* dgamma, float* dbeta,
-                     float* coef, float* ws, void* dxv, void* dresv, hipStream_t stream) {
+                     float* coef, float* ws, void* dxv, void* dresv, bool deterministic, hipStream_t stream) {
   GradOut o{gamma, save, dgamma, dbeta, coef};
+  const bool atomic = !deterministic && !bn_deterministic_env();
   if (fp32) {
     backward_2k(static_cast<const float*>(dyv), static_cast<const float*>(dy2v), static_cast<const float*>(xv), mask,
-                M, C, o, relu, coef, ws, static_cast<float*>(dxv), static_cast<float*>(dresv), stream);
+                M, C, o, relu, atomic, ws, static_cast<float*>(dxv), static_cast<float*>(dresv), stream);
     return;
   }
   const uint16_t* dy = static_cast<const uint16_t*>(dyv);
@@ -1518,7 +1605,7 @@ void bn_act_backward(const void* dyv, const void* dy2v, const void* xv, bool fp3
     GRACE_BN_BWD(8)
 #undef GRACE_BN_BWD
   }
-  backward_2k(dy, dy2, x, mask, M, C, o, relu, coef, ws, dx, dres, stream);
+  backward_2k(dy, dy2, x, mask, M, C, o, relu, atomic, ws, dx, dres, stream);
 }
 
 namespace {

@@ -41,7 +41,7 @@ const float* opt_f32(const c10::optional<Tensor>& t, int64_t C, const char* what
   return t->data_ptr<float>();
 }
 
-// returns (y, save[4C] = mean, invstd, scale, shift, relu mask [M*C/8] uint8 (undefined without relu))
+// returns (y, save[6C] = mean, invstd, scale, shift, backward totals [2C] (zeroed), relu mask [M*C/8] uint8 (undefined without relu))
 bool bn_supported(int64_t C) { return grace::bn_supported((int)C); }
 
 std::vector<Tensor> bn_act_fwd(const Tensor& x, const c10::optional<Tensor>& res, const c10::optional<Tensor>& weight,
@@ -63,7 +63,7 @@ std::vector<Tensor> bn_act_fwd(const Tensor& x, const c10::optional<Tensor>& res
   DevGuard guard(x.device());
   Tensor y = at::empty_like(x);
   auto f32 = x.options().dtype(at::kFloat);
-  Tensor save = at::empty({4 * C}, f32);
+  Tensor save = at::empty({6 * C}, f32);  // + the backward's atomic totals [2C]
   // ReLU: 1 bit per element (bit j of byte i = output element 8i+j > 0), read by the backward
   Tensor mask = relu ? at::empty({M * C / 8}, x.options().dtype(at::kByte)) : Tensor();
   Tensor ws = at::empty({grace::bn_workspace_floats(M, (int)C)}, f32);
@@ -97,7 +97,7 @@ std::vector<Tensor> bn_act_fwd_partials(const Tensor& x, const c10::optional<Ten
   }
   DevGuard guard(x.device());
   Tensor y = at::empty_like(x);
-  Tensor save = at::empty({4 * C}, x.options());
+  Tensor save = at::empty({6 * C}, x.options());
   Tensor mask = relu ? at::empty({M * C / 8}, x.options().dtype(at::kByte)) : Tensor();
   grace::bn_act_forward_from_partials(x.data_ptr<float>(), has_res ? res->data_ptr<float>() : nullptr,
                                       part.data_ptr<float>(), (int)tiles, M, (int)C, opt_f32(weight, C, "weight"),
@@ -110,7 +110,8 @@ std::vector<Tensor> bn_act_fwd_partials(const Tensor& x, const c10::optional<Ten
 // returns (dx, dres (undefined unless want_dres), dweight, dbias)
 std::vector<Tensor> bn_act_bwd(const Tensor& dy, const c10::optional<Tensor>& dy2, const Tensor& x,
                                const c10::optional<Tensor>& mask, const c10::optional<Tensor>& weight,
-                               const Tensor& save, bool relu, bool want_dres, bool want_dweight) {
+                               const Tensor& save, bool relu, bool want_dres, bool want_dweight,
+                               bool deterministic) {
   int64_t M, C;
   check_rows(x, "x", &M, &C);
   same_layout(x, dy, "grad_output");
@@ -124,7 +125,7 @@ std::vector<Tensor> bn_act_bwd(const Tensor& dy, const c10::optional<Tensor>& dy
   }
   // relu without a mask: recomputed from x and save (scale, shift); one dy only
   TORCH_CHECK(!(relu && !has_mask && dy2.has_value() && dy2->defined()), "maskless relu backward takes one dy");
-  TORCH_CHECK(save.is_cuda() && save.scalar_type() == at::kFloat && save.numel() == 4 * C, "save");
+  TORCH_CHECK(save.is_cuda() && save.scalar_type() == at::kFloat && save.numel() == 6 * C, "save");
   DevGuard guard(x.device());
   auto f32 = x.options().dtype(at::kFloat);
   Tensor dx = at::empty_like(x);
@@ -138,7 +139,7 @@ std::vector<Tensor> bn_act_bwd(const Tensor& dy, const c10::optional<Tensor>& dy
                          opt_f32(weight, C, "weight"), save.data_ptr<float>(), relu,
                          want_dweight ? dg.data_ptr<float>() : nullptr, want_dweight ? db.data_ptr<float>() : nullptr,
                          coef.data_ptr<float>(), ws.data_ptr<float>(), dx.data_ptr(),
-                         want_dres ? dres.data_ptr() : nullptr, cur_stream());
+                         want_dres ? dres.data_ptr() : nullptr, deterministic, cur_stream());
   return {dx, dres, dg, db};
 }
 
@@ -211,7 +212,7 @@ std::vector<Tensor> bias_act_bwd(const Tensor& dy, const Tensor& y, bool relu) {
 }
 
 // BN (training statistics, running stats) + ReLU + k x k max pool over channels_last x.
-// returns (pooled y, save[4C], code)
+// returns (pooled y, save[6C], code)
 std::vector<Tensor> bn_act_pool_fwd(const Tensor& x, const c10::optional<Tensor>& weight,
                                     const c10::optional<Tensor>& bias, const c10::optional<Tensor>& running_mean,
                                     const c10::optional<Tensor>& running_var, const c10::optional<Tensor>& nbt,
@@ -234,7 +235,7 @@ std::vector<Tensor> bn_act_pool_fwd(const Tensor& x, const c10::optional<Tensor>
   auto f32 = x.options().dtype(at::kFloat);
   Tensor y = at::empty({N, C, OH, OW}, x.options(), at::MemoryFormat::ChannelsLast);
   Tensor code = at::empty({N, C, OH, OW}, x.options().dtype(at::kByte), at::MemoryFormat::ChannelsLast);
-  Tensor save = at::empty({4 * C}, f32);
+  Tensor save = at::empty({6 * C}, f32);  // + the backward's atomic totals [2C]
   Tensor ws = at::empty({grace::bn_workspace_floats(M, (int)C)}, f32);
   grace::bn_act_pool_forward(x.data_ptr(), x.scalar_type() == at::kFloat, (int)N, (int)H, (int)W, (int)C,
                              opt_f32(weight, C, "weight"), opt_f32(bias, C, "bias"), rm, rv, nb, (float)momentum,

@@ -9,7 +9,9 @@ four CDNA4 kernels of ``csrc/kernels/bnact.hip`` per layer (statistics with the 
 it is exactly ``relu(F.batch_norm(x) + residual)``.  fp32 activations use the two-kernel path
 (the single-launch variants keep bf16 rows in registers).
 
-Numerics: statistics and the affine are fp32 (fp64 fold of the per-block partial sums); for
+Numerics: statistics and the affine are fp32 (fp64 fold of the per-block partial sums; the
+backward's two sums are accumulated with fp32 atomics across blocks unless
+GRACE_BN_DETERMINISTIC=1 -- run-to-run order differences ~1e-7 relative); for
 bf16 the output is rounded to bf16 once (the unfused bf16 path rounds after BN, after the add and after
 the ReLU); the ReLU mask is taken from the bf16 output, as ``threshold_backward`` does, and kept as 1 bit per
 element for the backward (which then reads dy, x and M*C/8 mask bytes instead of dy, x and y).
@@ -84,8 +86,12 @@ class _BNActFn(torch.autograd.Function):
         dy = _kernel_grad(dy, x)
         dy2 = _kernel_grad(dy2, x)
         want_w = weight is not None and ctx.needs_input_grad[2]
+        # the reduce accumulates into totals the forward zeroed: a second backward through the same
+        # forward (retain_graph) takes the deterministic fixed-order tree instead
+        again = getattr(ctx, "bwd_done", False)
+        ctx.bwd_done = True
         dx, dres, dw, db = _native.lib().bn_act_bwd(dy, dy2, x, mask, weight, save, ctx.relu,
-                                                    ctx.has_res and ctx.needs_input_grad[1], want_w)
+                                                    ctx.has_res and ctx.needs_input_grad[1], want_w, again)
         return (dx, dres if ctx.has_res and ctx.needs_input_grad[1] else None,
                 dw if want_w else None, db if want_w and ctx.needs_input_grad[3] else None,
                 None, None, None, None, None, None, None, None, None)
@@ -149,7 +155,9 @@ class _BNActPoolFn(torch.autograd.Function):
         dy = C.maxpool_bwd(dp, code, x.shape[2], x.shape[3], k, s, pad)  # gradient of relu(bn(x))
         want_w = weight is not None and ctx.needs_input_grad[1]
         # mask None: the ReLU mask is recomputed from x and save's scale / shift
-        dx, _, dw, db = C.bn_act_bwd(dy, None, x, None, weight, save, True, False, want_w)
+        again = getattr(ctx, "bwd_done", False)
+        ctx.bwd_done = True
+        dx, _, dw, db = C.bn_act_bwd(dy, None, x, None, weight, save, True, False, want_w, again)
         return (dx, dw if want_w else None, db if want_w and ctx.needs_input_grad[2] else None,
                 None, None, None, None, None, None, None, None)
 

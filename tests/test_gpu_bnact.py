@@ -291,3 +291,24 @@ def test_bn_relu_maxpool_fused_matches_reference(shape, k, s, p, dtype):
         rel = (xa.grad.float() - xr.grad).norm() / xr.grad.norm()
         assert rel < 0.05, rel
         torch.testing.assert_close(m.bias.grad, b.grad, rtol=5e-2, atol=0.5)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape,relu,with_res", [((32, 256, 14, 14), True, True), ((8, 2048, 7, 7), True, False),
+                                                 ((16, 64, 28, 28), False, False)])
+def test_bnact_atomic_and_tree_backward_agree(dtype, shape, relu, with_res):
+    """the default backward accumulates its two sums with fp32 atomics into totals the forward
+    zeroed; a second backward through the same forward (retain_graph) must take the fixed-order
+    tree instead -- both passes give the same gradients (so every grad doubles)"""
+    m, x, res, dy = _case(*shape, relu, with_res, dtype=dtype)
+    xx = x.clone().requires_grad_(True)
+    rr = res.clone().requires_grad_(True) if res is not None else None
+    y = m(xx, rr)
+    y.backward(dy, retain_graph=True)
+    g1 = [xx.grad.float().clone(), m.weight.grad.clone(), m.bias.grad.clone()]
+    y.backward(dy)
+    g2 = [xx.grad.float(), m.weight.grad, m.bias.grad]
+    for a, b in zip(g1, g2):
+        tol = 1e-4 * float(a.abs().max()) + 1e-6
+        torch.testing.assert_close(b, 2 * a, rtol=1e-3 if dtype == torch.float32 else 2e-2,
+                                   atol=tol if dtype == torch.float32 else 100 * tol)
