@@ -189,6 +189,11 @@ void bn_act_forward_from_partials(const float* x, const float* res, const float*
                                   const float* gamma, const float* beta, float* running_mean, float* running_var,
                                   int64_t* nbt, float momentum, float eps, bool relu, float* save, float* y,
                                   uint8_t* mask, hipStream_t stream);
+// fixed-order tree reductions in every BN backward (run-to-run bitwise reproducible) instead of
+// the default atomic totals (GRACE_BN_DETERMINISTIC=1 at start-up does the same)
+void bn_set_deterministic(bool on);
+// layers with <= n row chunks per channel tile use the atomic backward totals (0: none)
+void bn_set_atomic_chunks(int n);
 void bn_act_backward(const void* dy, const void* dy2, const void* x, bool fp32, const uint8_t* relu_mask, int64_t M,
                      int C, const float* gamma, const float* save, bool relu, float* dgamma, float* dbeta,
                      float* coef, float* ws, void* dx, void* dres, bool deterministic, hipStream_t stream);

@@ -1337,6 +1337,8 @@ int bn_fused_v(int64_t M, int C, bool bwd) { return pick_fused_v(M, C, bwd); }
 
 void bn_set_fused(bool on) { g_fused_mode = on ? 1 : 0; }
 
+void bn_set_deterministic(bool on);
+
 unsigned bn_spin_timeouts() {
   unsigned h = 0;
   GRACE_HIP_CHECK(hipMemcpyFromSymbol(&h, HIP_SYMBOL(g_bn_spin_timeouts), sizeof(h), 0, hipMemcpyDeviceToHost));
@@ -1410,15 +1412,24 @@ __global__ __launch_bounds__(kB) void bn_stats_fold_kernel(const float* __restri
   if (threadIdx.x == 0 && blockIdx.x == 0 && o.nbt) *o.nbt += 1;
 }
 
-// ATOMIC mode (default; GRACE_BN_DETERMINISTIC=1 or a repeated backward of one forward selects the
-// fixed-order tree): the reduce kernel adds its blocks' partial rows into save[4C..6C) (zeroed by
+// ATOMIC mode (opt-in per chunk count, GRACE_BN_ATOMIC_CHUNKS; GRACE_BN_DETERMINISTIC=1 or a
+// repeated backward of one forward always select the fixed-order tree): the reduce kernel adds its blocks' partial rows into save[4C..6C) (zeroed by
 // the forward's statistics finisher) and the dx kernel derives the coefficients (CoefSrc).
+// GRACE_BN_ATOMIC_CHUNKS: the largest per-tile chunk count whose backward uses the atomic totals
+// (default 0: the fixed-order tree everywhere)
+int g_atomic_chunks = -1;
+int bn_atomic_max_chunks() {
+  if (g_atomic_chunks < 0) g_atomic_chunks = env_int("GRACE_BN_ATOMIC_CHUNKS", 0);
+  return g_atomic_chunks;
+}
+
+int g_det_mode = -1;  // -1: from GRACE_BN_DETERMINISTIC (default off), 0 atomic, 1 deterministic tree
 bool bn_deterministic_env() {
-  static const bool on = [] {
+  if (g_det_mode < 0) {
     const char* e = std::getenv("GRACE_BN_DETERMINISTIC");
-    return e != nullptr && e[0] == '1';
-  }();
-  return on;
+    g_det_mode = (e != nullptr && e[0] == '1') ? 1 : 0;
+  }
+  return g_det_mode == 1;
 }
 
 CoefSrc coef_src(const GradOut& o, int64_t M, bool atomic) {
@@ -1567,11 +1578,17 @@ void bn_act_forward_from_partials(const float* x, const float* res, const float*
     hipLaunchKernelGGL((bn_apply_kernel<float, false, false>), dim3(gb), dim3(kB), 0, stream, x, res, save, y, mask, n_vec, C);
 }
 
+void bn_set_deterministic(bool on) { g_det_mode = on ? 1 : 0; }
+void bn_set_atomic_chunks(int n) { g_atomic_chunks = n < 0 ? 0 : n; }
+
 void bn_act_backward(const void* dyv, const void* dy2v, const void* xv, bool fp32, const uint8_t* mask, int64_t M,
                      int C, const float* gamma, const float* save, bool relu, float* dgamma, float* dbeta,
                      float* coef, float* ws, void* dxv, void* dresv, bool deterministic, hipStream_t stream) {
   GradOut o{gamma, save, dgamma, dbeta, coef};
-  const bool atomic = !deterministic && !bn_deterministic_env();
+  // atomic totals only where a tile has few chunks (few same-address atomics per total): with
+  // hundreds of chunks per tile the L2 serialises them -- measured on the fp32 ResNet-50
+  // headline with every layer atomic: 2709 -> 2454 img/s (profiles/r3_bn_atomic_ab.txt)
+  const bool atomic = !deterministic && !bn_deterministic_env() && plan(M, C).nchunks <= bn_atomic_max_chunks();
   if (fp32) {
     backward_2k(static_cast<const float*>(dyv), static_cast<const float*>(dy2v), static_cast<const float*>(xv), mask,
                 M, C, o, relu, atomic, ws, static_cast<float*>(dxv), static_cast<float*>(dresv), stream);

@@ -73,21 +73,36 @@ __global__ __launch_bounds__(kBlock) void sgd_kernel(SgdTable t, SgdHyper h, con
                    (reinterpret_cast<uintptr_t>(w) & 7) == 0;
   if (vec) {
     const int64_t nv = n >> 2;
-    for (int64_t i = threadIdx.x; i < nv; i += stride) {
-      float4 pv = reinterpret_cast<float4*>(p)[i];
-      const float4 gv = reinterpret_cast<const float4*>(g)[i];
-      float4 bv = buf ? reinterpret_cast<float4*>(buf)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-      const bool m = buf != nullptr;
-      sgd_elem(pv.x, gv.x, m ? &bv.x : nullptr, h);
-      sgd_elem(pv.y, gv.y, m ? &bv.y : nullptr, h);
-      sgd_elem(pv.z, gv.z, m ? &bv.z : nullptr, h);
-      sgd_elem(pv.w, gv.w, m ? &bv.w : nullptr, h);
-      reinterpret_cast<float4*>(p)[i] = pv;
-      if (buf) reinterpret_cast<float4*>(buf)[i] = bv;
+    const bool m = buf != nullptr;
+    // all of a thread's (up to) 4 vectors' loads are issued before the first store: 12 16-B
+    // loads in flight per thread instead of 3 (the per-iteration store -> next load ordering
+    // otherwise serialises the passes; 3.9 TB/s measured before)
+    constexpr int U = kTile / 4 / kBlock;
+    float4 pv[U], gv[U], bv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = threadIdx.x + (int64_t)u * stride;
+      pv[u] = gv[u] = bv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < nv) {
+        pv[u] = reinterpret_cast<float4*>(p)[i];
+        gv[u] = reinterpret_cast<const float4*>(g)[i];
+        if (m) bv[u] = reinterpret_cast<float4*>(buf)[i];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = threadIdx.x + (int64_t)u * stride;
+      if (i >= nv) continue;
+      sgd_elem(pv[u].x, gv[u].x, m ? &bv[u].x : nullptr, h);
+      sgd_elem(pv[u].y, gv[u].y, m ? &bv[u].y : nullptr, h);
+      sgd_elem(pv[u].z, gv[u].z, m ? &bv[u].z : nullptr, h);
+      sgd_elem(pv[u].w, gv[u].w, m ? &bv[u].w : nullptr, h);
+      reinterpret_cast<float4*>(p)[i] = pv[u];
+      if (m) reinterpret_cast<float4*>(buf)[i] = bv[u];
       if (w) {
         uint2 o;
-        o.x = (uint32_t)f32_to_bf16_rne(pv.x) | ((uint32_t)f32_to_bf16_rne(pv.y) << 16);
-        o.y = (uint32_t)f32_to_bf16_rne(pv.z) | ((uint32_t)f32_to_bf16_rne(pv.w) << 16);
+        o.x = (uint32_t)f32_to_bf16_rne(pv[u].x) | ((uint32_t)f32_to_bf16_rne(pv[u].y) << 16);
+        o.y = (uint32_t)f32_to_bf16_rne(pv[u].z) | ((uint32_t)f32_to_bf16_rne(pv[u].w) << 16);
         reinterpret_cast<uint2*>(w)[i] = o;
       }
     }

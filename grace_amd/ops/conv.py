@@ -126,9 +126,11 @@ def _cl_from_2d(y2d: torch.Tensor, nb: int, h: int, w: int) -> torch.Tensor:
     return y2d.view(nb, h, w, -1).permute(0, 3, 1, 2)
 
 
-def _run(direction: str, backend: str, x, wt, dy, wshape):
+def _run(direction: str, backend: str, x, wt, dy, wshape, out=None):
     """One direction on one backend.  x: [N, Cin, H, W] channels_last; wt: [Cout, Cin]; dy:
-    [N, Cout, H, W] channels_last (backward) -- returns y / dx (channels_last) / dw [Cout, Cin]."""
+    [N, Cout, H, W] channels_last (backward) -- returns y / dx (channels_last) / dw [Cout, Cin].
+    ``out`` (wgrad only): a dense [Cout, Cin] destination (the engine's bucket view) the GEMM
+    backends write in place."""
     nb, cin, h, w = x.shape
     cout = wt.shape[0]
     m = nb * h * w
@@ -145,6 +147,8 @@ def _run(direction: str, backend: str, x, wt, dy, wshape):
             return _cl_from_2d(torch.mm(_x2d(x), wt.t()), nb, h, w)
         if direction == "dgrad":
             return _cl_from_2d(torch.mm(_x2d(dy), wt), nb, h, w)
+        if out is not None:
+            return torch.mm(_x2d(dy).t(), _x2d(x), out=out)
         return torch.mm(_x2d(dy).t(), _x2d(x))
     # mfma[_tN]: csrc/kernels/gemm_f32.hip with the launcher's tile rule or a forced tile
     tile = int(backend[6:]) if backend.startswith("mfma_t") else 0
@@ -156,7 +160,7 @@ def _run(direction: str, backend: str, x, wt, dy, wshape):
         dx = torch.empty_like(x, memory_format=torch.channels_last)
         gemm(dy, True, cout, wt, False, cin, dx, cin, m, cin, cout, 0, tile)
         return dx
-    dw = torch.empty((cout, cin), device=x.device, dtype=torch.float32)
+    dw = out if out is not None else torch.empty((cout, cin), device=x.device, dtype=torch.float32)
     gemm(dy, False, cout, x, False, cin, dw, cin, cout, cin, m, _splits(cout, cin, m), tile)
     return dw
 
@@ -214,8 +218,10 @@ class _Conv1x1AutoFn(torch.autograd.Function):
             dx = _run("dgrad", _pick("dgrad", x, wt, dy, ctx.wshape), x, wt, dy, ctx.wshape)
         if f is not None:
             be = _pick("wgrad", x, wt, dy, ctx.wshape)  # autotuned on the current stream, never on the side one
+            tgt = _wg.grad_target(ctx.weight)  # the engine's bucket view: written in place
             with f as side:  # wgrad off the critical path (ops/wgrad.py)
-                dw = _run("wgrad", be, x, wt, dy, ctx.wshape).view(ctx.wshape)
+                o2 = tgt.reshape(wt.shape) if tgt is not None else None
+                dw = _wg.into_target(_run("wgrad", be, x, wt, dy, ctx.wshape, out=o2).view(ctx.wshape), tgt)
                 if side:
                     s = torch.cuda.current_stream(dy.device)
                     _wg.tag(dy, s)

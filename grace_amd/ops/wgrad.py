@@ -108,6 +108,37 @@ class fork:
         return False
 
 
+# ---------------------------------------------------------------- gradients straight into the bucket
+# The GRACE engine (parallel/engine.py) marks each dense parameter with the bucket view its
+# gradient belongs in (``_grace_grad_view``).  When the parameter has no .grad yet (the
+# zero_grad(set_to_none=True) step), a weight-gradient producer may write the gradient into that
+# view directly -- on the side stream, off the critical path -- and return a fresh alias of it:
+# AccumulateGrad steals the alias, the engine sees a gradient that already lives in its bucket,
+# and the per-bucket gather launch (a full read + write of every gradient on the critical path
+# after the join) has nothing left to copy.  GRACE_WGRAD_DIRECT=0 disables it.
+_DIRECT = os.environ.get("GRACE_WGRAD_DIRECT", "1") == "1"
+
+
+def grad_target(weight: torch.Tensor) -> Optional[torch.Tensor]:
+    """The engine's bucket view for ``weight``'s gradient when backward may write it in place."""
+    if not _DIRECT:
+        return None
+    v = getattr(weight, "_grace_grad_view", None)
+    if v is None or weight.grad is not None or v.dtype != weight.dtype or v.device != weight.device:
+        return None
+    return v
+
+
+def into_target(dw: torch.Tensor, tgt: Optional[torch.Tensor]) -> torch.Tensor:
+    """dw written into tgt (if given; a no-op when dw already is tgt's memory), returned as a FRESH
+    alias of tgt (no other reference: AccumulateGrad steals it instead of cloning)."""
+    if tgt is None:
+        return dw
+    if dw.data_ptr() != tgt.data_ptr():
+        tgt.copy_(dw.view_as(tgt) if dw.shape == tgt.shape else dw.reshape(tgt.shape))
+    return tgt.view_as(tgt)
+
+
 def tag(t: Optional[torch.Tensor], stream: "torch.cuda.Stream") -> None:
     """The caching allocator must not recycle ``t`` before ``stream``'s work on it ran."""
     if t is not None and t.is_cuda:
@@ -214,8 +245,10 @@ class _ConvSplitFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = _dgrad(dy, x, w, stride, padding, dilation, groups)
         if f is not None:
+            tgt = grad_target(w)
             with f as side:
                 dw = cb(dy, x, w, None, stride, padding, dilation, False, [0, 0], groups, [False, True, False])[1]
+                dw = into_target(dw, tgt)
                 if side:
                     s = torch.cuda.current_stream(dy.device)
                     tag(dy, s)

@@ -174,6 +174,12 @@ class GraceEngine:
                 if src is not p:
                     src.grad = None
                 self._where[id(src)] = (b, i, v)
+        # producers of weight gradients may write straight into the bucket (ops/wgrad.py
+        # grad_target): the parameter carries its view
+        for b in self.buckets:
+            for p, src, v in zip(b.params, b.srcs, b.views):
+                if src is p:
+                    p._grace_grad_view = v
         self._passes: Dict[int, int] = {}
         self._hooks = []
         self.stream = torch.cuda.Stream(self.device) if (self.device.type == "cuda" and overlap) else None
@@ -420,6 +426,10 @@ class GraceEngine:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+        for b in self.buckets:
+            for p, v in zip(b.params, b.views):
+                if getattr(p, "_grace_grad_view", None) is v:
+                    del p._grace_grad_view
 
     def state_dict(self):
         return {"grc": self.grc.state_dict()}

@@ -152,8 +152,16 @@ def test_no_spin_timeouts():
     assert _native.lib().bn_spin_timeouts() == 0
 
 
-def test_bnact_graph_replay():
-    """Arrival counters re-arm in-kernel: repeated graph replays give the eager result."""
+@pytest.fixture
+def deterministic():
+    _native.lib().bn_set_deterministic(True)
+    yield
+    _native.lib().bn_set_deterministic(False)
+
+
+def test_bnact_graph_replay(deterministic):
+    """Arrival counters re-arm in-kernel: repeated graph replays give the eager result bit for
+    bit (fixed-order tree reductions; the default atomic backward is checked to tolerance below)."""
     m, x, res, dy = _case(8, 256, 14, 14, True, True, seed=3)
     xs = x.clone().requires_grad_(True)
     out = {}
@@ -181,6 +189,36 @@ def test_bnact_graph_replay():
     torch.testing.assert_close(out["y"], y_e, rtol=0, atol=0)
     torch.testing.assert_close(xs.grad, dx_e, rtol=0, atol=0)
     assert int(m.num_batches_tracked) == 2 + 3  # warmup + replays (the capture itself runs nothing)
+
+
+def test_bnact_graph_replay_atomic(atomic_bn):
+    """the atomic-totals backward under graph replay: the totals the forward zeroes are
+    re-zeroed on every replay (replays match eager to fp32 summation order)"""
+    m, x, res, dy = _case(8, 256, 14, 14, True, True, seed=3, dtype=torch.float32)
+    xs = x.clone().requires_grad_(True)
+    out = {}
+
+    def step():
+        xs.grad = None
+        y = m(xs, res)
+        y.backward(dy)
+        return y
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            step()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    dx_e = xs.grad.clone()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out["y"] = step()
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(xs.grad, dx_e, rtol=1e-4, atol=1e-5 * float(dx_e.abs().max()))
 
 
 def test_resnet_fused_step_as_accurate_as_unfused():
@@ -293,13 +331,20 @@ def test_bn_relu_maxpool_fused_matches_reference(shape, k, s, p, dtype):
         torch.testing.assert_close(m.bias.grad, b.grad, rtol=5e-2, atol=0.5)
 
 
+@pytest.fixture
+def atomic_bn():
+    _native.lib().bn_set_atomic_chunks(1 << 30)
+    yield
+    _native.lib().bn_set_atomic_chunks(0)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("shape,relu,with_res", [((32, 256, 14, 14), True, True), ((8, 2048, 7, 7), True, False),
                                                  ((16, 64, 28, 28), False, False)])
-def test_bnact_atomic_and_tree_backward_agree(dtype, shape, relu, with_res):
-    """the default backward accumulates its two sums with fp32 atomics into totals the forward
-    zeroed; a second backward through the same forward (retain_graph) must take the fixed-order
-    tree instead -- both passes give the same gradients (so every grad doubles)"""
+def test_bnact_atomic_and_tree_backward_agree(dtype, shape, relu, with_res, atomic_bn):
+    """the opt-in atomic backward accumulates its two sums with fp32 atomics into totals the
+    forward zeroed; a second backward through the same forward (retain_graph) must take the
+    fixed-order tree instead -- both passes give the same gradients (so every grad doubles)"""
     m, x, res, dy = _case(*shape, relu, with_res, dtype=dtype)
     xx = x.clone().requires_grad_(True)
     rr = res.clone().requires_grad_(True) if res is not None else None
