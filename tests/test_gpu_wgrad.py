@@ -128,8 +128,12 @@ def test_engine_graph_with_side_stream_wgrad(bn_deterministic):
     for _ in range(4):
         g()
     torch.cuda.synchronize()
+    # parameters after 7 SGD steps: fp32 order noise of MIOpen's / the split-K GEMM's atomic weight
+    # gradients (~1e-7 relative per step) grows in cancellation-heavy sums (a BN bias gradient is a
+    # sum of +-terms ~1e3 x its value); a missing join would corrupt whole tensors at the 1e-2 level
     for (n, a), b in zip(m1.named_parameters(), m2.parameters()):
-        _close(a, b, msg=n)
+        err = float((a - b).abs().max())
+        assert err <= 1e-3 * float(b.abs().max()) + 2e-5, f"{n}: max abs err {err:.3g}"
 
 
 def test_topk_graph_with_side_stream_runs():
