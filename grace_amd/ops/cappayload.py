@@ -105,7 +105,7 @@ class AdaptiveCapacity:
 
     def _poll(self, name: str, unit_max: int) -> None:
         pr = self._probe.get(name)
-        if pr is None:
+        if pr is None or _capturing():  # no host wait inside a capture: the probe waits for an eager step
             return
         words, ev, need_fn = pr
         if ev is not None:

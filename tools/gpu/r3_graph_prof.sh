@@ -10,4 +10,12 @@ cd "$R" && python3 tools/prof_summary.py gpurun_out/prof_$TAG/run_kernel_trace.c
 python3 tools/trace_seq.py gpurun_out/prof_$TAG/run_kernel_trace.csv > gpurun_out/prof_${TAG}_allseq.txt &&
 python3 tools/trace_streams.py gpurun_out/prof_$TAG/run_kernel_trace.csv --steps 8 --tail 40 > gpurun_out/prof_${TAG}_streams.txt || exit 1
 head -12 gpurun_out/prof_${TAG}_streams.txt
-rm -f gpurun_out/prof_$TAG/run_kernel_trace.csv; head -40 gpurun_out/prof_${TAG}_steps.txt
+python3 -c "
+import csv, gzip, sys
+rows = csv.DictReader(open('gpurun_out/prof_$TAG/run_kernel_trace.csv'))
+with gzip.open('gpurun_out/prof_${TAG}_trace.csv.gz', 'wt') as f:
+    w = csv.writer(f)
+    w.writerow(['Start_Timestamp', 'End_Timestamp', 'Queue_Id', 'Stream_Id', 'Kernel_Name'])
+    for r in rows:
+        w.writerow([r['Start_Timestamp'], r['End_Timestamp'], r.get('Queue_Id', ''), r.get('Stream_Id', ''), r['Kernel_Name'][:120]])
+" && rm -f gpurun_out/prof_$TAG/run_kernel_trace.csv; head -40 gpurun_out/prof_${TAG}_steps.txt
