@@ -52,6 +52,9 @@ PIPELINES = {
     "onebit": ("resnet50", {"compressor": "onebit", "memory": "residual", "communicator": "allreduce"}),
     "u8bit": ("resnet50", {"compressor": "u8bit", "memory": "none", "communicator": "allreduce"}),
     "sketch": ("resnet50", {"compressor": "sketch", "memory": "none", "communicator": "allreduce"}),
+    "dgc": ("resnet50", {"compressor": "dgc", "compress_ratio": 0.01, "memory": "dgc", "communicator": "allgather"}),
+    "threshold": ("resnet50", {"compressor": "threshold", "threshold": 0.01, "memory": "residual",
+                               "communicator": "allgather"}),
 }
 
 

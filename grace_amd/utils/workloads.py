@@ -90,6 +90,12 @@ WORKLOADS: Dict[str, Workload] = {
         "resnet50_dgc", "resnet50", 32, "images",
         {"compressor": "dgc", "compress_ratio": 0.01, "memory": "dgc", "communicator": "allgather"},
         _img_batch(224, 1000), _img_loss, channels_last=True),
+    # Threshold 0.01 + Residual via Allgather: bounded capacity payload (1/32 of the bucket with
+    # error feedback, grown lagged from the gathered counts): the bytes-on-wire check
+    "resnet50_threshold": Workload(
+        "resnet50_threshold", "resnet50", 32, "images",
+        {"compressor": "threshold", "threshold": 0.01, "memory": "residual", "communicator": "allgather"},
+        _img_batch(224, 1000), _img_loss, channels_last=True),
     "resnet18_cifar_none": Workload(
         "resnet18_cifar_none", "resnet18_cifar", 128, "images",
         {"compressor": "none", "memory": "none", "communicator": "allreduce"},
