@@ -283,6 +283,7 @@ def main():
     for i in range(args.steps):
         loss = run()
         evs[i + 1].record()
+    issue_s = time.perf_counter() - t0  # host time to issue the steps (graph replays) before the wait
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -412,6 +413,7 @@ def main():
             "grace_ms_per_step": None if grace_ms is None else round(grace_ms, 3),
             "noop_exchange_ms_per_step": None if noop_ms is None else round(noop_ms, 3),
             "exposed_exchange_ms_eager": round(float(ex.item()) * 1e3, 3),
+            "host_issue_ms_per_step": round(issue_s / args.steps * 1e3, 3),
             "final_loss": round(float(loss.float().item()), 4),
         }
         print(json.dumps(out), flush=True)

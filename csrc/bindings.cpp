@@ -460,8 +460,8 @@ void dgc_refine(const Tensor& x, const Tensor& state, const Tensor& target, int6
   CHECK_I32(count);
   CHECK_I32(done);
   const int n_seg = (int)target.numel();
-  TORCH_CHECK(thr.numel() == n_seg && count.numel() == n_seg && done.numel() == n_seg && state.numel() >= 2 * n_seg,
-              "per-segment tables");
+  TORCH_CHECK(thr.numel() == n_seg && count.numel() >= 8 * n_seg && done.numel() == n_seg && state.numel() >= 2 * n_seg,
+              "per-segment tables (count: 8 words per segment)");
   auto ct = make_ct(seg, cb, ce);
   DevGuard guard(x.device());
   grace::dgc_refine(ct, n_seg, x.data_ptr<float>(), reinterpret_cast<const grace::TopkState*>(state.data_ptr<int32_t>()),

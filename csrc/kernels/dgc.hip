@@ -7,9 +7,11 @@
 // Here, for all segments of a bucket at once:
 //   dgc_sample   : Philox-uniform sample positions per segment, |x| gathered (1 thread/sample)
 //   (top-k of the samples reuses the segmented radix select of topk.hip -> exact k'-th key)
-//   dgc_count    : per-chunk count of |x| >= thr[seg] (segments already converged exit early),
-//                  workgroup-reduced, one atomic per workgroup
-//   dgc_adjust   : per segment, the reference's rule; marks converged segments done
+//   dgc_count_tree: per-chunk counts of |x| >= each of the 7 thresholds the next 3 refinement
+//                  steps can reach (segments already converged exit early), one atomic per
+//                  workgroup and threshold
+//   dgc_adjust_tree: per segment, the reference's rule walked 3 steps down the counted tree;
+//                  marks converged segments done
 //   dgc_compact  : ballot compaction of |x| >= thr[seg] into (value, flat index)
 //   dgc_compact  : capacity-bounded (the payload has a fixed capacity and an in-band count, so
 //                  the exchange needs no host sync and is graph-capturable), DgcMemory's u / v
@@ -64,42 +66,91 @@ __global__ void dgc_init_kernel(int n_seg, const TopkState* __restrict__ st, flo
   done[s] = 0;
 }
 
-__global__ __launch_bounds__(kBlock) void dgc_count_kernel(ChunkTable ct, const float* __restrict__ x,
-                                                           const float* __restrict__ thr,
-                                                           const int32_t* __restrict__ done,
-                                                           int32_t* __restrict__ count) {
+// Speculative refinement: the reference's loop (count at thr; x1.3 when too many, x0.7 when too
+// few; stop inside [0.7, 1.3] x target or after max_iters adjustments) needs one count pass per
+// step.  Its next kDepth thresholds form a binary tree from the current root (node k's children:
+// 2k+1 = node x 1.3f, 2k+2 = node x 0.7f, the same float products the sequential loop forms),
+// so ONE pass counts all kTree tree thresholds and the adjust kernel then walks kDepth steps
+// down the tree: ceil(max_iters / kDepth) passes (4 for the reference's 10) instead of
+// max_iters, with bit-identical thresholds and counts.  Per segment, count[8s + k] (k < kTree)
+// holds the tree counts and count[8s + 7] the adjustments made so far.
+constexpr int kDepth = 3;
+constexpr int kTree = (1 << kDepth) - 1;  // 7
+constexpr int kCntStride = 8;
+
+__device__ __forceinline__ void tree_thresholds(float root, float* t) {
+  t[0] = root;
+#pragma unroll
+  for (int k = 0; k < kTree / 2; ++k) {
+    t[2 * k + 1] = t[k] * 1.3f;
+    t[2 * k + 2] = t[k] * 0.7f;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void dgc_count_tree_kernel(ChunkTable ct, const float* __restrict__ x,
+                                                                const float* __restrict__ thr,
+                                                                const int32_t* __restrict__ done,
+                                                                int32_t* __restrict__ count) {
   const int c = blockIdx.x;
   const int s = ct.seg[c];
   if (done[s]) return;
   const int64_t b = ct.begin[c], e = ct.end[c];
-  const float t = thr[s];
-  unsigned cnt = 0;
-  for (int64_t i = b + threadIdx.x; i < e; i += kBlock) cnt += fabsf(x[i]) >= t ? 1u : 0u;
-  cnt = wave_sum_u32(cnt);
-  __shared__ unsigned red[kBlock / kWave];
-  if (lane_id() == 0) red[wave_id()] = cnt;
+  float t[kTree];
+  tree_thresholds(thr[s], t);
+  unsigned cnt[kTree];
+#pragma unroll
+  for (int k = 0; k < kTree; ++k) cnt[k] = 0;
+  for (int64_t i = b + threadIdx.x; i < e; i += kBlock) {
+    const float v = fabsf(x[i]);
+#pragma unroll
+    for (int k = 0; k < kTree; ++k) cnt[k] += v >= t[k] ? 1u : 0u;
+  }
+  __shared__ unsigned red[kBlock / kWave][kTree];
+#pragma unroll
+  for (int k = 0; k < kTree; ++k) {
+    const unsigned w = wave_sum_u32(cnt[k]);
+    if (lane_id() == 0) red[wave_id()][k] = w;
+  }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < kTree) {
     unsigned tot = 0;
-    for (int w = 0; w < kBlock / kWave; ++w) tot += red[w];
-    if (tot) atomicAdd(&count[s], (int32_t)tot);
+    for (int w = 0; w < kBlock / kWave; ++w) tot += red[w][threadIdx.x];
+    if (tot) atomicAdd(&count[s * kCntStride + threadIdx.x], (int32_t)tot);
   }
 }
 
-__global__ void dgc_adjust_kernel(int n_seg, const float* __restrict__ target, float* __restrict__ thr,
-                                  int32_t* __restrict__ count, int32_t* __restrict__ done) {
+// walk up to kDepth adjustments down the counted tree; the node reached becomes the next root
+__global__ void dgc_adjust_tree_kernel(int n_seg, const float* __restrict__ target, float* __restrict__ thr,
+                                       int32_t* __restrict__ count, int32_t* __restrict__ done, int max_iters) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n_seg || done[s]) return;
-  const float sel = (float)count[s];
-  if (sel > 1.3f * target[s]) {
-    thr[s] *= 1.3f;
-  } else if (sel < 0.7f * target[s]) {
-    thr[s] *= 0.7f;
-  } else {
-    done[s] = 1;
-    return;
+  int32_t* cs = count + s * kCntStride;
+  int it = cs[kTree];
+  float t = thr[s];
+  int node = 0;
+  bool fin = false;
+  for (int d = 0; d < kDepth; ++d) {
+    if (it >= max_iters) {
+      fin = true;
+      break;
+    }
+    const float sel = (float)cs[node];
+    ++it;
+    if (sel > 1.3f * target[s]) {
+      t *= 1.3f;
+      node = 2 * node + 1;
+    } else if (sel < 0.7f * target[s]) {
+      t *= 0.7f;
+      node = 2 * node + 2;
+    } else {
+      fin = true;
+      break;
+    }
   }
-  count[s] = 0;  // recounted by the next dgc_count
+  thr[s] = t;
+  if (fin || it >= max_iters) done[s] = 1;
+  for (int k = 0; k < kTree; ++k) cs[k] = 0;  // recounted by the next pass
+  cs[kTree] = it;
 }
 
 constexpr int kPer = 32;
@@ -207,11 +258,11 @@ void dgc_refine(const ChunkTable& ct, int n_seg, const float* x, const TopkState
                 int max_iters, float* thr, int32_t* count, int32_t* done, hipStream_t stream) {
   const int g = (n_seg + 255) / 256;
   dgc_init_kernel<<<g, 256, 0, stream>>>(n_seg, st, thr, count, done);
-  dgc_count_kernel<<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, thr, done, count);
-  for (int it = 0; it < max_iters; ++it) {
-    dgc_adjust_kernel<<<g, 256, 0, stream>>>(n_seg, target, thr, count, done);
-    // the count after the last adjustment would be unused (the reference computes and drops it)
-    if (it + 1 < max_iters) dgc_count_kernel<<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, thr, done, count);
+  GRACE_HIP_CHECK(hipMemsetAsync(count, 0, sizeof(int32_t) * (size_t)n_seg * kCntStride, stream));
+  // ceil(max_iters / kDepth) count passes; the count after the last adjustment is never formed
+  for (int it = 0; it < max_iters; it += kDepth) {
+    dgc_count_tree_kernel<<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, thr, done, count);
+    dgc_adjust_tree_kernel<<<g, 256, 0, stream>>>(n_seg, target, thr, count, done, max_iters);
   }
 }
 

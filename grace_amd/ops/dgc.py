@@ -48,7 +48,7 @@ def dgc_select(x: torch.Tensor, layout: SegmentLayout, ratio: float, sample_rati
                 "samp_off": torch.tensor(slay.offsets, dtype=torch.int64, device=dev),
                 "target": torch.tensor([n * ratio for n in layout.numels], dtype=torch.float32, device=dev),
                 "thr": torch.empty(layout.n_seg, dtype=torch.float32, device=dev),
-                "count": torch.empty(layout.n_seg, dtype=torch.int32, device=dev),
+                "count": torch.empty(8 * layout.n_seg, dtype=torch.int32, device=dev),  # tree counts + steps
                 "done": torch.empty(layout.n_seg, dtype=torch.int32, device=dev),
                 "samples": torch.empty(max(1, slay.total), dtype=torch.float32, device=dev),
             }

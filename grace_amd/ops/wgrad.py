@@ -57,7 +57,7 @@ def _side(device: torch.device) -> "torch.cuda.Stream":
             s = _streams.get(idx)
             if s is None:
                 with torch.cuda.device(idx):
-                    s = torch.cuda.Stream()
+                    s = torch.cuda.Stream(priority=int(os.environ.get("GRACE_WGRAD_PRIORITY", "0")))
                 _streams[idx] = s
     return s
 

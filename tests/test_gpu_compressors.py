@@ -439,3 +439,39 @@ def test_powersgd_rank_deficient_is_exact_gpu():
         out = g.step(m.clone(), "w")
         torch.cuda.synchronize()
         assert (out - m).abs().max() <= 1e-5 * m.abs().max(), shape
+
+
+def test_dgc_tree_refinement_matches_sequential_rule():
+    """the speculative tree refinement (3 steps per count pass) ends on exactly the thresholds the
+    reference's sequential loop reaches (dist/compressor/dgc.py:27-36: x1.3 above 1.3 x target,
+    x0.7 below 0.7 x target, at most 10 steps) from the same sampled start, in float32"""
+    from grace_amd.ops import dgc as D
+    from grace_amd.ops.dgc import _sizes
+    from grace_amd.ops.topk import _workspace as topk_ws
+
+    flat, lay = _bucket()
+    x = flat.cuda() * torch.linspace(0.2, 3.0, flat.numel(), device="cuda")  # spread the scales
+    dev = x.device
+    cap = D.dgc_capacity(lay, 0.01, 2.0)
+    D.dgc_select(x, lay, 0.01, 0.01, 10, 7, cap)
+    ws = lay.cached(dev, "dgc_ws:0.01:0.01", lambda: None)
+    ns, ks = _sizes(lay, 0.01, 0.01)
+    slay = lay.cached(dev, "dgc_sample_layout:0.01", lambda: None)
+    st = topk_ws(slay, ks, dev)["state"].cpu().view(-1, 2)
+    thr0 = st[:, 0].contiguous().view(torch.float32)
+    got = ws["thr"].cpu()
+    xa = x.abs().cpu()
+    f13, f07 = torch.tensor(1.3, dtype=torch.float32), torch.tensor(0.7, dtype=torch.float32)
+    for s, (_, o, n) in enumerate(lay.segments()):
+        t = thr0[s].clone()
+        target = torch.tensor(n * 0.01, dtype=torch.float32)
+        seg = xa[o:o + n]
+        for _ in range(10):
+            sel = (seg >= t).sum().to(torch.float32)
+            if sel > f13 * target:
+                t = t * f13
+            elif sel < f07 * target:
+                t = t * f07
+            else:
+                break
+        assert torch.equal(got[s], t), (s, float(got[s]), float(t))
