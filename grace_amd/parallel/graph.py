@@ -71,7 +71,9 @@ class GraphedStep:
     """
 
     def __init__(self, fn: Callable[[], torch.Tensor], warmup: int = 3, pool=None,
-                 capture_error_mode: str = "global"):
+                 capture_error_mode: str = "global", copies: Optional[int] = None):
+        import os
+
         self.fn = fn
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
@@ -80,14 +82,33 @@ class GraphedStep:
                 fn()
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, pool=pool, capture_error_mode=capture_error_mode):
-            self.loss = fn()
-        torch.cuda.synchronize()
+        # copies > 1: the step is captured that many times into one memory pool and the copies
+        # are replayed round-robin (stream-ordered, so they may share every buffer).  A forked
+        # graph (parallel branches) is launched node by node by the HIP runtime, and a graph
+        # cannot be re-submitted while its previous launch still runs; alternating copies lets
+        # the host submit step N+1 while step N executes.
+        copies = int(os.environ.get("GRACE_GRAPH_COPIES", "1")) if copies is None else int(copies)
+        self.graphs = []
+        self.losses = []
+        for i in range(max(1, copies)):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool, capture_error_mode=capture_error_mode):
+                loss = fn()
+            torch.cuda.synchronize()
+            if pool is None:
+                pool = g.pool()
+            self.graphs.append(g)
+            self.losses.append(loss)
+        self.graph = self.graphs[0]
+        self.loss = self.losses[0]
+        self._next = 0
 
     def __call__(self) -> torch.Tensor:
         _health.check()
-        self.graph.replay()
+        i = self._next
+        self._next = (i + 1) % len(self.graphs)
+        self.graphs[i].replay()
+        self.loss = self.losses[i]
         return self.loss
 
 
