@@ -214,19 +214,26 @@ class _Conv1x1AutoFn(torch.autograd.Function):
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = None
         f = _wg.fork(dy, ctx.weight) if ctx.needs_input_grad[1] else None
-        if ctx.needs_input_grad[0]:
-            dx = _run("dgrad", _pick("dgrad", x, wt, dy, ctx.wshape), x, wt, dy, ctx.wshape)
-        if f is not None:
+
+        def wg():
             be = _pick("wgrad", x, wt, dy, ctx.wshape)  # autotuned on the current stream, never on the side one
             tgt = _wg.grad_target(ctx.weight)  # the engine's bucket view: written in place
             with f as side:  # wgrad off the critical path (ops/wgrad.py)
                 o2 = tgt.reshape(wt.shape) if tgt is not None else None
-                dw = _wg.into_target(_run("wgrad", be, x, wt, dy, ctx.wshape, out=o2).view(ctx.wshape), tgt)
+                d = _wg.into_target(_run("wgrad", be, x, wt, dy, ctx.wshape, out=o2).view(ctx.wshape), tgt)
                 if side:
                     s = torch.cuda.current_stream(dy.device)
                     _wg.tag(dy, s)
                     _wg.tag(x, s)
-                    _wg.tag(dw, f.main)
+                    _wg.tag(d, f.main)
+            return d
+
+        if f is not None and _wg._WG_FIRST:
+            dw = wg()
+        if ctx.needs_input_grad[0]:
+            dx = _run("dgrad", _pick("dgrad", x, wt, dy, ctx.wshape), x, wt, dy, ctx.wshape)
+        if f is not None and not _wg._WG_FIRST:
+            dw = wg()
         return dx, dw
 
 

@@ -35,6 +35,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 _ENABLED = os.environ.get("GRACE_WGRAD_STREAM", "1") == "1"
+# issue (capture) the side-stream wgrad before the in-line dgrad of the same conv
+_WG_FIRST = os.environ.get("GRACE_WGRAD_FIRST", "0") == "1"
 _streams: Dict[int, "torch.cuda.Stream"] = {}
 _pending: Dict[int, bool] = {}  # device -> side work issued since the last join
 _lock = threading.Lock()
@@ -242,18 +244,25 @@ class _ConvSplitFn(torch.autograd.Function):
         cb = torch.ops.aten.convolution_backward
         dx = dw = None
         f = fork(dy, w) if ctx.needs_input_grad[1] else None
-        if ctx.needs_input_grad[0]:
-            dx = _dgrad(dy, x, w, stride, padding, dilation, groups)
-        if f is not None:
+
+        def wg():
             tgt = grad_target(w)
             with f as side:
-                dw = cb(dy, x, w, None, stride, padding, dilation, False, [0, 0], groups, [False, True, False])[1]
-                dw = into_target(dw, tgt)
+                d = cb(dy, x, w, None, stride, padding, dilation, False, [0, 0], groups, [False, True, False])[1]
+                d = into_target(d, tgt)
                 if side:
                     s = torch.cuda.current_stream(dy.device)
                     tag(dy, s)
                     tag(x, s)
-                    tag(dw, f.main)
+                    tag(d, f.main)
+            return d
+
+        if f is not None and _WG_FIRST:
+            dw = wg()
+        if ctx.needs_input_grad[0]:
+            dx = _dgrad(dy, x, w, stride, padding, dilation, groups)
+        if f is not None and not _WG_FIRST:
+            dw = wg()
         return dx, dw, None, None, None, None
 
 
