@@ -35,7 +35,9 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 _ENABLED = os.environ.get("GRACE_WGRAD_STREAM", "1") == "1"
-# issue (capture) the side-stream wgrad before the in-line dgrad of the same conv
+# issue (capture) the side-stream wgrad before the in-line dgrad of the same conv: measured
+# 2677 -> 2394-2468 img/s (the wgrads then compete with the dgrad chain from its start;
+# profiles/r3_graph_fork_knobs.txt), so off
 _WG_FIRST = os.environ.get("GRACE_WGRAD_FIRST", "0") == "1"
 _streams: Dict[int, "torch.cuda.Stream"] = {}
 _pending: Dict[int, bool] = {}  # device -> side work issued since the last join
