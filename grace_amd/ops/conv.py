@@ -213,7 +213,19 @@ class _Conv1x1AutoFn(torch.autograd.Function):
         x, wt = ctx.saved_tensors
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = None
-        f = _wg.fork(dy, ctx.weight) if ctx.needs_input_grad[1] else None
+        f = None
+        if ctx.needs_input_grad[1]:
+            tgt = _wg.grad_target(ctx.weight) if _wg._DEFER else None
+            if tgt is not None:
+                be = _pick("wgrad", x, wt, dy, ctx.wshape)
+                wshape = ctx.wshape
+
+                def late(dy=dy, x=x, wt=wt, tgt=tgt, be=be):
+                    _wg.into_target(_run("wgrad", be, x, wt, dy, wshape, out=tgt.reshape(wt.shape)).view(wshape), tgt)
+            if tgt is not None and _wg.defer(dy.device, late):
+                dw = tgt.view_as(tgt)
+            else:
+                f = _wg.fork(dy, ctx.weight)
 
         def wg():
             be = _pick("wgrad", x, wt, dy, ctx.wshape)  # autotuned on the current stream, never on the side one

@@ -70,6 +70,41 @@ def _final_join():
     join()
 
 
+# ---------------------------------------------------------------- deferred weight gradients
+# GRACE_WGRAD_DEFER=1: a weight gradient whose destination is an engine bucket view is not
+# computed when its conv's backward runs; its closure is queued and every queued one runs, in
+# order, on the compute stream at the join (the engine's bucket launch / the end of backward).
+# The dgrad chain then runs uninterrupted and the weight gradients back to back after it, in a
+# single-stream graph.  The fresh alias of the bucket view handed to AccumulateGrad is only
+# READ after the join, so the late write is invisible to the engine.
+_DEFER = os.environ.get("GRACE_WGRAD_DEFER", "0") == "1"
+_deferred: Dict[int, list] = {}
+
+
+def defer(device: torch.device, fn) -> bool:
+    """Queue ``fn`` (computes and stores one weight gradient) for the next join; False when
+    deferral is off or impossible (no backward to attach the final callback to)."""
+    if not (_DEFER and _ENABLED):
+        return False
+    idx = device.index
+    q = _deferred.setdefault(idx, [])
+    if not q and not _pending.get(idx):
+        try:
+            torch.autograd.Variable._execution_engine.queue_callback(_final_join)
+        except RuntimeError:
+            return False
+    q.append(fn)
+    return True
+
+
+def _run_deferred(idx: int) -> None:
+    q = _deferred.get(idx)
+    if q:
+        _deferred[idx] = []
+        for fn in q:
+            fn()
+
+
 class fork:
     """``f = fork(t)`` marks the current stream's position NOW (before the caller issues its
     critical-path kernels); ``with f as go:`` then runs the body on the side stream of ``t``'s
@@ -150,8 +185,9 @@ def tag(t: Optional[torch.Tensor], stream: "torch.cuda.Stream") -> None:
 
 
 def join(stream: Optional["torch.cuda.Stream"] = None, device=None) -> None:
-    """Make ``stream`` (default: the current stream) wait for every side-stream wgrad issued so far."""
-    if not _pending:
+    """Make ``stream`` (default: the current stream) wait for every side-stream wgrad issued so
+    far, after running the deferred ones (on ``stream``)."""
+    if not _pending and not _deferred:
         return
     if stream is not None:
         devs = [stream.device.index]
@@ -160,6 +196,12 @@ def join(stream: Optional["torch.cuda.Stream"] = None, device=None) -> None:
     else:
         devs = [torch.cuda.current_device()]
     for idx in devs:
+        if _deferred.get(idx):
+            if stream is not None:
+                with torch.cuda.stream(stream):
+                    _run_deferred(idx)
+            else:
+                _run_deferred(idx)
         if _pending.get(idx):
             tgt = stream if stream is not None else torch.cuda.current_stream(idx)
             tgt.wait_stream(_streams[idx])
@@ -245,7 +287,17 @@ class _ConvSplitFn(torch.autograd.Function):
         stride, padding, dilation, groups = ctx.conf
         cb = torch.ops.aten.convolution_backward
         dx = dw = None
-        f = fork(dy, w) if ctx.needs_input_grad[1] else None
+        f = None
+        if ctx.needs_input_grad[1]:
+            tgt = grad_target(w) if _DEFER and dy.is_cuda else None
+            if tgt is not None:
+                def late(dy=dy, x=x, w=w, tgt=tgt):
+                    into_target(cb(dy, x, w, None, stride, padding, dilation, False, [0, 0], groups,
+                                   [False, True, False])[1], tgt)
+            if tgt is not None and defer(dy.device, late):
+                dw = tgt.view_as(tgt)
+            else:
+                f = fork(dy, w)
 
         def wg():
             tgt = grad_target(w)

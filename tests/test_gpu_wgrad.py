@@ -223,3 +223,50 @@ def test_projection_branch_stream_matches_inline():
                 _close(a, b)
     finally:
         wgrad._BRANCH = False
+
+
+def test_deferred_wgrad_engine_graph(bn_deterministic):
+    """GRACE_WGRAD_DEFER: weight gradients queued and run at the engine's join, eager and inside a
+    captured whole-step graph, match the side-stream run"""
+    from grace_amd import grace_from_params
+    from grace_amd.parallel import DistributedOptimizer, FusedSGD
+    from grace_amd.parallel.graph import GraphedStep
+
+    x = torch.randn(16, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (16,), device="cuda")
+
+    def run(defer, graph):
+        torch.manual_seed(1)
+        m = _small_cnn().cuda().to(memory_format=torch.channels_last)
+        grc = grace_from_params({"compressor": "none", "memory": "none", "communicator": "allreduce",
+                                 "world_size": 1})
+        opt = DistributedOptimizer(FusedSGD(list(m.parameters()), lr=0.05, momentum=0.5), grc,
+                                   named_parameters=list(m.named_parameters()), overlap=False)
+
+        def step():
+            opt.zero_grad(set_to_none=True)
+            loss = F.cross_entropy(m(x), y)
+            loss.backward()
+            opt.step()
+            return loss
+
+        old = wgrad._DEFER
+        wgrad._DEFER = defer
+        try:
+            if graph:
+                g = GraphedStep(step, warmup=3)
+                for _ in range(4):
+                    g()
+            else:
+                for _ in range(7):
+                    step()
+            torch.cuda.synchronize()
+        finally:
+            wgrad._DEFER = old
+        return [p.detach().clone() for p in m.parameters()]
+
+    ref = run(False, False)
+    for got in (run(True, False), run(True, True)):
+        for a, b in zip(got, ref):
+            err = float((a - b).abs().max())
+            assert err <= 1e-3 * float(b.abs().max()) + 2e-5, err
