@@ -75,7 +75,9 @@ def _final_join():
 # computed when its conv's backward runs; its closure is queued and every queued one runs, in
 # order, on the compute stream at the join (the engine's bucket launch / the end of backward).
 # The dgrad chain then runs uninterrupted and the weight gradients back to back after it, in a
-# single-stream graph.  The fresh alias of the bucket view handed to AccumulateGrad is only
+# single-stream graph.  Measured at the in-line speed (2516 vs 2708 img/s for the side stream,
+# profiles/r3_graph_fork_knobs.txt): the side stream's gain is the overlap of its wgrads with
+# the tail of the dgrad chain, not the reordering -- so opt-in.  The fresh alias of the bucket view handed to AccumulateGrad is only
 # READ after the join, so the late write is invisible to the engine.
 _DEFER = os.environ.get("GRACE_WGRAD_DEFER", "0") == "1"
 _deferred: Dict[int, list] = {}
