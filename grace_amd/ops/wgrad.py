@@ -332,10 +332,19 @@ class Conv2dSplitGrad(nn.Conv2d):
 
     def forward(self, x):
         if (_ENABLED and x.is_cuda and self.bias is None and self.padding_mode == "zeros"
-                and not isinstance(self.padding, str) and torch.is_grad_enabled() and self.weight.requires_grad
-                and not torch.is_autocast_enabled() and x.dtype == self.weight.dtype):
-            return _ConvSplitFn.apply(x, self.weight, _as2(self.stride), _as2(self.padding), _as2(self.dilation),
-                                      self.groups)
+                and not isinstance(self.padding, str) and torch.is_grad_enabled() and self.weight.requires_grad):
+            w = self.weight
+            if torch.is_autocast_enabled():
+                # autocast: only when the parameter already IS in the autocast dtype (bf16 working
+                # copies, parallel/precision.py) -- a per-step cast of an fp32 weight would put its
+                # backward copy on the compute stream, reading the side stream's gradient early
+                if w.dtype != torch.get_autocast_dtype("cuda"):
+                    return super().forward(x)
+                if x.dtype != w.dtype and x.is_floating_point():
+                    x = x.to(w.dtype)
+            if x.dtype == w.dtype:
+                return _ConvSplitFn.apply(x, w, _as2(self.stride), _as2(self.padding), _as2(self.dilation),
+                                          self.groups)
         return super().forward(x)
 
 
