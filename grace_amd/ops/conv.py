@@ -84,7 +84,7 @@ class _Conv1x1Fn(torch.autograd.Function):
             with f as side:
                 dw = torch.empty((cout, cin), device=x.device, dtype=torch.float32)
                 gemm(dy, False, cout, x, False, cin, dw, cin, cout, cin, m, _splits(cout, cin, m))
-                dw = dw.view(ctx.wshape)
+                dw = _as_param_layout(dw, ctx.weight)
                 if side:
                     s = torch.cuda.current_stream(dy.device)
                     _wg.tag(dy, s)
@@ -115,6 +115,16 @@ def set_autotune(on: bool) -> None:
 def autotune_table():
     """[(direction, M, Cin, Cout, chosen, {backend: ms})] of every tuned layer direction."""
     return [(k[0], k[1], k[2], k[3], v, dict(_TIMES.get(k, {}))) for k, v in sorted(_CHOICE.items())]
+
+
+def _as_param_layout(dw2d: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """A dense [Cout, Cin] weight gradient viewed with the 1x1 weight's own strides (the memory
+    image is the same whatever the strides of the size-1 dims): DDP's reducer compares strides
+    literally and would otherwise copy every such gradient into its bucket view."""
+    if dw2d.is_contiguous() and weight.dim() == 4 and weight.shape[2] == 1 and weight.shape[3] == 1 \
+            and weight.stride(1) == 1 and weight.stride(0) == weight.shape[1]:
+        return dw2d.as_strided(weight.shape, weight.stride())
+    return dw2d.view(weight.shape)
 
 
 def _x2d(t: torch.Tensor) -> torch.Tensor:
@@ -232,7 +242,7 @@ class _Conv1x1AutoFn(torch.autograd.Function):
             tgt = _wg.grad_target(ctx.weight)  # the engine's bucket view: written in place
             with f as side:  # wgrad off the critical path (ops/wgrad.py)
                 o2 = tgt.reshape(wt.shape) if tgt is not None else None
-                d = _wg.into_target(_run("wgrad", be, x, wt, dy, ctx.wshape, out=o2).view(ctx.wshape), tgt)
+                d = _wg.into_target(_as_param_layout(_run("wgrad", be, x, wt, dy, ctx.wshape, out=o2), ctx.weight), tgt)
                 if side:
                     s = torch.cuda.current_stream(dy.device)
                     _wg.tag(dy, s)

@@ -162,7 +162,11 @@ def grace_comm_hook(state: GraceHookState, bucket: dist.GradBucket) -> torch.fut
     ds.wait_stream(cs)  # decode after this bucket's compress/issue; the collective is waited on inside
     fut = torch.futures.Future(devices=[dev])
     with torch.cuda.stream(ds):
-        _record((handles, ctx), ds)
+        # the payload tensors and the context's per-call tensors cross to the decode stream
+        # (not a deep walk of the context: its layout holds long-lived cached device tables)
+        _record(handles, ds)
+        _record(getattr(ctx, "extra", None), ds)
+        _record(getattr(ctx, "out", None), ds)
         out = unpacked(grc.receive_step(handles, ctx))
         buf.record_stream(ds)
         g.record_stream(ds)
