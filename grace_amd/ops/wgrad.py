@@ -61,7 +61,7 @@ def _side(device: torch.device) -> "torch.cuda.Stream":
             s = _streams.get(idx)
             if s is None:
                 with torch.cuda.device(idx):
-                    s = torch.cuda.Stream(priority=int(os.environ.get("GRACE_WGRAD_PRIORITY", "0")))
+                    s = torch.cuda.Stream()  # a high-priority side stream measured 20 ms/step (r3_graph_fork_knobs)
                 _streams[idx] = s
     return s
 
