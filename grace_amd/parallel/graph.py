@@ -88,11 +88,15 @@ class GraphedStep:
         # cannot be re-submitted while its previous launch still runs; alternating copies lets
         # the host submit step N+1 while step N executes.
         copies = int(os.environ.get("GRACE_GRAPH_COPIES", "1")) if copies is None else int(copies)
+        # GRACE_GRAPH_PRIORITY=-1: capture and replay on a high-priority stream (the compute
+        # stream of the step then outranks the side streams it forks)
+        prio = int(os.environ.get("GRACE_GRAPH_PRIORITY", "0"))
+        self.stream = torch.cuda.Stream(priority=prio) if prio else None
         self.graphs = []
         self.losses = []
         for i in range(max(1, copies)):
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool, capture_error_mode=capture_error_mode):
+            with torch.cuda.graph(g, pool=pool, stream=self.stream, capture_error_mode=capture_error_mode):
                 loss = fn()
             torch.cuda.synchronize()
             if pool is None:
@@ -107,7 +111,14 @@ class GraphedStep:
         _health.check()
         i = self._next
         self._next = (i + 1) % len(self.graphs)
-        self.graphs[i].replay()
+        if self.stream is not None:
+            cur = torch.cuda.current_stream()
+            self.stream.wait_stream(cur)
+            with torch.cuda.stream(self.stream):
+                self.graphs[i].replay()
+            cur.wait_stream(self.stream)
+        else:
+            self.graphs[i].replay()
         self.loss = self.losses[i]
         return self.loss
 
