@@ -231,9 +231,9 @@ __device__ __forceinline__ bool arrive(unsigned* counter, unsigned expected_last
 
 // Per-thread 8-channel accumulators -> this block's partial row -> the tile's arrival tree.
 // True in every thread of the tile's final block; totals then in total[tile][0..2CT).
-// atot != nullptr (the backward's ATOMIC mode, see bn_reduce_kernel): the block's partial row is
-// added into atot[0..2C) with fp32 no-return atomics instead (no arrival, no finisher); returns
-// false everywhere.
+// atot != nullptr (the backward's ATOMIC mode): the block's partial row is added into atot[0..2C)
+// with fp32 no-return atomics instead of being stored and folded; one arrival per block, the
+// tile's last block reads the totals (no partial-row fold) and finishes as the tree does.
 __device__ bool block_reduce_tree(const Red& R, const float* a, const float* b, float* atot = nullptr) {
   __shared__ __align__(16) float sa[kB * 8];
   __shared__ float sb[kB * 8];
@@ -259,7 +259,22 @@ __device__ bool block_reduce_tree(const Red& R, const float* a, const float* b, 
       __hip_atomic_fetch_add(atot + cc, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_fetch_add(atot + R.C + cc, y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    return false;
+    // one arrival per block (the drain inside arrive() covers the no-return atomics); the tile's
+    // last block reads the totals (device-scope loads: never a stale L1 line), re-zeroes them and
+    // finishes exactly like the tree's finisher (coefficients, dgamma / dbeta)
+    unsigned* top = R.cnt + tile * (kMaxGroups + 1) + kMaxGroups;
+    if (!arrive(top, (unsigned)R.nchunks - 1)) return false;
+    double* total = R.total + (size_t)tile * C2;
+    for (int c = threadIdx.x; c < CT; c += kB) {
+      const int cc = tile * CT + c;
+      total[c] = (double)__hip_atomic_load(atot + cc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      total[CT + c] = (double)__hip_atomic_load(atot + R.C + cc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      atot[cc] = 0.f;
+      atot[R.C + cc] = 0.f;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) *top = 0;  // re-arm (visible at kernel end)
+    return true;
   }
   float* part = R.part + (size_t)tile * R.nchunks * C2;
   float* pb = part + (size_t)blockIdx.x * C2;
@@ -1433,7 +1448,9 @@ bool bn_deterministic_env() {
 }
 
 CoefSrc coef_src(const GradOut& o, int64_t M, bool atomic) {
-  return CoefSrc{atomic ? nullptr : o.coef, o.save, o.gamma, o.dgamma, o.dbeta, 1.0 / (double)M};
+  (void)atomic;  // both modes' finishers write coef (the per-thread derivation from the totals,
+                 // measured slow, stays available through CoefSrc.coef == nullptr)
+  return CoefSrc{o.coef, o.save, o.gamma, o.dgamma, o.dbeta, 1.0 / (double)M};
 }
 
 float* atot_of(const GradOut& o, int C, bool atomic) {
