@@ -194,6 +194,7 @@ void bn_act_forward_from_partials(const float* x, const float* res, const float*
 void bn_set_deterministic(bool on);
 // layers with <= n row chunks per channel tile use the atomic backward totals (0: none)
 void bn_set_atomic_chunks(int n);
+int bn_atomic_chunks();
 void bn_act_backward(const void* dy, const void* dy2, const void* x, bool fp32, const uint8_t* relu_mask, int64_t M,
                      int C, const float* gamma, const float* save, bool relu, float* dgamma, float* dbeta,
                      float* coef, float* ws, void* dx, void* dres, bool deterministic, hipStream_t stream);

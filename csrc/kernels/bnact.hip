@@ -1427,14 +1427,15 @@ __global__ __launch_bounds__(kB) void bn_stats_fold_kernel(const float* __restri
   if (threadIdx.x == 0 && blockIdx.x == 0 && o.nbt) *o.nbt += 1;
 }
 
-// ATOMIC mode (opt-in per chunk count, GRACE_BN_ATOMIC_CHUNKS; GRACE_BN_DETERMINISTIC=1 or a
-// repeated backward of one forward always select the fixed-order tree): the reduce kernel adds its blocks' partial rows into save[4C..6C) (zeroed by
+// ATOMIC mode (default; GRACE_BN_ATOMIC_CHUNKS bounds it by chunk count, GRACE_BN_DETERMINISTIC=1
+// or a repeated backward of one forward select the fixed-order tree): the reduce kernel adds its blocks' partial rows into save[4C..6C) (zeroed by
 // the forward's statistics finisher) and the dx kernel derives the coefficients (CoefSrc).
 // GRACE_BN_ATOMIC_CHUNKS: the largest per-tile chunk count whose backward uses the atomic totals
-// (default 0: the fixed-order tree everywhere)
+// (default: every layer -- fp32 ResNet-50 headline 2669 -> 2716 img/s, profiles/r3_bn_atomic_ab.txt;
+// 0 = the fixed-order tree everywhere, as GRACE_BN_DETERMINISTIC=1)
 int g_atomic_chunks = -1;
 int bn_atomic_max_chunks() {
-  if (g_atomic_chunks < 0) g_atomic_chunks = env_int("GRACE_BN_ATOMIC_CHUNKS", 0);
+  if (g_atomic_chunks < 0) g_atomic_chunks = env_int("GRACE_BN_ATOMIC_CHUNKS", 1 << 30);
   return g_atomic_chunks;
 }
 
@@ -1597,14 +1598,13 @@ void bn_act_forward_from_partials(const float* x, const float* res, const float*
 
 void bn_set_deterministic(bool on) { g_det_mode = on ? 1 : 0; }
 void bn_set_atomic_chunks(int n) { g_atomic_chunks = n < 0 ? 0 : n; }
+int bn_atomic_chunks() { return bn_atomic_max_chunks(); }
 
 void bn_act_backward(const void* dyv, const void* dy2v, const void* xv, bool fp32, const uint8_t* mask, int64_t M,
                      int C, const float* gamma, const float* save, bool relu, float* dgamma, float* dbeta,
                      float* coef, float* ws, void* dxv, void* dresv, bool deterministic, hipStream_t stream) {
   GradOut o{gamma, save, dgamma, dbeta, coef};
-  // atomic totals only where a tile has few chunks (few same-address atomics per total): with
-  // hundreds of chunks per tile the L2 serialises them -- measured on the fp32 ResNet-50
-  // headline with every layer atomic: 2709 -> 2454 img/s (profiles/r3_bn_atomic_ab.txt)
+  // atomic totals (one arrival + a totals-only finisher) up to the chunk-count threshold
   const bool atomic = !deterministic && !bn_deterministic_env() && plan(M, C).nchunks <= bn_atomic_max_chunks();
   if (fp32) {
     backward_2k(static_cast<const float*>(dyv), static_cast<const float*>(dy2v), static_cast<const float*>(xv), mask,

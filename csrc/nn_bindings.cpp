@@ -307,5 +307,6 @@ void grace_bind_nn(py::module& m) {
   m.def("bn_act_bwd", &bn_act_bwd);
   m.def("bn_set_deterministic", [](bool on) { grace::bn_set_deterministic(on); });
   m.def("bn_set_atomic_chunks", [](int64_t n) { grace::bn_set_atomic_chunks((int)n); });
+  m.def("bn_atomic_chunks", []() { return (int64_t)grace::bn_atomic_chunks(); });
   m.def("bn_act_fwd_partials", &bn_act_fwd_partials);
 }

@@ -9,9 +9,10 @@ four CDNA4 kernels of ``csrc/kernels/bnact.hip`` per layer (statistics with the 
 it is exactly ``relu(F.batch_norm(x) + residual)``.  fp32 activations use the two-kernel path
 (the single-launch variants keep bf16 rows in registers).
 
-Numerics: statistics and the affine are fp32 (fp64 fixed-order fold of the per-block partial
-sums: run-to-run deterministic; GRACE_BN_ATOMIC_CHUNKS=n opts layers with <= n row chunks per
-channel tile into fp32-atomic backward totals, order-dependent to ~1e-7 relative); for
+Numerics: statistics and the affine are fp32 (forward: fp64 fixed-order fold of the per-block
+partial sums; backward: the blocks' partial sums meet in fp32 atomic totals -- order-dependent
+to ~1e-7 relative -- unless GRACE_BN_DETERMINISTIC=1 / GRACE_BN_ATOMIC_CHUNKS=0 select the
+fixed-order fp64 tree); for
 bf16 the output is rounded to bf16 once (the unfused bf16 path rounds after BN, after the add and after
 the ReLU); the ReLU mask is taken from the bf16 output, as ``threshold_backward`` does, and kept as 1 bit per
 element for the backward (which then reads dy, x and M*C/8 mask bytes instead of dy, x and y).

@@ -333,9 +333,10 @@ def test_bn_relu_maxpool_fused_matches_reference(shape, k, s, p, dtype):
 
 @pytest.fixture
 def atomic_bn():
+    prev = _native.lib().bn_atomic_chunks()
     _native.lib().bn_set_atomic_chunks(1 << 30)
     yield
-    _native.lib().bn_set_atomic_chunks(0)
+    _native.lib().bn_set_atomic_chunks(prev)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
