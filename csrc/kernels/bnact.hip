@@ -150,6 +150,7 @@ struct Red {
   double* gpart;       // [tiles][ngroups][2*CT]
   double* total;       // [tiles][2*CT]
   unsigned* cnt;       // [tiles][kMaxGroups + 1]: group counters, top counter last
+  float* ftot;         // forward statistics in ATOMIC mode: [2C] self-cleaning totals of the slot, or null
 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -359,7 +360,7 @@ __global__ __launch_bounds__(kB) void bn_stats_kernel(const T* __restrict__ x, R
       }
     }
   });
-  if (!block_reduce_tree(R, s, q)) return;
+  if (!block_reduce_tree(R, s, q, R.ftot)) return;
   const int CT = R.CT, C = R.C;
   const double* total = R.total + (size_t)blockIdx.y * 2 * CT;
   const double inv_m = 1.0 / (double)R.M;
@@ -1125,22 +1126,38 @@ __global__ __launch_bounds__(kB) void bn_bwd_fused_kernel(const uint16_t* __rest
 constexpr int kSlots = 256;
 struct Slots {
   unsigned* counters = nullptr;
+  float* ftot = nullptr;
   int next = 0;
 };
 Slots g_slots[64];
 
-unsigned* next_slot(hipStream_t stream) {
+unsigned* next_slot(hipStream_t stream, float** ftot = nullptr) {
   int dev = 0;
   GRACE_HIP_CHECK(hipGetDevice(&dev));
   Slots& p = g_slots[dev];
   if (!p.counters) {  // first use happens eagerly (warm-up), never inside a graph capture
     GRACE_HIP_CHECK(hipMalloc(&p.counters, (size_t)kSlots * kSlotWords * sizeof(unsigned)));
     GRACE_HIP_CHECK(hipMemsetAsync(p.counters, 0, (size_t)kSlots * kSlotWords * sizeof(unsigned), stream));
+    // per-slot [2 kMaxC] fp32 totals of the atomic statistics: zero at allocation, re-zeroed by
+    // every finisher that reads them (so each launch finds them clean)
+    GRACE_HIP_CHECK(hipMalloc(&p.ftot, (size_t)kSlots * 2 * kMaxC * sizeof(float)));
+    GRACE_HIP_CHECK(hipMemsetAsync(p.ftot, 0, (size_t)kSlots * 2 * kMaxC * sizeof(float), stream));
     GRACE_HIP_CHECK(hipStreamSynchronize(stream));
   }
   const int s = p.next;
   p.next = (s + 1) % kSlots;
+  if (ftot) *ftot = p.ftot + (size_t)s * 2 * kMaxC;
   return p.counters + (size_t)s * kSlotWords;
+}
+
+// GRACE_BN_FWD_ATOMIC (default 1): the forward statistics' blocks meet in atomic fp32 totals
+// with a totals-only finisher (as the backward), 0 = the fixed-order fp64 tree
+bool bn_fwd_atomic() {
+  static const bool on = [] {
+    const char* e = std::getenv("GRACE_BN_FWD_ATOMIC");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
 }
 
 // Grid and tree shape.  Target ~512 blocks (2 per CU) with 8..32 row vectors per thread (knobs below).
@@ -1314,12 +1331,14 @@ int64_t ws_floats(const Red& R) {
   return even((int64_t)tiles * R.nchunks * C2) + 2 * (int64_t)tiles * (R.ngroups + 1) * C2;
 }
 
-void bind_ws(Red& R, float* ws, hipStream_t stream) {
+void bind_ws(Red& R, float* ws, hipStream_t stream, bool atomic_stats = false) {
   const int tiles = R.C / R.CT, C2 = 2 * R.CT;
   R.part = ws;
   R.gpart = reinterpret_cast<double*>(ws + even((int64_t)tiles * R.nchunks * C2));  // 8-B aligned
   R.total = R.gpart + (size_t)tiles * R.ngroups * C2;
-  R.cnt = next_slot(stream);
+  float* ft = nullptr;
+  R.cnt = next_slot(stream, &ft);
+  R.ftot = atomic_stats ? ft : nullptr;
 }
 
 int apply_grid(int64_t n_vec, int C) {
@@ -1362,11 +1381,13 @@ unsigned bn_spin_timeouts() {
 
 namespace {
 
+bool bn_deterministic_env();
+
 template <typename T>
 void forward_2k(const T* x, const T* res, int64_t M, int C, const StatsOut& o, bool relu, float* save, float* ws,
                 T* y, uint8_t* mask, hipStream_t stream) {
   Red R = plan(M, C);
-  bind_ws(R, ws, stream);
+  bind_ws(R, ws, stream, bn_fwd_atomic() && !bn_deterministic_env());
   hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(R.nchunks, C / R.CT), dim3(kB), 0, stream, x, R, o);
   const int64_t n_vec = M * C / 8;
   const int gb = apply_grid(n_vec, C);
@@ -1688,7 +1709,7 @@ template <typename T>
 void pool_fwd_t(const T* x, int64_t M, int C, const StatsOut& o, float* save, float* ws, const PoolShape& g, int N,
                 T* y, uint8_t* code, hipStream_t stream) {
   Red R = plan(M, C);
-  bind_ws(R, ws, stream);
+  bind_ws(R, ws, stream, bn_fwd_atomic() && !bn_deterministic_env());
   hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(R.nchunks, C / R.CT), dim3(kB), 0, stream, x, R, o);
   const int64_t n_vec = (int64_t)N * g.OH * g.OW * (C / 8);
   const int gb = (int)std::min<int64_t>((n_vec + kB - 1) / kB, 8192);
