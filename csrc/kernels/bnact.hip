@@ -1150,12 +1150,14 @@ unsigned* next_slot(hipStream_t stream, float** ftot = nullptr) {
   return p.counters + (size_t)s * kSlotWords;
 }
 
-// GRACE_BN_FWD_ATOMIC (default 1): the forward statistics' blocks meet in atomic fp32 totals
-// with a totals-only finisher (as the backward), 0 = the fixed-order fp64 tree
+// GRACE_BN_FWD_ATOMIC=1: the forward statistics' blocks meet in atomic fp32 totals with a
+// totals-only finisher (as the backward).  Measured no faster than the fixed-order fp64 tree
+// (2681-2706 vs 2700-2709 img/s, profiles/r3_bn_atomic_ab.txt), which also keeps the forward
+// statistics deterministic and fp64-folded, so off by default.
 bool bn_fwd_atomic() {
   static const bool on = [] {
     const char* e = std::getenv("GRACE_BN_FWD_ATOMIC");
-    return e == nullptr || e[0] != '0';
+    return e != nullptr && e[0] == '1';
   }();
   return on;
 }
