@@ -302,10 +302,11 @@ class _ConvSplitFn(torch.autograd.Function):
                 f = fork(dy, w)
 
         def wg():
-            tgt = grad_target(w)
+            # MIOpen returns its own gradient tensor: writing it into the bucket view would be one
+            # more copy kernel per conv at the END of the side stream (the step's critical tail
+            # once the dgrad chain is done); the engine's single gather launch copies these
             with f as side:
                 d = cb(dy, x, w, None, stride, padding, dilation, False, [0, 0], groups, [False, True, False])[1]
-                d = into_target(d, tgt)
                 if side:
                     s = torch.cuda.current_stream(dy.device)
                     tag(dy, s)
