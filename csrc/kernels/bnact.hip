@@ -567,50 +567,19 @@ __global__ __launch_bounds__(kB) void bn_reduce_kernel(const T* __restrict__ dy,
   }
 }
 
-// Where a dx pass gets its per-channel coefficients (dx = a*dz + b*x + c): the reduce kernel's
-// finisher wrote them to coef[3C] (deterministic tree), or -- ATOMIC mode -- every thread derives
-// its 8 channels' coefficients from the atomic totals tot = save + 4C ([sum dz | sum dz (x-mean)])
-// and the forward's mean / invstd, and block 0 writes dgamma / dbeta.  The atomic mode removes
-// the reduce kernel's arrival round trip and serial fold: on the small ResNet layers that tail
-// is most of the reduce kernel's time.
+// A dx pass's per-channel coefficients (dx = a*dz + b*x + c), written by the reduce kernel's
+// finisher (tree or atomic totals), plus the forward's save (the RX variant's scale / shift).
 struct CoefSrc {
-  const float* coef;   // [3C] (tree mode) or nullptr
-  const float* save;   // [6C] forward save: mean, invstd, scale, shift, tot[2C]
-  const float* gamma;  // may be null
-  float* dgamma;       // may be null
-  float* dbeta;        // may be null
-  double inv_m;
+  const float* coef;  // [3C]
+  const float* save;  // [6C] forward save: mean, invstd, scale, shift, atomic totals [2C]
 };
 
 __device__ __forceinline__ void get_coef(const CoefSrc& s, int C, int c0, float* ca, float* cb, float* cc) {
-  if (s.coef != nullptr) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      ca[j] = s.coef[c0 + j];
-      cb[j] = s.coef[C + c0 + j];
-      cc[j] = s.coef[2 * C + c0 + j];
-    }
-    return;
-  }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const int c = c0 + j;
-    const double S1 = s.save[4 * C + c], S2 = s.save[5 * C + c];
-    const double mean = s.save[c], invstd = s.save[C + c];
-    const double a = (double)(s.gamma ? s.gamma[c] : 1.f) * invstd;
-    const double b = -a * invstd * (S2 * invstd) * s.inv_m;
-    ca[j] = (float)a;
-    cb[j] = (float)b;
-    cc[j] = (float)(-a * S1 * s.inv_m - b * mean);
-  }
-}
-
-__device__ __forceinline__ void put_dgamma(const CoefSrc& s, int C) {
-  if (s.coef != nullptr || blockIdx.x != 0) return;
-  for (int c = threadIdx.x; c < C; c += kB) {
-    const float S1 = s.save[4 * C + c], S2 = s.save[5 * C + c];
-    if (s.dgamma) s.dgamma[c] = (float)((double)S2 * (double)s.save[C + c]);  // sum dz * xhat
-    if (s.dbeta) s.dbeta[c] = S1;
+    ca[j] = s.coef[c0 + j];
+    cb[j] = s.coef[C + c0 + j];
+    cc[j] = s.coef[2 * C + c0 + j];
   }
 }
 
@@ -624,7 +593,6 @@ __global__ __launch_bounds__(kB) void bn_dx_kernel(const T* __restrict__ dy, con
   const int64_t stride = (int64_t)gridDim.x * kB;
   int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x;
   const int cg = (int)(i % tpr);
-  put_dgamma(cs, C);
   float ca[8], cb[8], cc[8], rsc[8], rsh[8];
   get_coef(cs, C, cg * 8, ca, cb, cc);
 #pragma unroll
@@ -664,7 +632,6 @@ __global__ __launch_bounds__(kB) void bn_dx_dz_kernel(const T* __restrict__ dz, 
   const int64_t stride = (int64_t)gridDim.x * kB;
   int64_t i = (int64_t)blockIdx.x * kB + threadIdx.x;
   const int cg = (int)(i % tpr);
-  put_dgamma(cs, C);
   float ca[8], cb[8], cc[8];
   get_coef(cs, C, cg * 8, ca, cb, cc);
   for (; i < n_vec; i += stride) {
@@ -1472,9 +1439,9 @@ bool bn_deterministic_env() {
 }
 
 CoefSrc coef_src(const GradOut& o, int64_t M, bool atomic) {
-  (void)atomic;  // both modes' finishers write coef (the per-thread derivation from the totals,
-                 // measured slow, stays available through CoefSrc.coef == nullptr)
-  return CoefSrc{o.coef, o.save, o.gamma, o.dgamma, o.dbeta, 1.0 / (double)M};
+  (void)M;
+  (void)atomic;  // both modes' finishers write coef
+  return CoefSrc{o.coef, o.save};
 }
 
 float* atot_of(const GradOut& o, int C, bool atomic) {
