@@ -702,7 +702,7 @@ __global__ __launch_bounds__(kB) void bias_act_bwd_kernel(const T* __restrict__ 
       one(d, v, dz + e);
     }
   });
-  if (!block_reduce_tree(R, s, s)) return;
+  if (!block_reduce_tree(R, s, s, R.ftot)) return;  // atomic totals (self-cleaning slot) or the tree
   const double* total = R.total + (size_t)blockIdx.y * 2 * R.CT;
   for (int cl = threadIdx.x; cl < R.CT; cl += kB) dbias[blockIdx.y * R.CT + cl] = (float)total[cl];
 }
@@ -1646,7 +1646,8 @@ template <typename T>
 void bias_bwd_t(const T* dy, const T* y, int64_t M, int C, bool relu, float* dbias, float* ws, T* dz,
                 hipStream_t stream) {
   Red R = plan(M, C);
-  bind_ws(R, ws, stream);
+  // the bias gradient's blocks meet in the slot's self-cleaning atomic totals, like the BN backward
+  bind_ws(R, ws, stream, !bn_deterministic_env() && plan(M, C).nchunks <= bn_atomic_max_chunks());
   const dim3 grid(R.nchunks, C / R.CT);
   if (relu)
     hipLaunchKernelGGL((bias_act_bwd_kernel<T, true>), grid, dim3(kB), 0, stream, dy, y, dz, R, dbias);
