@@ -18,6 +18,7 @@ maximum elapsed time over ranks is used.  Rank 0 prints one JSON line.
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -195,15 +196,21 @@ def main():
             else:
                 comm_kind = "torch (native comm failed)"
     grc = grace_from_params(dict(w.grace, world_size=world))
-    ddp_state = None
+    ddp_state = ddp_stream = None
     if args.surface == "ddp":
         from grace_amd.parallel import GraceHookState, grace_comm_hook
 
         if weights is not None:
             raise SystemExit("--surface ddp trains fp32 masters directly (use --bf16-weights off)")
-        model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], bucket_cap_mb=args.bucket_mb,
-                                                          gradient_as_bucket_view=True)
-        ddp_state = GraceHookState(grc)
+        # buffers (BN running statistics) are broadcast once at start like the engine path and the
+        # reference's Horovod harness, not before every forward
+        # a captured DDP step: the reducer's AccumulateGrad nodes take the stream current at
+        # construction, so build DDP under the stream the step is captured and replayed on
+        ddp_stream = torch.cuda.Stream(dev) if mode == "full" else None
+        with torch.cuda.stream(ddp_stream) if ddp_stream is not None else contextlib.nullcontext():
+            model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], bucket_cap_mb=args.bucket_mb,
+                                                              gradient_as_bucket_view=True, broadcast_buffers=False)
+        ddp_state = GraceHookState(grc, model=model)
         model.register_comm_hook(ddp_state, grace_comm_hook)
 
         class _DdpOpt:  # the bench loop's optimizer interface over DDP + a plain optimizer
@@ -245,7 +252,10 @@ def main():
     run = step
     try:
         if mode == "full":
-            run = GraphedStep(step, warmup=max(3, args.warmup // 2),
+            # DDP records runtime-logging events (and reads them back with a host sync) in its
+            # first 10 iterations: capture only after those
+            cap_warm = max(3, args.warmup // 2) if args.surface == "engine" else max(11, args.warmup)
+            run = GraphedStep(step, warmup=cap_warm, stream=ddp_stream,
                               capture_error_mode="thread_local" if world > 1 else "global")
             graph_note = "full"
         elif mode == "compute":
@@ -253,6 +263,9 @@ def main():
                 fwd_model = graph_compute(model, data[0], engine=opt.engine)
             graph_note = "compute"
     except Exception as e:  # capture unsupported -> stay eager
+        import traceback
+
+        traceback.print_exc(file=sys.stderr)
         graph_note = f"failed: {type(e).__name__}: {str(e)[:120]}"
         torch.cuda.synchronize()
         opt.abort_step()  # a capture that raised mid-backward leaves buckets half launched

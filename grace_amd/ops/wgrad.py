@@ -119,8 +119,12 @@ class fork:
         self.main = None
         self.ev = None
         # a parameter that already holds a .grad gets the new one ADDED by AccumulateGrad on the
-        # current stream right after this backward returns (before any join): stay in line
-        if _ENABLED and t.is_cuda and (param is None or param.grad is None):
+        # current stream right after this backward returns (before any join): stay in line.  So
+        # does a parameter whose gradient a DistributedDataParallel reducer consumes (marked by
+        # parallel/ddp_hook.py): the reducer reads it from its AccumulateGrad hook, mid-backward,
+        # on the current stream -- before any join could order it after the side stream
+        if (_ENABLED and t.is_cuda and (param is None or param.grad is None)
+                and not getattr(param, "_grace_ddp", False)):
             self.main = torch.cuda.current_stream(t.device)
             self.ev = torch.cuda.Event()
             self.ev.record(self.main)

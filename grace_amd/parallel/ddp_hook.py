@@ -31,10 +31,23 @@ from ..core import Communicator, register_layout
 from ..ops.layout import SegmentLayout
 
 
+def mark_ddp_params(params) -> None:
+    """Weight gradients of these parameters are computed in line (ops/wgrad.py): DDP's reducer
+    reads each gradient from its AccumulateGrad hook, during backward, on the current stream."""
+    for p in params:
+        p._grace_ddp = True
+
+
 class GraceHookState:
-    def __init__(self, grc: Communicator, name: str = "ddp"):
+    def __init__(self, grc: Communicator, name: str = "ddp", model: Optional[torch.nn.Module] = None):
+        """``model``: the DistributedDataParallel module the hook is registered on -- pass it so
+        its parameters are marked before the first backward (otherwise they are marked by the
+        hook's first call, and the first backward may compute weight gradients on a side stream
+        that the reducer does not wait for)."""
         self.grc = grc
         self.name = name
+        if model is not None:
+            mark_ddp_params(model.parameters())
         # bucket index -> (layout, packed index or None, buffer numel, GRACE name, param signature)
         self.layouts: Dict[int, tuple] = {}
         self.streams: Dict[int, Tuple[torch.cuda.Stream, torch.cuda.Stream]] = {}
@@ -50,6 +63,7 @@ class GraceHookState:
         buf = bucket.buffer()
         params = bucket.parameters()
         sig = tuple(id(p) for p in params)
+        mark_ddp_params(params)
         ent = self.layouts.get(idx)
         if ent is None or ent[2] != buf.numel() or ent[4] != sig:
             from ..ops.randomk import fnv1a64
@@ -71,6 +85,12 @@ class GraceHookState:
             key = f"{self.name}.b{idx}.{fnv1a64(shapes.encode()):016x}.g{self._gen[idx]}"
             register_layout(key, lay)
             self._migrate(key, params, lay)
+            # with gradient_as_bucket_view DDP makes each .grad a view of the bucket: mark those views
+            # as the parameters' gradient targets, so weight-gradient producers (ops/wgrad.py) write
+            # straight into the bucket (in line) and the reducer finds an alias instead of copying
+            for p, g in zip(params, grads):
+                if p.grad is not None and p.grad.data_ptr() == g.data_ptr() and p.grad.shape == g.shape:
+                    p._grace_grad_view = g
             ent = (lay, pidx, buf.numel(), key, sig)
             self.layouts[idx] = ent
         return ent[3], ent[1]

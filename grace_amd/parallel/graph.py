@@ -71,11 +71,16 @@ class GraphedStep:
     """
 
     def __init__(self, fn: Callable[[], torch.Tensor], warmup: int = 3, pool=None,
-                 capture_error_mode: str = "global", copies: Optional[int] = None):
+                 capture_error_mode: str = "global", copies: Optional[int] = None,
+                 stream: Optional[torch.cuda.Stream] = None):
         import os
 
         self.fn = fn
-        side = torch.cuda.Stream()
+        # ``stream``: warm up, capture and replay on this stream.  Needed when long-lived autograd
+        # nodes were created under it -- DDP's reducer keeps the parameters' AccumulateGrad nodes,
+        # which run on the stream current at DDP's construction; a capture on any other stream
+        # would see them on a non-capturing stream
+        side = stream if stream is not None else torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             for _ in range(warmup):
@@ -91,7 +96,7 @@ class GraphedStep:
         # GRACE_GRAPH_PRIORITY=-1: capture and replay on a high-priority stream (the compute
         # stream of the step then outranks the side streams it forks)
         prio = int(os.environ.get("GRACE_GRAPH_PRIORITY", "0"))
-        self.stream = torch.cuda.Stream(priority=prio) if prio else None
+        self.stream = stream if stream is not None else (torch.cuda.Stream(priority=prio) if prio else None)
         self.graphs = []
         self.losses = []
         for i in range(max(1, copies)):
