@@ -153,7 +153,9 @@ def main():
 
     mode = args.graph
     if args.surface == "ddp" and mode == "auto":
-        mode = "off"  # DDP's reducer is not captured by default (--graph full to try)
+        # the whole DDP step (reducer + comm hook) captures: 2341 vs 2309 img/s eager
+        # (profiles/r3_ddp_surface.txt); a failed capture falls back to eager below
+        mode = "off" if (gloo and world > 1) else "full"
     if mode == "auto":
         # measured on MI355X (ResNet-50 Top-K 1%): full 3205 img/s, compute 2640, eager 2520-3240
         # (eager is host-launch bound: ~1100 kernels per step); full without overlap 3525

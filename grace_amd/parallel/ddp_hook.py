@@ -56,6 +56,7 @@ class GraceHookState:
         # id(param) -> (GRACE bucket name, flat offset, numel, layout total) of its current bucket
         self._loc: Dict[int, Tuple[str, int, int, int]] = {}
         self._gen: Dict[int, int] = {}
+        self._views: Dict[int, int] = {}  # bucket index -> buffer address its gradient targets point into
 
     def layout_for(self, bucket) -> Tuple[str, Optional[torch.Tensor]]:
         """(registered layout name, None | int64 index of the packed elements in the buffer)."""
@@ -85,14 +86,17 @@ class GraceHookState:
             key = f"{self.name}.b{idx}.{fnv1a64(shapes.encode()):016x}.g{self._gen[idx]}"
             register_layout(key, lay)
             self._migrate(key, params, lay)
-            # with gradient_as_bucket_view DDP makes each .grad a view of the bucket: mark those views
-            # as the parameters' gradient targets, so weight-gradient producers (ops/wgrad.py) write
-            # straight into the bucket (in line) and the reducer finds an alias instead of copying
-            for p, g in zip(params, grads):
-                if p.grad is not None and p.grad.data_ptr() == g.data_ptr() and p.grad.shape == g.shape:
-                    p._grace_grad_view = g
             ent = (lay, pidx, buf.numel(), key, sig)
             self.layouts[idx] = ent
+        if self._views.get(idx) != buf.data_ptr():  # new layout, or DDP rebuilt the same one
+            self._views[idx] = buf.data_ptr()
+            # with gradient_as_bucket_view DDP makes each .grad a view of the bucket: mark those
+            # views as the parameters' gradient targets, so weight-gradient producers
+            # (ops/wgrad.py) write straight into the bucket (in line) and the reducer finds an
+            # alias instead of copying
+            for p, g in zip(params, bucket.gradients()):
+                if p.grad is not None and p.grad.data_ptr() == g.data_ptr() and p.grad.shape == g.shape:
+                    p._grace_grad_view = g
         return ent[3], ent[1]
 
     def _containers(self):

@@ -340,3 +340,26 @@ def _ddp_randomk_body(rank, world):
 
 def test_ddp_hook_randomk_shared_indices_gloo():
     run_distributed(_ddp_randomk_body, 2)
+
+
+def _ddp_views_body(rank, world):
+    from grace_amd import grace_from_params
+    from grace_amd.parallel import GraceHookState, grace_comm_hook
+
+    m = _model(seed=0)
+    ddp = nn.parallel.DistributedDataParallel(m, bucket_cap_mb=0.002, gradient_as_bucket_view=True)
+    st = GraceHookState(grace_from_params({"compressor": "none", "world_size": world}), model=ddp)
+    ddp.register_comm_hook(st, grace_comm_hook)
+    assert all(getattr(p, "_grace_ddp", False) for p in m.parameters())  # marked before any backward
+    opt = torch.optim.SGD(ddp.parameters(), lr=0.05)
+    for s in range(3):  # DDP rebuilds its buckets after the first iteration
+        x, y = _batch(rank, s)
+        opt.zero_grad(set_to_none=True)
+        F.cross_entropy(ddp(x), y).backward()
+        opt.step()
+    for p in m.parameters():  # the gradient targets are the CURRENT bucket views
+        assert p._grace_grad_view.data_ptr() == p.grad.data_ptr()
+
+
+def test_ddp_hook_marks_current_bucket_views_gloo():
+    run_distributed(_ddp_views_body, 2)
