@@ -88,16 +88,26 @@ __device__ __forceinline__ uint32_t sk_key(float v) {  // ascending order-preser
 // this pass is VALU-issue bound, a per-element binary search was 4x slower.  Bin codes are
 // stored 4 per 4/8-B store; per-bin sums / counts in per-wave LDS copies, folded once per
 // workgroup into one global atomic per bin.
+//
+// Means finisher (means != nullptr): sums / counts / arrive are a persistent zeroed workspace; every
+// workgroup adds its bin totals, then counts itself in arrive[seg]; the segment's last workgroup
+// turns the totals into the bin means (0 for an empty bin) and re-zeroes the workspace for the next
+// call -- no separate zero-fills and no elementwise mean kernels.  Dynamic LDS: per-wave sums and
+// counts of the q bins (NW * q * 8 B).
 template <typename BinT>
 __global__ __launch_bounds__(kBlock) void sketch_encode_kernel(ChunkTable ct, const float* __restrict__ x,
                                                                const float* __restrict__ edges, int q,
                                                                BinT* __restrict__ bins, float* __restrict__ sums,
-                                                               float* __restrict__ counts) {
+                                                               float* __restrict__ counts, int32_t* __restrict__ arrive,
+                                                               const int32_t* __restrict__ seg_chunk_begin,
+                                                               float* __restrict__ means) {
   constexpr int NW = kBlock / kWave;
   __shared__ float le[kMaxQ + 2];
   __shared__ uint16_t start[2048];
-  __shared__ float ls[NW][kMaxQ];
-  __shared__ uint32_t lc[NW][kMaxQ];
+  __shared__ int last;
+  extern __shared__ __align__(16) uint32_t sk_dyn[];
+  float* ls_all = reinterpret_cast<float*>(sk_dyn);  // [NW][q]
+  uint32_t* lc_all = sk_dyn + NW * q;                // [NW][q]
   const int c = blockIdx.x;
   const int sg = ct.seg[c];
   const int64_t b = ct.begin[c], e = ct.end[c];
@@ -105,8 +115,8 @@ __global__ __launch_bounds__(kBlock) void sketch_encode_kernel(ChunkTable ct, co
   for (int i = threadIdx.x; i <= q; i += kBlock) le[i] = E[i];
   if (threadIdx.x == 0) le[q + 1] = __int_as_float(0x7fc00000);  // NaN sentinel: `<= v` is false
   for (int i = threadIdx.x; i < NW * q; i += kBlock) {
-    ls[i / q][i % q] = 0.f;
-    lc[i / q][i % q] = 0u;
+    ls_all[i] = 0.f;
+    lc_all[i] = 0u;
   }
   __syncthreads();
   for (int d = threadIdx.x; d < 2048; d += kBlock) {  // lower bound of bucket d among the edge keys
@@ -122,8 +132,8 @@ __global__ __launch_bounds__(kBlock) void sketch_encode_kernel(ChunkTable ct, co
     start[d] = (uint16_t)l;
   }
   __syncthreads();
-  float* wls = ls[wave_id()];
-  uint32_t* wlc = lc[wave_id()];
+  float* wls = ls_all + wave_id() * q;
+  uint32_t* wlc = lc_all + wave_id() * q;
   auto bin_of = [&](float v) {
     int cnt = start[sk_key(v) >> 21];
     while (le[cnt] <= v) ++cnt;  // stops at the NaN sentinel (index q + 1) at the latest
@@ -185,14 +195,37 @@ __global__ __launch_bounds__(kBlock) void sketch_encode_kernel(ChunkTable ct, co
     uint32_t cv = 0;
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
-      sv += ls[w][i];
-      cv += lc[w][i];
+      sv += ls_all[w * q + i];
+      cv += lc_all[w * q + i];
     }
     if (cv != 0) {
-      atomicAdd(&sums[(int64_t)sg * q + i], sv);
-      atomicAdd(&counts[(int64_t)sg * q + i], (float)cv);
+      __hip_atomic_fetch_add(&sums[(int64_t)sg * q + i], sv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(&counts[(int64_t)sg * q + i], (float)cv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  if (means == nullptr) return;  // block-uniform
+  // hand-off without fences (cdna_hip_programming.md Guideline 16; as bnact.hip arrive()): every
+  // wave drains its no-return atomics, barrier, ONE relaxed agent add; the last block reads the
+  // totals with device-scope loads.  (A __threadfence() here is an L2 write-back per block -- it
+  // flushed the bin codes and made this kernel 1.7x slower.)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int n = seg_chunk_begin[sg + 1] - seg_chunk_begin[sg];
+    last = __hip_atomic_fetch_add(&arrive[sg], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  for (int i = threadIdx.x; i < q; i += kBlock) {
+    float* sp = sums + (int64_t)sg * q + i;
+    float* cp = counts + (int64_t)sg * q + i;
+    const float sv = __hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const float cv = __hip_atomic_load(cp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    means[(int64_t)sg * q + i] = cv > 0.f ? __fdiv_rn(sv, cv) : 0.f;  // torch: where(c > 0, s / c, 0)
+    __hip_atomic_store(sp, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(cp, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(&arrive[sg], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <typename BinT>
@@ -267,12 +300,24 @@ void decode16_sum(const uint8_t* base, int64_t rank_stride, int n_ranks, int64_t
 }
 
 void sketch_encode(const ChunkTable& ct, const float* x, const float* edges, int q, void* bins, int bin_bytes,
-                   float* sums, float* counts, hipStream_t stream) {
+                   float* sums, float* counts, int32_t* arrive, const int32_t* seg_chunk_begin, float* means,
+                   hipStream_t stream) {
   if (ct.n_chunks == 0) return;
+  static bool lds_attr = false;  // q up to 1024: 4 waves x 1024 x 8 B = 32 KB of dynamic LDS
+  if (!lds_attr) {
+    GRACE_HIP_CHECK(hipFuncSetAttribute((const void*)sketch_encode_kernel<uint8_t>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));
+    GRACE_HIP_CHECK(hipFuncSetAttribute((const void*)sketch_encode_kernel<uint16_t>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));
+    lds_attr = true;
+  }
+  const size_t lds = (size_t)(kBlock / kWave) * q * 8;
   if (bin_bytes == 1)
-    sketch_encode_kernel<uint8_t><<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, edges, q, (uint8_t*)bins, sums, counts);
+    sketch_encode_kernel<uint8_t><<<ct.n_chunks, kBlock, lds, stream>>>(ct, x, edges, q, (uint8_t*)bins, sums, counts,
+                                                                        arrive, seg_chunk_begin, means);
   else
-    sketch_encode_kernel<uint16_t><<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, edges, q, (uint16_t*)bins, sums, counts);
+    sketch_encode_kernel<uint16_t><<<ct.n_chunks, kBlock, lds, stream>>>(ct, x, edges, q, (uint16_t*)bins, sums,
+                                                                         counts, arrive, seg_chunk_begin, means);
 }
 
 void sketch_decode(const ChunkTable& ct, const uint8_t* base, int64_t rank_stride, int64_t bins_off, int64_t means_off,

@@ -108,12 +108,15 @@ __global__ __launch_bounds__(kHBlock) void qsel_hist0_kernel(ChunkTable ct, cons
 }
 
 // Count digit D of every element whose known (32 - shift - bits)-bit prefix is one of the
-// segment's slot prefixes.  Slots are found through an open-addressing LDS hash table (4096
-// entries for <= 256 slots: ~1 probe), so the common miss costs a hash, one LDS read and one
-// compare -- these passes are VALU-issue bound, not memory bound, so every instruction per
-// element counts.  Dynamic LDS: [max_slots] prefixes + [max_slots][128] counts.
-constexpr int kHash = 4096;
-__device__ __forceinline__ uint32_t qhash(uint32_t p) { return (p * 0x9E3779B1u) >> 20; }
+// segment's slot prefixes.  Slots are found through an open-addressing LDS hash table (1024
+// entries for <= 256 slots: load <= 1/4, ~1 probe), so the common miss costs a hash, one LDS read
+// and one compare.  Dynamic LDS: [max_slots] prefixes + [max_slots][64] words of two packed 16-bit
+// bin counts (a chunk holds < 65536 elements -- sketch.py clamps GRACE_QSEL_CHUNK -- so a
+// half-word never carries into its neighbour):
+// ~38 KB for q = 64, four 512-thread workgroups per CU -- with 32-bit counts and a 4096-entry
+// table it was 83 KB, one workgroup (8 waves) per CU, and the passes were latency bound.
+constexpr int kHash = 1024;
+__device__ __forceinline__ uint32_t qhash(uint32_t p) { return (p * 0x9E3779B1u) >> 22; }
 
 template <int D>
 __global__ __launch_bounds__(kHBlock) void qsel_hist_kernel(ChunkTable ct, const float* __restrict__ x, int max_slots,
@@ -125,13 +128,13 @@ __global__ __launch_bounds__(kHBlock) void qsel_hist_kernel(ChunkTable ct, const
   extern __shared__ __align__(16) uint32_t dyn[];
   __shared__ int32_t tab[kHash];  // slot + 1, 0 = empty
   uint32_t* up = dyn;
-  int32_t* lh = reinterpret_cast<int32_t*>(dyn + max_slots);
+  uint32_t* lh = dyn + max_slots;  // [slot][64] packed 16-bit pairs
   const int seg = ct.seg[blockIdx.x];
   const int nu = nuniq[seg];
   if (nu == 0) return;  // block-uniform
   const uint32_t* su = uniq + (int64_t)seg * max_slots;
   for (int i = threadIdx.x; i < kHash; i += kHBlock) tab[i] = 0;
-  for (int i = threadIdx.x; i < nu * 128; i += kHBlock) lh[i] = 0;
+  for (int i = threadIdx.x; i < nu * 64; i += kHBlock) lh[i] = 0u;
   __syncthreads();
   for (int sl = threadIdx.x; sl < nu; sl += kHBlock) {
     const uint32_t p = su[sl];
@@ -148,7 +151,8 @@ __global__ __launch_bounds__(kHBlock) void qsel_hist_kernel(ChunkTable ct, const
     int32_t ent = tab[idx];
     while (ent != 0) {
       if (up[ent - 1] == p) {
-        atomicAdd(&lh[(ent - 1) * 128 + ((k >> shift) & 127)], 1);
+        const uint32_t d = (k >> shift) & 127;
+        atomicAdd(&lh[(ent - 1) * 64 + (d >> 1)], 1u << ((d & 1) << 4));
         return;
       }
       idx = (idx + 1) & (kHash - 1);
@@ -180,9 +184,10 @@ __global__ __launch_bounds__(kHBlock) void qsel_hist_kernel(ChunkTable ct, const
   }
   __syncthreads();
   int32_t* gh = h + (int64_t)seg * max_slots * 128;
-  for (int i = threadIdx.x; i < nu * 128; i += kHBlock) {
-    const int32_t n = lh[i];
-    if (n) atomicAdd(&gh[i], n);
+  for (int i = threadIdx.x; i < nu * 64; i += kHBlock) {
+    const uint32_t n = lh[i];
+    if (n & 0xffffu) atomicAdd(&gh[2 * i], (int32_t)(n & 0xffffu));
+    if (n >> 16) atomicAdd(&gh[2 * i + 1], (int32_t)(n >> 16));
   }
 }
 
@@ -305,7 +310,7 @@ void quantile_select(const ChunkTable& ct, int n_seg, const float* x, int max_sl
   static bool lds_attr = false;  // > 64 KB of dynamic LDS has to be opted into per kernel
   if (!lds_attr) {
     const int mx = 150 * 1024;
-    const int mxh = 140 * 1024;  // + 16 KB static hash table <= 160 KB; max_slots <= 256 needs 132 KB
+    const int mxh = 140 * 1024;  // + 4 KB static hash table <= 160 KB; max_slots <= 256 needs 66 KB
     GRACE_HIP_CHECK(hipFuncSetAttribute((const void*)qsel_hist_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, mxh));
     GRACE_HIP_CHECK(hipFuncSetAttribute((const void*)qsel_hist_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, mxh));
     GRACE_HIP_CHECK(hipFuncSetAttribute((const void*)qsel_hist_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, mxh));
@@ -314,7 +319,7 @@ void quantile_select(const ChunkTable& ct, int n_seg, const float* x, int max_sl
     GRACE_HIP_CHECK(hipFuncSetAttribute((const void*)qsel_select_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, mx));
     lds_attr = true;
   }
-  const size_t hist_lds = (size_t)max_slots * (sizeof(uint32_t) + 128 * sizeof(int32_t));
+  const size_t hist_lds = (size_t)max_slots * (sizeof(uint32_t) + 64 * sizeof(uint32_t));
   const size_t cum_lds = (size_t)max_slots * 128 * sizeof(int32_t);
   if (ct.n_chunks > 0) qsel_hist0_kernel<<<ct.n_chunks, kHBlock, 0, stream>>>(ct, x, h0);
   qsel_select_kernel<0><<<n_seg, kSelBlock, 2048 * sizeof(int32_t), stream>>>(

@@ -56,7 +56,8 @@ import os as _os
 
 # elements per workgroup of the selection passes (LDS setup amortised) and of encode / decode
 # (per-workgroup LDS bin tables amortised); env-tunable for sweeps on the GPU box
-_QSEL_CHUNK = int(_os.environ.get("GRACE_QSEL_CHUNK", 32768))
+# (< 65536: the selection histograms pack two 16-bit bin counts per LDS word)
+_QSEL_CHUNK = min(int(_os.environ.get("GRACE_QSEL_CHUNK", 32768)), 65535)
 _CODEC_CHUNK = int(_os.environ.get("GRACE_CODEC_CHUNK", 8192))
 
 
@@ -168,11 +169,15 @@ class SketchCompressor(BucketCompressor):
         bins, means = self.payload(x.device, [(bdt, (lay.total,)), (torch.float32, (q * lay.n_seg,))])
         if _native.use_native(x) and q <= 1024:
             edges = native_quantile_edges(x, lay, q)
-            sums = torch.zeros(lay.n_seg * q, device=x.device)
-            cnts = torch.zeros(lay.n_seg * q, device=x.device)
             t = lay.device_tables(x.device, _CODEC_CHUNK)
-            _native.lib().sketch_encode(x, edges, q, bins, sums, cnts, t["seg"], t["begin"], t["end"])
-            torch.where(cnts > 0, sums / cnts.clamp_min(1), torch.zeros_like(sums), out=means)
+            # persistent, self-cleaning totals: the segment's last encode block writes the means and
+            # re-zeroes them (no fills, no elementwise mean kernels)
+            ws = lay.cached(x.device, f"sketch_ws:{q}", lambda: {
+                "sums": torch.zeros(lay.n_seg * q, device=x.device),
+                "cnts": torch.zeros(lay.n_seg * q, device=x.device),
+                "arrive": torch.zeros(lay.n_seg, dtype=torch.int32, device=x.device)})
+            _native.lib().sketch_encode(x, edges, q, bins, ws["sums"], ws["cnts"], t["seg"], t["begin"], t["end"],
+                                        ws["arrive"], t["seg_chunk_begin"], means)
             return [bins, means], ctx
         # edges at float64 quantile positions j (n-1) / q (the native select's exact ranks and
         # weights: fp32 positions mis-round for q not a power of two)

@@ -5,8 +5,12 @@ Separates per-element cost (LDS bin search + LDS atomics) from per-workgroup set
 global-atomic contention on the per-segment totals: the same 25.5 M N(0,1) elements split as
 ResNet-50's per-parameter segments, as ONE segment (every workgroup adds into the same q totals),
 and as equal 64 K segments.  Prints one line per configuration: us per encode call."""
+import os
+import sys
+
 import torch
 
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
 from grace_amd.compressor.sketch import native_quantile_edges
 from grace_amd.models.resnet import resnet50
 from grace_amd.ops import _native
