@@ -584,39 +584,31 @@ void decode16_sum(const Tensor& base, int64_t rank_stride, int64_t n_ranks, bool
                       out.data_ptr<float>(), cur_stream());
 }
 
-// means given: sums / counts / arrive ([n_seg] int32, seg_chunk_begin [n_seg + 1]) are a persistent
-// workspace that is zero on entry and left zero; the last block of every segment writes its means
+// sums (int64, fixed point) / counts (int32) [n_seg * q] and arrive (int32 [n_seg]) are a persistent
+// workspace that is zero on entry and left zero; seg_chunk_begin [n_seg + 1]; the last block of
+// every segment writes its means
 void sketch_encode(const Tensor& x, const Tensor& edges, int64_t q, const Tensor& bins, const Tensor& sums,
-                   const Tensor& counts, const Tensor& seg, const Tensor& cb, const Tensor& ce,
-                   const c10::optional<Tensor>& arrive, const c10::optional<Tensor>& seg_chunk_begin,
-                   const c10::optional<Tensor>& means) {
+                   const Tensor& counts, const Tensor& seg, const Tensor& cb, const Tensor& ce, const Tensor& arrive,
+                   const Tensor& seg_chunk_begin, const Tensor& means) {
   CHECK_F32(x);
   CHECK_F32(edges);
-  CHECK_F32(sums);
-  CHECK_F32(counts);
+  CHECK_F32(means);
   CHECK_DEV(bins);
   TORCH_CHECK(q >= 1 && q <= 1024, "quantiles must be in [1, 1024]");
   TORCH_CHECK(bins.numel() >= x.numel(), "bins too small");
+  TORCH_CHECK(sums.scalar_type() == at::kLong && counts.scalar_type() == at::kInt && arrive.scalar_type() == at::kInt &&
+                  seg_chunk_begin.scalar_type() == at::kInt,
+              "sketch_encode: int64 sums, int32 counts / arrive / seg_chunk_begin");
+  const int64_t n_seg = seg_chunk_begin.numel() - 1;
+  TORCH_CHECK(arrive.numel() >= n_seg && means.numel() >= n_seg * q && sums.numel() >= n_seg * q &&
+                  counts.numel() >= n_seg * q && edges.numel() >= n_seg * (q + 1),
+              "sketch_encode: tables too small");
   auto ct = make_ct(seg, cb, ce);
-  int32_t* ap = nullptr;
-  const int32_t* scb = nullptr;
-  float* mp = nullptr;
-  if (means.has_value()) {
-    TORCH_CHECK(arrive.has_value() && seg_chunk_begin.has_value(), "means finisher needs arrive and seg_chunk_begin");
-    CHECK_F32(*means);
-    TORCH_CHECK(arrive->scalar_type() == at::kInt && seg_chunk_begin->scalar_type() == at::kInt, "int32 tables");
-    const int64_t n_seg = seg_chunk_begin->numel() - 1;
-    TORCH_CHECK(arrive->numel() >= n_seg && means->numel() >= n_seg * q && sums.numel() >= n_seg * q &&
-                    counts.numel() >= n_seg * q,
-                "sketch finisher tables too small");
-    ap = arrive->data_ptr<int32_t>();
-    scb = seg_chunk_begin->data_ptr<int32_t>();
-    mp = means->data_ptr<float>();
-  }
   DevGuard guard(x.device());
   grace::sketch_encode(ct, x.data_ptr<float>(), edges.data_ptr<float>(), (int)q, bins.data_ptr(),
-                       (int)bins.element_size(), sums.data_ptr<float>(), counts.data_ptr<float>(), ap, scb, mp,
-                       cur_stream());
+                       (int)bins.element_size(), reinterpret_cast<unsigned long long*>(sums.data_ptr<int64_t>()),
+                       reinterpret_cast<uint32_t*>(counts.data_ptr<int32_t>()), arrive.data_ptr<int32_t>(),
+                       seg_chunk_begin.data_ptr<int32_t>(), means.data_ptr<float>(), cur_stream());
 }
 
 void sketch_decode(const Tensor& base, int64_t rank_stride, int64_t bins_off, int64_t means_off, int64_t q,
@@ -996,9 +988,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("philox_normal", &philox_normal);
   m.def("cast16", &cast16);
   m.def("decode16_sum", &decode16_sum);
-  m.def("sketch_encode", &sketch_encode, py::arg("x"), py::arg("edges"), py::arg("q"), py::arg("bins"),
-        py::arg("sums"), py::arg("counts"), py::arg("seg"), py::arg("begin"), py::arg("end"),
-        py::arg("arrive") = py::none(), py::arg("seg_chunk_begin") = py::none(), py::arg("means") = py::none());
+  m.def("sketch_encode", &sketch_encode);
   m.def("sketch_decode", &sketch_decode);
   m.def("quantile_select", &quantile_select);
   m.def("gemm_f32", &gemm_f32, py::arg("A"), py::arg("a_kc"), py::arg("lda"), py::arg("B"), py::arg("b_kc"),

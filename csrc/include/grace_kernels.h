@@ -116,8 +116,8 @@ void cast16(const float* x, uint16_t* y, int64_t n, bool bf16, hipStream_t strea
 void decode16_sum(const uint8_t* base, int64_t rank_stride, int n_ranks, int64_t n, bool bf16, float scale, float* out,
                   hipStream_t stream);
 void sketch_encode(const ChunkTable& ct, const float* x, const float* edges, int q, void* bins, int bin_bytes,
-                   float* sums, float* counts, int32_t* arrive, const int32_t* seg_chunk_begin, float* means,
-                   hipStream_t stream);
+                   unsigned long long* sums, uint32_t* counts, int32_t* arrive, const int32_t* seg_chunk_begin,
+                   float* means, hipStream_t stream);
 void sketch_decode(const ChunkTable& ct, const uint8_t* base, int64_t rank_stride, int64_t bins_off, int64_t means_off,
                    int q, int bin_bytes, int n_ranks, float scale, float* out, hipStream_t stream);
 

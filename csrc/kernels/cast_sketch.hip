@@ -80,45 +80,64 @@ __device__ __forceinline__ uint32_t sk_key(float v) {  // ascending order-preser
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
-// bins: uint8 (q <= 256) or uint16; edges: [n_seg][q+1]; sums/counts: [n_seg][q] (zeroed).
+// bins: uint8 (q <= 256) or uint16; edges: [n_seg][q+1].
 // Bin = (#edges <= v) - 1 clamped to [0, q-1] (torch.searchsorted(right=True) - 1).  The edges
 // are staged in LDS with a 2048-entry table over the top 11 bits of the order-preserving key:
 // start[d] = #edges whose key is below bucket d, so an element only scans the few edges inside
-// its own bucket (quantile edges spread over the value range: ~1-2 per populated bucket) --
-// this pass is VALU-issue bound, a per-element binary search was 4x slower.  Bin codes are
-// stored 4 per 4/8-B store; per-bin sums / counts in per-wave LDS copies, folded once per
-// workgroup into one global atomic per bin.
+// its own bucket (quantile edges spread over the value range: ~1-2 per populated bucket) -- a
+// per-element binary search was 4x slower.  Bin codes are stored 4 per 4/8-B store.
 //
-// Means finisher (means != nullptr): sums / counts / arrive are a persistent zeroed workspace; every
-// workgroup adds its bin totals, then counts itself in arrive[seg]; the segment's last workgroup
-// turns the totals into the bin means (0 for an empty bin) and re-zeroes the workspace for the next
-// call -- no separate zero-fills and no elementwise mean kernels.  Dynamic LDS: per-wave sums and
-// counts of the q bins (NW * q * 8 B).
+// Bin sums in FIXED POINT with integer LDS atomics: an LDS fp32 atomic add (ds_add_f32) costs
+// ~25x an integer one on gfx950 -- measured with tools/diag/sketch_encode_probe.py on ResNet-50's
+// 25.5 M elements: 178 us with fp32 bin sums, 61 us without them, 171 us without the u32 counts.
+// Every value of bin j lies between edges j and j+1, so |v| <= M_j = max(|e_j|, |e_j+1|) < 2^E_j;
+// with 2^L >= the segment's size, v * 2^(62 - L - E_j) rounded to int64 sums over the whole
+// segment without overflow, at a resolution of 2^-50 (or finer) of the bin's magnitude -- finer
+// than an fp32 accumulation, and order-independent: the means are deterministic.  Per-wave LDS
+// copies of the q sums (u64) and counts (u32), folded once per workgroup into one global integer
+// atomic per bin.
+//
+// Means finisher: sums / counts / arrive are a persistent zeroed workspace; every workgroup adds
+// its bin totals, then counts itself in arrive[seg]; the segment's last workgroup turns the totals
+// into the bin means (0 for an empty bin) and re-zeroes the workspace for the next call -- no
+// zero-fills and no elementwise mean kernels.  (Non-finite edges -- a gradient holding inf/NaN --
+// give meaningless means, as any average of such a segment is.)
 template <typename BinT>
 __global__ __launch_bounds__(kBlock) void sketch_encode_kernel(ChunkTable ct, const float* __restrict__ x,
                                                                const float* __restrict__ edges, int q,
-                                                               BinT* __restrict__ bins, float* __restrict__ sums,
-                                                               float* __restrict__ counts, int32_t* __restrict__ arrive,
+                                                               BinT* __restrict__ bins,
+                                                               unsigned long long* __restrict__ sums,
+                                                               uint32_t* __restrict__ counts, int32_t* __restrict__ arrive,
                                                                const int32_t* __restrict__ seg_chunk_begin,
                                                                float* __restrict__ means) {
   constexpr int NW = kBlock / kWave;
   __shared__ float le[kMaxQ + 2];
   __shared__ uint16_t start[2048];
   __shared__ int last;
-  extern __shared__ __align__(16) uint32_t sk_dyn[];
-  float* ls_all = reinterpret_cast<float*>(sk_dyn);  // [NW][q]
-  uint32_t* lc_all = sk_dyn + NW * q;                // [NW][q]
+  extern __shared__ __align__(16) unsigned long long sk_dyn[];
+  unsigned long long* ls_all = sk_dyn;                                    // [NW][q] fixed-point sums
+  double* scale = reinterpret_cast<double*>(sk_dyn + NW * q);            // [q] 2^(62 - L - E_j)
+  uint32_t* lc_all = reinterpret_cast<uint32_t*>(sk_dyn + NW * q + q);   // [NW][q] counts
   const int c = blockIdx.x;
   const int sg = ct.seg[c];
   const int64_t b = ct.begin[c], e = ct.end[c];
+  const int c0 = seg_chunk_begin[sg], c1 = seg_chunk_begin[sg + 1];
+  const int64_t nseg = ct.end[c1 - 1] - ct.begin[c0];
+  const int L = nseg > 1 ? 64 - __clzll((unsigned long long)(nseg - 1)) : 0;  // 2^L >= nseg
   const float* E = edges + (int64_t)sg * (q + 1);
   for (int i = threadIdx.x; i <= q; i += kBlock) le[i] = E[i];
   if (threadIdx.x == 0) le[q + 1] = __int_as_float(0x7fc00000);  // NaN sentinel: `<= v` is false
   for (int i = threadIdx.x; i < NW * q; i += kBlock) {
-    ls_all[i] = 0.f;
+    ls_all[i] = 0ull;
     lc_all[i] = 0u;
   }
   __syncthreads();
+  for (int j = threadIdx.x; j < q; j += kBlock) {
+    const float m = fmaxf(fabsf(le[j]), fabsf(le[j + 1]));
+    int ex = 0;
+    if (m > 0.f && isfinite(m)) frexpf(m, &ex);  // m = f 2^ex, f in [0.5, 1): every |v| of bin j < 2^ex
+    scale[j] = ldexp(1.0, 62 - L - ex);          // a power of two: exact in double
+  }
   for (int d = threadIdx.x; d < 2048; d += kBlock) {  // lower bound of bucket d among the edge keys
     const uint32_t lo = (uint32_t)d << 21;
     int l = 0, r = q + 1;
@@ -132,7 +151,7 @@ __global__ __launch_bounds__(kBlock) void sketch_encode_kernel(ChunkTable ct, co
     start[d] = (uint16_t)l;
   }
   __syncthreads();
-  float* wls = ls_all + wave_id() * q;
+  unsigned long long* wls = ls_all + wave_id() * q;
   uint32_t* wlc = lc_all + wave_id() * q;
   auto bin_of = [&](float v) {
     int cnt = start[sk_key(v) >> 21];
@@ -140,12 +159,15 @@ __global__ __launch_bounds__(kBlock) void sketch_encode_kernel(ChunkTable ct, co
     const int bb = cnt - 1;
     return bb < 0 ? 0 : (bb > q - 1 ? q - 1 : bb);
   };
+  auto add = [&](int bin, float v) {
+    atomicAdd(&wls[bin], (unsigned long long)__double2ll_rn((double)v * scale[bin]));  // two's complement
+    atomicAdd(&wlc[bin], 1u);
+  };
   auto one = [&](int64_t i) {
     const float v = x[i];
     const int bin = bin_of(v);
     bins[i] = (BinT)bin;
-    atomicAdd(&wls[bin], v);
-    atomicAdd(&wlc[bin], 1u);
+    add(bin, v);
   };
   const int64_t a0 = vec4_begin(x, b, e);
   const int64_t a1 = a0 + ((e - a0) & ~(int64_t)3);
@@ -153,7 +175,7 @@ __global__ __launch_bounds__(kBlock) void sketch_encode_kernel(ChunkTable ct, co
   for (int64_t i = a1 + threadIdx.x; i < e; i += kBlock) one(i);
   const bool vec_bins = ((reinterpret_cast<uintptr_t>(bins + a0)) % (4 * sizeof(BinT))) == 0;
   // 8 x 16 B in flight per thread before any use: one vector at a time left every wave waiting
-  // on HBM latency with ~12 KB in flight per CU (this pass was latency bound, not LDS bound)
+  // on HBM latency with ~12 KB in flight per CU
   constexpr int U = 8;
   for (int64_t i0 = a0 + 4 * (int64_t)threadIdx.x; i0 < a1; i0 += 4 * kBlock * U) {
    float4 xs[U];
@@ -172,8 +194,7 @@ __global__ __launch_bounds__(kBlock) void sketch_encode_kernel(ChunkTable ct, co
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       bn[j] = bin_of(v[j]);
-      atomicAdd(&wls[bn[j]], v[j]);
-      atomicAdd(&wlc[bn[j]], 1u);
+      add(bn[j], v[j]);
     }
     if (vec_bins) {
       if constexpr (sizeof(BinT) == 1) {
@@ -191,7 +212,7 @@ __global__ __launch_bounds__(kBlock) void sketch_encode_kernel(ChunkTable ct, co
   }
   __syncthreads();
   for (int i = threadIdx.x; i < q; i += kBlock) {
-    float sv = 0.f;
+    unsigned long long sv = 0ull;
     uint32_t cv = 0;
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
@@ -200,30 +221,27 @@ __global__ __launch_bounds__(kBlock) void sketch_encode_kernel(ChunkTable ct, co
     }
     if (cv != 0) {
       __hip_atomic_fetch_add(&sums[(int64_t)sg * q + i], sv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_add(&counts[(int64_t)sg * q + i], (float)cv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(&counts[(int64_t)sg * q + i], cv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  if (means == nullptr) return;  // block-uniform
   // hand-off without fences (cdna_hip_programming.md Guideline 16; as bnact.hip arrive()): every
   // wave drains its no-return atomics, barrier, ONE relaxed agent add; the last block reads the
   // totals with device-scope loads.  (A __threadfence() here is an L2 write-back per block -- it
   // flushed the bin codes and made this kernel 1.7x slower.)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const int n = seg_chunk_begin[sg + 1] - seg_chunk_begin[sg];
-    last = __hip_atomic_fetch_add(&arrive[sg], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n - 1;
-  }
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(&arrive[sg], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == c1 - c0 - 1;
   __syncthreads();
   if (!last) return;
   for (int i = threadIdx.x; i < q; i += kBlock) {
-    float* sp = sums + (int64_t)sg * q + i;
-    float* cp = counts + (int64_t)sg * q + i;
-    const float sv = __hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const float cv = __hip_atomic_load(cp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    means[(int64_t)sg * q + i] = cv > 0.f ? __fdiv_rn(sv, cv) : 0.f;  // torch: where(c > 0, s / c, 0)
-    __hip_atomic_store(sp, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(cp, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long* sp = sums + (int64_t)sg * q + i;
+    uint32_t* cp = counts + (int64_t)sg * q + i;
+    const long long sv = (long long)__hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t cv = __hip_atomic_load(cp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    means[(int64_t)sg * q + i] = cv ? (float)((double)sv / scale[i] / (double)cv) : 0.f;
+    __hip_atomic_store(sp, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(cp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (threadIdx.x == 0) __hip_atomic_store(&arrive[sg], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -300,10 +318,10 @@ void decode16_sum(const uint8_t* base, int64_t rank_stride, int n_ranks, int64_t
 }
 
 void sketch_encode(const ChunkTable& ct, const float* x, const float* edges, int q, void* bins, int bin_bytes,
-                   float* sums, float* counts, int32_t* arrive, const int32_t* seg_chunk_begin, float* means,
-                   hipStream_t stream) {
+                   unsigned long long* sums, uint32_t* counts, int32_t* arrive, const int32_t* seg_chunk_begin,
+                   float* means, hipStream_t stream) {
   if (ct.n_chunks == 0) return;
-  static bool lds_attr = false;  // q up to 1024: 4 waves x 1024 x 8 B = 32 KB of dynamic LDS
+  static bool lds_attr = false;  // q up to 1024: 4 waves x 1024 x 12 B + 8 KB of scales = 56 KB of dynamic LDS
   if (!lds_attr) {
     GRACE_HIP_CHECK(hipFuncSetAttribute((const void*)sketch_encode_kernel<uint8_t>,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));
@@ -311,7 +329,8 @@ void sketch_encode(const ChunkTable& ct, const float* x, const float* edges, int
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));
     lds_attr = true;
   }
-  const size_t lds = (size_t)(kBlock / kWave) * q * 8;
+  constexpr int NW = kBlock / kWave;
+  const size_t lds = (size_t)NW * q * 8 + (size_t)q * 8 + (size_t)NW * q * 4;
   if (bin_bytes == 1)
     sketch_encode_kernel<uint8_t><<<ct.n_chunks, kBlock, lds, stream>>>(ct, x, edges, q, (uint8_t*)bins, sums, counts,
                                                                         arrive, seg_chunk_begin, means);

@@ -172,9 +172,10 @@ class SketchCompressor(BucketCompressor):
             t = lay.device_tables(x.device, _CODEC_CHUNK)
             # persistent, self-cleaning totals: the segment's last encode block writes the means and
             # re-zeroes them (no fills, no elementwise mean kernels)
+            # (bin sums in int64 fixed point: csrc/kernels/cast_sketch.hip)
             ws = lay.cached(x.device, f"sketch_ws:{q}", lambda: {
-                "sums": torch.zeros(lay.n_seg * q, device=x.device),
-                "cnts": torch.zeros(lay.n_seg * q, device=x.device),
+                "sums": torch.zeros(lay.n_seg * q, dtype=torch.int64, device=x.device),
+                "cnts": torch.zeros(lay.n_seg * q, dtype=torch.int32, device=x.device),
                 "arrive": torch.zeros(lay.n_seg, dtype=torch.int32, device=x.device)})
             _native.lib().sketch_encode(x, edges, q, bins, ws["sums"], ws["cnts"], t["seg"], t["begin"], t["end"],
                                         ws["arrive"], t["seg_chunk_begin"], means)

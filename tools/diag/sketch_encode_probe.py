@@ -31,6 +31,7 @@ def timed(fn, iters=20):
 
 
 def main():
+    dbg = os.environ.get("GRACE_SKETCH_DBG", "0")  # honoured by builds that have the diagnostic modes
     lib = _native.lib()
     shapes = [p.shape for p in resnet50().parameters()]
     n = sum(torch.Size(s).numel() for s in shapes)
@@ -40,19 +41,22 @@ def main():
         "one_segment": SegmentLayout.from_tensors([torch.empty(n)]),
         "64k_segments": SegmentLayout.from_tensors([torch.empty(65536)] * (n // 65536) + [torch.empty(n % 65536)]),
     }
+    quick = os.environ.get("GRACE_SKETCH_PROBE_QUICK") == "1"  # one configuration (diagnostic sweeps)
+    if quick:
+        layouts = {"resnet50": layouts["resnet50"]}
     for lname, lay in layouts.items():
-        for q in (16, 64):
+        for q in ((64,) if quick else (16, 64)):
             edges = native_quantile_edges(x, lay, q)
             bins = torch.empty(n, dtype=torch.uint8, device="cuda")
             means = torch.empty(lay.n_seg * q, device="cuda")
-            sums = torch.zeros(lay.n_seg * q, device="cuda")
-            cnts = torch.zeros(lay.n_seg * q, device="cuda")
+            sums = torch.zeros(lay.n_seg * q, dtype=torch.int64, device="cuda")
+            cnts = torch.zeros(lay.n_seg * q, dtype=torch.int32, device="cuda")
             arrive = torch.zeros(lay.n_seg, dtype=torch.int32, device="cuda")
-            for chunk in (2048, 8192, 32768):
+            for chunk in ((8192,) if quick else (2048, 8192, 32768)):
                 t = lay.device_tables(x.device, chunk)
                 us = timed(lambda: lib.sketch_encode(x, edges, q, bins, sums, cnts, t["seg"], t["begin"], t["end"],
                                                      arrive, t["seg_chunk_begin"], means))
-                print(f"{lname:13s} q={q:3d} chunk={chunk:6d} blocks={t['n_chunks']:6d}  {us:8.1f} us", flush=True)
+                print(f"dbg={dbg:2s} {lname:13s} q={q:3d} chunk={chunk:6d} blocks={t['n_chunks']:6d}  {us:8.1f} us", flush=True)
 
 
 if __name__ == "__main__":
