@@ -247,15 +247,27 @@ __global__ __launch_bounds__(kSelBlock) void qsel_select_kernel(
   } else {
     const int nu = nuniq[seg];
     int32_t* gh = h + tb * 128;
-    // wave w scans slots w, w + 4, ...: two bins per lane
-    for (int sl = wave_id(); sl < nu; sl += kSelBlock / kWave) {
-      const int l = lane_id();
-      const int32_t c0 = gh[sl * 128 + 2 * l], c1 = gh[sl * 128 + 2 * l + 1];
-      gh[sl * 128 + 2 * l] = 0;
-      gh[sl * 128 + 2 * l + 1] = 0;
-      const int incl = wave_inclusive_scan(c0 + c1);
-      cum[sl * 128 + 2 * l] = incl - c1;  // inclusive counts
-      cum[sl * 128 + 2 * l + 1] = incl;
+    // wave w scans slots w, w + 4, ...: two bins per lane (one 8-B load); the loads of B slots are
+    // issued before any of them is used (one HBM round trip per B slots, not per slot: these
+    // one-workgroup-per-segment kernels are latency bound)
+    constexpr int NWv = kSelBlock / kWave, B = 4;
+    const int l = lane_id();
+    for (int s0 = wave_id(); s0 < nu; s0 += NWv * B) {
+      int2 cc[B];
+#pragma unroll
+      for (int k = 0; k < B; ++k) {
+        const int sl = s0 + k * NWv;
+        cc[k] = sl < nu ? reinterpret_cast<const int2*>(gh + sl * 128)[l] : make_int2(0, 0);
+      }
+#pragma unroll
+      for (int k = 0; k < B; ++k) {
+        const int sl = s0 + k * NWv;
+        if (sl >= nu) break;  // wave-uniform
+        reinterpret_cast<int2*>(gh + sl * 128)[l] = make_int2(0, 0);
+        const int incl = wave_inclusive_scan(cc[k].x + cc[k].y);
+        cum[sl * 128 + 2 * l] = incl - cc[k].y;  // inclusive counts
+        cum[sl * 128 + 2 * l + 1] = incl;
+      }
     }
     __syncthreads();
     if (t < nr) {
