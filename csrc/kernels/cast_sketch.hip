@@ -190,10 +190,23 @@ __global__ __launch_bounds__(kBlock) void sketch_encode_kernel(ChunkTable ct, co
     if (i >= a1) break;
     const float4 v4 = xs[u];
     const float v[4] = {v4.x, v4.y, v4.z, v4.w};
-    int bn[4];
+    // the bucket-table reads and the first edge reads of the four elements are independent LDS
+    // reads issued together; only the (short) scans past the first edge are per element
+    int bn[4], cn[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cn[j] = start[sk_key(v[j]) >> 21];
+    float fe[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fe[j] = le[cn[j]];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      bn[j] = bin_of(v[j]);
+      int cnt = cn[j];
+      if (fe[j] <= v[j]) {
+        ++cnt;
+        while (le[cnt] <= v[j]) ++cnt;  // stops at the NaN sentinel (index q + 1) at the latest
+      }
+      const int bb = cnt - 1;
+      bn[j] = bb < 0 ? 0 : (bb > q - 1 ? q - 1 : bb);
       add(bn[j], v[j]);
     }
     if (vec_bins) {
