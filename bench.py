@@ -152,6 +152,12 @@ def main():
     from grace_amd.parallel.graph import GraphedStep, graph_compute, graph_safe
 
     mode = args.graph
+    # a gloo group cannot capture its collectives, but an ALL-GATHER-only pipeline's exchange can
+    # run on the xGMI one-shot comm (peer memory, gloo only bootstraps it): that is the W > 1
+    # whole-step-graph rehearsal on a 1-GPU box (ranks share the card)
+    gloo_graph = (gloo and world > 1 and args.comm in ("xgmi", "auto") and args.surface == "engine"
+                  and w.grace.get("communicator") == "allgather"
+                  and w.grace.get("compressor") not in ("powersgd",) and w.grace.get("memory") != "dgc")
     if args.surface == "ddp" and mode == "auto":
         # the whole DDP step (reducer + comm hook) captures: 2341 vs 2309 img/s eager
         # (profiles/r3_ddp_surface.txt); a failed capture falls back to eager below
@@ -162,30 +168,52 @@ def main():
         probe = grace_from_params(dict(w.grace, world_size=world))
         mode = "full" if graph_safe(probe) is None else "off"
         del probe
-        if gloo and world > 1:
+        if gloo and world > 1 and not (gloo_graph and mode == "full"):
             mode = "compute"  # gloo collectives cannot be captured
-    if gloo and world > 1 and mode == "full":
-        raise SystemExit("--graph full needs a capturable collective (--backend nccl)")
+    if gloo and world > 1 and mode == "full" and not gloo_graph:
+        raise SystemExit("--graph full with gloo needs an all-gather-only pipeline and --comm xgmi/auto "
+                         "(the exchange on the xGMI one-shot comm); else use --backend nccl")
     if args.no_overlap:
         args.overlap = "off"
     overlap = args.overlap == "on" or (args.overlap == "auto" and mode != "full")
     comm_kind = "local"
+    comm_obj = None
     if dist.is_initialized():
         comm_kind = args.comm
         if comm_kind == "auto":
-            comm_kind = "native-inline" if (mode == "full" and not overlap) else "torch"
+            # whole-step graph without overlap: the in-line native RCCL runtime, wrapped by the
+            # xGMI one-shot comm whose all-gathers pick their path per payload size by a start-up
+            # MEASUREMENT against RCCL's (MAX over ranks; XgmiComm select="probe"); a box where
+            # the peer mapping fails keeps plain RCCL
+            comm_kind = "auto-probe" if (mode == "full" and not overlap) else "torch"
         if gloo:
-            comm_kind = "torch"
+            comm_kind = ("xgmi" if args.comm == "xgmi" else "auto-probe") if (gloo_graph and mode == "full") \
+                else "torch"
         if comm_kind != "torch":
             from grace_amd.parallel import set_default_comm
             from grace_amd.parallel.native_comm import RcclComm
 
             try:
-                native = RcclComm.from_process_group(inline=comm_kind in ("native-inline", "xgmi"))
-                if comm_kind == "xgmi":
+                if gloo:
+                    from grace_amd.parallel.comm import TorchComm
+
+                    native = TorchComm()
+                else:
+                    native = RcclComm.from_process_group(
+                        inline=comm_kind in ("native-inline", "xgmi", "auto-probe"))
+                if comm_kind in ("xgmi", "auto-probe"):
                     from grace_amd.parallel.xgmi import XgmiComm
 
-                    native = XgmiComm(native, capacity_mb=8.0)
+                    try:
+                        native = XgmiComm(native, capacity_mb=8.0,
+                                          select="probe" if comm_kind == "auto-probe" else "size")
+                    except Exception as e:  # every rank raised together (XgmiComm agrees)
+                        if comm_kind == "xgmi" or gloo:
+                            raise
+                        print(f"[rank {rank}] xGMI one-shot comm unavailable ({str(e)[:120]}); RCCL only",
+                              file=sys.stderr, flush=True)
+                        comm_kind = "native-inline (xgmi setup failed)"
+                comm_obj = native
                 ok = 1
             except Exception as e:  # every rank must agree before the first GRACE collective
                 print(f"[rank {rank}] native RCCL comm unavailable ({type(e).__name__}: {str(e)[:120]}); "
@@ -409,7 +437,8 @@ def main():
                 "per_gpu_batch": batch,
                 "seq_len": w.seq_len,
                 "parallelism": f"dp{world}",
-                "backend": "gloo (ranks share GPUs: rehearsal, not a scaling number)" if gloo else "nccl (RCCL)",
+                "backend": ("gloo (ranks share GPUs: rehearsal, not a scaling number)" if gloo else "nccl (RCCL)")
+                if dist.is_initialized() else "none (W=1, no process group: local comm)",
                 "grace": w.grace,
                 "bucket_mb": args.bucket_mb,
                 "overlap": overlap,
@@ -422,8 +451,15 @@ def main():
             },
             "per_gpu": {"mean": round(mean_pg, 2), "ci95": round(1.96 * std_pg, 2),
                         "note": f"{w.unit}/sec per GPU on rank 0, mean +- 1.96 std over {len(per_gpu)} steps"},
-            "exchange_ms": {k.replace("_ms_per_step", ""): round(v, 4) for k, v in split.items()
-                            if k.endswith("_ms_per_step")},
+            "exchange_ms": dict({k.replace("_ms_per_step", ""): round(v, 4) for k, v in split.items()
+                                 if k.endswith("_ms_per_step")},
+                                **({} if dist.is_initialized() else
+                                   {"note": "W=1 without a process group: 'comm' is a local device copy, "
+                                            "not a collective"})),
+            "comm_choice": (list(getattr(comm_obj, "choices", {}).values()) or None) if comm_obj is not None else None,
+            "bn_backward": ("fixed-order fp64 tree (deterministic)" if os.environ.get("GRACE_BN_DETERMINISTIC") == "1"
+                            else "atomic fp32 totals (run-to-run order noise ~1e-7 rel.; GRACE_BN_DETERMINISTIC=1 "
+                                 "for bitwise reproducibility)"),
             "bytes_on_wire_per_rank": int(split.get("bytes_per_step", 0)),
             "grace_ms_per_step": None if grace_ms is None else round(grace_ms, 3),
             "noop_exchange_ms_per_step": None if noop_ms is None else round(noop_ms, 3),

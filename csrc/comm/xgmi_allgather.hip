@@ -12,14 +12,17 @@
 // Memory: every rank allocates ONE region, exported to the peers as a HIP IPC handle (the
 // handles travel through the torch.distributed Store on the Python side):
 //
-//     [ Ctrl (256 B): ready gen @0, consumed gen @128 ][ slot D: cap ][ slot S: cap ]
+//     [ Ctrl (256 B): ready gen @0, ready slot @4, consumed gen @128 ][ slot D: cap ][ slot S: cap ]
 //
 // allocated uncached (hipDeviceMallocUncached: stores bypass the XCD L2s, so a payload written
 // by ANY earlier kernel is peer-visible once that kernel is done) when the IPC export accepts
 // it, plain hipMalloc otherwise.  Slot D ("direct", uncached regions only): the payload builder
 // assembles ONE bucket's payload straight into it (XgmiComm.payload_buffer) -- no staging
-// copy; every other payload is staged into slot S.  A call's mode is a property of its input
-// address, the same on every rank.
+// copy; every other payload is staged into slot S.  Which slot a rank's payload sits in is
+// decided by THAT rank (its input address, its own uncached allocation) and published next to
+// its ready generation ("ready slot" word, stored before the release of `ready`): a puller
+// reads the peer's choice instead of assuming its own, so ranks that disagree (one fell back
+// to a cached region, or gave slot D to a different bucket) still read the right bytes.
 //
 // Per all_gather(out, in) call g (every rank issues the same sequence; g = a DEVICE counter,
 // so the launches are graph-capturable and replay correctly):
@@ -68,6 +71,7 @@ constexpr int kThreads = 256;
 constexpr int kMaxWorld = 16;
 constexpr int64_t kCtrlBytes = 256;
 constexpr int kReadyWord = 0;
+constexpr int kReadySlotWord = 1;  // 0 = slot D (direct), 1 = slot S (staged); same line as ready
 constexpr int kConsumedWord = 32;  // own 128-B line
 constexpr int kMaxRanges = 8;
 
@@ -139,9 +143,12 @@ __global__ __launch_bounds__(kThreads) void xg_stage(const uint4* __restrict__ i
   uint4* dst = reinterpret_cast<uint4*>(my_base + kCtrlBytes + slot_bytes);  // slot S
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * kThreads)
     dst[i] = in[i];
-  if (arrive_last(&L->arrive1, gridDim.x))
+  if (arrive_last(&L->arrive1, gridDim.x)) {
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(my_base) + kReadySlotWord, 1u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(reinterpret_cast<uint32_t*>(my_base) + kReadyWord, g, __ATOMIC_RELEASE,
                        __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // valid 16-B vectors of range i of the payload starting at p (counts read with system loads)
@@ -164,11 +171,14 @@ __global__ __launch_bounds__(kThreads) void xg_pull(const char* __restrict__ in,
                                                     char* __restrict__ out, Local* L, Fault F) {
   __shared__ int64_t nv[kMaxRanges];
   __shared__ int ok;
+  __shared__ int64_t src_off;  // peer q's slot, as q published it
   const int q = blockIdx.y;
   const uint32_t g = __hip_atomic_load(&L->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
   char* my_base = peers.base[rank];
   if (direct && blockIdx.x == 0 && q == rank && threadIdx.x == 0) {
     // the payload builder wrote the (uncached) slot in earlier kernels of this stream
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(my_base) + kReadySlotWord, 0u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     __hip_atomic_store(reinterpret_cast<uint32_t*>(my_base) + kReadyWord, g, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
@@ -183,11 +193,13 @@ __global__ __launch_bounds__(kThreads) void xg_pull(const char* __restrict__ in,
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: no stale line of q's slot
     }
-    const char* s = q == rank ? in : peers.base[q] + kCtrlBytes + (direct ? 0 : slot_bytes);
+    src_off = (q != rank && ld_sys(reinterpret_cast<const uint32_t*>(peers.base[q]) + kReadySlotWord) != 0u)
+                  ? slot_bytes : 0;
+    const char* s = q == rank ? in : peers.base[q] + kCtrlBytes + src_off;
     for (int i = 0; i < R.n; ++i) nv[i] = ok ? range_vecs(R, i, s) : 0;
   }
   __syncthreads();
-  if (q != rank) src = peers.base[q] + kCtrlBytes + (direct ? 0 : slot_bytes);
+  if (q != rank) src = peers.base[q] + kCtrlBytes + src_off;
   char* o = out + (int64_t)q * span;
   const int64_t tid = (int64_t)blockIdx.x * kThreads + threadIdx.x, stride = (int64_t)gridDim.x * kThreads;
   if (ok) {
@@ -223,7 +235,7 @@ class XgmiPeers {
     if (world < 1 || world > kMaxWorld) throw std::runtime_error("xgmi all-gather: world size must be 1..16");
     if (rank < 0 || rank >= world) throw std::runtime_error("xgmi all-gather: bad rank");
     XG_HIP(hipSetDevice(device));
-    grace::health_init();
+    grace::health_init(device);
     const size_t bytes = (size_t)(kCtrlBytes + 2 * cap_);
     void* p = nullptr;
     uncached_ = hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached) == hipSuccess;
@@ -327,7 +339,7 @@ class XgmiPeers {
     }
     int b2 = (int)std::min<int64_t>(std::max<int64_t>((nvec + per_blk - 1) / per_blk, 1), 64);
     const auto& hw = grace::health_words();
-    Fault F{hw.host_dev, hw.dev};
+    Fault F{hw.host_dev, grace::health_dev(device_)};
     hipLaunchKernelGGL(xg_pull, dim3(b2, world_), dim3(kThreads), 0, s, static_cast<const char*>(in.data_ptr()), R,
                        peers_, rank_, world_, direct ? 1 : 0, spin_, n, cap_, static_cast<char*>(out.data_ptr()),
                        local_, F);

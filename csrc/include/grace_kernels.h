@@ -233,13 +233,27 @@ constexpr int kSgdSegs = 64;
 constexpr int kHealthWords = 16;
 constexpr int kHealthFault = 0;
 constexpr int kHealthXgmiTimeouts = 1;
+// capacity payloads (ops/cappayload.py) whose selection did not fit: the sent subset was cut
+// (Threshold / DGC: spilled into the residual or dropped; INCEPTIONN: classes dropped).  Counted
+// by the kernels themselves, so a lossy step is visible also inside a replayed HIP graph.
+constexpr int kHealthCapOverflow = 2;
+// host-mapped overflow counter (nullptr before health_init): one system-scope add per event
+__device__ __forceinline__ void health_count_overflow(uint32_t* host_dev) {
+  if (host_dev != nullptr)
+    __hip_atomic_fetch_add(host_dev + kHealthCapOverflow, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+constexpr int kHealthMaxDevices = 64;
 struct HealthWords {
   uint32_t* host;      // host pointer
-  uint32_t* host_dev;  // device alias of the host words
-  uint32_t* dev;       // device memory
+  uint32_t* host_dev;  // device alias of the host words (portable: valid on every device)
+  uint32_t* dev[kHealthMaxDevices];  // per-device copy of the fault flag, by device ordinal (null until init)
 };
 const HealthWords& health_words();
-void health_init();
+// allocates the host words once and the device words of `device` (-1: the current device)
+void health_init(int device = -1);
+// the fault words of `device` (nullptr when health_init never ran for it; never allocates, so
+// it is safe while a stream is being captured)
+uint32_t* health_dev(int device);
 
 void sgd_step(float* const* p, const float* const* g, float* const* buf, uint16_t* const* w16, const int64_t* len,
               int n_seg, float lr, float momentum, float dampening, float wd, bool nesterov, bool maximize,

@@ -155,9 +155,11 @@ __global__ __launch_bounds__(kBlock) void inc_encode_kernel(const float* __restr
                                                             const int32_t* __restrict__ off,
                                                             const int32_t* __restrict__ tot,
                                                             uint8_t* __restrict__ stream, int64_t cap,
-                                                            uint8_t* __restrict__ codes) {
+                                                            uint8_t* __restrict__ codes, uint32_t* health) {
   __shared__ int lds[kBlock / kWave];
   const IncPlan pl = inc_plan(tot, cap);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && (!pl.keep1 && tot[1] > 0 || !pl.keep2 && tot[2] > 0 || tot[3] > pl.cap3))
+    health_count_overflow(health);  // a class (or class-3 tail) is dropped this step
   float* v32 = reinterpret_cast<float*>(stream);
   uint16_t* v16 = reinterpret_cast<uint16_t*>(stream + pl.off16);
   uint8_t* v8 = stream + pl.off8;
@@ -317,7 +319,8 @@ void inceptionn_encode(const float* x, int64_t n, int e_b, int mid, const int32_
                        uint8_t* stream, int64_t cap_bytes, uint8_t* codes, hipStream_t stream_) {
   const int64_t nt = inceptionn_tiles(n);
   if (nt == 0) return;
-  inc_encode_kernel<<<(unsigned)nt, kBlock, 0, stream_>>>(x, n, e_b, mid, off, totals, stream, cap_bytes, codes);
+  inc_encode_kernel<<<(unsigned)nt, kBlock, 0, stream_>>>(x, n, e_b, mid, off, totals, stream, cap_bytes, codes,
+                                                       health_words().host_dev);
 }
 
 void inceptionn_decode(const uint8_t* base, int64_t rank_stride, int64_t stream_off, int64_t codes_off, int n_ranks,

@@ -121,6 +121,13 @@ __global__ __launch_bounds__(kBlock) void sgd_kernel(SgdTable t, SgdHyper h, con
 void sgd_step(float* const* p, const float* const* g, float* const* buf, uint16_t* const* w16, const int64_t* len,
               int n_seg, float lr, float momentum, float dampening, float wd, bool nesterov, bool maximize,
               bool first, hipStream_t stream) {
+  // the fault word of the device this stream launches on (never another GPU's memory)
+  int dev = -1;
+  if (hipStreamGetDevice(stream, &dev) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipGetDevice(&dev);
+  }
+  const uint32_t* dev_fault = health_dev(dev);
   SgdHyper h{lr, momentum, dampening, wd, nesterov ? 1 : 0, maximize ? 1 : 0, first ? 1 : 0};
   for (int s0 = 0; s0 < n_seg; s0 += kSgdSegs) {
     const int m = n_seg - s0 < kSgdSegs ? n_seg - s0 : kSgdSegs;
@@ -137,7 +144,7 @@ void sgd_step(float* const* p, const float* const* g, float* const* buf, uint16_
     }
     t.start[m] = nb;
     t.n = m;
-    const uint32_t* fault = health_words().dev ? health_words().dev + kHealthFault : nullptr;
+    const uint32_t* fault = dev_fault ? dev_fault + kHealthFault : nullptr;
     if (nb > 0) hipLaunchKernelGGL(sgd_kernel, dim3((unsigned)nb), dim3(kBlock), 0, stream, t, h, fault);
   }
 }

@@ -604,9 +604,11 @@ __global__ __launch_bounds__(kBlock) void sparse_scatter_add_dev_kernel(const fl
                                                                         const int32_t* __restrict__ idx,
                                                                         const int32_t* __restrict__ count,
                                                                         int64_t cap, float* __restrict__ out,
-                                                                        float scale, int accumulate) {
+                                                                        float scale, int accumulate,
+                                                                        uint32_t* health) {
   const int64_t c = *count;
   const int64_t K = c < cap ? c : cap;
+  if (c > cap && blockIdx.x == 0 && threadIdx.x == 0) health_count_overflow(health);
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < K; j += stride) {
     const int32_t t = idx[j];
@@ -670,7 +672,7 @@ void sparse_scatter_add_dev(const float* val, const int32_t* idx, const int32_t*
   int64_t blocks = (cap + kBlock - 1) / kBlock;
   if (blocks > 2048) blocks = 2048;
   sparse_scatter_add_dev_kernel<<<(int)blocks, kBlock, 0, stream>>>(val, idx, count, cap, out, scale,
-                                                                    accumulate ? 1 : 0);
+                                                                    accumulate ? 1 : 0, health_words().host_dev);
 }
 
 }  // namespace grace

@@ -159,6 +159,7 @@ void sgd_step(const std::vector<Tensor>& params, const std::vector<Tensor>& grad
     const Tensor& t = params[i];
     TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_non_overlapping_and_dense(),
                 "sgd_step: parameters must be dense fp32 GPU tensors");
+    TORCH_CHECK(t.device() == params[0].device(), "sgd_step: every parameter on one device");
     auto same = [&](const Tensor& u, at::ScalarType dt, const char* what) {
       bool ok = u.is_cuda() && u.scalar_type() == dt && u.sizes() == t.sizes();
       for (int64_t d = 0; ok && d < t.dim(); ++d)  // strides of size-1 dims do not move memory

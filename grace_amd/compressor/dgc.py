@@ -35,6 +35,9 @@ class DgcCompressor(BucketCompressor):
         self.capacity = capacity
 
     def _select(self, g, ctx, name, vmask=None, umask=None):
+        from ..parallel import health as _health
+
+        _health.init_for(g)  # capacity overflows are counted by the decoder (health.overflows())
         cap = D.dgc_capacity(ctx.layout, self.compress_ratio, self.capacity)
         seed, step = self.next_rng(name, g.device)
         hdr, vals, idx = D.dgc_select(g, ctx.layout, self.compress_ratio, self.sample_ratio, self.max_iters,

@@ -16,8 +16,10 @@ recounts classes from every rank's codes and decodes + sums all W ranks in one p
 order, deterministic).  The payload has a FIXED capacity (ops/cappayload.py idea): an int32
 header with the class totals, ONE value stream of 4 * ceil(capacity * n) bytes holding the fp32,
 16-bit and 8-bit values back to back, and the codes -- no host read of a size, graph-capturable.
-capacity 1.0 always fits (every element as fp32); below it the lowest-precision classes are
-dropped first when the step's values do not fit.  ``capacity=None`` (default, "auto"): the value
+capacity 1.0 (the default: INCEPTIONN has no error feedback, so nothing may be dropped) always
+fits (every element as fp32); below it the lowest-precision classes are dropped first when the
+step's values do not fit, and the encoder counts that step in ``parallel.health.overflows()``
+(also inside a replayed HIP graph).  ``capacity="auto"`` (opt-in): the value
 stream starts at n bytes (1 byte per element: every element in the 8-bit class or dropped, the
 common case for gradients below 2^-5; tensors <= 16K elements start at full size) and grows lagged and sync-free when a step needed more
 (ops/cappayload.py AdaptiveCapacity, decided from every rank's gathered header: ranks stay in
@@ -53,15 +55,21 @@ def _leading_bin(v: torch.Tensor) -> torch.Tensor:
 class INCEPTIONNCompressor(BucketCompressor):
     AUTO_BYTES_PER_ELEMENT = 1.0
 
-    def __init__(self, error_bound: float = 2e-10, capacity=None):
+    def __init__(self, error_bound: float = 2e-10, capacity=1.0):
         super().__init__(tensors_size_are_same=True)  # fixed-capacity payload
         self.error_bound = error_bound
         self.e_b = 127 + int(math.log(error_bound / 2, 10))
         self.mid = self.e_b + math.ceil((127 - self.e_b) / 2)
+        # INCEPTIONN has no error feedback: a class that does not fit is LOST, so the default is
+        # the lossless capacity 1.0 (the reference's semantics); "auto" (opt-in) sizes the value
+        # stream adaptively and counts every lossy step in health.overflows()
+        if capacity is None or capacity == "auto":
+            capacity = None
         self.capacity = capacity
         self.adaptive = (None if capacity is not None else
                          __import__("grace_amd.ops.cappayload", fromlist=["x"]).AdaptiveCapacity(
                              self.AUTO_BYTES_PER_ELEMENT))
+
         self._name = None
 
     def _cap_bytes(self, n: int) -> int:
@@ -80,6 +88,9 @@ class INCEPTIONNCompressor(BucketCompressor):
                                   (torch.uint8, ((n + 3) // 4,))])
 
     def _native_compress(self, x, ctx):
+        from ..parallel import health as _health
+
+        _health.init_for(x)  # the overflow counter (allocated in the first, eager step)
         C = _native.lib()
         n = x.numel()
         nt = C.inceptionn_tiles(n)

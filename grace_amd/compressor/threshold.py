@@ -14,7 +14,9 @@ of the selected entries are sent per step.  ``None`` (default, "auto"):
     (ops/cappayload.py AdaptiveCapacity); entries past the capacity stay in the residual and go
     out in a later step -- spill, not loss;
   * without error feedback: 1.0 (exact reference semantics, never spills).
-Which subset is sent when a step spills is unspecified on the GPU (atomic slot order).  On the
+Which subset is sent when a step spills is unspecified on the GPU (atomic slot order).  Every
+spilled payload is counted by the decode kernel in ``parallel.health.overflows()`` -- also for
+steps replayed from a HIP graph, whose capacity is frozen at capture.  On the
 xGMI one-shot path only each peer's selected entries move regardless (count-aware pull).
 
 Default threshold 0.01 (the dist helper's 256 selects nothing: survey 2.14 #19).
@@ -44,6 +46,9 @@ class ThresholdCtx:
 def _compact(g, thr, cap, r=None, r_valid=False, beta=1.0, gamma=1.0):
     hdr, v, i = P.sparse_payload(g.device, cap)
     if _native.use_native(g):
+        from ..parallel import health as _health
+
+        _health.init_for(g)  # spilled steps are counted by the decoder (health.overflows())
         mode = 1 if (r is not None and r_valid) else 0
         _native.lib().threshold_compact(g, r if mode else None, mode, beta, gamma, thr, v, i, hdr[:1], r)
         return hdr, v, i
@@ -69,6 +74,7 @@ class ThresholdCompressor(Compressor):
         self.threshold = threshold
         self.capacity = capacity
         self.adaptive = P.AdaptiveCapacity(self.AUTO_EF_RATIO) if capacity is None else None
+
 
     def _ctx(self, tensor, name, ef: bool):
         n = tensor.numel()

@@ -40,7 +40,7 @@ COMPRESSORS: Dict[str, Callable[[Dict[str, Any]], Any]] = {
                                                warm_start=p.get("warm_start", False),
                                                world_size=p.get("world_size")),
     "adaq": lambda p: Z.AdaqCompressor(p.get("compress_ratio", 0.01), capacity=p.get("capacity", 2.0)),
-    "inceptionn": lambda p: Z.INCEPTIONNCompressor(p.get("error_bound", 2e-10), capacity=p.get("capacity")),
+    "inceptionn": lambda p: Z.INCEPTIONNCompressor(p.get("error_bound", 2e-10), capacity=p.get("capacity", 1.0)),
     "sketch": lambda p: Z.SketchCompressor(p.get("quantiles", 64)),
     "u8bit": lambda p: Z.U8bitCompressor(),
 }

@@ -10,6 +10,11 @@ wgrad of layer L runs while the BN backward and dgrad of layer L-1 run, so laten
 launches share the chip with MFMA work instead of leaving it idle.  In a whole-step HIP graph
 the fork becomes a parallel branch of the graph (no host involvement at replay).
 
+Who may fork: only parameters whose gradient consumer is known to join (``mark_joinable``: the
+GRACE engine tags its own parameters).  Plain DDP, post-accumulate-grad hooks or user code that
+reads ``p.grad`` mid-backward would read a gradient the side stream may still be writing, so
+every untagged parameter computes its weight gradient in line.
+
 Joins: (1) the GRACE engine's bucket launch (parallel/engine.py ``_launch`` / ``synchronize``)
 makes its consuming stream wait for every wgrad issued so far; (2) a final-callback of every
 backward that forked joins the side stream into the caller's current stream, so a user reading
@@ -70,6 +75,21 @@ def _final_join():
     join()
 
 
+def mark_joinable(params, on: bool = True) -> None:
+    """Declare that the consumer of these parameters' gradients joins the side stream (``join``)
+    before it reads them: their weight gradients may then run on the side stream.  The GRACE
+    engine marks its own parameters; everything else computes weight gradients in line."""
+    for p in params:
+        if on:
+            p._grace_wgrad_join = True
+        elif hasattr(p, "_grace_wgrad_join"):
+            del p._grace_wgrad_join
+
+
+def joinable(param: torch.Tensor) -> bool:
+    return bool(getattr(param, "_grace_wgrad_join", False))
+
+
 # ---------------------------------------------------------------- deferred weight gradients
 # GRACE_WGRAD_DEFER=1: a weight gradient whose destination is an engine bucket view is not
 # computed when its conv's backward runs; its closure is queued and every queued one runs, in
@@ -118,13 +138,16 @@ class fork:
         self.ctx = None
         self.main = None
         self.ev = None
-        # a parameter that already holds a .grad gets the new one ADDED by AccumulateGrad on the
-        # current stream right after this backward returns (before any join): stay in line.  So
-        # does a parameter whose gradient a DistributedDataParallel reducer consumes (marked by
-        # parallel/ddp_hook.py): the reducer reads it from its AccumulateGrad hook, mid-backward,
-        # on the current stream -- before any join could order it after the side stream
-        if (_ENABLED and t.is_cuda and (param is None or param.grad is None)
-                and not getattr(param, "_grace_ddp", False)):
+        # Only a parameter whose gradient consumer is KNOWN to join the side stream before
+        # reading it may fork (``joinable``): the GRACE engine's parameters (it joins at every
+        # bucket launch) and explicitly tagged ones.  Any other consumer -- plain DDP, a
+        # post-accumulate-grad hook, a user reading p.grad mid-backward -- reads the gradient on
+        # the current stream while the side stream may still be writing it, so those stay in
+        # line.  A parameter that already holds a .grad gets the new one ADDED by AccumulateGrad
+        # on the current stream right after this backward returns: in line as well.  So does a
+        # parameter whose gradient a DistributedDataParallel reducer consumes (parallel/ddp_hook.py
+        # clears the tag: the reducer reads it from its AccumulateGrad hook, mid-backward).
+        if (_ENABLED and t.is_cuda and param is not None and param.grad is None and joinable(param)):
             self.main = torch.cuda.current_stream(t.device)
             self.ev = torch.cuda.Event()
             self.ev.record(self.main)

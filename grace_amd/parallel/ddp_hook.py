@@ -34,8 +34,12 @@ from ..ops.layout import SegmentLayout
 def mark_ddp_params(params) -> None:
     """Weight gradients of these parameters are computed in line (ops/wgrad.py): DDP's reducer
     reads each gradient from its AccumulateGrad hook, during backward, on the current stream."""
+    from ..ops import wgrad as _wg
+
+    params = list(params)
     for p in params:
         p._grace_ddp = True
+    _wg.mark_joinable(params, on=False)
 
 
 class GraceHookState:

@@ -180,6 +180,9 @@ class GraceEngine:
             for p, src, v in zip(b.params, b.srcs, b.views):
                 if src is p:
                     p._grace_grad_view = v
+        # the engine joins the weight-gradient side stream before it reads any gradient (bucket
+        # launch / synchronize): its parameters may compute weight gradients there (ops/wgrad.py)
+        _wgrad.mark_joinable([src for b in self.buckets for src in b.srcs])
         self._passes: Dict[int, int] = {}
         self._hooks = []
         self.stream = torch.cuda.Stream(self.device) if (self.device.type == "cuda" and overlap) else None
@@ -430,6 +433,7 @@ class GraceEngine:
             for p, v in zip(b.params, b.views):
                 if getattr(p, "_grace_grad_view", None) is v:
                     del p._grace_grad_view
+        _wgrad.mark_joinable([src for b in self.buckets for src in b.srcs], on=False)
 
     def state_dict(self):
         return {"grc": self.grc.state_dict()}

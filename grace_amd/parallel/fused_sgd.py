@@ -47,10 +47,12 @@ class FusedSGD(SGD):
         self._working: Dict[int, torch.Tensor] = {}
         # the kernel honours the process-wide communication fault flag (parallel/health.py):
         # allocate it now, before any HIP-graph capture of the step
-        if any(p.is_cuda for g in self.param_groups for p in g["params"]):
+        devs = {p.device for g in self.param_groups for p in g["params"] if p.is_cuda}
+        if devs:
             from . import health
 
-            health.init()
+            for d in sorted(devs, key=lambda d: d.index or 0):
+                health.init(d)
 
     def attach_working_copies(self, weights) -> None:
         """Write ``weights``' bf16 working copies in the update kernel (BF16Weights)."""
@@ -93,9 +95,12 @@ class FusedSGD(SGD):
                 first.append(p)
             else:
                 later.append(p)
+        # one launch per device (the kernel reads that device's communication fault word)
+        devs = {}
         for ps, is_first in ((first, True), (later, False)):
-            if not ps:
-                continue
+            for p in ps:
+                devs.setdefault((p.device, is_first), []).append(p)
+        for (dev, is_first), ps in devs.items():
             bufs = [self.state[p].get("momentum_buffer") if mom != 0 else None for p in ps]
             w16 = [self._working_for(p) for p in ps]
             _native.lib().sgd_step(ps, [p.grad for p in ps], bufs, w16, float(group["lr"]), float(mom),

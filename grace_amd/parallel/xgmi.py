@@ -73,7 +73,12 @@ class XgmiComm(_comm.Comm):
     accepts_ranges = True
 
     def __init__(self, inner: _comm.Comm, capacity_mb: float = 8.0, verify: bool = True, store=None,
-                 spin_limit: int = 1 << 25, direct: bool = True):
+                 spin_limit: int = 1 << 25, direct: bool = True, select: str = "size"):
+        """``select``: "size" = every gather that fits the capacity takes the one-shot path;
+        "probe" = the FIRST eager gather of each payload size times both paths (the one-shot pull
+        and ``inner``'s all-gather, e.g. RCCL's ring) on that exact size, every rank takes the MAX
+        over ranks of each and all pick the faster one (``choices`` records it) -- the path
+        choice for the 7-link mesh is measured, not assumed."""
         if not dist.is_initialized():
             raise RuntimeError("XgmiComm needs torch.distributed (its Store carries the IPC handles)")
         self.inner = inner
@@ -82,11 +87,15 @@ class XgmiComm(_comm.Comm):
         _health.init()
         self._x = _native.lib().XgmiPeers(self.rank, self.world_size, self.device, int(capacity_mb * 2 ** 20),
                                           int(spin_limit))
+        if select not in ("size", "probe"):
+            raise ValueError(f"select must be 'size' or 'probe', not {select!r}")
+        self.select = select
+        self.choices = {}  # payload bytes -> {"path": "xgmi" | "inner", "xgmi_us": .., "inner_us": ..}
         self._direct_ok = bool(direct)
         self._slot_owner = None
+        self._owner_seen = 0   # payload_buffer calls when the owner last asked
+        self._buf_calls = 0
         self.direct_calls = 0
-        if self._direct_ok and self._x.uncached:
-            _comm.set_payload_provider(self.payload_buffer)
         store = store if store is not None else dist.distributed_c10d._get_default_store()
         key = f"grace_amd/xgmi/{next(_UID)}"
         store.set(f"{key}/{self.rank}", self._x.handle())
@@ -99,6 +108,12 @@ class XgmiComm(_comm.Comm):
         self._agree(err is None, f"xGMI peer mapping failed: {err}")
         self.capacity = int(self._x.capacity)
         self.one_shot_calls = 0
+        # direct slot writes only where EVERY rank got an uncached region (the kernel also reads
+        # each peer's published slot choice, so a disagreement could not read stale bytes, but
+        # uniform behaviour keeps the per-rank work and the bench labels identical)
+        self._direct_ok = self._all(self._direct_ok and bool(self._x.uncached))
+        if self._direct_ok:
+            _comm.set_payload_provider(self.payload_buffer)
         if verify:
             self._verify()
 
@@ -123,15 +138,73 @@ class XgmiComm(_comm.Comm):
         assembled there is gathered without the staging copy."""
         if not (self._direct_ok and self._x.uncached) or nbytes <= 0 or nbytes > self.capacity or nbytes % 16:
             return None
+        self._buf_calls += 1
+        # the owner is whoever asks first; an owner that stopped asking (e.g. a DDP bucket name
+        # retired by re-bucketing, ddp_hook.py `.g{n}` generations) hands the slot on after
+        # _OWNER_IDLE calls by other keys.  Every rank sees the same key sequence, and the pull
+        # kernel reads each peer's published slot anyway (csrc/comm/xgmi_allgather.hip)
+        if self._slot_owner is not None and self._slot_owner != key and \
+                self._buf_calls - self._owner_seen > self._OWNER_IDLE:
+            self._slot_owner = None
         if self._slot_owner is None:
             self._slot_owner = key
         if self._slot_owner != key:
             return None
+        self._owner_seen = self._buf_calls
         return self._x.slot_tensor(int(nbytes))
 
+    _OWNER_IDLE = 16
+
+    def _choose(self, out, inp) -> str:
+        """"xgmi" or "inner" for this payload size (identical on every rank: decided from
+        MAX-reduced timings in an eager call, or by size alone)."""
+        nbytes = inp.numel() * inp.element_size()
+        if self.select != "probe":
+            return "xgmi"
+        c = self.choices.get(nbytes)
+        if c is not None:
+            return c["path"]
+        if torch.cuda.is_current_stream_capturing():
+            # a size first seen inside a capture (the eager warm-up normally saw it): every rank
+            # is in the same capture, so the size rule is still rank-consistent
+            return "xgmi"
+        c = self.choices[nbytes] = self._probe(out, inp)
+        return c["path"]
+
+    def _probe(self, out, inp, iters: int = 8) -> dict:
+        dev = torch.device("cuda", self.device)
+        o = torch.empty_like(out)
+        i = inp.detach().clone() if self._aligned(inp) else inp.contiguous().clone()
+        import time
+
+        times = []
+        for path in ("xgmi", "inner"):
+            fn = (lambda: self._one_shot(o, i, None)) if path == "xgmi" else \
+                (lambda: self.inner.all_gather_into(o, i, False).wait())
+            fn()  # warm (RCCL lazily builds its channels for a new size)
+            torch.cuda.synchronize(dev)
+            self.inner.barrier()
+            torch.cuda.synchronize(dev)
+            # wall time around synchronised issue: also right for a host-driven inner (gloo)
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                fn()
+            torch.cuda.synchronize(dev)
+            times.append((time.perf_counter() - t0) * 1e6 / iters)
+        t = torch.tensor(times, dtype=torch.float64, device=dev)
+        self.inner.all_reduce(t, "max").wait()  # the slowest rank sets each path's time
+        torch.cuda.synchronize(dev)
+        xg, inn = (float(v) for v in t.tolist())
+        self.one_shot_calls -= iters + 1
+        return {"path": "xgmi" if xg <= inn else "inner", "xgmi_us": round(xg, 2), "inner_us": round(inn, 2),
+                "bytes": int(inp.numel() * inp.element_size())}
+
     def all_gather_into(self, out, inp, async_op=False, ranges=None):
-        if not self._fits(inp):
+        if not self._fits(inp) or self._choose(out, inp) != "xgmi":
             return self.inner.all_gather_into(out, inp, async_op)
+        return self._one_shot(out, inp, ranges)
+
+    def _one_shot(self, out, inp, ranges):
         o, i = out, inp
         if not self._aligned(i):  # staged, not a different path: every rank stays on the one-shot
             i = torch.empty(inp.numel() * inp.element_size(), dtype=torch.uint8, device=inp.device)
@@ -172,21 +245,36 @@ class XgmiComm(_comm.Comm):
             chk()
 
     def _verify(self):
-        """Gather a rank-dependent pattern through both paths (two calls: both slots) and
-        agree on the outcome across ranks; raise when any rank saw a mismatch."""
+        """Gather a rank-dependent pattern through both paths (staged twice, then from the
+        direct slot when available) and agree on the outcome across ranks; raise when any rank
+        saw a mismatch."""
         dev = torch.device("cuda", self.device)
         ok = 1
-        for salt in (1, 2):
-            n = 4099 * 4  # odd count of 16-B vectors (exercises the grid-stride tails)
-            inp = (torch.arange(n, device=dev, dtype=torch.int32) * (self.rank + 7) + salt * 1000003)
+        n = 4099 * 4  # odd count of 16-B vectors (exercises the grid-stride tails)
+        for salt in (1, 2, 3):
+            pat = (torch.arange(n, device=dev, dtype=torch.int32) * (self.rank + 7) + salt * 1000003)
+            inp = pat
+            if salt == 3:  # direct slot: assembled in place, read by the peers from slot D
+                if not self._direct_ok:
+                    break
+                inp = self._x.slot_tensor(n * 4).view(torch.int32)
+                inp.copy_(pat)
             got = torch.empty(self.world_size * n, dtype=torch.int32, device=dev)
             ref = torch.empty_like(got)
             self.all_gather_into(got, inp)
-            self.inner.all_gather_into(ref, inp).wait()
+            self.inner.all_gather_into(ref, pat).wait()
             torch.cuda.synchronize(dev)
             ok &= int(torch.equal(got, ref)) & int(_health.status()[1] == 0)
         self._agree(bool(ok), "xGMI one-shot all-gather failed its self-check against the inner comm")
-        self.one_shot_calls = 0
+        self.one_shot_calls = self.direct_calls = 0
+
+    def _all(self, flag: bool) -> bool:
+        """True on every rank iff ``flag`` is true on every rank."""
+        dev = torch.device("cuda", self.device)
+        t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+        self.inner.all_reduce(t, "min").wait()
+        torch.cuda.synchronize(dev)
+        return int(t.item()) == 1
 
     def _agree(self, ok: bool, msg: str):
         """All ranks raise together (MIN over ranks through the inner comm) or none does."""

@@ -92,13 +92,20 @@ def test_inceptionn_auto_capacity_payload_size():
     from grace_amd.parallel.comm import LocalComm
 
     n = 1 << 18  # buckets above 16K elements start at 1 byte per element
-    grc = grace_from_params({"compressor": "inceptionn", "communicator": "allgather"}, comm=LocalComm())
+    # opt-in: the default is the lossless capacity 1.0 (INCEPTIONN has no error feedback)
+    grc = grace_from_params({"compressor": "inceptionn", "communicator": "allgather", "capacity": "auto"},
+                            comm=LocalComm())
     payload, _ = grc.compress_step(torch.randn(n) * 0.01, "w")
     wire = sum(t.numel() * t.element_size() for t in payload)
     assert wire <= 1.3 * n, wire  # was >= 4.25 n with capacity 1.0
     # exact against capacity 1.0 when the step fits
     x = torch.randn(n) * 0.01
-    a = grace_from_params({"compressor": "inceptionn", "communicator": "allgather"}, comm=LocalComm()).step(x, "q")
+    a = grace_from_params({"compressor": "inceptionn", "communicator": "allgather", "capacity": "auto"},
+                          comm=LocalComm()).step(x, "q")
     b = grace_from_params({"compressor": "inceptionn", "communicator": "allgather", "capacity": 1.0},
                           comm=LocalComm()).step(x, "q")
     assert torch.equal(a, b)
+    # the default payload is the lossless one
+    d, _ = grace_from_params({"compressor": "inceptionn", "communicator": "allgather"},
+                             comm=LocalComm()).compress_step(torch.randn(n) * 0.01, "w")
+    assert sum(t.numel() * t.element_size() for t in d) >= 4 * n

@@ -343,3 +343,42 @@ def test_ddp_hook_graph_capture(nccl_group):
         finals.append([p.detach().clone() for p in m.parameters()])
     for a, b in zip(*finals):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
+
+
+def test_plain_ddp_resnet_grads_match_inline(nccl_group):
+    """grace_amd.models.resnet under PLAIN DDP (no GRACE hook, no engine): its parameters are not
+    tagged joinable, so every weight gradient is computed in line and the reducer's mid-backward
+    reads see finished gradients -- equal to the GRACE_WGRAD_STREAM=0 run"""
+    import copy
+
+    from grace_amd.models import resnet18_cifar
+    from grace_amd.ops import wgrad
+
+    torch.manual_seed(0)
+    base = resnet18_cifar().cuda().to(memory_format=torch.channels_last)
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(8, 3, 16, 16, generator=g).cuda().contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (8,), generator=g).cuda()
+
+    def grads(stream_on):
+        m = copy.deepcopy(base)
+        ddp = nn.parallel.DistributedDataParallel(m, device_ids=[0], broadcast_buffers=False)
+        wgrad.set_enabled(stream_on)
+        try:
+            out = []
+            for _ in range(2):
+                for p in m.parameters():
+                    p.grad = None
+                F.cross_entropy(ddp(x), y).backward()
+                out = [p.grad.detach().clone() for p in m.parameters()]
+        finally:
+            wgrad.set_enabled(True)
+        assert not any(wgrad.joinable(p) for p in m.parameters())
+        return out
+
+    ref = grads(False)
+    got = grads(True)
+    torch.cuda.synchronize()
+    for a, b in zip(got, ref):
+        tol = 1e-4 * float(b.abs().max()) + 1e-6
+        assert float((a - b).abs().max()) <= tol

@@ -87,3 +87,44 @@ def _w2_body(rank, world, name, out):
 def test_capacity_exchange_w2_gloo(name, tmp_path):
     run_distributed(_w2_body, 2, name, str(tmp_path / "p.pt"), timeout=180)
     assert torch.isfinite(torch.load(str(tmp_path / "p.pt"), weights_only=True)).all()
+
+
+def test_capacity_overflow_counted_in_graph_replays():
+    """A capacity payload that cannot hold the step's selection is counted on the device
+    (parallel.health.overflows(): Threshold's decoder, INCEPTIONN's encoder) -- also for steps
+    replayed from a HIP graph, where the capacity is frozen and nothing reaches the host
+    (lossy replayed steps must not go unnoticed)."""
+    from grace_amd import grace_from_params
+    from grace_amd.parallel import health
+
+    dev = torch.device("cuda", 0)
+    x = torch.randn(1 << 16, device=dev)
+    for params in ({"compressor": "threshold", "threshold": 0.5, "memory": "residual",
+                    "communicator": "allgather", "capacity": 0.01},  # ~62 % selected, 1 % fits
+                   {"compressor": "inceptionn", "memory": "none", "communicator": "allgather",
+                    "capacity": 0.05}):
+        grc = grace_from_params(dict(params, world_size=1))
+        grc.step(x.clone(), "warm")  # eager: allocates the counter and the payload buffers
+        torch.cuda.synchronize()
+        base = health.overflows()
+        assert base >= 1, params["compressor"]
+        graph = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            grc.step(x.clone(), "warm")
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        base = health.overflows()
+        with torch.cuda.graph(graph):
+            grc.step(x, "warm")
+        for _ in range(3):
+            graph.replay()
+        torch.cuda.synchronize()
+        assert health.overflows() >= base + 3, (params["compressor"], base, health.overflows())
+    # the lossless INCEPTIONN default never overflows
+    base = health.overflows()
+    grace_from_params({"compressor": "inceptionn", "memory": "none", "communicator": "allgather",
+                       "world_size": 1}).step(x.clone(), "lossless")
+    torch.cuda.synchronize()
+    assert health.overflows() == base

@@ -48,6 +48,7 @@ def test_split_conv_matches_conv2d(stride, pad, k):
     ref = torch.nn.Conv2d(16, 32, k, stride=stride, padding=pad, bias=False).cuda()
     ref.load_state_dict(conv.state_dict())
     x = torch.randn(4, 16, 20, 20, device="cuda").contiguous(memory_format=torch.channels_last)
+    wgrad.mark_joinable(conv.parameters())  # fork: the final callback joins before the compare
     xa, xb = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
     ya, yb = conv(xa), ref(xb)
     dy = torch.randn_like(ya)
@@ -77,6 +78,7 @@ def _small_cnn(num_classes=10):
 def test_side_stream_grads_equal_inline():
     torch.manual_seed(0)
     model = _small_cnn().cuda().to(memory_format=torch.channels_last)
+    wgrad.mark_joinable(model.parameters())  # backward's final callback joins before _grads clones
     x = torch.randn(16, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
     y = torch.randint(0, 10, (16,), device="cuda")
     wgrad.set_enabled(False)
@@ -270,3 +272,33 @@ def test_deferred_wgrad_engine_graph(bn_deterministic):
         for a, b in zip(got, ref):
             err = float((a - b).abs().max())
             assert err <= 1e-3 * float(b.abs().max()) + 2e-5, err
+
+
+def test_untagged_parameters_stay_in_line():
+    """a model whose gradients nobody joins (no GRACE engine: plain DDP, hooks, user code) never
+    forks a weight gradient, so a post-accumulate-grad hook reading .grad mid-backward on the
+    compute stream sees the finished gradient (side-stream race)"""
+    torch.manual_seed(0)
+    model = _small_cnn().cuda().to(memory_format=torch.channels_last)
+    x = torch.randn(16, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (16,), device="cuda")
+    wgrad.set_enabled(False)
+    try:
+        _grads(model, x, y)
+        ref = _grads(model, x, y)
+    finally:
+        wgrad.set_enabled(True)
+    seen = {}
+    hooks = [p.register_post_accumulate_grad_hook(lambda p: seen.__setitem__(id(p), p.grad.clone()))
+             for p in model.parameters()]
+    try:
+        for _ in range(2):
+            seen.clear()
+            got = _grads(model, x, y)
+            assert not wgrad._pending.get(torch.cuda.current_device())
+            for (n, p), a, b in zip(model.named_parameters(), got, ref):
+                _close(a, b, msg=n)
+                _close(seen[id(p)], b, msg=f"hook {n}")  # the clone ran mid-backward
+    finally:
+        for h in hooks:
+            h.remove()

@@ -69,6 +69,11 @@ def test_xgmi_allgather_two_ranks_one_gpu():
     run_distributed(_xgmi_body, 2, timeout=180)
 
 
+def test_xgmi_allgather_four_ranks_one_gpu():
+    """W = 4 (three peers per puller: the grid's rank dimension, the consumed fan-in)"""
+    run_distributed(_xgmi_body, 4, timeout=240)
+
+
 def test_xgmi_allgather_engine_topk():
     """The bucketed Top-K + Allgather engine at W = 2 with the one-shot comm as the default comm:
     parameters stay identical across ranks and the one-shot path carried the payloads."""
@@ -218,6 +223,24 @@ def _xgmi_direct_body(rank, world):
         assert torch.equal(a, b), f"step {step}"
     if comm._x.uncached:
         assert comm.direct_calls >= 3
+    # ranks that DISAGREE on the slot (rank 0 assembles in slot D, rank 1 is staged): every
+    # puller reads the slot its peer published, not its own choice
+    if comm._direct_ok:
+        n = 4096
+        pat = torch.arange(n, device=dev, dtype=torch.int32) * (rank + 3) + 17
+        inp = comm._x.slot_tensor(n * 4).view(torch.int32) if rank == 0 else pat.clone()
+        inp.copy_(pat)
+        out = torch.empty(world * n, dtype=torch.int32, device=dev)
+        comm._x.all_gather(out.view(torch.uint8), inp.view(torch.uint8), torch.empty(0, 8, dtype=torch.int64))
+        torch.cuda.synchronize()
+        want = torch.cat([torch.arange(n, device=dev, dtype=torch.int32) * (r + 3) + 17 for r in range(world)])
+        assert torch.equal(out, want)
+        # a retired owner hands the slot on after _OWNER_IDLE calls by other keys
+        comm._slot_owner = None
+        assert comm.payload_buffer(64, "old") is not None
+        got = [comm.payload_buffer(64, "new") is not None for _ in range(comm._OWNER_IDLE + 2)]
+        assert not got[0] and got[-1]
+        assert comm.payload_buffer(64, "old") is None
     comm.check()
     dist.barrier()
     torch.cuda.synchronize()
@@ -226,3 +249,65 @@ def _xgmi_direct_body(rank, world):
 
 def test_xgmi_direct_payload_no_staging():
     run_distributed(_xgmi_direct_body, 2, timeout=180)
+
+
+def _xgmi_whole_step_graph_body(rank, world):
+    """The W > 1 measured configuration, rehearsed on one GPU: forward + backward + Top-K 1 %
+    exchange (xGMI one-shot all-gather, GroupedComm) + FusedSGD captured as ONE HIP graph and
+    replayed 10 times.  Ranks train on different data; after every replay the weights must be
+    bit-identical across ranks (the exchange averaged the same decoded gradient everywhere),
+    and the device health words must stay clean."""
+    import torch.nn.functional as F
+
+    from grace_amd import grace_from_params
+    from grace_amd.models import resnet18_cifar
+    from grace_amd.parallel import DistributedOptimizer, FusedSGD, broadcast_parameters, set_default_comm
+    from grace_amd.parallel.comm import TorchComm
+    from grace_amd.parallel.graph import GraphedStep
+    from grace_amd.parallel.xgmi import XgmiComm
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    comm = XgmiComm(TorchComm(), capacity_mb=8.0, select="probe")
+    set_default_comm(comm)
+    try:
+        torch.manual_seed(0)
+        model = resnet18_cifar().to(dev).to(memory_format=torch.channels_last)
+        broadcast_parameters(model.state_dict(), root_rank=0)
+        grc = grace_from_params({"compressor": "topk", "compress_ratio": 0.01, "memory": "residual",
+                                 "communicator": "allgather", "world_size": world})
+        opt = DistributedOptimizer(FusedSGD(list(model.parameters()), lr=0.02, momentum=0.5), grc,
+                                   named_parameters=list(model.named_parameters()), overlap=False)
+        g = torch.Generator().manual_seed(100 + rank)  # different data per rank
+        x = torch.randn(16, 3, 32, 32, generator=g).to(dev).contiguous(memory_format=torch.channels_last)
+        y = torch.randint(0, 10, (16,), generator=g).to(dev)
+
+        def step():
+            opt.zero_grad(set_to_none=True)
+            loss = F.cross_entropy(model(x), y)
+            loss.backward()
+            opt.step()
+            return loss
+
+        run = GraphedStep(step, warmup=3, capture_error_mode="thread_local")
+        assert comm.choices, "the eager warm-up must have probed the payload size"
+        calls = comm.one_shot_calls
+        for it in range(10):
+            run()
+            torch.cuda.synchronize()
+            for p in model.parameters():
+                ref = p.detach().clone()
+                dist.broadcast(ref, 0)
+                assert torch.equal(ref, p.detach()), f"replay {it}: weights diverged across ranks"
+        # replays do not pass through Python: the counter moved only in the eager warm-up
+        assert comm.one_shot_calls == calls
+        comm.check()
+        dist.barrier()
+        torch.cuda.synchronize()
+    finally:
+        set_default_comm(None)
+        comm.close()
+
+
+def test_xgmi_whole_step_graph_two_ranks():
+    run_distributed(_xgmi_whole_step_graph_body, 2, timeout=300)

@@ -69,3 +69,23 @@ def test_engine_marks_bucket_views_and_steal_keeps_them():
     assert torch.all(views[id(w)] == 2.0)
     eng.remove()
     assert not hasattr(w, "_grace_grad_view")
+
+
+def test_only_engine_parameters_may_fork():
+    """weight gradients go to the side stream only for parameters whose consumer joins it: the
+    engine tags its own (and untags on remove), DDP-managed ones are never tagged"""
+    from grace_amd import grace_from_params
+    from grace_amd.parallel.ddp_hook import mark_ddp_params
+    from grace_amd.parallel.engine import GraceEngine
+
+    model = nn.Sequential(nn.Linear(5, 7), nn.Linear(7, 3))
+    assert not any(wgrad.joinable(p) for p in model.parameters())  # plain model: in line
+    grc = grace_from_params({"compressor": "none", "memory": "none", "communicator": "allreduce",
+                             "world_size": 1})
+    eng = GraceEngine(list(model.named_parameters()), grc, overlap=False)
+    assert all(wgrad.joinable(p) for p in model.parameters())
+    eng.remove()
+    assert not any(wgrad.joinable(p) for p in model.parameters())
+    wgrad.mark_joinable(model.parameters())
+    mark_ddp_params(model.parameters())
+    assert not any(wgrad.joinable(p) for p in model.parameters())
