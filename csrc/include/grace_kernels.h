@@ -180,6 +180,8 @@ bool bn_supported(int C);  // C % 8 == 0, C <= 2048, C % 256 == 0 above 256
 int64_t bn_workspace_floats(int64_t M, int C);  // `ws` size (fp32 words, 8-B aligned base)
 int bn_fused_v(int64_t M, int C, bool bwd);      // single-launch vectors/thread, 0 = two-kernel path
 void bn_set_fused(bool on);                       // runtime switch (default: env GRACE_BN_FUSED == 1)
+int bn_fused_v_f32(int64_t M, int C, bool bwd);  // fp32 single-launch rows/thread, 0 = two-kernel path
+void bn_set_fused_f32(bool on);                   // runtime switch (default off; env GRACE_BN_FUSED_F32=1 on)
 unsigned bn_spin_timeouts();                     // bounded co-residency waits that timed out (must stay 0)
 // x/res/y/dy/dx/dres: bf16 (uint16_t) or fp32 (`fp32`) elements; fp32 uses the two-kernel path
 void bn_act_forward(const void* x, const void* res, bool fp32, int64_t M, int C, const float* gamma,

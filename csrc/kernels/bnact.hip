@@ -1086,6 +1086,204 @@ __global__ __launch_bounds__(kB) void bn_bwd_fused_kernel(const uint16_t* __rest
   }
 }
 
+// ---------------------------------------------------------------- fp32 single-launch variants
+// The fp32 step (the reference harness's precision) runs ~28 small BN layers per direction in
+// ResNet-50 (stages 2-4 at batch 32: 1.6-13 MB per tensor) where the two-kernel path is bound by
+// two launches and two serial reduction tails, not by bytes.  Same structure as the bf16
+// kernels above -- the block's rows stay in REGISTERS (V 8-channel rows of 32 B per thread per
+// operand: two 16-B buffer loads), the arrival tree publishes the coefficients, every block
+// waits for its tile's finisher and finishes the elementwise pass from the registers -- with
+// the fp32 numerics of the two-kernel path (fp64 fixed-order tree: deterministic).
+// Backward variants: RELU (saved 1-bit mask), DY2 (dual output: dz = [y>0] (dy + dy2)), RES
+// (write d(residual) = dz).  Buffers < 1 GiB (32-bit offsets with the +1 GiB out-of-range push).
+__device__ __forceinline__ void ldf8(__amdgpu_buffer_rsrc_t rs, int voff, int soff, float* v) {
+  const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0);
+  const u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 16, soff, 0);
+  v[0] = __uint_as_float(a.x); v[1] = __uint_as_float(a.y); v[2] = __uint_as_float(a.z); v[3] = __uint_as_float(a.w);
+  v[4] = __uint_as_float(b.x); v[5] = __uint_as_float(b.y); v[6] = __uint_as_float(b.z); v[7] = __uint_as_float(b.w);
+}
+
+// whole offset in the VGPR, soffset 0 (see store_raw: the register-soffset store hazard)
+__device__ __forceinline__ void stf8(__amdgpu_buffer_rsrc_t rs, int off, const float* v) {
+  __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                                               __float_as_uint(v[3])}, rs, off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]),
+                                               __float_as_uint(v[7])}, rs, off + 16, 0, 0);
+}
+
+// fp32 row map: byte offsets of 4-byte elements (row_map is the bf16 one)
+__device__ __forceinline__ RowMap row_map_f32(const Red& R, int V) {
+  RowMap m = row_map(R, V);
+  const int cg = threadIdx.x % R.tprp, rs = threadIdx.x / R.tprp;
+  const int64_t b0 = (int64_t)blockIdx.x * R.rows_per_blk;
+  m.voff = (int)(((int64_t)rs * R.C + m.col) * 4);
+  m.sbase = (int)(b0 * R.C * 4);
+  m.sstep = R.rpi * R.C * 4;
+  (void)cg;
+  return m;
+}
+
+template <int V>
+__device__ __forceinline__ void load_rows_f32(const float* __restrict__ p, const Red& R, const RowMap& m,
+                                              float (&buf)[V][8]) {
+  const __amdgpu_buffer_rsrc_t rs = rsrc(p, R.M * R.C * 4);
+#pragma unroll
+  for (int u = 0; u < V; ++u) ldf8(rs, voff_u(m, u), m.sbase + u * m.sstep, buf[u]);
+}
+
+template <int V>
+__device__ __forceinline__ void launder_f32(float (&b)[V][8]) {
+#pragma unroll
+  for (int u = 0; u < V; ++u)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(b[u][j]));
+}
+
+template <int V, bool RELU, bool RES>
+__global__ __launch_bounds__(kB) void bn_fwd_fused_f32_kernel(const float* __restrict__ x, const float* __restrict__ res,
+                                                              Red R, StatsOut o, float* __restrict__ y,
+                                                              uint8_t* __restrict__ mask) {
+  const RowMap m = row_map_f32(R, V);
+  float xb[V][8];
+  load_rows_f32<V>(x, R, m, xb);
+  float s[8], q[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
+#pragma unroll
+  for (int u = 0; u < V; ++u)  // rows past the end load as zeros: no effect on the sums
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s[j] += xb[u][j];
+      q[j] = fmaf(xb[u][j], xb[u][j], q[j]);
+    }
+  const Flag f = tile_flag(R);
+  if (block_reduce_tree(R, s, q)) {
+    finish_stats(R, o, [](float* p, float v) { store_sc1(p, v); });
+    publish(f);
+  }
+  wait_published(f);
+  launder_f32<V>(xb);
+  float sc[8], sh[8];
+  if (m.active) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sc[j] = ld_sc1(o.save + 2 * R.C + m.col + j);
+      sh[j] = ld_sc1(o.save + 3 * R.C + m.col + j);
+    }
+  }
+  const __amdgpu_buffer_rsrc_t ys = rsrc(y, R.M * R.C * 4);
+  const __amdgpu_buffer_rsrc_t rr = rsrc(RES ? res : x, R.M * R.C * 4);
+#pragma unroll
+  for (int u = 0; u < V; ++u) {
+    float out[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out[j] = fmaf(xb[u][j], sc[j], sh[j]);
+    if constexpr (RES) {  // the residual is read only now (no registers held across the wait)
+      float rv[8];
+      ldf8(rr, voff_u(m, u), m.sbase + u * m.sstep, rv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) out[j] += rv[j];
+    }
+    uint32_t b = 0;
+    if constexpr (RELU) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        out[j] = fmaxf(out[j], 0.f);
+        b |= (out[j] > 0.f ? 1u : 0u) << j;
+      }
+    }
+    stf8(ys, voff_u(m, u) + m.sbase + u * m.sstep, out);
+    if constexpr (RELU)
+      if (u < m.nvalid) mask[(m.row0 + (int64_t)u * R.rpi) * (R.C >> 3) + (m.col >> 3)] = (uint8_t)b;
+  }
+}
+
+template <int V, bool RELU, bool DY2, bool RES>
+__global__ __launch_bounds__(kB) void bn_bwd_fused_f32_kernel(const float* __restrict__ dy, const float* __restrict__ dy2,
+                                                              const float* __restrict__ x,
+                                                              const uint8_t* __restrict__ mask, Red R, GradOut o,
+                                                              float* __restrict__ dx, float* __restrict__ dres) {
+  const RowMap m = row_map_f32(R, V);
+  float db[V][8], xb[V][8];
+  load_rows_f32<V>(dy, R, m, db);
+  load_rows_f32<V>(x, R, m, xb);
+  if constexpr (DY2) {
+    const __amdgpu_buffer_rsrc_t r2 = rsrc(dy2, R.M * R.C * 4);
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+      float e[8];
+      ldf8(r2, voff_u(m, u), m.sbase + u * m.sstep, e);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) db[u][j] += e[j];
+    }
+  }
+  if constexpr (RELU) {  // db <- dz = dy * [y > 0]
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+      const uint32_t mb = u < m.nvalid ? mask[(m.row0 + (int64_t)u * R.rpi) * (R.C >> 3) + (m.col >> 3)] : 0u;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) db[u][j] = (mb >> j) & 1u ? db[u][j] : 0.f;
+    }
+  }
+  float mu[8], s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    mu[j] = m.active ? o.save[m.col + j] : 0.f;
+    s1[j] = s2[j] = 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < V; ++u)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s1[j] += db[u][j];
+      s2[j] = fmaf(db[u][j], xb[u][j] - mu[j], s2[j]);
+    }
+  const Flag f = tile_flag(R);
+  if (block_reduce_tree(R, s1, s2)) {
+    const int CT = R.CT, C = R.C;
+    const double* total = R.total + (size_t)blockIdx.y * 2 * CT;
+    const double inv_m = 1.0 / (double)R.M;
+    for (int cl = threadIdx.x; cl < CT; cl += kB) {
+      const int c = blockIdx.y * CT + cl;
+      const double S1 = total[cl], S2 = total[CT + cl];
+      const float mean = o.save[c], invstd = o.save[C + c];
+      const float ga = o.gamma ? o.gamma[c] : 1.f;
+      const double dg = S2 * (double)invstd;
+      if (o.dgamma) o.dgamma[c] = (float)dg;
+      if (o.dbeta) o.dbeta[c] = (float)S1;
+      const double a = (double)ga * invstd;
+      const double b = -a * invstd * dg * inv_m;
+      store_sc1(o.coef + c, (float)a);
+      store_sc1(o.coef + C + c, (float)b);
+      store_sc1(o.coef + 2 * C + c, (float)(-a * S1 * inv_m - b * mean));
+    }
+    publish(f);
+  }
+  wait_published(f);
+  launder_f32<V>(db);
+  launder_f32<V>(xb);
+  float ca[8], cb[8], cc[8];
+  if (m.active) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ca[j] = ld_sc1(o.coef + m.col + j);
+      cb[j] = ld_sc1(o.coef + R.C + m.col + j);
+      cc[j] = ld_sc1(o.coef + 2 * R.C + m.col + j);
+    }
+  }
+  const __amdgpu_buffer_rsrc_t dxs = rsrc(dx, R.M * R.C * 4);
+  const __amdgpu_buffer_rsrc_t drs = rsrc(RES ? dres : dx, R.M * R.C * 4);
+#pragma unroll
+  for (int u = 0; u < V; ++u) {
+    float out[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out[j] = fmaf(ca[j], db[u][j], fmaf(cb[j], xb[u][j], cc[j]));
+    const int off = voff_u(m, u) + m.sbase + u * m.sstep;
+    stf8(dxs, off, out);
+    if constexpr (RES) stf8(drs, off, db[u]);  // d(residual) = dz
+  }
+}
+
 // ---------------------------------------------------------------- host-side geometry
 // Arrival counters: a device pool of per-launch slots (kSlotWords counters each) taken
 // round-robin; the final blocks re-arm their tile's counters, so graph replays reuse a slot and
@@ -1293,6 +1491,81 @@ int pick_fused_v(int64_t M, int C, bool bwd) {
   return 0;
 }
 
+// fp32 single-launch variants (bn_fwd_fused_f32_kernel / bn_bwd_fused_f32_kernel): opt-in
+// (GRACE_BN_FUSED_F32=1 or bn_set_fused_f32(true)).  Measured SLOWER than the two-kernel path
+// on MI355X (profiles/r4_bnfused_bench.txt, graph-replayed per shape: c256@14 fwd 17.2 vs 14.3 us,
+// c512@7 fwd 13.8 vs 10.5 / bwd 19.6 vs 13.1 us; whole fp32 headline 2648 vs 2678 img/s): in a
+// graph the second launch costs ~1.5 us while the in-kernel hand-off (tree -> publish -> every
+// block's wait -> coefficient loads) serialises the elementwise pass behind the slowest block.
+int g_fused32_mode = -1;
+bool fused32_enabled() {
+  if (g_fused32_mode < 0) {
+    const char* e = getenv("GRACE_BN_FUSED_F32");
+    g_fused32_mode = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_fused32_mode == 1;
+}
+
+template <int V>
+int fwd_cap_f32(int cus) {
+  return std::min(std::min(half_occupancy(bn_fwd_fused_f32_kernel<V, true, true>, cus),
+                           half_occupancy(bn_fwd_fused_f32_kernel<V, true, false>, cus)),
+                  std::min(half_occupancy(bn_fwd_fused_f32_kernel<V, false, true>, cus),
+                           half_occupancy(bn_fwd_fused_f32_kernel<V, false, false>, cus)));
+}
+template <int V>
+int bwd_cap_f32(int cus) {
+  int c = half_occupancy(bn_bwd_fused_f32_kernel<V, true, true, true>, cus);
+  c = std::min(c, half_occupancy(bn_bwd_fused_f32_kernel<V, true, false, false>, cus));
+  c = std::min(c, half_occupancy(bn_bwd_fused_f32_kernel<V, false, false, false>, cus));
+  c = std::min(c, half_occupancy(bn_bwd_fused_f32_kernel<V, false, false, true>, cus));
+  c = std::min(c, half_occupancy(bn_bwd_fused_f32_kernel<V, true, true, false>, cus));
+  return c;
+}
+
+struct FusedCaps32 {
+  int cap[2][4] = {};  // [bwd][V index of kFusedVs]
+  int target = 256;
+  bool init = false;
+};
+FusedCaps32 g_caps32[64];
+
+const FusedCaps32& caps32() {
+  int dev = 0;
+  GRACE_HIP_CHECK(hipGetDevice(&dev));
+  FusedCaps32& c = g_caps32[dev];
+  if (!c.init) {
+    int cus = 0;
+    GRACE_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    c.target = cus;
+    c.cap[0][0] = fwd_cap_f32<2>(cus);
+    c.cap[0][1] = fwd_cap_f32<4>(cus);
+    c.cap[0][2] = fwd_cap_f32<8>(cus);
+    c.cap[0][3] = fwd_cap_f32<16>(cus);
+    c.cap[1][0] = bwd_cap_f32<2>(cus);
+    c.cap[1][1] = bwd_cap_f32<4>(cus);
+    c.cap[1][2] = bwd_cap_f32<8>(cus);
+    c.cap[1][3] = 0;  // 2-3 operands x 16 rows x 8 fp32: too many registers
+    c.init = true;
+  }
+  return c;
+}
+
+// The V whose grid holds between half a block and one block per CU (and fits co-resident in
+// half of the kernel's occupancy); 0 = the two-kernel path.  Largest V first (fuller blocks).
+int pick_fused_v_f32(int64_t M, int C, bool bwd) {
+  if (!fused32_enabled() || M * C * 4 >= ((int64_t)1 << 30)) return 0;
+  const FusedCaps32& c = caps32();
+  const int tiles = C / (C < kTileC ? C : kTileC);
+  for (int i = 3; i >= 0; --i) {
+    const Red R = plan(M, C, kFusedVs[i]);
+    const int64_t blocks = (int64_t)R.nchunks * tiles;
+    if (c.cap[bwd][i] > 0 && blocks <= std::min(c.cap[bwd][i], c.target) && 2 * blocks >= c.target)
+      return kFusedVs[i];
+  }
+  return 0;
+}
+
 int64_t even(int64_t n) { return (n + 1) & ~(int64_t)1; }
 
 int64_t ws_floats(const Red& R) {
@@ -1339,6 +1612,10 @@ int64_t bn_workspace_floats(int64_t M, int C) {
 int bn_fused_v(int64_t M, int C, bool bwd) { return pick_fused_v(M, C, bwd); }
 
 void bn_set_fused(bool on) { g_fused_mode = on ? 1 : 0; }
+
+void bn_set_fused_f32(bool on) { g_fused32_mode = on ? 1 : 0; }
+
+int bn_fused_v_f32(int64_t M, int C, bool bwd) { return pick_fused_v_f32(M, C, bwd); }
 
 void bn_set_deterministic(bool on);
 
@@ -1534,9 +1811,33 @@ void bn_act_forward(const void* xv, const void* resv, bool fp32, int64_t M, int 
                     const float* beta, float* running_mean, float* running_var, int64_t* nbt, float momentum,
                     float eps, bool relu, float* save, float* ws, void* yv, uint8_t* mask, hipStream_t stream) {
   StatsOut o{gamma, beta, running_mean, running_var, nbt, momentum, eps, save};
-  if (fp32) {  // two-kernel path only (the single-launch variants hold bf16 rows in registers)
-    forward_2k(static_cast<const float*>(xv), static_cast<const float*>(resv), M, C, o, relu, save, ws,
-               static_cast<float*>(yv), mask, stream);
+  if (fp32) {
+    const float* xf = static_cast<const float*>(xv);
+    const float* rf = static_cast<const float*>(resv);
+    float* yf = static_cast<float*>(yv);
+    if (const int v = pick_fused_v_f32(M, C, false)) {
+      Red R = plan(M, C, v);
+      bind_ws(R, ws, stream);
+      const dim3 grid(R.nchunks, C / R.CT);
+#define GRACE_BN_FWD32(V)                                                                                         \
+  if (v == V) {                                                                                                   \
+    if (relu && rf)                                                                                               \
+      hipLaunchKernelGGL((bn_fwd_fused_f32_kernel<V, true, true>), grid, dim3(kB), 0, stream, xf, rf, R, o, yf, mask);   \
+    else if (relu)                                                                                                \
+      hipLaunchKernelGGL((bn_fwd_fused_f32_kernel<V, true, false>), grid, dim3(kB), 0, stream, xf, rf, R, o, yf, mask);  \
+    else if (rf)                                                                                                  \
+      hipLaunchKernelGGL((bn_fwd_fused_f32_kernel<V, false, true>), grid, dim3(kB), 0, stream, xf, rf, R, o, yf, mask);  \
+    else                                                                                                          \
+      hipLaunchKernelGGL((bn_fwd_fused_f32_kernel<V, false, false>), grid, dim3(kB), 0, stream, xf, rf, R, o, yf, mask); \
+    return;                                                                                                       \
+  }
+      GRACE_BN_FWD32(2)
+      GRACE_BN_FWD32(4)
+      GRACE_BN_FWD32(8)
+      GRACE_BN_FWD32(16)
+#undef GRACE_BN_FWD32
+    }
+    forward_2k(xf, rf, M, C, o, relu, save, ws, yf, mask, stream);
     return;
   }
   const uint16_t* x = static_cast<const uint16_t*>(xv);
@@ -1597,8 +1898,43 @@ void bn_act_backward(const void* dyv, const void* dy2v, const void* xv, bool fp3
   // atomic totals (one arrival + a totals-only finisher) up to the chunk-count threshold
   const bool atomic = !deterministic && !bn_deterministic_env() && plan(M, C).nchunks <= bn_atomic_max_chunks();
   if (fp32) {
-    backward_2k(static_cast<const float*>(dyv), static_cast<const float*>(dy2v), static_cast<const float*>(xv), mask,
-                M, C, o, relu, atomic, ws, static_cast<float*>(dxv), static_cast<float*>(dresv), stream);
+    const float* dyf = static_cast<const float*>(dyv);
+    const float* dy2f = static_cast<const float*>(dy2v);
+    const float* xf = static_cast<const float*>(xv);
+    float* dxf = static_cast<float*>(dxv);
+    float* drf = static_cast<float*>(dresv);
+    // the single-launch variant needs the saved mask for a ReLU (the stem's RX form stays 2-kernel)
+    const int v = (relu && mask == nullptr) ? 0 : pick_fused_v_f32(M, C, true);
+    if (v) {
+      Red R = plan(M, C, v);
+      bind_ws(R, ws, stream);
+      const dim3 grid(R.nchunks, C / R.CT);
+#define GRACE_BN_BWD32_K(V, RL, D2, RS) \
+  hipLaunchKernelGGL((bn_bwd_fused_f32_kernel<V, RL, D2, RS>), grid, dim3(kB), 0, stream, dyf, dy2f, xf, mask, R, o, dxf, drf)
+#define GRACE_BN_BWD32(V)                                                   \
+  if (v == V) {                                                             \
+    if (relu) {                                                             \
+      if (dy2f && drf) GRACE_BN_BWD32_K(V, true, true, true);               \
+      else if (dy2f) GRACE_BN_BWD32_K(V, true, true, false);                \
+      else if (drf) GRACE_BN_BWD32_K(V, true, false, true);                 \
+      else GRACE_BN_BWD32_K(V, true, false, false);                         \
+    } else {                                                                \
+      if (dy2f && drf) GRACE_BN_BWD32_K(V, false, true, true);              \
+      else if (dy2f) GRACE_BN_BWD32_K(V, false, true, false);               \
+      else if (drf) GRACE_BN_BWD32_K(V, false, false, true);                \
+      else GRACE_BN_BWD32_K(V, false, false, false);                        \
+    }                                                                       \
+    return;                                                                 \
+  }
+      GRACE_BN_BWD32(2)
+      GRACE_BN_BWD32(4)
+      GRACE_BN_BWD32(8)
+#undef GRACE_BN_BWD32
+#undef GRACE_BN_BWD32_K
+    }
+    // atomic totals contend on 2C addresses from every block: for C <= 64 (one narrow tile) the
+    // fixed-order tree is faster (benchmarks/bnact_bench.py fp32, profiles/r4_bnbench.txt)
+    backward_2k(dyf, dy2f, xf, mask, M, C, o, relu, atomic && C > 64, ws, dxf, drf, stream);
     return;
   }
   const uint16_t* dy = static_cast<const uint16_t*>(dyv);

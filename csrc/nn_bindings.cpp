@@ -303,6 +303,8 @@ void grace_bind_nn(py::module& m) {
   m.def("bn_supported", &bn_supported);
   m.def("bn_fused_v", [](int64_t M, int64_t C, bool bwd) { return grace::bn_fused_v(M, (int)C, bwd); });
   m.def("bn_set_fused", &grace::bn_set_fused);
+  m.def("bn_fused_v_f32", [](int64_t M, int64_t C, bool bwd) { return grace::bn_fused_v_f32(M, (int)C, bwd); });
+  m.def("bn_set_fused_f32", &grace::bn_set_fused_f32);
   m.def("bn_spin_timeouts", []() { return (int64_t)grace::bn_spin_timeouts(); });
   m.def("bn_act_fwd", &bn_act_fwd);
   m.def("bn_act_bwd", &bn_act_bwd);

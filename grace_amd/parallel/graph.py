@@ -111,7 +111,10 @@ class GraphedStep:
             if pool is None:
                 pool = g.pool()
             self.graphs.append(g)
-            self.losses.append(loss)
+            # keep the static output, not its autograd graph: the graph would keep the captured
+            # AccumulateGrad nodes (bound to the capture stream) alive into later eager
+            # backwards on other streams (autograd's stream-mismatch warning and syncs)
+            self.losses.append(loss.detach() if isinstance(loss, torch.Tensor) else loss)
         self.graph = self.graphs[0]
         self.loss = self.losses[0]
         self._next = 0

@@ -358,3 +358,55 @@ def test_bnact_atomic_and_tree_backward_agree(dtype, shape, relu, with_res, atom
         tol = 1e-4 * float(a.abs().max()) + 1e-6
         torch.testing.assert_close(b, 2 * a, rtol=1e-3 if dtype == torch.float32 else 2e-2,
                                    atol=tol if dtype == torch.float32 else 100 * tol)
+
+
+def _run_bn(m, x, res, dy, dual, dy2):
+    xx = x.clone().requires_grad_(True)
+    rr = res.clone().requires_grad_(True) if res is not None else None
+    out = m(xx, rr, dual=dual)
+    if dual:
+        torch.autograd.backward([out[0], out[1]], [dy, dy2])
+        y = out[0]
+    else:
+        out.backward(dy)
+        y = out
+    torch.cuda.synchronize()
+    return [y.detach().clone(), xx.grad.clone(), m.weight.grad.clone(), m.bias.grad.clone(),
+            m.running_mean.clone(), m.running_var.clone()] + ([rr.grad.clone()] if rr is not None else [])
+
+
+@pytest.mark.parametrize("shape", [(32, 128, 28, 28), (32, 256, 14, 14), (32, 512, 7, 7), (32, 2048, 7, 7),
+                                   (32, 512, 14, 14), (32, 1024, 14, 14), (7, 256, 9, 11)])
+@pytest.mark.parametrize("relu,with_res,dual", [(True, False, False), (True, True, True), (False, False, False),
+                                                (False, True, False), (True, False, True)])
+def test_bnact_fp32_single_launch_matches_two_kernel(shape, relu, with_res, dual):
+    """fp32 single-launch kernels (rows held in registers, one co-resident launch per direction;
+    opt-in: measured slower than the two-kernel path) give the two-kernel path's results up to
+    the summation order of their differently chunked fixed-order trees."""
+    C = _native.lib()
+    n, c, h, w = shape
+    m, x, res, dy = _case(*shape, relu, with_res, dtype=torch.float32)
+    dy2 = torch.randn_like(dy) if dual else None
+    got = None
+    try:
+        C.bn_set_fused_f32(True)
+        vf, vb = C.bn_fused_v_f32(n * h * w, c, False), C.bn_fused_v_f32(n * h * w, c, True)
+        got = []
+        for _ in range(2):  # second call: the tile counters / generation words were re-armed
+            m.weight.grad = m.bias.grad = None
+            m.running_mean.zero_()
+            m.running_var.fill_(1.0)
+            got = _run_bn(m, x, res, dy, dual, dy2)
+        C.bn_set_fused_f32(False)
+        m.weight.grad = m.bias.grad = None
+        m.running_mean.zero_()
+        m.running_var.fill_(1.0)
+        ref = _run_bn(m, x, res, dy, dual, dy2)
+    finally:
+        C.bn_set_fused_f32(False)
+    if shape[0] == 32 and shape[1] != 1024:
+        assert vf > 0 and vb > 0, (shape, vf, vb)  # the small ResNet-50 shapes take the fused path
+    for a, b in zip(got, ref):
+        tol = 1e-5 * float(b.abs().max()) + 1e-6
+        assert float((a - b).abs().max()) <= tol
+    assert C.bn_spin_timeouts() == 0
