@@ -111,7 +111,8 @@ std::vector<Tensor> bn_act_fwd_partials(const Tensor& x, const c10::optional<Ten
 std::vector<Tensor> bn_act_bwd(const Tensor& dy, const c10::optional<Tensor>& dy2, const Tensor& x,
                                const c10::optional<Tensor>& mask, const c10::optional<Tensor>& weight,
                                const Tensor& save, bool relu, bool want_dres, bool want_dweight,
-                               bool deterministic) {
+                               bool deterministic, const c10::optional<Tensor>& dweight_out,
+                               const c10::optional<Tensor>& dbias_out) {
   int64_t M, C;
   check_rows(x, "x", &M, &C);
   same_layout(x, dy, "grad_output");
@@ -130,8 +131,18 @@ std::vector<Tensor> bn_act_bwd(const Tensor& dy, const c10::optional<Tensor>& dy
   auto f32 = x.options().dtype(at::kFloat);
   Tensor dx = at::empty_like(x);
   Tensor dres = want_dres ? at::empty_like(x) : Tensor();
-  Tensor dg = want_dweight ? at::empty({C}, f32) : Tensor();
-  Tensor db = want_dweight ? at::empty({C}, f32) : Tensor();
+  // dweight_out / dbias_out: the parameters' gradient buffers (a GRACE / DDP bucket view), written
+  // in place so no copy into the bucket follows
+  auto out_or = [&](const c10::optional<Tensor>& o) {
+    if (o.has_value() && o->defined()) {
+      TORCH_CHECK(o->is_cuda() && o->scalar_type() == at::kFloat && o->is_contiguous() && o->numel() == C &&
+                      o->get_device() == x.get_device(), "bn_act_bwd: gradient output must be contiguous fp32 [C]");
+      return *o;
+    }
+    return at::empty({C}, f32);
+  };
+  Tensor dg = want_dweight ? out_or(dweight_out) : Tensor();
+  Tensor db = want_dweight ? out_or(dbias_out) : Tensor();
   Tensor coef = at::empty({3 * C}, f32);
   Tensor ws = at::empty({grace::bn_workspace_floats(M, (int)C)}, f32);
   grace::bn_act_backward(dy.data_ptr(), two ? dy2->data_ptr() : nullptr, x.data_ptr(), x.scalar_type() == at::kFloat,
@@ -307,7 +318,9 @@ void grace_bind_nn(py::module& m) {
   m.def("bn_set_fused_f32", &grace::bn_set_fused_f32);
   m.def("bn_spin_timeouts", []() { return (int64_t)grace::bn_spin_timeouts(); });
   m.def("bn_act_fwd", &bn_act_fwd);
-  m.def("bn_act_bwd", &bn_act_bwd);
+  m.def("bn_act_bwd", &bn_act_bwd, py::arg("dy"), py::arg("dy2"), py::arg("x"), py::arg("mask"), py::arg("weight"),
+        py::arg("save"), py::arg("relu"), py::arg("want_dres"), py::arg("want_dweight"), py::arg("deterministic"),
+        py::arg("dweight_out") = py::none(), py::arg("dbias_out") = py::none());
   m.def("bn_set_deterministic", [](bool on) { grace::bn_set_deterministic(on); });
   m.def("bn_set_atomic_chunks", [](int64_t n) { grace::bn_set_atomic_chunks((int)n); });
   m.def("bn_atomic_chunks", []() { return (int64_t)grace::bn_atomic_chunks(); });

@@ -26,6 +26,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _native
+from . import wgrad as _wg
 
 
 def _fusable(x: torch.Tensor, bn: nn.BatchNorm2d, residual: Optional[torch.Tensor]) -> bool:
@@ -43,6 +44,23 @@ def _fusable(x: torch.Tensor, bn: nn.BatchNorm2d, residual: Optional[torch.Tenso
     if bn.track_running_stats and bn.momentum is None:
         return False
     return True
+
+
+_TARGETS = __import__("os").environ.get("GRACE_BN_GRAD_TARGET", "1") == "1"
+
+
+def _param_targets(ctx, want_w: bool):
+    """The bucket views (GRACE engine / DDP comm hook: ops/wgrad.py grad_target) the BN weight
+    and bias gradients are written into by the backward kernel itself -- AccumulateGrad then
+    steals an alias of the bucket, and neither the engine's gather nor DDP's reducer copies it.
+    (None, None) unless both targets exist (a contiguous fp32 [C] view each)."""
+    if not want_w or not _TARGETS:
+        return None, None
+    w, b = ctx.bn_params
+    tw = _wg.grad_target(w) if w is not None else None
+    tb = _wg.grad_target(b) if b is not None else None
+    ok = all(t is not None and t.is_contiguous() and t.dim() == 1 for t in (tw, tb))
+    return (tw, tb) if ok else (None, None)
 
 
 def _kernel_grad(g: Optional[torch.Tensor], like: torch.Tensor) -> Optional[torch.Tensor]:
@@ -68,6 +86,7 @@ class _BNActFn(torch.autograd.Function):
                                                      float(momentum), float(eps), bool(relu))
         ctx.relu = bool(relu)
         ctx.has_res = residual is not None
+        ctx.bn_params = (weight, bias)
         # the backward needs only the ReLU mask (1 bit per element), not the bf16 output
         ctx.save_for_backward(x, mask if relu else None, weight, save)
         if dual:
@@ -91,10 +110,12 @@ class _BNActFn(torch.autograd.Function):
         # forward (retain_graph) takes the deterministic fixed-order tree instead
         again = getattr(ctx, "bwd_done", False)
         ctx.bwd_done = True
+        tw, tb = _param_targets(ctx, want_w)
         dx, dres, dw, db = _native.lib().bn_act_bwd(dy, dy2, x, mask, weight, save, ctx.relu,
-                                                    ctx.has_res and ctx.needs_input_grad[1], want_w, again)
+                                                    ctx.has_res and ctx.needs_input_grad[1], want_w, again, tw, tb)
+        dw, db = _wg.into_target(dw, tw) if want_w else None, _wg.into_target(db, tb) if want_w else None
         return (dx, dres if ctx.has_res and ctx.needs_input_grad[1] else None,
-                dw if want_w else None, db if want_w and ctx.needs_input_grad[3] else None,
+                dw, db if ctx.needs_input_grad[3] else None,
                 None, None, None, None, None, None, None, None, None)
 
 
@@ -141,6 +162,7 @@ class _BNActPoolFn(torch.autograd.Function):
         y, save, code = _native.lib().bn_act_pool_fwd(x, weight, bias, running_mean, running_var, nbt,
                                                       float(momentum), float(eps), k, s, pad)
         ctx.geom = (k, s, pad)
+        ctx.bn_params = (weight, bias)
         ctx.save_for_backward(x, code, weight, save)
         return y
 
@@ -158,8 +180,10 @@ class _BNActPoolFn(torch.autograd.Function):
         # mask None: the ReLU mask is recomputed from x and save's scale / shift
         again = getattr(ctx, "bwd_done", False)
         ctx.bwd_done = True
-        dx, _, dw, db = C.bn_act_bwd(dy, None, x, None, weight, save, True, False, want_w, again)
-        return (dx, dw if want_w else None, db if want_w and ctx.needs_input_grad[2] else None,
+        tw, tb = _param_targets(ctx, want_w)
+        dx, _, dw, db = C.bn_act_bwd(dy, None, x, None, weight, save, True, False, want_w, again, tw, tb)
+        dw, db = _wg.into_target(dw, tw) if want_w else None, _wg.into_target(db, tb) if want_w else None
+        return (dx, dw, db if ctx.needs_input_grad[2] else None,
                 None, None, None, None, None, None, None, None)
 
 

@@ -42,6 +42,12 @@ def mark_ddp_params(params) -> None:
     _wg.mark_joinable(params, on=False)
 
 
+# DDP-managed weight gradients stay in line.  Side-stream weight gradients for stable DDP buckets
+# were measured slower on the graphed ResNet-50 step (2384-2388 vs 2487-2488 img/s in line, host
+# issue 10.2 vs 0.15 ms per step: the forked capture falls off HIP's packet-capture launch path;
+# profiles/r4_ddp_surface.txt), so the reducer's mid-backward reads never race a side stream.
+
+
 class GraceHookState:
     def __init__(self, grc: Communicator, name: str = "ddp", model: Optional[torch.nn.Module] = None):
         """``model``: the DistributedDataParallel module the hook is registered on -- pass it so
@@ -96,8 +102,8 @@ class GraceHookState:
             self._views[idx] = buf.data_ptr()
             # with gradient_as_bucket_view DDP makes each .grad a view of the bucket: mark those
             # views as the parameters' gradient targets, so weight-gradient producers
-            # (ops/wgrad.py) write straight into the bucket (in line) and the reducer finds an
-            # alias instead of copying
+            # (ops/wgrad.py) write straight into the bucket and the reducer finds an alias
+            # instead of copying
             for p, g in zip(params, bucket.gradients()):
                 if p.grad is not None and p.grad.data_ptr() == g.data_ptr() and p.grad.shape == g.shape:
                     p._grace_grad_view = g
@@ -184,18 +190,33 @@ def grace_comm_hook(state: GraceHookState, bucket: dist.GradBucket) -> torch.fut
     cs, ds = state._streams(dev)
     cur = torch.cuda.current_stream(dev)
     cs.wait_stream(cur)
+    from ..ops import wgrad as _wg
+
+    _wg.join(cs)  # any side-stream weight gradient issued so far (none for DDP-managed weights)
     with torch.cuda.stream(cs):
         g = packed(buf)
         handles, ctx = grc.send_step(g, name)  # compress + async collective (comm stream or inline)
     ds.wait_stream(cs)  # decode after this bucket's compress/issue; the collective is waited on inside
     fut = torch.futures.Future(devices=[dev])
+    in_place = pidx is None and buf.dtype == torch.float32 and g.data_ptr() == buf.data_ptr()
     with torch.cuda.stream(ds):
         # the payload tensors and the context's per-call tensors cross to the decode stream
         # (not a deep walk of the context: its layout holds long-lived cached device tables)
         _record(handles, ds)
         _record(getattr(ctx, "extra", None), ds)
         _record(getattr(ctx, "out", None), ds)
-        out = unpacked(grc.receive_step(handles, ctx))
+        if in_place and hasattr(ctx, "out"):
+            ctx.out = buf  # decode straight into the bucket (compress has consumed it)
+        out = grc.receive_step(handles, ctx)
+        if in_place:
+            # hand DDP its OWN bucket buffer: the reducer then finds every parameter's gradient
+            # already aliasing its bucket view; any other tensor makes it copy the result into
+            # each parameter's gradient, one copy kernel per parameter (161 for ResNet-50)
+            if out.data_ptr() != buf.data_ptr():
+                buf.copy_(out.reshape(-1).view_as(buf))
+            out = buf
+        else:
+            out = unpacked(out)
         buf.record_stream(ds)
         g.record_stream(ds)
         fut.set_result(out)

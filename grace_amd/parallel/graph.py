@@ -96,11 +96,7 @@ class GraphedStep:
         # GRACE_GRAPH_PRIORITY=-1: capture and replay on a high-priority stream (the compute
         # stream of the step then outranks the side streams it forks)
         prio = int(os.environ.get("GRACE_GRAPH_PRIORITY", "0"))
-        # capture on the warm-up stream: the parameters' AccumulateGrad nodes (kept alive across
-        # iterations, e.g. by a returned loss's graph or a DDP reducer) remember the stream they
-        # were created on, and a capture on another stream makes autograd warn about (and sync
-        # for) the mismatch on every backward
-        self.stream = stream if stream is not None else (torch.cuda.Stream(priority=prio) if prio else side)
+        self.stream = stream if stream is not None else (torch.cuda.Stream(priority=prio) if prio else None)
         self.graphs = []
         self.losses = []
         for i in range(max(1, copies)):
