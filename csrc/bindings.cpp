@@ -438,21 +438,34 @@ void u8_aggregate(const Tensor& base, int64_t rank_stride, int64_t codes_off, in
 }
 
 // ------------------------------------------------------------------------------ DGC
+// u / v (optional, DgcMemory state of x's layout): x is the raw gradient, the samples are taken
+// of the compensated v' = v + (m u + g) (first: g) without writing it
 void dgc_sample(const Tensor& x, const Tensor& seg_off, const Tensor& samp_off, int64_t seed,
-                const c10::optional<Tensor>& step, const Tensor& samples) {
+                const c10::optional<Tensor>& step, const Tensor& samples, const c10::optional<Tensor>& u,
+                const c10::optional<Tensor>& v, double momentum, bool first) {
   CHECK_F32(x);
   CHECK_I64(seg_off);
   CHECK_I64(samp_off);
   CHECK_F32(samples);
   TORCH_CHECK(seg_off.numel() == samp_off.numel(), "offset tables");
+  const bool comp = u.has_value() && u->defined();
+  if (comp) {
+    CHECK_F32(*u);
+    CHECK_F32(*v);
+    TORCH_CHECK(u->numel() == x.numel() && v->numel() == x.numel(), "dgc_sample: u / v like x");
+  }
   DevGuard guard(x.device());
   grace::dgc_sample(x.data_ptr<float>(), (int)seg_off.numel() - 1, seg_off.data_ptr<int64_t>(),
                     samp_off.data_ptr<int64_t>(), samples.numel(), seed_arg(seed, step), samples.data_ptr<float>(),
-                    cur_stream());
+                    comp ? u->data_ptr<float>() : nullptr, comp ? v->data_ptr<float>() : nullptr, (float)momentum,
+                    first ? 1 : 0, cur_stream());
 }
 
+// u / v (optional): x is the raw gradient; the first count pass applies DgcMemory's compensate in
+// place (u = m u + g; v = v + u; first: u = v = g) and later passes read v
 void dgc_refine(const Tensor& x, const Tensor& state, const Tensor& target, int64_t max_iters, const Tensor& thr,
-                const Tensor& count, const Tensor& done, const Tensor& seg, const Tensor& cb, const Tensor& ce) {
+                const Tensor& count, const Tensor& done, const Tensor& seg, const Tensor& cb, const Tensor& ce,
+                const c10::optional<Tensor>& u, const c10::optional<Tensor>& v, double momentum, bool first) {
   CHECK_F32(x);
   CHECK_I32(state);
   CHECK_F32(target);
@@ -460,13 +473,23 @@ void dgc_refine(const Tensor& x, const Tensor& state, const Tensor& target, int6
   CHECK_I32(count);
   CHECK_I32(done);
   const int n_seg = (int)target.numel();
-  TORCH_CHECK(thr.numel() == n_seg && count.numel() >= 8 * n_seg && done.numel() == n_seg && state.numel() >= 2 * n_seg,
-              "per-segment tables (count: 8 words per segment)");
+  TORCH_CHECK(thr.numel() == n_seg && count.numel() >= 32 * n_seg && done.numel() == n_seg && state.numel() >= 2 * n_seg,
+              "per-segment tables (count: 32 words per segment)");
+  const bool comp = u.has_value() && u->defined();
+  if (comp) {
+    CHECK_F32(*u);
+    CHECK_F32(*v);
+    TORCH_CHECK(u->numel() == x.numel() && v->numel() == x.numel() && u->is_contiguous() && v->is_contiguous() &&
+                    (reinterpret_cast<uintptr_t>(u->data_ptr()) - reinterpret_cast<uintptr_t>(x.data_ptr())) % 16 == 0 &&
+                    (reinterpret_cast<uintptr_t>(v->data_ptr()) - reinterpret_cast<uintptr_t>(x.data_ptr())) % 16 == 0,
+                "dgc_refine: u / v contiguous like x with x's 16-B alignment");
+  }
   auto ct = make_ct(seg, cb, ce);
   DevGuard guard(x.device());
   grace::dgc_refine(ct, n_seg, x.data_ptr<float>(), reinterpret_cast<const grace::TopkState*>(state.data_ptr<int32_t>()),
                     target.data_ptr<float>(), (int)max_iters, thr.data_ptr<float>(), count.data_ptr<int32_t>(),
-                    done.data_ptr<int32_t>(), cur_stream());
+                    done.data_ptr<int32_t>(), comp ? u->data_ptr<float>() : nullptr,
+                    comp ? v->data_ptr<float>() : nullptr, (float)momentum, first ? 1 : 0, x.numel(), cur_stream());
 }
 
 // capacity = out_val.numel(); vmask/umask (optional, DgcMemory fused): zeroed where sent
@@ -594,7 +617,8 @@ void sketch_encode(const Tensor& x, const Tensor& edges, int64_t q, const Tensor
   CHECK_F32(edges);
   CHECK_F32(means);
   CHECK_DEV(bins);
-  TORCH_CHECK(q >= 1 && q <= 1024, "quantiles must be in [1, 1024]");
+  TORCH_CHECK(q >= 1 && q <= 65535, "quantiles must be in [1, 65535]");
+  TORCH_CHECK(q < 256 || bins.element_size() == 2, "q >= 256 needs 16-bit bin codes");
   TORCH_CHECK(bins.numel() >= x.numel(), "bins too small");
   TORCH_CHECK(sums.scalar_type() == at::kLong && counts.scalar_type() == at::kInt && arrive.scalar_type() == at::kInt &&
                   seg_chunk_begin.scalar_type() == at::kInt,
@@ -605,6 +629,13 @@ void sketch_encode(const Tensor& x, const Tensor& edges, int64_t q, const Tensor
               "sketch_encode: tables too small");
   auto ct = make_ct(seg, cb, ce);
   DevGuard guard(x.device());
+  if (q > 1024) {  // global bin accumulators (csrc/kernels/cast_sketch.hip sketch_encode_big)
+    grace::sketch_encode_big(ct, (int)n_seg, x.data_ptr<float>(), edges.data_ptr<float>(), (int)q, bins.data_ptr(),
+                             (int)bins.element_size(), reinterpret_cast<unsigned long long*>(sums.data_ptr<int64_t>()),
+                             reinterpret_cast<uint32_t*>(counts.data_ptr<int32_t>()), arrive.data_ptr<int32_t>(),
+                             seg_chunk_begin.data_ptr<int32_t>(), means.data_ptr<float>(), cur_stream());
+    return;
+  }
   grace::sketch_encode(ct, x.data_ptr<float>(), edges.data_ptr<float>(), (int)q, bins.data_ptr(),
                        (int)bins.element_size(), reinterpret_cast<unsigned long long*>(sums.data_ptr<int64_t>()),
                        reinterpret_cast<uint32_t*>(counts.data_ptr<int32_t>()), arrive.data_ptr<int32_t>(),
@@ -967,8 +998,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("natural_aggregate", &natural_aggregate);
   m.def("u8_encode", &u8_encode);
   m.def("u8_aggregate", &u8_aggregate);
-  m.def("dgc_sample", &dgc_sample);
-  m.def("dgc_refine", &dgc_refine);
+  m.def("dgc_sample", &dgc_sample, py::arg("x"), py::arg("seg_off"), py::arg("samp_off"), py::arg("seed"),
+        py::arg("step"), py::arg("samples"), py::arg("u") = py::none(), py::arg("v") = py::none(),
+        py::arg("momentum") = 0.0, py::arg("first") = false);
+  m.def("dgc_refine", &dgc_refine, py::arg("x"), py::arg("state"), py::arg("target"), py::arg("max_iters"),
+        py::arg("thr"), py::arg("count"), py::arg("done"), py::arg("seg"), py::arg("cb"), py::arg("ce"),
+        py::arg("u") = py::none(), py::arg("v") = py::none(), py::arg("momentum") = 0.0, py::arg("first") = false);
   m.def("dgc_compact", &dgc_compact);
   m.def("dgc_compensate", &dgc_compensate);
   m.def("powersgd_mq", &powersgd_mq);

@@ -90,10 +90,14 @@ void u8_aggregate(const ChunkTable& ct, const uint8_t* base, int64_t rank_stride
                   int n_ranks, float scale, float* out, bool accumulate, hipStream_t stream);
 
 // ---------------------------------------------------------------- dgc.hip
+// u / v non-null: x is the raw gradient and DgcMemory's compensate is applied on the fly (sample)
+// and in place (the first refinement count pass writes u, v); count: int32 [32 n_seg]
 void dgc_sample(const float* x, int n_seg, const int64_t* seg_off, const int64_t* samp_off, int64_t n_samples,
-                SeedArg seed, float* samples, hipStream_t stream);
+                SeedArg seed, float* samples, const float* u, const float* v, float momentum, int first,
+                hipStream_t stream);
 void dgc_refine(const ChunkTable& ct, int n_seg, const float* x, const TopkState* st, const float* target,
-                int max_iters, float* thr, int32_t* count, int32_t* done, hipStream_t stream);
+                int max_iters, float* thr, int32_t* count, int32_t* done, float* u, float* v, float momentum,
+                int first, int64_t n, hipStream_t stream);
 void dgc_compact(const ChunkTable& ct, const float* x, const float* thr, float* out_val, int32_t* out_idx,
                  int64_t cap, int32_t* counter, float* vmask, float* umask, hipStream_t stream);
 void dgc_compensate(const float* g, float* u, float* v, float momentum, int64_t n, bool first, hipStream_t stream);
@@ -118,6 +122,10 @@ void decode16_sum(const uint8_t* base, int64_t rank_stride, int n_ranks, int64_t
 void sketch_encode(const ChunkTable& ct, const float* x, const float* edges, int q, void* bins, int bin_bytes,
                    unsigned long long* sums, uint32_t* counts, int32_t* arrive, const int32_t* seg_chunk_begin,
                    float* means, hipStream_t stream);
+// q > 1024: global fixed-point bin accumulators, torch.searchsorted's binary search
+void sketch_encode_big(const ChunkTable& ct, int n_seg, const float* x, const float* edges, int q, void* bins,
+                       int bin_bytes, unsigned long long* sums, uint32_t* counts, int32_t* arrive,
+                       const int32_t* seg_chunk_begin, float* means, hipStream_t stream);
 void sketch_decode(const ChunkTable& ct, const uint8_t* base, int64_t rank_stride, int64_t bins_off, int64_t means_off,
                    int q, int bin_bytes, int n_ranks, float scale, float* out, hipStream_t stream);
 

@@ -259,6 +259,73 @@ __global__ __launch_bounds__(kBlock) void sketch_encode_kernel(ChunkTable ct, co
   if (threadIdx.x == 0) __hip_atomic_store(&arrive[sg], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ---- q > 1024 (up to 65535 with uint16 bins, the reference's range: sketch.py:22-27) --------
+// The per-wave LDS bin tables above do not fit (56 q bytes per workgroup), so the large-q encode
+// keeps the bin accumulators in global memory: the same int64 fixed-point sums (order-independent,
+// deterministic) and u32 counts, added per element with device-scope atomics, and the same
+// last-workgroup means finisher.  The bin is found by torch.searchsorted's own upper-bound
+// binary search over the whole edge row (start 0, end q + 1, mid = lo + (hi - lo) / 2, step right
+// while !(edge > v)): interpolated quantile edges are NOT always monotone (a (1 - w) + b w with
+// a == b can land one ulp off a), and only the identical probe sequence gives identical bins.
+__device__ __forceinline__ double sk_scale(const float* E, int j, int L) {
+  const float m = fmaxf(fabsf(E[j]), fabsf(E[j + 1]));
+  int ex = 0;
+  if (m > 0.f && isfinite(m)) frexpf(m, &ex);
+  return ldexp(1.0, 62 - L - ex);
+}
+
+template <typename BinT>
+__global__ __launch_bounds__(kBlock) void sketch_encode_big_kernel(ChunkTable ct, const float* __restrict__ x,
+                                                                   const float* __restrict__ edges, int q,
+                                                                   BinT* __restrict__ bins,
+                                                                   unsigned long long* __restrict__ sums,
+                                                                   uint32_t* __restrict__ counts,
+                                                                   int32_t* __restrict__ arrive,
+                                                                   const int32_t* __restrict__ seg_chunk_begin,
+                                                                   float* __restrict__ means) {
+  __shared__ int last;
+  const int c = blockIdx.x;
+  const int sg = ct.seg[c];
+  const int64_t b = ct.begin[c], e = ct.end[c];
+  const int c0 = seg_chunk_begin[sg], c1 = seg_chunk_begin[sg + 1];
+  const int64_t nseg = ct.end[c1 - 1] - ct.begin[c0];
+  const int L = nseg > 1 ? 64 - __clzll((unsigned long long)(nseg - 1)) : 0;
+  const float* E = edges + (int64_t)sg * (q + 1);
+  unsigned long long* SU = sums + (int64_t)sg * q;
+  uint32_t* CN = counts + (int64_t)sg * q;
+  for (int64_t i = b + threadIdx.x; i < e; i += kBlock) {
+    const float v = x[i];
+    int l = 0, r = q + 1;  // torch's cus_upper_bound, probe for probe
+    while (l < r) {
+      const int m = l + ((r - l) >> 1);
+      if (!(E[m] > v))
+        l = m + 1;
+      else
+        r = m;
+    }
+    const int bb = l - 1;
+    const int bin = bb < 0 ? 0 : (bb > q - 1 ? q - 1 : bb);
+    bins[i] = (BinT)bin;
+    __hip_atomic_fetch_add(&SU[bin], (unsigned long long)__double2ll_rn((double)v * sk_scale(E, bin, L)),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(&CN[bin], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave drained its atomics (as above)
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(&arrive[sg], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == c1 - c0 - 1;
+  __syncthreads();
+  if (!last) return;
+  for (int i = threadIdx.x; i < q; i += kBlock) {
+    const long long sv = (long long)__hip_atomic_load(&SU[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t cv = __hip_atomic_load(&CN[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    means[(int64_t)sg * q + i] = cv ? (float)((double)sv / sk_scale(E, i, L) / (double)cv) : 0.f;
+    __hip_atomic_store(&SU[i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&CN[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(&arrive[sg], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <typename BinT>
 __global__ __launch_bounds__(kBlock) void sketch_decode_kernel(ChunkTable ct, const uint8_t* __restrict__ base,
                                                                int64_t rank_stride, int64_t bins_off,
@@ -350,6 +417,18 @@ void sketch_encode(const ChunkTable& ct, const float* x, const float* edges, int
   else
     sketch_encode_kernel<uint16_t><<<ct.n_chunks, kBlock, lds, stream>>>(ct, x, edges, q, (uint16_t*)bins, sums,
                                                                          counts, arrive, seg_chunk_begin, means);
+}
+
+void sketch_encode_big(const ChunkTable& ct, int n_seg, const float* x, const float* edges, int q, void* bins,
+                       int bin_bytes, unsigned long long* sums, uint32_t* counts, int32_t* arrive,
+                       const int32_t* seg_chunk_begin, float* means, hipStream_t stream) {
+  if (ct.n_chunks == 0 || n_seg == 0) return;
+  if (bin_bytes == 1)
+    sketch_encode_big_kernel<uint8_t><<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, edges, q, (uint8_t*)bins, sums,
+                                                                          counts, arrive, seg_chunk_begin, means);
+  else
+    sketch_encode_big_kernel<uint16_t><<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, edges, q, (uint16_t*)bins, sums,
+                                                                           counts, arrive, seg_chunk_begin, means);
 }
 
 void sketch_decode(const ChunkTable& ct, const uint8_t* base, int64_t rank_stride, int64_t bins_off, int64_t means_off,

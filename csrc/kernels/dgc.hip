@@ -38,10 +38,26 @@ __device__ __forceinline__ int find_seg64(const int64_t* __restrict__ off, int n
   return lo;
 }
 
+// Comp (optional): DgcMemory's compensate evaluated AT THE SAMPLE POSITIONS ONLY -- x is g and
+// the sampled value is v' = v + fmaf(m, u, g) (first call: g), the exact float ops of
+// dgc_compensate_kernel -- so the full compensate pass can run fused into the first count pass.
+struct Comp {
+  const float* u;
+  const float* v;
+  float m;
+  int first;  // -1: off (x is the compensated v itself)
+};
+
+__device__ __forceinline__ float comp_at(const float* x, const Comp& c, int64_t i) {
+  const float g = x[i];
+  if (c.first < 0 || c.first == 1) return g;
+  return c.v[i] + fmaf(c.m, c.u[i], g);
+}
+
 __global__ __launch_bounds__(kBlock) void dgc_sample_kernel(const float* __restrict__ x, int n_seg,
                                                             const int64_t* __restrict__ seg_off,
                                                             const int64_t* __restrict__ samp_off, SeedArg sa,
-                                                            float* __restrict__ samples) {
+                                                            float* __restrict__ samples, Comp cp) {
   const int64_t S = samp_off[n_seg];
   const uint64_t seed = sa.get();  // device step mixed in: fresh samples on every graph replay
   const int64_t stride = (int64_t)gridDim.x * kBlock;
@@ -52,7 +68,7 @@ __global__ __launch_bounds__(kBlock) void dgc_sample_kernel(const float* __restr
     // 48 random bits -> uniform position in [0, n)
     const uint64_t u = ((uint64_t)r.x << 16) ^ (uint64_t)(r.y >> 16);
     const int64_t pos = (int64_t)__umul64hi(u << 16, (uint64_t)n);  // floor(u * n / 2^48)
-    samples[j] = fabsf(x[seg_off[s] + (pos < n ? pos : n - 1)]);
+    samples[j] = fabsf(comp_at(x, cp, seg_off[s] + (pos < n ? pos : n - 1)));
   }
 }
 
@@ -71,12 +87,14 @@ __global__ void dgc_init_kernel(int n_seg, const TopkState* __restrict__ st, flo
 // step.  Its next kDepth thresholds form a binary tree from the current root (node k's children:
 // 2k+1 = node x 1.3f, 2k+2 = node x 0.7f, the same float products the sequential loop forms),
 // so ONE pass counts all kTree tree thresholds and the adjust kernel then walks kDepth steps
-// down the tree: ceil(max_iters / kDepth) passes (4 for the reference's 10) instead of
-// max_iters, with bit-identical thresholds and counts.  Per segment, count[8s + k] (k < kTree)
-// holds the tree counts and count[8s + 7] the adjustments made so far.
-constexpr int kDepth = 3;
-constexpr int kTree = (1 << kDepth) - 1;  // 7
-constexpr int kCntStride = 8;
+// down the tree: ceil(max_iters / kDepth) passes (2 for the reference's 10) instead of
+// max_iters, with bit-identical thresholds and counts.  Per segment, count[32s + k] (k < kTree)
+// holds the tree counts and count[32s + 31] the adjustments made so far.  (Depth 5: 31 register
+// counters and 31 compares per element -- VALU work well under the pass's HBM time; depth 3
+// needed 4 passes over the bucket.)
+constexpr int kDepth = 5;
+constexpr int kTree = (1 << kDepth) - 1;  // 31
+constexpr int kCntStride = 32;
 
 __device__ __forceinline__ void tree_thresholds(float root, float* t) {
   t[0] = root;
@@ -87,23 +105,70 @@ __device__ __forceinline__ void tree_thresholds(float root, float* t) {
   }
 }
 
+// FUSE: the first count pass also performs DgcMemory's compensate for its chunk: x is g, and
+// u / v are updated in place (u = m u + g; v = v + u; first: u = v = g) -- the counted value is
+// the new v, exactly as a separate compensate pass followed by a count pass would see it.
+template <bool FUSE>
 __global__ __launch_bounds__(kBlock) void dgc_count_tree_kernel(ChunkTable ct, const float* __restrict__ x,
                                                                 const float* __restrict__ thr,
                                                                 const int32_t* __restrict__ done,
-                                                                int32_t* __restrict__ count) {
+                                                                int32_t* __restrict__ count, float* __restrict__ uu,
+                                                                float* __restrict__ vv, float m, int first) {
   const int c = blockIdx.x;
   const int s = ct.seg[c];
-  if (done[s]) return;
+  if (!FUSE && done[s]) return;  // (the fused pass runs before any segment converged)
   const int64_t b = ct.begin[c], e = ct.end[c];
   float t[kTree];
   tree_thresholds(thr[s], t);
   unsigned cnt[kTree];
 #pragma unroll
   for (int k = 0; k < kTree; ++k) cnt[k] = 0;
-  for (int64_t i = b + threadIdx.x; i < e; i += kBlock) {
-    const float v = fabsf(x[i]);
+  auto one = [&](float val) {
+    const float a = fabsf(val);
 #pragma unroll
-    for (int k = 0; k < kTree; ++k) cnt[k] += v >= t[k] ? 1u : 0u;
+    for (int k = 0; k < kTree; ++k) cnt[k] += a >= t[k] ? 1u : 0u;
+  };
+  auto comp1 = [&](int64_t i) -> float {
+    const float g = x[i];
+    if (!FUSE) return g;
+    float un, vn;
+    if (first) {
+      un = vn = g;
+    } else {
+      un = fmaf(m, uu[i], g);
+      vn = vv[i] + un;
+    }
+    uu[i] = un;
+    vv[i] = vn;
+    return vn;
+  };
+  // 16-B body (x, u, v share their alignment: same offsets into equally aligned buffers)
+  const int64_t mis = (int64_t)((reinterpret_cast<uintptr_t>(x) >> 2) & 3);
+  int64_t a0 = b + ((4 - ((b + mis) & 3)) & 3);
+  if (a0 > e) a0 = e;
+  const int64_t a1 = a0 + ((e - a0) & ~(int64_t)3);
+  for (int64_t i = b + threadIdx.x; i < a0; i += kBlock) one(comp1(i));
+  for (int64_t i = a1 + threadIdx.x; i < e; i += kBlock) one(comp1(i));
+  for (int64_t i = a0 + 4 * (int64_t)threadIdx.x; i < a1; i += 4 * kBlock) {
+    float4 g4 = *reinterpret_cast<const float4*>(x + i);
+    if constexpr (FUSE) {
+      float4 u4, v4;
+      if (first) {
+        u4 = v4 = g4;
+      } else {
+        u4 = *reinterpret_cast<const float4*>(uu + i);
+        v4 = *reinterpret_cast<const float4*>(vv + i);
+        u4 = make_float4(fmaf(m, u4.x, g4.x), fmaf(m, u4.y, g4.y), fmaf(m, u4.z, g4.z), fmaf(m, u4.w, g4.w));
+        v4 = make_float4(v4.x + u4.x, v4.y + u4.y, v4.z + u4.z, v4.w + u4.w);
+      }
+      *reinterpret_cast<float4*>(uu + i) = u4;
+      *reinterpret_cast<float4*>(vv + i) = v4;
+      g4 = v4;
+    }
+    one(g4.x);
+    one(g4.y);
+    one(g4.z);
+    one(g4.w);
   }
   __shared__ unsigned red[kBlock / kWave][kTree];
 #pragma unroll
@@ -249,19 +314,33 @@ inline int grid_for(int64_t n) {
 }  // namespace
 
 void dgc_sample(const float* x, int n_seg, const int64_t* seg_off, const int64_t* samp_off, int64_t n_samples,
-                SeedArg seed, float* samples, hipStream_t stream) {
+                SeedArg seed, float* samples, const float* u, const float* v, float momentum, int first,
+                hipStream_t stream) {
   if (n_samples <= 0) return;
-  dgc_sample_kernel<<<grid_for(n_samples), kBlock, 0, stream>>>(x, n_seg, seg_off, samp_off, seed, samples);
+  const Comp cp{u, v, momentum, u != nullptr ? first : -1};
+  dgc_sample_kernel<<<grid_for(n_samples), kBlock, 0, stream>>>(x, n_seg, seg_off, samp_off, seed, samples, cp);
 }
 
 void dgc_refine(const ChunkTable& ct, int n_seg, const float* x, const TopkState* st, const float* target,
-                int max_iters, float* thr, int32_t* count, int32_t* done, hipStream_t stream) {
+                int max_iters, float* thr, int32_t* count, int32_t* done, float* u, float* v, float momentum,
+                int first, int64_t n, hipStream_t stream) {
   const int g = (n_seg + 255) / 256;
   dgc_init_kernel<<<g, 256, 0, stream>>>(n_seg, st, thr, count, done);
   GRACE_HIP_CHECK(hipMemsetAsync(count, 0, sizeof(int32_t) * (size_t)n_seg * kCntStride, stream));
-  // ceil(max_iters / kDepth) count passes; the count after the last adjustment is never formed
+  const bool fuse = u != nullptr;
+  if (fuse && max_iters <= 0) {  // no count pass to carry the compensate: run it alone
+    dgc_compensate(x, u, v, momentum, n, first != 0, stream);
+    return;
+  }
+  // ceil(max_iters / kDepth) count passes; the count after the last adjustment is never formed.
+  // With u / v given, x is the raw gradient and the FIRST pass applies DgcMemory's compensate
+  // (writing u, v); later passes (and the compaction) read v.
   for (int it = 0; it < max_iters; it += kDepth) {
-    dgc_count_tree_kernel<<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, thr, done, count);
+    if (fuse && it == 0)
+      dgc_count_tree_kernel<true><<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, thr, done, count, u, v, momentum, first);
+    else
+      dgc_count_tree_kernel<false><<<ct.n_chunks, kBlock, 0, stream>>>(ct, fuse ? v : x, thr, done, count, nullptr,
+                                                                       nullptr, 0.f, 0);
     dgc_adjust_tree_kernel<<<g, 256, 0, stream>>>(n_seg, target, thr, count, done, max_iters);
   }
 }

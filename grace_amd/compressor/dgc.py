@@ -34,14 +34,14 @@ class DgcCompressor(BucketCompressor):
         self.max_iters = max_iters
         self.capacity = capacity
 
-    def _select(self, g, ctx, name, vmask=None, umask=None):
+    def _select(self, g, ctx, name, vmask=None, umask=None, compensate=None):
         from ..parallel import health as _health
 
         _health.init_for(g)  # capacity overflows are counted by the decoder (health.overflows())
         cap = D.dgc_capacity(ctx.layout, self.compress_ratio, self.capacity)
         seed, step = self.next_rng(name, g.device)
         hdr, vals, idx = D.dgc_select(g, ctx.layout, self.compress_ratio, self.sample_ratio, self.max_iters,
-                                      seed, cap, step, vmask, umask)
+                                      seed, cap, step, vmask, umask, compensate)
         ctx.extra["sent"] = (hdr, idx)
         return [hdr, vals, idx], ctx
 
@@ -60,9 +60,11 @@ class DgcCompressor(BucketCompressor):
             tensor = memory._clip(tensor, name)
         g = self.flat(tensor)
         u, v, first = memory.state_buffers(name, g)
-        _native.lib().dgc_compensate(g, u, v, memory.momentum, first)
         ctx = self.ctx(tensor, name)
-        return self._select(v, ctx, name, vmask=v, umask=u)
+        # compensate fused into the selection: samples read v + (m u + g) on the fly and the first
+        # refinement count pass writes u and v (csrc/kernels/dgc.hip) -- one pass over the bucket
+        # fewer than compensate-then-select
+        return self._select(g, ctx, name, vmask=v, umask=u, compensate=(memory.momentum, first))
 
     def wire_counts(self, tensors):
         return [None, (0, [4]), (0, [4])]  # [header(selected, cap), values, indices]

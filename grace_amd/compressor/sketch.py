@@ -8,9 +8,10 @@ Here per segment: edges from torch.quantile (linear interpolation, as the refere
 searchsorted clamped to [0, q-1] (values equal to the last edge go to the last bin), bin means
 by index_add.  Payload [bins uint8/int16 | means fp32 (q per segment)].  On the GPU the edges of
 ALL segments come from the native segmented multi-rank radix select (csrc/kernels/quantile.hip;
-any q up to 1024: q >= 128 runs it in batches of 256 ranks per segment), and bucketisation +
-per-bin sums/counts (csrc/kernels/cast_sketch.hip) and the W-rank decode are single passes --
-no sort on the GPU path, graph-capturable for every q.
+any q up to 65535, the reference's uint16 range: q >= 128 runs it in batches of 256 ranks per
+segment), and bucketisation + per-bin sums/counts (csrc/kernels/cast_sketch.hip: per-wave LDS bin
+tables up to q = 1024, global fixed-point accumulators above) and the W-rank decode are single
+passes -- no sort on the GPU path, graph-capturable for every q.
 """
 from __future__ import annotations
 
@@ -167,7 +168,7 @@ class SketchCompressor(BucketCompressor):
         lay, q = ctx.layout, self.quantiles
         bdt = torch.uint8 if q < 256 else torch.int16
         bins, means = self.payload(x.device, [(bdt, (lay.total,)), (torch.float32, (q * lay.n_seg,))])
-        if _native.use_native(x) and q <= 1024:
+        if _native.use_native(x) and q <= 65535:
             edges = native_quantile_edges(x, lay, q)
             t = lay.device_tables(x.device, _CODEC_CHUNK)
             # persistent, self-cleaning totals: the segment's last encode block writes the means and

@@ -281,10 +281,16 @@ class _Conv1x1StatsFn(torch.autograd.Function):
         ctx.wshape = weight.shape
         ctx.weight = weight
         ctx.mark_non_differentiable(part)
+        # the statistics output never gets a gradient: without this autograd would materialise a
+        # zero tensor for it in every backward (one fill kernel per layer on the critical path)
+        ctx.set_materialize_grads(False)
         return y, part
 
     @staticmethod
     def backward(ctx, dy, _dpart=None):
+        if dy is None:  # (not materialised) nothing flowed into the conv output
+            x, wt = ctx.saved_tensors
+            return None, None, None
         dx, dw = _Conv1x1AutoFn.backward(ctx, dy)
         return dx, dw, None
 

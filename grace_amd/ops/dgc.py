@@ -27,10 +27,15 @@ def dgc_capacity(layout: SegmentLayout, ratio: float, capacity: float) -> int:
 
 def dgc_select(x: torch.Tensor, layout: SegmentLayout, ratio: float, sample_ratio: float, max_iters: int,
                seed: int, cap: int, step: Optional[torch.Tensor] = None, vmask: Optional[torch.Tensor] = None,
-               umask: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+               umask: Optional[torch.Tensor] = None, compensate: Optional[Tuple[float, bool]] = None
+               ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """DGC selection of |x| >= thr_i per segment into a capacity payload (header, values, indices).
     ``step``: device step counter mixed into the sampling seed on the device (graph replays draw
-    fresh samples); ``vmask`` / ``umask``: DgcMemory's v / u, zeroed at the SENT entries."""
+    fresh samples); ``vmask`` / ``umask``: DgcMemory's v / u, zeroed at the SENT entries.
+    ``compensate=(momentum, first)`` (native, with vmask / umask): ``x`` is the RAW gradient and
+    DgcMemory's compensate (u = m u + g; v = v + u) is fused into the selection -- the samples
+    read the compensated values on the fly and the first refinement pass writes u and v -- so the
+    selection runs on v without a separate pass over the bucket."""
     from .cappayload import sparse_payload
 
     ns, ks = _sizes(layout, ratio, sample_ratio)
@@ -48,7 +53,7 @@ def dgc_select(x: torch.Tensor, layout: SegmentLayout, ratio: float, sample_rati
                 "samp_off": torch.tensor(slay.offsets, dtype=torch.int64, device=dev),
                 "target": torch.tensor([n * ratio for n in layout.numels], dtype=torch.float32, device=dev),
                 "thr": torch.empty(layout.n_seg, dtype=torch.float32, device=dev),
-                "count": torch.empty(8 * layout.n_seg, dtype=torch.int32, device=dev),  # tree counts + steps
+                "count": torch.empty(32 * layout.n_seg, dtype=torch.int32, device=dev),  # tree counts + steps
                 "done": torch.empty(layout.n_seg, dtype=torch.int32, device=dev),
                 "samples": torch.empty(max(1, slay.total), dtype=torch.float32, device=dev),
             }
@@ -57,14 +62,20 @@ def dgc_select(x: torch.Tensor, layout: SegmentLayout, ratio: float, sample_rati
         sd = seed & 0xFFFFFFFFFFFFFFFF
         sd = sd - (1 << 64) if sd >= (1 << 63) else sd
         samples = ws["samples"][: slay.total]
-        C.dgc_sample(x, t["offsets"], ws["samp_off"], sd, step, samples)
+        fuse = compensate is not None and vmask is not None and umask is not None
+        cu, cv = (umask, vmask) if fuse else (None, None)
+        mom, first = compensate if fuse else (0.0, False)
+        C.dgc_sample(x, t["offsets"], ws["samp_off"], sd, step, samples, cu, cv, float(mom), bool(first))
         tw = _topk_ws(slay, ks, dev)
         C.topk_select(samples, None, samples, 1.0, 1.0, 0, st["seg"], st["begin"], st["end"], tw["kseg"],
                       tw["state"], tw["hist"])
         C.dgc_refine(x, tw["state"], ws["target"], max_iters, ws["thr"], ws["count"], ws["done"], t["seg"],
-                     t["begin"], t["end"])
-        C.dgc_compact(x, ws["thr"], v, i, hdr[:1], t["seg"], t["begin"], t["end"], vmask, umask)
+                     t["begin"], t["end"], cu, cv, float(mom), bool(first))
+        sel = vmask if fuse else x  # after the fused refinement v holds the compensated values
+        C.dgc_compact(sel, ws["thr"], v, i, hdr[:1], t["seg"], t["begin"], t["end"], vmask, umask)
         return hdr, v, i
+    if compensate is not None:
+        raise ValueError("fused compensate needs the native path")
     # ---- PyTorch reference path (per segment, reference dgc.py:12-43 semantics)
     gen = torch.Generator(device=dev)
     gen.manual_seed(seed & 0x7FFFFFFFFFFFFFFF)

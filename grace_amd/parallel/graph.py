@@ -41,8 +41,8 @@ def graph_safe(grc, allow_static_seeds: bool = False) -> Optional[str]:
     if name == "SketchCompressor":
         from ..ops import _native
 
-        # the native multi-rank select (any q <= 1024) is capturable; the CPU sort path is not
-        if grc.compressor.quantiles > 1024 or not _native.available():
+        # the native multi-rank select + encode (any q <= 65535) is capturable; the sort path is not
+        if grc.compressor.quantiles > 65535 or not _native.available():
             return f"{name} with {grc.compressor.quantiles} quantiles sorts the bucket (no native select)"
     if not grc.compressor.tensors_size_are_same:
         return f"{name} has variable-size payloads"

@@ -475,3 +475,42 @@ def test_dgc_tree_refinement_matches_sequential_rule():
             else:
                 break
         assert torch.equal(got[s], t), (s, float(got[s]), float(t))
+
+
+def test_dgc_fused_compensate_equals_compensate_then_select():
+    """DgcMemory's compensate fused into the DGC selection (samples read v + (m u + g) on the fly,
+    the first refinement count pass writes u and v) gives the compensate-pass-then-select
+    payload and state bit for bit, over steps (first step: u = v = g)."""
+    from grace_amd import compressor as Z
+    from grace_amd import memory as M
+    from grace_amd.core import register_layout
+    from grace_amd.ops import _native
+    from grace_amd.ops import dgc as D
+    from grace_amd.ops.layout import SegmentLayout
+
+    g0 = torch.Generator().manual_seed(11)
+    shapes = [(512, 300), (1000,), (64, 3, 3, 3), (70001,)]
+    lay = SegmentLayout.from_tensors([torch.empty(s) for s in shapes])
+    register_layout("dgc_fuse", lay)
+    comp_a, comp_b = Z.DgcCompressor(0.01), Z.DgcCompressor(0.01)
+    mem_a, mem_b = M.DgcMemory(0.9, gradient_clipping=False), M.DgcMemory(0.9, gradient_clipping=False)
+    C = _native.lib()
+    for step in range(3):
+        g = torch.randn(lay.total, generator=g0).cuda()
+        pa, ca = comp_a.fused_compress(g.clone(), "dgc_fuse", mem_a)  # fused path
+        # reference: explicit compensate pass, then the native selection on v
+        gb = g.clone()
+        u, v, first = mem_b.state_buffers("dgc_fuse", gb)
+        C.dgc_compensate(gb, u, v, mem_b.momentum, first)
+        cb = comp_b.ctx(gb, "dgc_fuse")
+        pb, _ = comp_b._select(v, cb, "dgc_fuse", vmask=v, umask=u)
+        torch.cuda.synchronize()
+        ha, hb = pa[0].cpu(), pb[0].cpu()
+        assert torch.equal(ha, hb), (step, ha, hb)
+        k = min(int(ha[0]), int(ha[1]))
+        ia, ib = pa[2][:k].long().cpu(), pb[2][:k].long().cpu()
+        oa, ob = torch.argsort(ia), torch.argsort(ib)
+        assert torch.equal(ia[oa], ib[ob]), step
+        assert torch.equal(pa[1][:k].cpu()[oa], pb[1][:k].cpu()[ob]), step
+        ua, va, _ = mem_a.state_buffers("dgc_fuse", g)
+        assert torch.equal(ua, u) and torch.equal(va, v), step

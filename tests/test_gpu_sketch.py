@@ -124,3 +124,47 @@ def test_sketch_large_q_codec_and_graph(q):
     got = out.clone()
     ref = comp_g.decompress(*comp_g.compress(x.clone(), f"skq{q}")).clone()
     torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("q", [1024, 1500, 4096])
+def test_large_q_native_codec_matches_sort_path(q):
+    """q > 1024 (the reference's uint16 bins go to 65535; tensorflow/compressor/sketch.py:22-27):
+    the batched native select gives the sort path's edges bit for bit, the global-accumulator
+    encode gives its bin codes bit for bit and its means to fp32 summation order, deterministic
+    across calls, and the whole codec replays from a captured graph (no sort, no host read)."""
+    from grace_amd.parallel.graph import graph_safe
+    from grace_amd import grace_from_params
+
+    segs = _segments(3)
+    flat = torch.cat(segs)
+    lay = SegmentLayout.from_tensors(segs)
+    name = f"sk_big{q}"
+    register_layout(name, lay)
+    x = flat.cuda()
+    assert torch.equal(native_quantile_edges(x, lay, q), segmented_quantile_edges(x, lay, q))
+    comp_c, comp_g = Z.SketchCompressor(q), Z.SketchCompressor(q)
+    pc, cc = comp_c.compress(flat, name)
+    pg, cg = comp_g.compress(x, name)
+    assert pg[0].dtype == torch.int16
+    assert torch.equal(pg[0].cpu(), pc[0])  # bin codes
+    torch.testing.assert_close(pg[1].cpu(), pc[1], rtol=1e-5, atol=1e-6)
+    m1 = pg[1].clone()
+    assert torch.equal(comp_g.compress(x, name)[0][1], m1)  # fixed-point sums: order-independent
+    torch.testing.assert_close(comp_g.decompress(pg, cg).cpu(), comp_c.decompress(pc, cc), rtol=1e-5, atol=1e-6)
+    grc = grace_from_params({"compressor": "sketch", "quantiles": q, "memory": "none", "communicator": "allgather",
+                             "world_size": 1})
+    assert graph_safe(grc) is None
+    eager = grc.step(x.clone(), name).clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        grc.step(x.clone(), name)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    xs = x.clone()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = grc.step(xs, name)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, eager)
