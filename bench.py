@@ -96,6 +96,9 @@ def parse():
                          "under a whole-step graph without overlap (measured 0.44 ms/step less than torch "
                          "for ResNet-50 Top-K), torch otherwise; xgmi = native-inline plus the one-shot "
                          "peer-memory all-gather for payloads <= 8 MB (parallel/xgmi.py, self-checked at start)")
+    ap.add_argument("--xgmi-capacity-mb", type=float, default=8.0,
+                    help="per-rank payload capacity of the xGMI one-shot comm (two slots of this size are exported "
+                         "per rank); collectives above it go to RCCL / the inner comm")
     return ap.parse_args()
 
 
@@ -193,8 +196,11 @@ def main():
     # a gloo group cannot capture its collectives, but an ALL-GATHER-only pipeline's exchange can
     # run on the xGMI one-shot comm (peer memory, gloo only bootstraps it): that is the W > 1
     # whole-step-graph rehearsal on a 1-GPU box (ranks share the card)
+    # (all-gather pipelines, and linear codecs under Allreduce: XgmiComm's one-shot gather + local
+    # rank-ordered reduction when the bucket fits --xgmi-capacity-mb)
     gloo_graph = (gloo and world > 1 and args.comm in ("xgmi", "auto") and args.surface == "engine"
-                  and w.grace.get("communicator") == "allgather"
+                  and (w.grace.get("communicator") == "allgather"
+                       or (w.grace.get("communicator") == "allreduce" and w.grace.get("compressor") in ("none", "fp16")))
                   and w.grace.get("compressor") not in ("powersgd",) and w.grace.get("memory") != "dgc")
     if args.surface == "ddp" and mode == "auto":
         # the whole DDP step (reducer + comm hook) captures: 2341 vs 2309 img/s eager
@@ -243,7 +249,7 @@ def main():
                     from grace_amd.parallel.xgmi import XgmiComm
 
                     try:
-                        native = XgmiComm(native, capacity_mb=8.0,
+                        native = XgmiComm(native, capacity_mb=args.xgmi_capacity_mb,
                                           select="probe" if comm_kind == "auto-probe" else "size")
                     except Exception as e:  # every rank raised together (XgmiComm agrees)
                         if comm_kind == "xgmi" or gloo:

@@ -197,7 +197,7 @@ class XgmiComm(_comm.Comm):
         xg, inn = (float(v) for v in t.tolist())
         self.one_shot_calls -= iters + 1
         return {"path": "xgmi" if xg <= inn else "inner", "xgmi_us": round(xg, 2), "inner_us": round(inn, 2),
-                "bytes": int(inp.numel() * inp.element_size())}
+                "bytes": int(inp.numel() * inp.element_size()), "collective": "all_gather"}
 
     def all_gather_into(self, out, inp, async_op=False, ranges=None):
         if not self._fits(inp) or self._choose(out, inp) != "xgmi":
@@ -222,7 +222,64 @@ class XgmiComm(_comm.Comm):
         return _comm.Work()
 
     def all_reduce(self, t, op="sum", async_op=False):
-        return self.inner.all_reduce(t, op, async_op)
+        """Small all-reduces as a one-shot gather + a rank-ordered local reduction (the same bytes
+        summed in the same order on every rank: bit-identical results); larger ones -- or when
+        ``select="probe"`` measured ``inner`` faster for this size -- go to ``inner``."""
+        if (op not in ("sum", "max", "min") or not t.is_contiguous() or not t.is_floating_point()
+                or not self._fits(t)):
+            return self.inner.all_reduce(t, op, async_op)
+        n = t.numel() * t.element_size()
+        if self.select == "probe":
+            c = self.choices.get(("ar", n))
+            if c is None:
+                if torch.cuda.is_current_stream_capturing():
+                    c = {"path": "xgmi"}
+                else:
+                    c = self.choices[("ar", n)] = self._probe_reduce(t, op)
+            if c["path"] != "xgmi":
+                return self.inner.all_reduce(t, op, async_op)
+        self._gather_reduce(t, op)
+        return _comm.Work()
+
+    def _gather_reduce(self, t, op):
+        rows = torch.empty((self.world_size, t.numel()), dtype=t.dtype, device=t.device)
+        self._one_shot(rows.view(-1), t.reshape(-1), None)
+        if op == "sum":
+            torch.sum(rows, 0, out=t.view(-1))
+        elif op == "max":
+            torch.amax(rows, 0, out=t.view(-1))
+        else:
+            torch.amin(rows, 0, out=t.view(-1))
+
+    def _probe_reduce(self, t, op, iters: int = 8) -> dict:
+        import time
+
+        dev = torch.device("cuda", self.device)
+        buf = t.detach().clone()
+        times = []
+        for path in ("xgmi", "inner"):
+            def fn():
+                buf.copy_(t)
+                if path == "xgmi":
+                    self._gather_reduce(buf, op)
+                else:
+                    self.inner.all_reduce(buf, op, False).wait()
+            fn()
+            torch.cuda.synchronize(dev)
+            self.inner.barrier()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                fn()
+            torch.cuda.synchronize(dev)
+            times.append((time.perf_counter() - t0) * 1e6 / iters)
+        tt = torch.tensor(times, dtype=torch.float64, device=dev)
+        self.inner.all_reduce(tt, "max").wait()
+        torch.cuda.synchronize(dev)
+        xg, inn = (float(v) for v in tt.tolist())
+        self.one_shot_calls -= iters + 1
+        return {"path": "xgmi" if xg <= inn else "inner", "xgmi_us": round(xg, 2), "inner_us": round(inn, 2),
+                "bytes": int(t.numel() * t.element_size()), "collective": "all_reduce"}
 
     def broadcast(self, t, src, async_op=False):
         return self.inner.broadcast(t, src, async_op)

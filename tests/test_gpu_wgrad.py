@@ -302,3 +302,51 @@ def test_untagged_parameters_stay_in_line():
     finally:
         for h in hooks:
             h.remove()
+
+
+def test_second_capture_after_eager_steps(bn_deterministic):
+    """bench.py's sequence: a captured engine step, eager (profiled) steps whose last loss stays
+    referenced, then a second engine captured for the no-op split.  The eager steps' autograd
+    graph must be released before the second capture (bench.py drops it) -- kept alive it binds the
+    parameters' AccumulateGrad nodes to the eager stream and the capture fails with unjoined work."""
+    from grace_amd import grace_from_params
+    from grace_amd.parallel import DistributedOptimizer, FusedSGD
+    from grace_amd.parallel.comm import LocalComm
+    from grace_amd.parallel.graph import GraphedStep
+
+    torch.manual_seed(2)
+    m = _small_cnn().cuda().to(memory_format=torch.channels_last)
+    x = torch.randn(16, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (16,), device="cuda")
+    base = FusedSGD(list(m.parameters()), lr=0.05, momentum=0.5)
+
+    def make(opt):
+        def step():
+            opt.zero_grad(set_to_none=True)
+            loss = F.cross_entropy(m(x), y)
+            loss.backward()
+            opt.step()
+            return loss
+        return step
+
+    grc = grace_from_params({"compressor": "topk", "compress_ratio": 0.05, "memory": "residual",
+                             "communicator": "allgather", "world_size": 1})
+    o1 = DistributedOptimizer(base, grc, named_parameters=list(m.named_parameters()), overlap=False)
+    g1 = GraphedStep(make(o1), warmup=3)
+    for _ in range(2):
+        g1()
+    for _ in range(2):  # eager steps, as bench.py's exposed-exchange split
+        o1.zero_grad(set_to_none=True)
+        l2 = F.cross_entropy(m(x), y)
+        l2.backward()
+        o1.step()
+    l2 = None  # noqa: F841  (bench.py releases it the same way)
+    o1.engine.remove()
+    o2 = DistributedOptimizer(base, grace_from_params({"compressor": "none", "communicator": "allreduce"},
+                                                      comm=LocalComm()),
+                              named_parameters=list(m.named_parameters()), overlap=False)
+    g2 = GraphedStep(make(o2), warmup=3)
+    for _ in range(2):
+        loss = g2()
+    torch.cuda.synchronize()
+    assert torch.isfinite(loss).item()

@@ -59,6 +59,22 @@ def _xgmi_body(rank, world):
         torch.cuda.synchronize()
         want = torch.cat([torch.arange(8192, device=dev, dtype=torch.float32) * (r + 1) + it for r in range(world)])
         assert torch.equal(dst, want), f"replay {it}"
+    # all-reduce as a one-shot gather + rank-ordered local reduction (sum / max)
+    for op in ("sum", "max"):
+        t = torch.randn(10000, generator=torch.Generator().manual_seed(40 + rank)).to(dev)
+        ref = t.clone()
+        calls = comm.one_shot_calls
+        comm.all_reduce(t, op)
+        inner.all_reduce(ref, op)
+        torch.cuda.synchronize()
+        assert comm.one_shot_calls == calls + 1
+        if world == 2 or op == "max":  # two fp32 terms: order-free, so gloo's sum is bit-comparable
+            assert torch.equal(t, ref), op
+        else:
+            torch.testing.assert_close(t, ref, rtol=1e-6, atol=1e-6)
+        same = t.clone()
+        dist.broadcast(same, 0)
+        assert torch.equal(same, t), "ranks disagree"  # identical bytes reduced in identical order
     comm.check()  # no timed-out waits
     dist.barrier()
     torch.cuda.synchronize()
