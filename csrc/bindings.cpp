@@ -163,6 +163,40 @@ void sparse_scatter_add_dev(const Tensor& val, const Tensor& idx, const Tensor& 
                                 val.numel(), out.data_ptr<float>(), (float)scale, accumulate, cur_stream());
 }
 
+void sparse_decode_ranks(const std::vector<Tensor>& vals, const std::vector<Tensor>& idxs,
+                         const std::vector<c10::optional<Tensor>>& counts, const Tensor& out, double scale,
+                         const Tensor& ctr) {
+  const int W = (int)vals.size();
+  TORCH_CHECK(W >= 1 && W <= grace::kDecodeMaxRanks, "sparse_decode_ranks: 1..", grace::kDecodeMaxRanks, " ranks");
+  TORCH_CHECK((int)idxs.size() == W && (int)counts.size() == W, "sparse_decode_ranks: per-rank list sizes differ");
+  CHECK_F32(out);
+  CHECK_I32(ctr);
+  TORCH_CHECK(ctr.numel() >= 2 && ctr.device() == out.device(), "sparse_decode_ranks: ctr");
+  TORCH_CHECK(out.numel() < (int64_t(1) << 31), "sparse_decode_ranks: int32 indices");
+  const float* v[grace::kDecodeMaxRanks];
+  const int32_t* ix[grace::kDecodeMaxRanks];
+  const int32_t* c[grace::kDecodeMaxRanks];
+  int64_t cap[grace::kDecodeMaxRanks];
+  for (int r = 0; r < W; ++r) {
+    CHECK_F32(vals[r]);
+    CHECK_I32(idxs[r]);
+    TORCH_CHECK(vals[r].numel() == idxs[r].numel(), "sparse_decode_ranks: val/idx size mismatch at rank ", r);
+    TORCH_CHECK(vals[r].device() == out.device() && idxs[r].device() == out.device(), "sparse_decode_ranks: device");
+    v[r] = vals[r].data_ptr<float>();
+    ix[r] = idxs[r].data_ptr<int32_t>();
+    cap[r] = vals[r].numel();
+    c[r] = nullptr;
+    if (counts[r].has_value()) {
+      CHECK_I32((*counts[r]));
+      TORCH_CHECK(counts[r]->numel() >= 1 && counts[r]->device() == out.device(), "sparse_decode_ranks: count");
+      c[r] = counts[r]->data_ptr<int32_t>();
+    }
+  }
+  DevGuard guard(out.device());
+  grace::sparse_decode_ranks(W, v, ix, c, cap, out.data_ptr<float>(), out.numel(), (float)scale,
+                             ctr.data_ptr<int32_t>(), grace::health_dev(out.device().index()), cur_stream());
+}
+
 void sparse_scatter_add(const Tensor& val, const Tensor& idx, const Tensor& out, double scale,
                         bool accumulate) {
   CHECK_F32(val);
@@ -721,6 +755,59 @@ int64_t gemm_f32(const Tensor& A, bool a_kc, int64_t lda, const Tensor& B, bool 
                          (int)M, (int)N, (int)K, (int)splits, cur_stream(), (int)tile, st);
 }
 
+// 3x3 / pad 1 implicit-GEMM convolution (gemm_f32.hip).  Activations and the weight are NCHW-shaped
+// tensors in channels_last memory (NHWC / [Cout][3][3][Cin] images).
+static void check_cl(const Tensor& t, std::initializer_list<int64_t> shape, const char* what) {
+  CHECK_DEV(t);
+  CHECK_DT(t, at::kFloat);
+  TORCH_CHECK(t.dim() == 4 && t.sizes() == c10::IntArrayRef(shape), what, ": shape ", t.sizes(), " expected ",
+              c10::IntArrayRef(shape));
+  TORCH_CHECK(t.is_contiguous(at::MemoryFormat::ChannelsLast), what, ": channels_last memory required");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, what, ": 16-B alignment");
+}
+
+int64_t conv3x3_f32(int64_t dir, const Tensor& act, const Tensor& other, const Tensor& C, int64_t stride,
+                    int64_t splits, int64_t tile, const c10::optional<Tensor>& stats) {
+  TORCH_CHECK(dir >= 0 && dir <= 2, "conv3x3_f32: dir 0 (fwd) / 1 (dgrad) / 2 (wgrad)");
+  TORCH_CHECK(stride == 1 || (stride == 2 && dir != 1), "conv3x3_f32: stride 1, or 2 for fwd / wgrad");
+  int64_t N, H, W, Cin, Cout;
+  if (dir == 1) {  // act = dY [N, Cout, H, W], other = weight, C = dX [N, Cin, H, W]
+    N = act.size(0), Cout = act.size(1), H = act.size(2), W = act.size(3), Cin = C.size(1);
+    check_cl(act, {N, Cout, H, W}, "dY");
+    check_cl(other, {Cout, Cin, 3, 3}, "weight");
+    check_cl(C, {N, Cin, H, W}, "dX");
+    TORCH_CHECK(Cout % 32 == 0 && Cin % 4 == 0, "conv3x3_f32 dgrad: Cout % 32, Cin % 4");
+  } else {
+    N = act.size(0), Cin = act.size(1), H = act.size(2), W = act.size(3);
+    const int64_t Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+    if (dir == 0) {  // other = weight, C = y
+      Cout = other.size(0);
+      check_cl(other, {Cout, Cin, 3, 3}, "weight");
+      check_cl(C, {N, Cout, Ho, Wo}, "y");
+      TORCH_CHECK(Cin % 32 == 0 && Cout % 4 == 0, "conv3x3_f32 fwd: Cin % 32, Cout % 4");
+    } else {  // other = dY, C = dW
+      Cout = other.size(1);
+      check_cl(other, {N, Cout, Ho, Wo}, "dY");
+      check_cl(C, {Cout, Cin, 3, 3}, "dW");
+      TORCH_CHECK(Cin % 4 == 0 && Cout % 4 == 0, "conv3x3_f32 wgrad: Cin % 4, Cout % 4");
+    }
+    check_cl(act, {N, Cin, H, W}, "x");
+  }
+  TORCH_CHECK(N * H * W < (1 << 24), "conv3x3_f32: N*H*W < 2^24 (float pixel division)");
+  float* st = nullptr;
+  if (stats.has_value() && stats->defined()) {
+    TORCH_CHECK(dir == 0 && splits == 1, "conv3x3_f32: statistics on the forward with splits = 1");
+    CHECK_DEV((*stats));
+    CHECK_DT((*stats), at::kFloat);
+    const int64_t M = N * ((H - 1) / stride + 1) * ((W - 1) / stride + 1);
+    TORCH_CHECK(stats->is_contiguous() && stats->numel() >= ((M + 63) / 64) * 2 * Cout, "stats: [ceil(M/64)][2][Cout]");
+    st = stats->data_ptr<float>();
+  }
+  DevGuard guard(C.device());
+  return grace::conv3x3_f32((int)dir, act.data_ptr<float>(), other.data_ptr<float>(), C.data_ptr<float>(), (int)N,
+                            (int)H, (int)W, (int)Cin, (int)Cout, (int)stride, (int)splits, (int)tile, st, cur_stream());
+}
+
 // ------------------------------------------------------------------------------ segment stats
 void segment_stats(const Tensor& x, const c10::optional<Tensor>& r, int64_t mode, double beta, double gamma,
                    const c10::optional<Tensor>& xout, const Tensor& seg, const Tensor& cb, const Tensor& ce,
@@ -981,6 +1068,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("topk_ef", &topk_ef);
   m.def("sparse_scatter_add", &sparse_scatter_add);
   m.def("sparse_scatter_add_dev", &sparse_scatter_add_dev);
+  m.def("sparse_decode_ranks", &sparse_decode_ranks);
   m.def("segment_stats", &segment_stats);
   m.def("randk_gather", &randk_gather);
   m.def("randk_scatter", &randk_scatter);
@@ -1026,6 +1114,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sketch_encode", &sketch_encode);
   m.def("sketch_decode", &sketch_decode);
   m.def("quantile_select", &quantile_select);
+  m.def("conv3x3_f32", &conv3x3_f32, py::arg("dir"), py::arg("act"), py::arg("other"), py::arg("C"),
+        py::arg("stride") = 1, py::arg("splits") = 0, py::arg("tile") = 0, py::arg("stats") = py::none());
   m.def("gemm_f32", &gemm_f32, py::arg("A"), py::arg("a_kc"), py::arg("lda"), py::arg("B"), py::arg("b_kc"),
         py::arg("ldb"), py::arg("C"), py::arg("ldc"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("splits"),
         py::arg("tile") = 0, py::arg("stats") = py::none());

@@ -37,6 +37,14 @@ void sparse_scatter_add(const float* val, const int32_t* idx, int64_t K, float* 
 // K = min(*count, cap) read on the device (capacity payloads with an in-band count)
 void sparse_scatter_add_dev(const float* val, const int32_t* idx, const int32_t* count, int64_t cap, float* out,
                             float scale, bool accumulate, hipStream_t stream);
+// One launch: out = 0, then out[idx_r[j]] += scale * val_r[j] for r = 0..W-1 in rank order
+// (grid barriers between ranks; bit-identical to the sequential per-rank loop).  count[r] may be
+// null (K = cap[r]) or an in-band count (K = min(*count[r], cap[r])).  ctr: 2 int32 of device
+// memory, zero before the first launch, left zero by every launch (stream-ordered reuse).
+constexpr int kDecodeMaxRanks = 32;
+void sparse_decode_ranks(int W, const float* const* val, const int32_t* const* idx, const int32_t* const* count,
+                         const int64_t* cap, float* out, int64_t n, float scale, int32_t* ctr,
+                         uint32_t* health_dev, hipStream_t stream);
 
 // ---------------------------------------------------------------- segstats.hip
 // per segment: [sum, sumsq, max|x|, sum|x|, sum(x<0), count(x<0)]
@@ -142,6 +150,14 @@ void quantile_select(const ChunkTable& ct, int n_seg, const float* x, int max_sl
 int gemm_f32(const float* A, bool a_kcontig, int64_t lda, const float* B, bool b_kcontig, int64_t ldb, float* C,
               int64_t ldc, int M, int N, int K, int splits, hipStream_t stream, int tile = 0,
              float* stats = nullptr);
+// 3x3 (pad 1) convolution of NHWC fp32 activations as an implicit GEMM on the same kernel (no
+// im2col).  dir 0: C = y [N,Ho,Wo,Cout] from act = x, other = W [Cout][3][3][Cin] (+ stats as
+// gemm_f32); dir 1 (stride 1): C = dx [N,H,W,Cin] from act = dY, other = W; dir 2: C = dW
+// [Cout][3][3][Cin] from act = x, other = dY (splits 0 = auto split-K, C zeroed).  Cin % 32 == 0
+// (dir 0), Cout % 32 == 0 (dir 1), Cin % 4 == 0 (dir 2), N*Ho*Wo and N*H*W < 2^24.  Returns the
+// row tiles of C.
+int conv3x3_f32(int dir, const float* act, const float* other, float* C, int N, int H, int W, int Cin, int Cout,
+                int stride, int splits, int tile, float* stats, hipStream_t stream);
 
 // ---------------------------------------------------------------- ef.hip (elementwise)
 void axpby(const float* x, const float* y, float* out, int64_t n, float a, float b, hipStream_t stream);

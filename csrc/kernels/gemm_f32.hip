@@ -27,6 +27,18 @@
 // run of tiles, n fastest: neighbouring tiles share A rows in that XCD's L2.
 // Split-K (weight gradients: K = N*H*W up to 10^5 against a small output) accumulates with f32
 // atomics into a zeroed C.
+//
+// 3x3 convolutions (pad 1) run on the SAME kernel as implicit GEMMs: no im2col buffer, the
+// operand loader gathers the shifted NHWC pixels straight from the activation (zero outside the
+// image), with the weight in its channels_last image [Cout][3][3][Cin] (k = tap * C + c):
+//   forward      Y[(n,oy,ox)][co]  = sum_(tap,ci) x[n, s*oy+dy, s*ox+dx, ci] . W[co][tap][ci]
+//                A = implicit rows (mode 2), B = W K-contig (ld = 9 Cin)
+//   data grad    dX[(n,iy,ix)][ci] = sum_(tap,co) dY[n, iy-dy, ix-dx, co] . W[co][tap][ci]   (stride 1)
+//                A = implicit rows, flipped taps (mode 2), B = W per tap MN-contig (mode 4)
+//   weight grad  dW[co][(tap,ci)]  = sum_(n,oy,ox) dY[(n,oy,ox)][co] . x[n, s*oy+dy, s*ox+dx, ci]
+//                A = dY MN-contig, B = implicit MN rows (tap, ci) over k = output pixels (mode 3)
+// A BK = 32 k-slice never straddles a tap (C % 32 == 0 for the K-contig gathers), so the shift is
+// uniform per slice and each row costs one bounds test per slice.
 #include <algorithm>
 
 #include "grace_common.h"
@@ -52,16 +64,86 @@ struct GemmParams {
   int c_vec;  // C rows 16-B aligned (ldc % 4 == 0, C 16-B aligned): float4 stores
   float* stats;  // optional (non-split GEMMs): per (row tile, column) [sum | sum of squares] of C,
                  // [tiles_m][2][N] -- the BatchNorm statistics of a conv output, fused
+  // implicit-GEMM convolution geometry (modes 2-4)
+  int gHr, gWr;        // pixel grid of the implicit rows (mode 2) / of k (mode 3)
+  int gHs, gWs;        // grid of the gathered activation
+  int gC;              // its channels (k per tap, mode 2; rows per tap, mode 3)
+  int gS, gSign;       // row / k pixel -> source pixel: s * (y, x) + sign * (dy, dx)
+  float gInvWr, gInvHr;
+  int kt;              // mode 4: k per tap (Cout)
+  int64_t tap_off;     // mode 4: element offset between the taps of a weight row (Cin)
 };
 
-template <int R, bool KC>
+// Operand modes.  0: K-contig rows, 1: MN-contig, 2: implicit conv rows (K-contig gather of
+// shifted pixels), 3: implicit conv MN rows (r = tap * C + c, k = output pixel), 4: a 3x3 weight
+// per tap, MN-contig (r = ci, k = tap * kt + co)
+__host__ __device__ constexpr bool mode_kc(int mode) { return mode == 0 || mode == 2; }
+
+// m = q * d + r with 0 <= r < d for m < 2^24 (one float multiply and one correction step)
+__device__ __forceinline__ int fdivmod(int m, int d, float inv, int* r) {
+  int q = (int)((float)m * inv);
+  int rr = m - q * d;
+  if (rr < 0) {
+    --q;
+    rr += d;
+  } else if (rr >= d) {
+    ++q;
+    rr -= d;
+  }
+  *r = rr;
+  return q;
+}
+
+template <int R, int MODE>
 struct Operand {
+  static constexpr bool KC = mode_kc(MODE);
   static constexpr int NV = R * BK / 4 / kGB;          // float4 per thread per stage
   static constexpr int LDS = KC ? R * LDK : BK * R;    // floats per stage
   static constexpr int TPR = R / 4;                    // MN-contig: threads per k row
   float4 v[NV];
+  // mode 2: per row of this thread, the source pixel of tap (0, 0) and the image base row
+  int sy[MODE == 2 ? NV : 1], sx[MODE == 2 ? NV : 1], pn[MODE == 2 ? NV : 1];
+  // mode 3: this thread's (fixed) row r = tap * C + c
+  int rdy, rdx, rc;
+  bool rok;
 
-  __device__ __forceinline__ void load(const float* __restrict__ x, int64_t ld, int r0, int rmax, int k0, int kmax) {
+  __device__ __forceinline__ void init(const GemmParams& p, int r0, int rmax) {
+    if constexpr (MODE == 2) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int r = r0 + threadIdx.x / (BK / 4) + (kGB / (BK / 4)) * i;
+        int x, y;
+        const int q = fdivmod(r < rmax ? r : 0, p.gWr, p.gInvWr, &x);
+        const int n = fdivmod(q, p.gHr, p.gInvHr, &y);
+        sy[i] = r < rmax ? y * p.gS : -(1 << 20);  // invalid rows fail every bounds test
+        sx[i] = x * p.gS;
+        pn[i] = n * p.gHs;
+      }
+    } else if constexpr (MODE == 3) {
+      const int r = r0 + 4 * (threadIdx.x % TPR);
+      rok = r < rmax;
+      const int tap = r / p.gC;
+      rc = r - tap * p.gC;
+      rdy = tap / 3 - 1;
+      rdx = tap % 3 - 1;
+    }
+  }
+
+  __device__ __forceinline__ void load(const GemmParams& p, const float* __restrict__ x, int64_t ld, int r0, int rmax,
+                                       int k0, int kmax) {
+    if constexpr (MODE == 2) {
+      const int tap = k0 / p.gC;  // uniform over the slice (C % BK == 0)
+      const int dy = (tap / 3 - 1) * p.gSign, dx = (tap % 3 - 1) * p.gSign;
+      const int c = k0 - tap * p.gC + 4 * (threadIdx.x % (BK / 4));
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int iy = sy[i] + dy, ix = sx[i] + dx;
+        v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if ((unsigned)iy < (unsigned)p.gHs && (unsigned)ix < (unsigned)p.gWs && k0 < kmax)
+          v[i] = *reinterpret_cast<const float4*>(x + ((int64_t)(pn[i] + iy) * p.gWs + ix) * p.gC + c);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       int r, k;
@@ -73,7 +155,21 @@ struct Operand {
         k = k0 + threadIdx.x / TPR + (kGB / TPR) * i;
       }
       v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (r < rmax && k < kmax) {
+      if constexpr (MODE == 3) {
+        if (rok && k < kmax) {
+          int ox, oy;
+          const int q = fdivmod(k, p.gWr, p.gInvWr, &ox);
+          const int n = fdivmod(q, p.gHr, p.gInvHr, &oy);
+          const int iy = oy * p.gS + rdy, ix = ox * p.gS + rdx;
+          if ((unsigned)iy < (unsigned)p.gHs && (unsigned)ix < (unsigned)p.gWs)
+            v[i] = *reinterpret_cast<const float4*>(x + ((int64_t)(n * p.gHs + iy) * p.gWs + ix) * p.gC + rc);
+        }
+      } else if constexpr (MODE == 4) {
+        if (r < rmax && k < kmax) {
+          const int tap = k0 / p.kt;  // uniform over the slice (kt % BK == 0)
+          v[i] = *reinterpret_cast<const float4*>(x + tap * p.tap_off + (int64_t)(k - tap * p.kt) * ld + r);
+        }
+      } else if (r < rmax && k < kmax) {
         v[i] = KC ? *reinterpret_cast<const float4*>(x + (int64_t)r * ld + k)
                   : *reinterpret_cast<const float4*>(x + (int64_t)k * ld + r);
       }
@@ -104,10 +200,10 @@ struct Operand {
 
 __device__ __forceinline__ float f4get(const float4& v, int s) { return s == 0 ? v.x : s == 1 ? v.y : s == 2 ? v.z : v.w; }
 
-template <int BM, int BN, bool AKC, bool BKC>
+template <int BM, int BN, int AM, int BMD>
 __global__ __launch_bounds__(kGB, 2) void gemm_f32_kernel(GemmParams p) {
-  using OA = Operand<BM, AKC>;
-  using OB = Operand<BN, BKC>;
+  using OA = Operand<BM, AM>;
+  using OB = Operand<BN, BMD>;
   constexpr int STAGE = OA::LDS + OB::LDS;
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 32, FN = WN / 32;
   constexpr int CP = WN + 4;                  // padded row pitch of a wave's staged 32-row C slab
@@ -138,9 +234,11 @@ __global__ __launch_bounds__(kGB, 2) void gemm_f32_kernel(GemmParams p) {
 
   OA oa;
   OB ob;
+  oa.init(p, m0, p.M);
+  ob.init(p, n0, p.N);
   if (kb < ke) {
-    oa.load(p.A, p.lda, m0, p.M, kb, ke);
-    ob.load(p.B, p.ldb, n0, p.N, kb, ke);
+    oa.load(p, p.A, p.lda, m0, p.M, kb, ke);
+    ob.load(p, p.B, p.ldb, n0, p.N, kb, ke);
     oa.store(lds);
     ob.store(lds + OA::LDS);
   }
@@ -149,8 +247,8 @@ __global__ __launch_bounds__(kGB, 2) void gemm_f32_kernel(GemmParams p) {
   for (int k0 = kb; k0 < ke; k0 += BK) {
     const bool more = k0 + BK < ke;
     if (more) {
-      oa.load(p.A, p.lda, m0, p.M, k0 + BK, ke);
-      ob.load(p.B, p.ldb, n0, p.N, k0 + BK, ke);
+      oa.load(p, p.A, p.lda, m0, p.M, k0 + BK, ke);
+      ob.load(p, p.B, p.ldb, n0, p.N, k0 + BK, ke);
     }
     const float* As = lds + cur * STAGE;
     const float* Bs = As + OA::LDS;
@@ -274,12 +372,12 @@ __global__ __launch_bounds__(kGB, 2) void gemm_f32_kernel(GemmParams p) {
     }
 }
 
-template <int BM, int BN, bool AKC, bool BKC>
+template <int BM, int BN, int AM, int BMD>
 int launch_cfg(GemmParams p, hipStream_t stream) {
   p.tiles_m = (p.M + BM - 1) / BM;
   p.tiles_n = (p.N + BN - 1) / BN;
   const int64_t blocks = (int64_t)p.tiles_m * p.tiles_n * p.splits;
-  gemm_f32_kernel<BM, BN, AKC, BKC><<<(unsigned)blocks, kGB, 0, stream>>>(p);
+  gemm_f32_kernel<BM, BN, AM, BMD><<<(unsigned)blocks, kGB, 0, stream>>>(p);
   return p.tiles_m;
 }
 
@@ -287,30 +385,53 @@ inline int64_t ntiles(int M, int N, int bm, int bn) { return (int64_t)((M + bm -
 
 // tile shape: the largest of 128x128 / 128x64 / 64x128 / 64x64 that still gives >= 1.5 workgroups
 // per CU (small-M layers, e.g. the 7x7 stage at M = 1568, otherwise leave most of the chip idle)
-template <bool AKC, bool BKC>
+template <int AM, int BMD>
 int launch_layout(GemmParams p, hipStream_t stream) {
   const int64_t want = 384;
   const int64_t t128 = ntiles(p.M, p.N, 128, 128) * p.splits;
   const int64_t tm = ntiles(p.M, p.N, 128, 64) * p.splits, tn = ntiles(p.M, p.N, 64, 128) * p.splits;
-  if (p.M > 64 && p.N > 64 && t128 >= want) return launch_cfg<128, 128, AKC, BKC>(p, stream);
-  if (p.M > 64 && tm >= want && (p.N <= 64 || tm >= tn)) return launch_cfg<128, 64, AKC, BKC>(p, stream);
-  if (p.N > 64 && tn >= want) return launch_cfg<64, 128, AKC, BKC>(p, stream);
-  return launch_cfg<64, 64, AKC, BKC>(p, stream);
+  if (p.M > 64 && p.N > 64 && t128 >= want) return launch_cfg<128, 128, AM, BMD>(p, stream);
+  if (p.M > 64 && tm >= want && (p.N <= 64 || tm >= tn)) return launch_cfg<128, 64, AM, BMD>(p, stream);
+  if (p.N > 64 && tn >= want) return launch_cfg<64, 128, AM, BMD>(p, stream);
+  return launch_cfg<64, 64, AM, BMD>(p, stream);
 }
 
 }  // namespace
 
 namespace {
 // tile: 0 = by the launcher's rule, 1 = 128x128, 2 = 128x64, 3 = 64x128, 4 = 64x64
-template <bool AKC, bool BKC>
+template <int AM, int BMD>
 int launch_tile(GemmParams p, int tile, hipStream_t stream) {
   switch (tile) {
-    case 1: return launch_cfg<128, 128, AKC, BKC>(p, stream);
-    case 2: return launch_cfg<128, 64, AKC, BKC>(p, stream);
-    case 3: return launch_cfg<64, 128, AKC, BKC>(p, stream);
-    case 4: return launch_cfg<64, 64, AKC, BKC>(p, stream);
-    default: return launch_layout<AKC, BKC>(p, stream);
+    case 1: return launch_cfg<128, 128, AM, BMD>(p, stream);
+    case 2: return launch_cfg<128, 64, AM, BMD>(p, stream);
+    case 3: return launch_cfg<64, 128, AM, BMD>(p, stream);
+    case 4: return launch_cfg<64, 64, AM, BMD>(p, stream);
+    default: return launch_layout<AM, BMD>(p, stream);
   }
+}
+
+// split-K rule shared by the plain and the implicit GEMMs: split K when even 64x64 tiles leave
+// CUs idle (f32 atomics into a zeroed, dense C)
+int auto_splits(int M, int N, int K, int64_t ldc) {
+  const int64_t tiles = ntiles(M, N, 64, 64);
+  int splits = 1;
+  if (tiles < 256 && K >= 512 && ldc == N) splits = (int)std::min<int64_t>((384 + tiles - 1) / tiles, K / 256);
+  return splits;
+}
+
+// splits -> k per split (multiple of BK), C zeroed for split-K; returns whether atomic
+void set_splits(GemmParams& p, int splits, float* stats, hipStream_t stream) {
+  if (splits < 1) splits = 1;
+  int kps = (p.K + splits - 1) / splits;
+  kps = (kps + BK - 1) / BK * BK;
+  splits = p.K > 0 ? (p.K + kps - 1) / kps : 1;
+  p.splits = splits;
+  p.k_per_split = kps;
+  p.atomic = splits > 1;
+  p.c_vec = (reinterpret_cast<uintptr_t>(p.C) % 16 == 0) && (p.ldc % 4 == 0);
+  p.stats = p.atomic ? nullptr : stats;  // statistics need whole-K tiles (the binding checks)
+  if (p.atomic) GRACE_HIP_CHECK(hipMemsetAsync(p.C, 0, sizeof(float) * (size_t)p.M * p.ldc, stream));  // ldc == N
 }
 }  // namespace
 
@@ -327,25 +448,57 @@ int gemm_f32(const float* A, bool a_kcontig, int64_t lda, const float* B, bool b
   p.lda = lda;
   p.ldb = ldb;
   p.ldc = ldc;
-  if (splits == 0) {  // auto: split K when even 64x64 tiles leave CUs idle (f32 atomics into C)
-    const int64_t tiles = ntiles(M, N, 64, 64);
-    splits = 1;
-    if (tiles < 256 && K >= 512 && ldc == N) splits = (int)std::min<int64_t>((384 + tiles - 1) / tiles, K / 256);
+  if (splits == 0) splits = auto_splits(M, N, K, ldc);  // host-checked: split-K only with ldc == N
+  set_splits(p, splits, stats, stream);
+  if (a_kcontig && b_kcontig) return launch_tile<0, 0>(p, tile, stream);
+  if (a_kcontig && !b_kcontig) return launch_tile<0, 1>(p, tile, stream);
+  if (!a_kcontig && !b_kcontig) return launch_tile<1, 1>(p, tile, stream);
+  return launch_tile<1, 0>(p, tile, stream);
+}
+
+int conv3x3_f32(int dir, const float* act, const float* other, float* C, int N, int H, int W, int Cin, int Cout,
+                int stride, int splits, int tile, float* stats, hipStream_t stream) {
+  const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;  // 3x3, pad 1
+  GemmParams p{};
+  p.C = C;
+  if (dir == 0) {  // forward: rows = output pixels, k = (tap, ci)
+    p.A = act;
+    p.B = other;
+    p.M = N * Ho * Wo;
+    p.N = Cout;
+    p.K = 9 * Cin;
+    p.ldb = 9 * Cin;
+    p.ldc = Cout;
+    p.gHr = Ho, p.gWr = Wo, p.gHs = H, p.gWs = W, p.gC = Cin, p.gS = stride, p.gSign = 1;
+  } else if (dir == 1) {  // data grad (stride 1): rows = input pixels, k = (tap, co), flipped taps
+    p.A = act;  // dY [N, H, W, Cout]
+    p.B = other;
+    p.M = N * H * W;
+    p.N = Cin;
+    p.K = 9 * Cout;
+    p.ldb = 9 * Cin;
+    p.ldc = Cin;
+    p.kt = Cout;
+    p.tap_off = Cin;
+    p.gHr = H, p.gWr = W, p.gHs = H, p.gWs = W, p.gC = Cout, p.gS = 1, p.gSign = -1;
+  } else {  // weight grad: [Cout][(tap, ci)] over k = output pixels
+    p.A = other;  // dY [N, Ho, Wo, Cout]: MN-contig, ld = Cout
+    p.B = act;    // x
+    p.M = Cout;
+    p.N = 9 * Cin;
+    p.K = N * Ho * Wo;
+    p.lda = Cout;
+    p.ldc = 9 * Cin;
+    p.gHr = Ho, p.gWr = Wo, p.gHs = H, p.gWs = W, p.gC = Cin, p.gS = stride, p.gSign = 1;
   }
-  if (splits < 1) splits = 1;
-  int kps = (K + splits - 1) / splits;
-  kps = (kps + BK - 1) / BK * BK;
-  splits = K > 0 ? (K + kps - 1) / kps : 1;
-  p.splits = splits;
-  p.k_per_split = kps;
-  p.atomic = splits > 1;
-  p.c_vec = (reinterpret_cast<uintptr_t>(C) % 16 == 0) && (ldc % 4 == 0);
-  p.stats = p.atomic ? nullptr : stats;  // statistics need whole-K tiles (the binding checks)
-  if (p.atomic) GRACE_HIP_CHECK(hipMemsetAsync(C, 0, sizeof(float) * (size_t)M * ldc, stream));  // ldc == N (host-checked)
-  if (a_kcontig && b_kcontig) return launch_tile<true, true>(p, tile, stream);
-  if (a_kcontig && !b_kcontig) return launch_tile<true, false>(p, tile, stream);
-  if (!a_kcontig && !b_kcontig) return launch_tile<false, false>(p, tile, stream);
-  return launch_tile<false, true>(p, tile, stream);
+  p.gInvWr = 1.f / (float)p.gWr;
+  p.gInvHr = 1.f / (float)p.gHr;
+  if (p.M <= 0 || p.N <= 0) return 0;
+  if (splits == 0) splits = dir == 2 ? auto_splits(p.M, p.N, p.K, p.ldc) : 1;
+  set_splits(p, splits, dir == 0 ? stats : nullptr, stream);
+  if (dir == 0) return launch_tile<2, 0>(p, tile, stream);
+  if (dir == 1) return launch_tile<2, 4>(p, tile, stream);
+  return launch_tile<1, 3>(p, tile, stream);
 }
 
 }  // namespace grace

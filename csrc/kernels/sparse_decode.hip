@@ -1,0 +1,143 @@
+// One-launch, rank-ordered decode of W sparse payloads into a dense bucket (Top-K / Threshold /
+// DGC decompress + aggregate).
+//
+//   out[t] = ((0 + s*v_0(t)) + s*v_1(t)) + ... + s*v_{W-1}(t)     (terms of ranks that sent t)
+//
+// The reference decodes each rank's payload into its own dense tensor and sums the W tensors
+// (grace_dl/dist/communicator/allgather.py:40-45 + compressor/topk.py:30-36): W dense zero-fills
+// and W dense adds.  The per-rank scatter loop it became here still cost a zero-fill launch plus W
+// scatter launches on the critical tail of every step.  This kernel does all of it in ONE
+// persistent grid:
+//   phase 0        zero out[0, n) (16-B stores)
+//   phase 1 + r    out[idx_r[j]] += s * val_r[j]   for j < K_r  (indices unique within a payload)
+// separated by grid barriers, so every rank's adds land in the same order on every rank: the
+// result is bit-identical to the sequential loop (and across ranks, which all gather the same
+// payloads).  K_r is either fixed or read from the payload's in-band header (capacity payloads,
+// counted into the health words when a payload overflowed).
+//
+// Barrier: an arrival counter (agent scope) per phase; agent-scope release / acquire fences carry
+// the phase's stores across the 8 XCDs' L2s.  The grid is sized to be co-resident (<= 1 workgroup
+// per CU), and every spin is bounded: a barrier that does not complete raises the health fault
+// and the workgroup proceeds (the step's optimizer update is then skipped), so no wave can hang.
+// The last workgroup to leave resets the counters: the kernel is replayable from a HIP graph.
+#include "grace_common.h"
+#include "grace_kernels.h"
+
+namespace grace {
+namespace {
+
+constexpr int kDB = 256;
+
+struct DecodeArgs {
+  const float* val[kDecodeMaxRanks];
+  const int32_t* idx[kDecodeMaxRanks];
+  const int32_t* count[kDecodeMaxRanks];  // null: K = cap[r]
+  int64_t cap[kDecodeMaxRanks];
+};
+
+__device__ __forceinline__ void grid_barrier(int32_t* ctr, int32_t target, uint32_t* health_host, uint32_t* health_dev) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int64_t spins = 0;
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (int64_t(1) << 24)) {  // ~seconds: a workgroup never arrived
+        if (health_host != nullptr)
+          __hip_atomic_store(health_host + kHealthFault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (health_dev != nullptr)
+          __hip_atomic_store(health_dev + kHealthFault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kDB) void sparse_decode_kernel(DecodeArgs a, int W, float* __restrict__ out, int64_t n,
+                                                           float scale, int32_t* ctr, uint32_t* health_host,
+                                                           uint32_t* health_dev) {
+  const int G = gridDim.x;
+  const int64_t tid = (int64_t)blockIdx.x * kDB + threadIdx.x, stride = (int64_t)G * kDB;
+  // phase 0: zero (head to the first 16-B boundary, float4 body, tail)
+  const int64_t head = std::min<int64_t>(n, (int64_t)((16 - (reinterpret_cast<uintptr_t>(out) & 15)) & 15) / 4);
+  if (tid < head) out[tid] = 0.f;
+  float4* body = reinterpret_cast<float4*>(out + head);
+  const int64_t nv = (n - head) / 4;
+  for (int64_t v = tid; v < nv; v += stride) body[v] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t i = head + 4 * nv + tid; i < n; i += stride) out[i] = 0.f;
+  // phases 1..W: rank r's entries, in rank order
+  for (int r = 0; r < W; ++r) {
+    grid_barrier(ctr, (r + 1) * G, health_host, health_dev);
+    int64_t K = a.cap[r];
+    if (a.count[r] != nullptr) {
+      const int64_t c = a.count[r][0];
+      if (c > K && blockIdx.x == 0 && threadIdx.x == 0) health_count_overflow(health_host);
+      K = c < K ? c : K;
+    }
+    const float* __restrict__ val = a.val[r];
+    const int32_t* __restrict__ idx = a.idx[r];
+    // 4 entries per thread in flight (the idx -> out loads are dependent: latency-bound);
+    // out + round(val * scale), unfused, as torch's index_add_(v * scale)
+    for (int64_t j0 = tid; j0 < K; j0 += 4 * stride) {
+      int32_t t[4];
+      float v[4], o[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t j = j0 + u * stride;
+        t[u] = j < K ? idx[j] : -1;
+        v[u] = j < K ? val[j] : 0.f;
+        if (t[u] >= n) t[u] = -1;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) o[u] = t[u] >= 0 ? out[t[u]] : 0.f;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (t[u] >= 0) out[t[u]] = __fadd_rn(o[u], __fmul_rn(v[u], scale));
+    }
+  }
+  // leave: the last workgroup out resets both counters for the next launch / graph replay
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int32_t old = __hip_atomic_fetch_add(ctr + 1, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == G - 1) {
+      __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctr + 1, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+int decode_grid(int64_t n, int64_t kmax) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    GRACE_HIP_CHECK(hipGetDevice(&dev));
+    GRACE_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  // one workgroup per CU at most (co-resident even beside a concurrent kernel: the barrier never
+  // waits on a workgroup that cannot be scheduled); fewer for small buckets
+  const int64_t need = std::max<int64_t>((n / 4 + kDB * 8 - 1) / (kDB * 8), (kmax + kDB * 4 - 1) / (kDB * 4));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(cus, need));
+}
+
+}  // namespace
+
+void sparse_decode_ranks(int W, const float* const* val, const int32_t* const* idx, const int32_t* const* count,
+                         const int64_t* cap, float* out, int64_t n, float scale, int32_t* ctr,
+                         uint32_t* health_dev, hipStream_t stream) {
+  DecodeArgs a{};
+  int64_t kmax = 0;
+  for (int r = 0; r < W; ++r) {
+    a.val[r] = val[r];
+    a.idx[r] = idx[r];
+    a.count[r] = count[r];
+    a.cap[r] = cap[r];
+    kmax = std::max<int64_t>(kmax, cap[r]);
+  }
+  const int G = decode_grid(n, kmax);
+  sparse_decode_kernel<<<G, kDB, 0, stream>>>(a, W, out, n, scale, ctr, health_words().host_dev, health_dev);
+}
+
+}  // namespace grace

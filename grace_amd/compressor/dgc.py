@@ -70,9 +70,9 @@ class DgcCompressor(BucketCompressor):
         return [None, (0, [4]), (0, [4])]  # [header(selected, cap), values, indices]
 
     def decompress_aggregate_impl(self, per_rank, ctx, n_ranks, scale):
-        out = self.out_buffer(ctx, per_rank[0][1].device, zero=True)
-        for hdr, v, i in per_rank:  # rank order: identical on every rank
-            P.scatter_capped(hdr, v, i, out, scale, accumulate=True)
+        out = self.out_buffer(ctx, per_rank[0][1].device)
+        # zero + the W payloads in rank order, one launch: identical on every rank
+        P.decode_ranks([p[1] for p in per_rank], [p[2] for p in per_rank], [p[0] for p in per_rank], out, scale)
         return self.finish(out, ctx)
 
 

@@ -112,8 +112,8 @@ class ThresholdCompressor(Compressor):
 
     def decompress_aggregate(self, per_rank, ctx, world_size):
         self._observe(per_rank, ctx)
-        out = torch.zeros(ctx.numel, dtype=torch.float32, device=per_rank[0][1].device)
+        out = torch.empty(ctx.numel, dtype=torch.float32, device=per_rank[0][1].device)
         scale = 1.0 / world_size if self.average else 1.0
-        for hdr, v, i in per_rank:  # fixed rank order: identical result on every rank
-            P.scatter_capped(hdr, v, i, out, scale, accumulate=True)
+        # zero + the W payloads in fixed rank order, one launch: identical result on every rank
+        P.decode_ranks([p[1] for p in per_rank], [p[2] for p in per_rank], [p[0] for p in per_rank], out, scale)
         return out.view(ctx.shape).to(ctx.dtype)

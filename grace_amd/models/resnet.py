@@ -47,8 +47,8 @@ class BasicBlock(nn.Module):
     def forward(self, x):
         xm, xs = x if isinstance(x, tuple) else (x, x)
         idt = xs if self.downsample is None else self.downsample(xs)
-        y = self.bn1(self.conv1(xm))
-        return self.bn2(self.conv2(y), idt, dual=True)
+        y = conv_bn_act(self.conv1, self.bn1, xm)
+        return conv_bn_act(self.conv2, self.bn2, y, idt, dual=True)
 
 
 class Bottleneck(nn.Module):
@@ -78,7 +78,7 @@ class Bottleneck(nn.Module):
         # 1x1 conv -> BN pairs: the BN statistics may come from the conv GEMM's epilogue
         # (ops/conv.py conv_bn_act, autotuned; otherwise exactly bn(conv(x)))
         y = conv_bn_act(self.conv1, self.bn1, xm)
-        y = self.bn2(self.conv2(y))
+        y = conv_bn_act(self.conv2, self.bn2, y)
         if br is not None:
             idt = br.merge(idt)
         return conv_bn_act(self.conv3, self.bn3, y, idt, dual=True)

@@ -56,6 +56,42 @@ def scatter_capped(hdr: torch.Tensor, vals: torch.Tensor, idx: torch.Tensor, out
         out[il] = vals[:k] * scale
 
 
+MAX_DECODE_RANKS = 32  # csrc/include/grace_kernels.h kDecodeMaxRanks
+_DECODE_CTR = {}
+
+
+def _decode_ctr(device) -> torch.Tensor:
+    """The decode kernel's barrier counters, one pair per (device, stream): launches on one stream
+    are ordered and each leaves its counters zero, so they can share them."""
+    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
+    c = _DECODE_CTR.get(key)
+    if c is None:
+        c = torch.zeros(2, dtype=torch.int32, device=device)
+        _DECODE_CTR[key] = c
+    return c
+
+
+def decode_ranks(vals, idxs, counts, out: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
+    """``out`` = 0, then ``out[idxs[r]] += vals[r] * scale`` for r = 0..W-1 in rank order --
+    bit-identical on every rank.  ``counts[r]``: None (every entry) or the payload's in-band count
+    word (capacity payloads: the first min(count, capacity) entries).  Native path: ONE launch
+    (zero + W rank phases behind grid barriers, csrc/kernels/sparse_decode.hip) instead of a zero
+    fill plus W scatter launches."""
+    W = len(vals)
+    if _native.use_native(out) and 1 <= W <= MAX_DECODE_RANKS and out.is_contiguous():
+        _native.lib().sparse_decode_ranks(list(vals), list(idxs), [None if c is None else c[:1] for c in counts],
+                                          out, float(scale), _decode_ctr(out.device))
+        return out
+    out.zero_()
+    for v, i, c in zip(vals, idxs, counts):
+        if c is None:
+            il = i.long()
+            out.index_add_(0, il, v * scale)
+        else:
+            scatter_capped(c, v, i, out, scale, accumulate=True)
+    return out
+
+
 def zero_capped(hdr: torch.Tensor, idx: torch.Tensor, out: torch.Tensor, zeros: torch.Tensor) -> None:
     """out[idx[j]] = 0 for the sent entries (``zeros``: a cached all-zero fp32 buffer >= capacity)."""
     scatter_capped(hdr, zeros[: idx.numel()], idx, out, 1.0, accumulate=False)

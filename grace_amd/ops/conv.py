@@ -319,7 +319,9 @@ def _time(fn, reps=5):
 
 def _pick_bn(conv, bn, x, residual, relu) -> str:
     nb, cin, h, w = x.shape
-    key = (nb * h * w, cin, conv.out_channels, bool(relu), residual is not None)
+    k3 = conv.kernel_size == (3, 3)
+    s = conv.stride[0]
+    key = (nb * h * w, cin, conv.out_channels, bool(relu), residual is not None) + ((3, s) if k3 else ())
     c = _BN_CHOICE.get(key)
     if c is not None:
         return c
@@ -327,26 +329,33 @@ def _pick_bn(conv, bn, x, residual, relu) -> str:
         return "unfused"
     C = _native.lib()
     cout = conv.out_channels
-    wt = conv.weight.detach().reshape(cout, cin).contiguous()
+    wt = conv.weight.detach().reshape(cout, cin).contiguous() if not k3 else None
     w4 = conv.weight.detach()
     rm, rv = torch.zeros(cout, device=x.device), torch.ones(cout, device=x.device)
     nbt = torch.zeros((), dtype=torch.int64, device=x.device)
     g, b = bn.weight.detach(), bn.bias.detach()
     res = residual.detach() if residual is not None else None
     xd = x.detach()
-    m = nb * h * w
+    ho, wo = ((h - 1) // s + 1, (w - 1) // s + 1) if k3 else (h, w)
+    m = nb * ho * wo
     times = {}
 
     def unfused():
-        y = _run("fwd", _pick("fwd", xd, wt, None, w4.shape), xd, wt, None, w4.shape)
+        if k3:
+            y = _run3("fwd", _pick3("fwd", xd, w4, None, s), xd, w4, None, s)
+        else:
+            y = _run("fwd", _pick("fwd", xd, wt, None, w4.shape), xd, wt, None, w4.shape)
         C.bn_act_fwd(y, res, g, b, rm, rv, nbt, 0.1, 1e-5, bool(relu))
 
     times["unfused"] = _time(unfused)
     part = torch.empty(((m + 63) // 64) * 2 * cout, device=x.device)
     for tile in (1, 2, 3, 4):
         def fused(tile=tile):
-            y = torch.empty((nb, cout, h, w), device=x.device, memory_format=torch.channels_last)
-            t = C.gemm_f32(xd, True, cin, wt, True, cin, y, cout, m, cout, cin, 1, tile, part)
+            y = torch.empty((nb, cout, ho, wo), device=x.device, memory_format=torch.channels_last)
+            if k3:
+                t = C.conv3x3_f32(0, xd, w4, y, s, 1, tile, part)
+            else:
+                t = C.gemm_f32(xd, True, cin, wt, True, cin, y, cout, m, cout, cin, 1, tile, part)
             C.bn_act_fwd_partials(y, res, part, t, g, b, rm, rv, nbt, 0.1, 1e-5, bool(relu))
         try:
             times[f"stats_t{tile}"] = _time(fused)
@@ -364,7 +373,8 @@ def bn_autotune_table():
 
 
 def conv_bn_act(conv: nn.Module, bn: nn.Module, x: torch.Tensor, residual=None, dual: bool = False):
-    """``bn(conv(x), residual, dual)`` for a 1x1 stride-1 ``Conv1x1F32`` followed by a fused
+    """``bn(conv(x), residual, dual)`` for a 1x1 stride-1 ``Conv1x1F32`` or a 3x3 implicit-GEMM
+    convolution (``conv3x3_ok``) followed by a fused
     ``BatchNormAct2d``: when the autotuner measured it faster (GEMM + statistics epilogue + fold +
     apply vs the best conv backend + the BN statistics and apply passes, each timed whole), the
     conv runs on the MFMA GEMM that also emits the BN statistics, and the BN skips its
@@ -372,8 +382,8 @@ def conv_bn_act(conv: nn.Module, bn: nn.Module, x: torch.Tensor, residual=None, 
     from .bnact import _fusable, bn_act
 
     relu = getattr(bn, "relu", False)
-    if (_BN_FUSE and not _ENABLED and isinstance(conv, Conv1x1F32) and fast_ok(x, conv)
-            and bn.training and bn.track_running_stats and bn.momentum is not None
+    bn_ok = _BN_FUSE and bn.training and bn.track_running_stats and bn.momentum is not None
+    if (bn_ok and not _ENABLED and isinstance(conv, Conv1x1F32) and fast_ok(x, conv)
             and x.shape[0] * x.shape[2] * x.shape[3] < (1 << 31)):
         choice = _pick_bn(conv, bn, x, residual, relu)
         if choice.startswith("stats_t"):
@@ -381,6 +391,15 @@ def conv_bn_act(conv: nn.Module, bn: nn.Module, x: torch.Tensor, residual=None, 
             y, part = _Conv1x1StatsFn.apply(x, conv.weight, tile)
             if _fusable(y, bn, residual):
                 m = x.shape[0] * x.shape[2] * x.shape[3]
+                return bn_act(y, bn, residual, relu, dual, partials=part, tiles=_tiles_m(m, tile))
+            return bn(y, residual, dual=dual)
+    if bn_ok and isinstance(conv, _wg.Conv2dSplitGrad) and conv3x3_ok(x, conv):
+        choice = _pick_bn(conv, bn, x, residual, relu)
+        if choice.startswith("stats_t"):
+            tile = int(choice[7:])
+            y, part = _Conv3x3StatsFn.apply(x, conv.weight, conv.stride[0], tile)
+            if _fusable(y, bn, residual):
+                m = y.shape[0] * y.shape[2] * y.shape[3]
                 return bn_act(y, bn, residual, relu, dual, partials=part, tiles=_tiles_m(m, tile))
             return bn(y, residual, dual=dual)
     return bn(conv(x), residual, dual=dual)
@@ -400,6 +419,174 @@ def fast_ok(x: torch.Tensor, conv: nn.Conv2d, force: bool = False) -> bool:
         return False
     cin, cout = conv.in_channels, conv.out_channels
     return cin % 4 == 0 and cout % 4 == 0 and x.shape[0] * x.shape[2] * x.shape[3] % 4 == 0
+
+
+# ---------------------------------------------------------------- 3x3 convolutions
+# The 3x3 / pad 1 convolutions run as implicit GEMMs on the same f32 MFMA kernel (gemm_f32.hip:
+# the operand loader gathers the shifted NHWC pixels; no im2col buffer, no zero-fill kernel before
+# the forward or the data grad).  Per layer and direction the autotuner times MIOpen (including
+# its zero fills) against the implicit GEMM's tile shapes and keeps the fastest.
+_C3_CHOICE = {}
+_C3_TIMES = {}
+C3_BACKENDS = ("miopen", "mfma", "mfma_t1", "mfma_t2", "mfma_t3", "mfma_t4")
+_C3_ON = os.environ.get("GRACE_CONV3X3", "1") == "1"
+
+
+def conv3x3_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
+    """The implicit-GEMM path applies: fp32 channels_last activation and weight, 3x3 / pad 1 /
+    stride 1 or 2, no bias / groups / dilation, channels multiples of 32."""
+    if not (_C3_ON and (_AUTO or _ENABLED)):
+        return False
+    w = conv.weight
+    if not (x.is_cuda and x.dtype == torch.float32 and w.dtype == torch.float32):
+        return False
+    if torch.is_autocast_enabled() or not _native.native_on(x.device):
+        return False
+    if conv.kernel_size != (3, 3) or conv.padding != (1, 1) or conv.dilation != (1, 1) or conv.groups != 1 \
+            or conv.bias is not None or conv.stride not in ((1, 1), (2, 2)) or conv.padding_mode != "zeros":
+        return False
+    if x.dim() != 4 or not x.is_contiguous(memory_format=torch.channels_last) or x.data_ptr() % 16:
+        return False
+    if not w.is_contiguous(memory_format=torch.channels_last) or w.data_ptr() % 16:
+        return False
+    return conv.in_channels % 32 == 0 and conv.out_channels % 32 == 0 \
+        and x.shape[0] * x.shape[2] * x.shape[3] < (1 << 24)
+
+
+def _run3(direction: str, backend: str, x, w, dy, stride: int, out=None):
+    """One direction of a 3x3 / pad 1 conv on one backend (x, dy, w channels_last)."""
+    if backend == "miopen":
+        if direction == "fwd":
+            return F.conv2d(x, w, None, stride, 1)
+        mask = [direction == "dgrad", direction == "wgrad", False]
+        gi, gw, _ = torch.ops.aten.convolution_backward(dy, x, w, None, [stride, stride], [1, 1], [1, 1], False,
+                                                        [0, 0], 1, mask)
+        return gi if direction == "dgrad" else gw
+    tile = int(backend[6:]) if backend.startswith("mfma_t") else 0
+    C = _native.lib()
+    nb, cin, h, wd = x.shape
+    cout = w.shape[0]
+    if direction == "fwd":
+        ho, wo = (h - 1) // stride + 1, (wd - 1) // stride + 1
+        y = torch.empty((nb, cout, ho, wo), device=x.device, dtype=torch.float32, memory_format=torch.channels_last)
+        C.conv3x3_f32(0, x, w, y, stride, 1, tile)
+        return y
+    if direction == "dgrad":
+        if stride != 1:
+            raise ValueError("implicit-GEMM data grad: stride 1 only")
+        dx = torch.empty_like(x, memory_format=torch.channels_last)
+        C.conv3x3_f32(1, dy, w, dx, 1, 1, tile)
+        return dx
+    dw = out if (out is not None and out.is_contiguous(memory_format=torch.channels_last)
+                 and out.data_ptr() % 16 == 0) else \
+        torch.empty((cout, cin, 3, 3), device=x.device, dtype=torch.float32, memory_format=torch.channels_last)
+    C.conv3x3_f32(2, x, dy, dw, stride, 0, tile)
+    return dw
+
+
+def _pick3(direction: str, x, w, dy, stride: int) -> str:
+    nb, cin, h, wd = x.shape
+    key = (direction, nb, h, wd, cin, w.shape[0], stride)
+    c = _C3_CHOICE.get(key)
+    if c is not None:
+        return c
+    if _ENABLED and not (direction == "dgrad" and stride != 1):
+        return "mfma"
+    if torch.cuda.is_current_stream_capturing():
+        return "miopen"  # never time inside a capture
+    times = {}
+    for be in C3_BACKENDS:
+        try:
+            times[be] = _time(lambda be=be: _run3(direction, be, x, w, dy, stride))
+        except Exception:  # a backend that rejects the shape is simply not a candidate
+            continue
+    c = min(times, key=times.get) if times else "miopen"
+    _C3_CHOICE[key] = c
+    _C3_TIMES[key] = times
+    return c
+
+
+def conv3x3_autotune_table():
+    """[(direction, N, H, W, Cin, Cout, stride, chosen, {backend: ms})] of every tuned 3x3 direction."""
+    return [k + (v, dict(_C3_TIMES.get(k, {}))) for k, v in sorted(_C3_CHOICE.items())]
+
+
+class _Conv3x3Fn(torch.autograd.Function):
+    """3x3 / pad 1 conv: each direction on its autotuned backend; the weight gradient on the
+    side stream / deferred / into the engine's bucket view exactly like the 1x1 path."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride):
+        y = _run3("fwd", _pick3("fwd", x, weight, None, stride), x, weight, None, stride)
+        ctx.save_for_backward(x, weight)
+        ctx.stride = stride
+        ctx.weight = weight
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        stride = ctx.stride
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = dw = None
+        f = None
+        if ctx.needs_input_grad[1]:
+            be = _pick3("wgrad", x, w, dy, stride)
+            tgt = _wg.grad_target(ctx.weight) if _wg._DEFER else None
+            if tgt is not None:
+                def late(dy=dy, x=x, w=w, tgt=tgt, be=be):
+                    _wg.into_target(_run3("wgrad", be, x, w, dy, stride, out=tgt), tgt)
+            if tgt is not None and _wg.defer(dy.device, late):
+                dw = tgt.view_as(tgt)
+            else:
+                f = _wg.fork(dy, ctx.weight)
+
+        def wg():
+            be = _pick3("wgrad", x, w, dy, stride)  # autotuned on the current stream
+            tgt = _wg.grad_target(ctx.weight) if be != "miopen" else None
+            with f as side:
+                d = _wg.into_target(_run3("wgrad", be, x, w, dy, stride, out=tgt), tgt)
+                if side:
+                    s = torch.cuda.current_stream(dy.device)
+                    _wg.tag(dy, s)
+                    _wg.tag(x, s)
+                    _wg.tag(d, f.main)
+            return d
+
+        if f is not None and _wg._WG_FIRST:
+            dw = wg()
+        if ctx.needs_input_grad[0]:
+            dx = _run3("dgrad", _pick3("dgrad", x, w, dy, stride), x, w, dy, stride)
+        if f is not None and not _wg._WG_FIRST:
+            dw = wg()
+        return dx, dw, None
+
+
+class _Conv3x3StatsFn(torch.autograd.Function):
+    """3x3 forward on the implicit GEMM whose epilogue also emits the following BatchNorm's
+    per-(row tile, channel) sum / sum of squares; backward = _Conv3x3Fn's."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride, tile):
+        nb, cin, h, w = x.shape
+        cout = weight.shape[0]
+        ho, wo = (h - 1) // stride + 1, (w - 1) // stride + 1
+        y = torch.empty((nb, cout, ho, wo), device=x.device, dtype=torch.float32, memory_format=torch.channels_last)
+        part = torch.empty(((nb * ho * wo + 63) // 64) * 2 * cout, device=x.device, dtype=torch.float32)
+        _native.lib().conv3x3_f32(0, x, weight, y, stride, 1, int(tile), part)
+        ctx.save_for_backward(x, weight)
+        ctx.stride = stride
+        ctx.weight = weight
+        ctx.mark_non_differentiable(part)
+        ctx.set_materialize_grads(False)  # no zero tensor for the statistics' gradient
+        return y, part
+
+    @staticmethod
+    def backward(ctx, dy, _dpart=None):
+        if dy is None:
+            return None, None, None, None
+        dx, dw, _ = _Conv3x3Fn.backward(ctx, dy)
+        return dx, dw, None, None
 
 
 class Conv1x1F32(_wg.Conv2dSplitGrad):

@@ -359,6 +359,11 @@ class Conv2dSplitGrad(nn.Conv2d):
     on GPU; bias / string padding / non-zero padding modes / CPU fall back to ``nn.Conv2d``."""
 
     def forward(self, x):
+        if self.kernel_size == (3, 3) and x.is_cuda:
+            from . import conv as _conv  # (conv imports this module)
+
+            if _conv.conv3x3_ok(x, self):  # implicit GEMM on the f32 MFMA kernel, autotuned vs MIOpen
+                return _conv._Conv3x3Fn.apply(x, self.weight, self.stride[0])
         if (_ENABLED and x.is_cuda and self.bias is None and self.padding_mode == "zeros"
                 and not isinstance(self.padding, str) and torch.is_grad_enabled() and self.weight.requires_grad):
             w = self.weight
