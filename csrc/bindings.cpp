@@ -732,9 +732,34 @@ static void check_operand(const Tensor& x, bool kc, int64_t ld, int64_t rows, in
   TORCH_CHECK(x.numel() >= need && ld >= (kc ? K : rows), what, ": view exceeds the tensor");
 }
 
+// BN-backward epilogue operands: x [M][N] fp32 dense (the BN input), mask [M*N/8] uint8 (None: no
+// ReLU), save [>= 2N] fp32 (mean, invstd)
+static bool bn_epi(const c10::optional<Tensor>& bx, const c10::optional<Tensor>& bmask,
+                   const c10::optional<Tensor>& bsave, int64_t M, int64_t N, grace::BnBwdEpi* e) {
+  if (!(bx.has_value() && bx->defined())) return false;
+  CHECK_DEV((*bx));
+  CHECK_DT((*bx), at::kFloat);
+  TORCH_CHECK(bx->numel() == M * N && (bx->is_contiguous() || bx->is_contiguous(at::MemoryFormat::ChannelsLast)) &&
+                  reinterpret_cast<uintptr_t>(bx->data_ptr()) % 16 == 0 && N % 8 == 0,
+              "bn epilogue: x must be a dense 16-B aligned [M][N] image, N % 8 == 0");
+  TORCH_CHECK(bsave.has_value() && bsave->defined() && bsave->is_cuda() && bsave->scalar_type() == at::kFloat &&
+                  bsave->numel() >= 2 * N && reinterpret_cast<uintptr_t>(bsave->data_ptr()) % 16 == 0,
+              "bn epilogue: save [>= 2N] fp32");
+  e->x = bx->data_ptr<float>();
+  e->save = bsave->data_ptr<float>();
+  e->mask = nullptr;
+  if (bmask.has_value() && bmask->defined()) {
+    TORCH_CHECK(bmask->is_cuda() && bmask->scalar_type() == at::kByte && bmask->is_contiguous() &&
+                    bmask->numel() == M * N / 8, "bn epilogue: mask [M*N/8] uint8");
+    e->mask = bmask->data_ptr<uint8_t>();
+  }
+  return true;
+}
+
 int64_t gemm_f32(const Tensor& A, bool a_kc, int64_t lda, const Tensor& B, bool b_kc, int64_t ldb, const Tensor& C,
                  int64_t ldc, int64_t M, int64_t N, int64_t K, int64_t splits, int64_t tile,
-                 const c10::optional<Tensor>& stats) {
+                 const c10::optional<Tensor>& stats, const c10::optional<Tensor>& bn_x,
+                 const c10::optional<Tensor>& bn_mask, const c10::optional<Tensor>& bn_save) {
   check_operand(A, a_kc, lda, M, K, "A");
   check_operand(B, b_kc, ldb, N, K, "B");
   CHECK_DEV(C);
@@ -750,9 +775,12 @@ int64_t gemm_f32(const Tensor& A, bool a_kc, int64_t lda, const Tensor& B, bool 
     TORCH_CHECK(stats->is_contiguous() && stats->numel() >= ((M + 63) / 64) * 2 * N, "stats: [ceil(M/64)][2][N]");
     st = stats->data_ptr<float>();
   }
+  grace::BnBwdEpi epi{};
+  const bool has_epi = bn_epi(bn_x, bn_mask, bn_save, M, N, &epi);
+  TORCH_CHECK(!has_epi || (st != nullptr && ldc == N), "bn epilogue: needs stats and a dense C");
   DevGuard guard(C.device());
   return grace::gemm_f32(A.data_ptr<float>(), a_kc, lda, B.data_ptr<float>(), b_kc, ldb, C.data_ptr<float>(), ldc,
-                         (int)M, (int)N, (int)K, (int)splits, cur_stream(), (int)tile, st);
+                         (int)M, (int)N, (int)K, (int)splits, cur_stream(), (int)tile, st, has_epi ? &epi : nullptr);
 }
 
 // 3x3 / pad 1 implicit-GEMM convolution (gemm_f32.hip).  Activations and the weight are NCHW-shaped
@@ -767,14 +795,18 @@ static void check_cl(const Tensor& t, std::initializer_list<int64_t> shape, cons
 }
 
 int64_t conv3x3_f32(int64_t dir, const Tensor& act, const Tensor& other, const Tensor& C, int64_t stride,
-                    int64_t splits, int64_t tile, const c10::optional<Tensor>& stats) {
+                    int64_t splits, int64_t tile, const c10::optional<Tensor>& stats, int64_t ksize,
+                    const c10::optional<Tensor>& bn_x, const c10::optional<Tensor>& bn_mask,
+                    const c10::optional<Tensor>& bn_save) {
   TORCH_CHECK(dir >= 0 && dir <= 2, "conv3x3_f32: dir 0 (fwd) / 1 (dgrad) / 2 (wgrad)");
   TORCH_CHECK(stride == 1 || (stride == 2 && dir != 1), "conv3x3_f32: stride 1, or 2 for fwd / wgrad");
+  TORCH_CHECK(ksize == 3 || (ksize == 1 && dir != 1), "conv3x3_f32: 3x3 (pad 1), or 1x1 (pad 0) fwd / wgrad");
+  const int64_t K = ksize;
   int64_t N, H, W, Cin, Cout;
   if (dir == 1) {  // act = dY [N, Cout, H, W], other = weight, C = dX [N, Cin, H, W]
     N = act.size(0), Cout = act.size(1), H = act.size(2), W = act.size(3), Cin = C.size(1);
     check_cl(act, {N, Cout, H, W}, "dY");
-    check_cl(other, {Cout, Cin, 3, 3}, "weight");
+    check_cl(other, {Cout, Cin, K, K}, "weight");
     check_cl(C, {N, Cin, H, W}, "dX");
     TORCH_CHECK(Cout % 32 == 0 && Cin % 4 == 0, "conv3x3_f32 dgrad: Cout % 32, Cin % 4");
   } else {
@@ -782,30 +814,36 @@ int64_t conv3x3_f32(int64_t dir, const Tensor& act, const Tensor& other, const T
     const int64_t Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
     if (dir == 0) {  // other = weight, C = y
       Cout = other.size(0);
-      check_cl(other, {Cout, Cin, 3, 3}, "weight");
+      check_cl(other, {Cout, Cin, K, K}, "weight");
       check_cl(C, {N, Cout, Ho, Wo}, "y");
       TORCH_CHECK(Cin % 32 == 0 && Cout % 4 == 0, "conv3x3_f32 fwd: Cin % 32, Cout % 4");
     } else {  // other = dY, C = dW
       Cout = other.size(1);
       check_cl(other, {N, Cout, Ho, Wo}, "dY");
-      check_cl(C, {Cout, Cin, 3, 3}, "dW");
+      check_cl(C, {Cout, Cin, K, K}, "dW");
       TORCH_CHECK(Cin % 4 == 0 && Cout % 4 == 0, "conv3x3_f32 wgrad: Cin % 4, Cout % 4");
     }
     check_cl(act, {N, Cin, H, W}, "x");
   }
   TORCH_CHECK(N * H * W < (1 << 24), "conv3x3_f32: N*H*W < 2^24 (float pixel division)");
   float* st = nullptr;
+  grace::BnBwdEpi epi{};
+  const bool has_epi = dir == 1 && bn_epi(bn_x, bn_mask, bn_save, N * H * W, Cin, &epi);
   if (stats.has_value() && stats->defined()) {
-    TORCH_CHECK(dir == 0 && splits == 1, "conv3x3_f32: statistics on the forward with splits = 1");
+    TORCH_CHECK((dir == 0 || has_epi) && splits == 1,
+                "conv3x3_f32: statistics on the forward / the data grad's BN epilogue, splits = 1");
     CHECK_DEV((*stats));
     CHECK_DT((*stats), at::kFloat);
-    const int64_t M = N * ((H - 1) / stride + 1) * ((W - 1) / stride + 1);
-    TORCH_CHECK(stats->is_contiguous() && stats->numel() >= ((M + 63) / 64) * 2 * Cout, "stats: [ceil(M/64)][2][Cout]");
+    const int64_t M = dir == 1 ? N * H * W : N * ((H - 1) / stride + 1) * ((W - 1) / stride + 1);
+    const int64_t NC = dir == 1 ? Cin : Cout;
+    TORCH_CHECK(stats->is_contiguous() && stats->numel() >= ((M + 63) / 64) * 2 * NC, "stats: [ceil(M/64)][2][N]");
     st = stats->data_ptr<float>();
   }
+  TORCH_CHECK(!has_epi || st != nullptr, "bn epilogue: needs stats");
   DevGuard guard(C.device());
   return grace::conv3x3_f32((int)dir, act.data_ptr<float>(), other.data_ptr<float>(), C.data_ptr<float>(), (int)N,
-                            (int)H, (int)W, (int)Cin, (int)Cout, (int)stride, (int)splits, (int)tile, st, cur_stream());
+                            (int)H, (int)W, (int)Cin, (int)Cout, (int)stride, (int)splits, (int)tile, st, cur_stream(), (int)ksize,
+                            has_epi ? &epi : nullptr);
 }
 
 // ------------------------------------------------------------------------------ segment stats
@@ -1115,10 +1153,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sketch_decode", &sketch_decode);
   m.def("quantile_select", &quantile_select);
   m.def("conv3x3_f32", &conv3x3_f32, py::arg("dir"), py::arg("act"), py::arg("other"), py::arg("C"),
-        py::arg("stride") = 1, py::arg("splits") = 0, py::arg("tile") = 0, py::arg("stats") = py::none());
+        py::arg("stride") = 1, py::arg("splits") = 0, py::arg("tile") = 0, py::arg("stats") = py::none(),
+        py::arg("ksize") = 3, py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(),
+        py::arg("bn_save") = py::none());
   m.def("gemm_f32", &gemm_f32, py::arg("A"), py::arg("a_kc"), py::arg("lda"), py::arg("B"), py::arg("b_kc"),
         py::arg("ldb"), py::arg("C"), py::arg("ldc"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("splits"),
-        py::arg("tile") = 0, py::arg("stats") = py::none());
+        py::arg("tile") = 0, py::arg("stats") = py::none(), py::arg("bn_x") = py::none(),
+        py::arg("bn_mask") = py::none(), py::arg("bn_save") = py::none());
   m.def("axpby", &axpby);
   m.def("scale_", &scale_);
   m.def("gather_segments", &gather_segments);

@@ -147,17 +147,27 @@ void quantile_select(const ChunkTable& ct, int n_seg, const float* x, int max_sl
 // ---------------------------------------------------------------- gemm_f32.hip
 // C[m][n] (+)= sum_k A(m,k) B(n,k) on the f32 MFMA; X(r,k) = x[r*ld+k] (kcontig) or x[k*ld+r];
 // splits > 1: split-K with f32 atomics into C (zeroed here; needs ldc == N)
+// BatchNorm-backward epilogue operands (gemm_f32 / conv3x3_f32 data grad with stats): C is the
+// gradient of a BN(+ReLU) output; x / mask / save are that BN's input, forward ReLU mask bits and
+// save (mean, invstd); stats receives [tiles][2][N] = [sum dz | sum dz (x - mean)].
+struct BnBwdEpi {
+  const float* x;
+  const uint8_t* mask;
+  const float* save;
+};
 int gemm_f32(const float* A, bool a_kcontig, int64_t lda, const float* B, bool b_kcontig, int64_t ldb, float* C,
               int64_t ldc, int M, int N, int K, int splits, hipStream_t stream, int tile = 0,
-             float* stats = nullptr);
+             float* stats = nullptr, const BnBwdEpi* bnb = nullptr);
 // 3x3 (pad 1) convolution of NHWC fp32 activations as an implicit GEMM on the same kernel (no
 // im2col).  dir 0: C = y [N,Ho,Wo,Cout] from act = x, other = W [Cout][3][3][Cin] (+ stats as
 // gemm_f32); dir 1 (stride 1): C = dx [N,H,W,Cin] from act = dY, other = W; dir 2: C = dW
 // [Cout][3][3][Cin] from act = x, other = dY (splits 0 = auto split-K, C zeroed).  Cin % 32 == 0
 // (dir 0), Cout % 32 == 0 (dir 1), Cin % 4 == 0 (dir 2), N*Ho*Wo and N*H*W < 2^24.  Returns the
 // row tiles of C.
+// ksize 1: a strided 1x1 (pad 0) convolution on the same path (one tap).
 int conv3x3_f32(int dir, const float* act, const float* other, float* C, int N, int H, int W, int Cin, int Cout,
-                int stride, int splits, int tile, float* stats, hipStream_t stream);
+                int stride, int splits, int tile, float* stats, hipStream_t stream, int ksize = 3,
+                const BnBwdEpi* bnb = nullptr);
 
 // ---------------------------------------------------------------- ef.hip (elementwise)
 void axpby(const float* x, const float* y, float* out, int64_t n, float a, float b, hipStream_t stream);
@@ -216,6 +226,10 @@ void bn_act_forward_from_partials(const float* x, const float* res, const float*
                                   const float* gamma, const float* beta, float* running_mean, float* running_var,
                                   int64_t* nbt, float momentum, float eps, bool relu, float* save, float* y,
                                   uint8_t* mask, hipStream_t stream);
+// Backward from the consuming conv's data-grad GEMM epilogue partials (BnBwdEpi): fold + dx pass.
+void bn_act_backward_from_partials(const float* dy, const float* x, const uint8_t* mask, const float* part, int tiles,
+                                   int64_t M, int C, const float* gamma, const float* save, bool relu, float* dgamma,
+                                   float* dbeta, float* coef, float* dx, hipStream_t stream);
 // fixed-order tree reductions in every BN backward (run-to-run bitwise reproducible) instead of
 // the default atomic totals (GRACE_BN_DETERMINISTIC=1 at start-up does the same)
 void bn_set_deterministic(bool on);

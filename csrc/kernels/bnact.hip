@@ -1694,6 +1694,45 @@ __global__ __launch_bounds__(kB) void bn_stats_fold_kernel(const float* __restri
   if (threadIdx.x == 0 && blockIdx.x == 0 && o.nbt) *o.nbt += 1;
 }
 
+// BN backward totals from the consuming conv's data-grad GEMM epilogue (gemm_f32.hip bx / bmask:
+// per (row tile, channel) [sum dz | sum dz (x - mean)]): the reduction pass over (dy, x)
+// disappears; this fold reads tiles x 2C floats (fp64, fixed order: deterministic) and writes the
+// dx pass's coefficients and the parameter gradients exactly as bn_reduce_kernel's finisher.
+__global__ __launch_bounds__(kB) void bn_grad_fold_kernel(const float* __restrict__ part, int tiles, int64_t M,
+                                                          int C, GradOut o) {
+  const int cl = threadIdx.x & 31, ph = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
+  double s1 = 0.0, s2 = 0.0;
+  if (c < C)
+    for (int t = ph; t < tiles; t += 8) {
+      s1 += (double)part[(int64_t)t * 2 * C + c];
+      s2 += (double)part[(int64_t)t * 2 * C + C + c];
+    }
+  __shared__ double l1[8][32], l2[8][32];
+  l1[ph][cl] = s1;
+  l2[ph][cl] = s2;
+  __syncthreads();
+  if (ph == 0 && c < C) {
+    double S1 = 0.0, S2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      S1 += l1[i][cl];
+      S2 += l2[i][cl];
+    }
+    const double inv_m = 1.0 / (double)M;
+    const float mean = o.save[c], invstd = o.save[C + c];
+    const float ga = o.gamma ? o.gamma[c] : 1.f;
+    const double dg = S2 * (double)invstd;  // dgamma = sum dz x^
+    if (o.dgamma) o.dgamma[c] = (float)dg;
+    if (o.dbeta) o.dbeta[c] = (float)S1;
+    const double a = (double)ga * invstd;
+    const double b = -a * invstd * dg * inv_m;
+    o.coef[c] = (float)a;
+    o.coef[C + c] = (float)b;
+    o.coef[2 * C + c] = (float)(-a * S1 * inv_m - b * mean);
+  }
+}
+
 // ATOMIC mode (default; GRACE_BN_ATOMIC_CHUNKS bounds it by chunk count, GRACE_BN_DETERMINISTIC=1
 // or a repeated backward of one forward select the fixed-order tree): the reduce kernel adds its blocks' partial rows into save[4C..6C) (zeroed by
 // the forward's statistics finisher) and the dx kernel derives the coefficients (CoefSrc).
@@ -1885,6 +1924,22 @@ void bn_act_forward_from_partials(const float* x, const float* res, const float*
     hipLaunchKernelGGL((bn_apply_kernel<float, false, true>), dim3(gb), dim3(kB), 0, stream, x, res, save, y, mask, n_vec, C);
   else
     hipLaunchKernelGGL((bn_apply_kernel<float, false, false>), dim3(gb), dim3(kB), 0, stream, x, res, save, y, mask, n_vec, C);
+}
+
+void bn_act_backward_from_partials(const float* dy, const float* x, const uint8_t* mask, const float* part, int tiles,
+                                   int64_t M, int C, const float* gamma, const float* save, bool relu, float* dgamma,
+                                   float* dbeta, float* coef, float* dx, hipStream_t stream) {
+  GradOut o{gamma, save, dgamma, dbeta, coef};
+  hipLaunchKernelGGL(bn_grad_fold_kernel, dim3((C + 31) / 32), dim3(kB), 0, stream, part, tiles, M, C, o);
+  const int64_t n_vec = M * C / 8;
+  const int gb = apply_grid(n_vec, C);
+  const CoefSrc cs = CoefSrc{coef, save};
+  if (relu && mask != nullptr)
+    hipLaunchKernelGGL((bn_dx_kernel<float, true, false, false>), dim3(gb), dim3(kB), 0, stream, dy, (const float*)nullptr,
+                       x, mask, cs, dx, (float*)nullptr, n_vec, C);
+  else
+    hipLaunchKernelGGL((bn_dx_kernel<float, false, false, false>), dim3(gb), dim3(kB), 0, stream, dy,
+                       (const float*)nullptr, x, (const uint8_t*)nullptr, cs, dx, (float*)nullptr, n_vec, C);
 }
 
 void bn_set_deterministic(bool on) { g_det_mode = on ? 1 : 0; }

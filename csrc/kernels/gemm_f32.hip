@@ -69,9 +69,17 @@ struct GemmParams {
   int gHs, gWs;        // grid of the gathered activation
   int gC;              // its channels (k per tap, mode 2; rows per tap, mode 3)
   int gS, gSign;       // row / k pixel -> source pixel: s * (y, x) + sign * (dy, dx)
+  int gT;              // taps per side: 3 (3x3, pad 1) or 1 (1x1, pad 0)
   float gInvWr, gInvHr;
   int kt;              // mode 4: k per tap (Cout)
   int64_t tap_off;     // mode 4: element offset between the taps of a weight row (Cin)
+  // BatchNorm-backward epilogue (with stats): C is the gradient dy of a BN(+ReLU) output whose
+  // input x, ReLU mask bits and forward save (mean [N], invstd [N] at +N) are given; the epilogue
+  // writes per (row tile, column) [sum dz | sum dz * (x - mean)], dz = dy masked by the ReLU --
+  // the BN backward's reduction pass over (dy, x) disappears (ops/bnact.py hand-off)
+  const float* bx;
+  const uint8_t* bmask;  // null: no ReLU
+  const float* bsave;
 };
 
 // Operand modes.  0: K-contig rows, 1: MN-contig, 2: implicit conv rows (K-contig gather of
@@ -124,8 +132,8 @@ struct Operand {
       rok = r < rmax;
       const int tap = r / p.gC;
       rc = r - tap * p.gC;
-      rdy = tap / 3 - 1;
-      rdx = tap % 3 - 1;
+      rdy = p.gT == 3 ? tap / 3 - 1 : 0;  // 3x3 pad 1, or 1x1 pad 0 (strided)
+      rdx = p.gT == 3 ? tap % 3 - 1 : 0;
     }
   }
 
@@ -133,7 +141,7 @@ struct Operand {
                                        int k0, int kmax) {
     if constexpr (MODE == 2) {
       const int tap = k0 / p.gC;  // uniform over the slice (C % BK == 0)
-      const int dy = (tap / 3 - 1) * p.gSign, dx = (tap % 3 - 1) * p.gSign;
+      const int dy = p.gT == 3 ? (tap / 3 - 1) * p.gSign : 0, dx = p.gT == 3 ? (tap % 3 - 1) * p.gSign : 0;
       const int c = k0 - tap * p.gC + 4 * (threadIdx.x % (BK / 4));
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
@@ -288,6 +296,9 @@ __global__ __launch_bounds__(kGB, 2) void gemm_f32_kernel(GemmParams p) {
     constexpr int RPI = kWave / LPR;     // rows per wave instruction
     const int cq = lane % LPR;
     const int col = n0 + wn * WN + 4 * cq;
+    const bool bnb = p.stats != nullptr && p.bx != nullptr;
+    float4 bmean = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (bnb && col + 3 < p.N) bmean = *reinterpret_cast<const float4*>(p.bsave + col);
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
 #pragma unroll
@@ -303,7 +314,18 @@ __global__ __launch_bounds__(kGB, 2) void gemm_f32_kernel(GemmParams p) {
         if (row < p.M) {
           const float4 v = *reinterpret_cast<const float4*>(slab + rr * CP + 4 * cq);
           float* dst = p.C + (int64_t)row * p.ldc + col;
-          if (p.stats != nullptr) {
+          if (bnb) {
+            if (col + 3 < p.N) {
+              const int64_t e = (int64_t)row * p.N + col;  // dense [M][N] BN activation (ldc == N)
+              const float4 xv = *reinterpret_cast<const float4*>(p.bx + e);
+              const uint32_t mb = p.bmask != nullptr ? (uint32_t)(p.bmask[e >> 3] >> (e & 7)) : 0xfu;
+              const float d0 = (mb & 1u) ? v.x : 0.f, d1 = (mb & 2u) ? v.y : 0.f;
+              const float d2 = (mb & 4u) ? v.z : 0.f, d3 = (mb & 8u) ? v.w : 0.f;
+              st_s[0] += d0; st_s[1] += d1; st_s[2] += d2; st_s[3] += d3;
+              st_q[0] = fmaf(d0, xv.x - bmean.x, st_q[0]); st_q[1] = fmaf(d1, xv.y - bmean.y, st_q[1]);
+              st_q[2] = fmaf(d2, xv.z - bmean.z, st_q[2]); st_q[3] = fmaf(d3, xv.w - bmean.w, st_q[3]);
+            }
+          } else if (p.stats != nullptr) {
             st_s[0] += v.x; st_s[1] += v.y; st_s[2] += v.z; st_s[3] += v.w;
             st_q[0] = fmaf(v.x, v.x, st_q[0]); st_q[1] = fmaf(v.y, v.y, st_q[1]);
             st_q[2] = fmaf(v.z, v.z, st_q[2]); st_q[3] = fmaf(v.w, v.w, st_q[3]);
@@ -436,9 +458,15 @@ void set_splits(GemmParams& p, int splits, float* stats, hipStream_t stream) {
 }  // namespace
 
 int gemm_f32(const float* A, bool a_kcontig, int64_t lda, const float* B, bool b_kcontig, int64_t ldb, float* C,
-             int64_t ldc, int M, int N, int K, int splits, hipStream_t stream, int tile, float* stats) {
+             int64_t ldc, int M, int N, int K, int splits, hipStream_t stream, int tile, float* stats,
+             const BnBwdEpi* bnb) {
   if (M <= 0 || N <= 0) return 0;
   GemmParams p{};
+  if (bnb != nullptr) {
+    p.bx = bnb->x;
+    p.bmask = bnb->mask;
+    p.bsave = bnb->save;
+  }
   p.A = A;
   p.B = B;
   p.C = C;
@@ -457,17 +485,23 @@ int gemm_f32(const float* A, bool a_kcontig, int64_t lda, const float* B, bool b
 }
 
 int conv3x3_f32(int dir, const float* act, const float* other, float* C, int N, int H, int W, int Cin, int Cout,
-                int stride, int splits, int tile, float* stats, hipStream_t stream) {
-  const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;  // 3x3, pad 1
+                int stride, int splits, int tile, float* stats, hipStream_t stream, int ksize, const BnBwdEpi* bnb) {
+  const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;  // 3x3 pad 1, or 1x1 pad 0
+  const int T = ksize * ksize;
   GemmParams p{};
+  if (bnb != nullptr && dir == 1) {
+    p.bx = bnb->x;
+    p.bmask = bnb->mask;
+    p.bsave = bnb->save;
+  }
   p.C = C;
   if (dir == 0) {  // forward: rows = output pixels, k = (tap, ci)
     p.A = act;
     p.B = other;
     p.M = N * Ho * Wo;
     p.N = Cout;
-    p.K = 9 * Cin;
-    p.ldb = 9 * Cin;
+    p.K = T * Cin;
+    p.ldb = T * Cin;
     p.ldc = Cout;
     p.gHr = Ho, p.gWr = Wo, p.gHs = H, p.gWs = W, p.gC = Cin, p.gS = stride, p.gSign = 1;
   } else if (dir == 1) {  // data grad (stride 1): rows = input pixels, k = (tap, co), flipped taps
@@ -475,8 +509,8 @@ int conv3x3_f32(int dir, const float* act, const float* other, float* C, int N, 
     p.B = other;
     p.M = N * H * W;
     p.N = Cin;
-    p.K = 9 * Cout;
-    p.ldb = 9 * Cin;
+    p.K = T * Cout;
+    p.ldb = T * Cin;
     p.ldc = Cin;
     p.kt = Cout;
     p.tap_off = Cin;
@@ -485,17 +519,18 @@ int conv3x3_f32(int dir, const float* act, const float* other, float* C, int N, 
     p.A = other;  // dY [N, Ho, Wo, Cout]: MN-contig, ld = Cout
     p.B = act;    // x
     p.M = Cout;
-    p.N = 9 * Cin;
+    p.N = T * Cin;
     p.K = N * Ho * Wo;
     p.lda = Cout;
-    p.ldc = 9 * Cin;
+    p.ldc = T * Cin;
     p.gHr = Ho, p.gWr = Wo, p.gHs = H, p.gWs = W, p.gC = Cin, p.gS = stride, p.gSign = 1;
   }
+  p.gT = ksize;
   p.gInvWr = 1.f / (float)p.gWr;
   p.gInvHr = 1.f / (float)p.gHr;
   if (p.M <= 0 || p.N <= 0) return 0;
   if (splits == 0) splits = dir == 2 ? auto_splits(p.M, p.N, p.K, p.ldc) : 1;
-  set_splits(p, splits, dir == 0 ? stats : nullptr, stream);
+  set_splits(p, splits, (dir == 0 || p.bx != nullptr) ? stats : nullptr, stream);
   if (dir == 0) return launch_tile<2, 0>(p, tile, stream);
   if (dir == 1) return launch_tile<2, 4>(p, tile, stream);
   return launch_tile<1, 3>(p, tile, stream);

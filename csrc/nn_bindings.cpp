@@ -154,6 +154,48 @@ std::vector<Tensor> bn_act_bwd(const Tensor& dy, const c10::optional<Tensor>& dy
   return {dx, dres, dg, db};
 }
 
+// BN backward whose reduction came from the consumer conv's data-grad GEMM epilogue (part:
+// [tiles][2][C] = [sum dz | sum dz (x - mean)]); dy is that GEMM's output (unmasked).
+std::vector<Tensor> bn_act_bwd_partials(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& mask,
+                                        const c10::optional<Tensor>& weight, const Tensor& save, const Tensor& part,
+                                        int64_t tiles, bool relu, bool want_dweight,
+                                        const c10::optional<Tensor>& dweight_out,
+                                        const c10::optional<Tensor>& dbias_out) {
+  int64_t M, C;
+  check_rows(x, "x", &M, &C);
+  same_layout(x, dy, "grad_output");
+  TORCH_CHECK(x.scalar_type() == at::kFloat, "bn_act_bwd_partials: fp32 activations");
+  const bool has_mask = mask.has_value() && mask->defined();
+  TORCH_CHECK(!relu || has_mask, "bn_act_bwd_partials: a ReLU needs the forward's mask");
+  if (has_mask)
+    TORCH_CHECK(mask->is_cuda() && mask->scalar_type() == at::kByte && mask->is_contiguous() && mask->numel() == M * C / 8,
+                "mask [M*C/8] uint8");
+  TORCH_CHECK(save.is_cuda() && save.scalar_type() == at::kFloat && save.numel() == 6 * C, "save");
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() && tiles >= 1 &&
+                  part.numel() >= tiles * 2 * C, "part [tiles][2][C]");
+  DevGuard guard(x.device());
+  auto f32 = x.options().dtype(at::kFloat);
+  auto out_or = [&](const c10::optional<Tensor>& o) {
+    if (o.has_value() && o->defined()) {
+      TORCH_CHECK(o->is_cuda() && o->scalar_type() == at::kFloat && o->is_contiguous() && o->numel() == C &&
+                      o->get_device() == x.get_device(), "bn_act_bwd_partials: gradient output must be contiguous fp32 [C]");
+      return *o;
+    }
+    return at::empty({C}, f32);
+  };
+  Tensor dg = want_dweight ? out_or(dweight_out) : Tensor();
+  Tensor db = want_dweight ? out_or(dbias_out) : Tensor();
+  Tensor coef = at::empty({3 * C}, f32);
+  Tensor dx = at::empty_like(x);
+  grace::bn_act_backward_from_partials(dy.data_ptr<float>(), x.data_ptr<float>(),
+                                       relu ? mask->data_ptr<uint8_t>() : nullptr, part.data_ptr<float>(), (int)tiles,
+                                       M, (int)C, opt_f32(weight, C, "weight"), save.data_ptr<float>(), relu,
+                                       want_dweight ? dg.data_ptr<float>() : nullptr,
+                                       want_dweight ? db.data_ptr<float>() : nullptr, coef.data_ptr<float>(),
+                                       dx.data_ptr<float>(), cur_stream());
+  return {dx, dg, db};
+}
+
 // Fused SGD over a list of fp32 parameters (dense, grads / momentum buffers / bf16 working copies
 // with the parameter's strides).  bufs / w16 entries may be None.
 void sgd_step(const std::vector<Tensor>& params, const std::vector<Tensor>& grads,
@@ -325,4 +367,7 @@ void grace_bind_nn(py::module& m) {
   m.def("bn_set_atomic_chunks", [](int64_t n) { grace::bn_set_atomic_chunks((int)n); });
   m.def("bn_atomic_chunks", []() { return (int64_t)grace::bn_atomic_chunks(); });
   m.def("bn_act_fwd_partials", &bn_act_fwd_partials);
+  m.def("bn_act_bwd_partials", &bn_act_bwd_partials, py::arg("dy"), py::arg("x"), py::arg("mask"), py::arg("weight"),
+        py::arg("save"), py::arg("part"), py::arg("tiles"), py::arg("relu"), py::arg("want_dweight"),
+        py::arg("dweight_out") = py::none(), py::arg("dbias_out") = py::none());
 }

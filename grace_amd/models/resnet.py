@@ -33,6 +33,13 @@ def _conv1x1(cin, cout, stride=1):
     return Conv2dSplitGrad(cin, cout, 1, stride=stride, bias=False)
 
 
+def _down(down: nn.Module, x):
+    """The projection shortcut (conv -> BN): the BN statistics may come from the conv's epilogue."""
+    if isinstance(down, nn.Sequential) and len(down) == 2 and isinstance(down[1], BatchNormAct2d):
+        return conv_bn_act(down[0], down[1], x)
+    return down(x)
+
+
 class BasicBlock(nn.Module):
     expansion = 1
 
@@ -46,8 +53,8 @@ class BasicBlock(nn.Module):
 
     def forward(self, x):
         xm, xs = x if isinstance(x, tuple) else (x, x)
-        idt = xs if self.downsample is None else self.downsample(xs)
-        y = conv_bn_act(self.conv1, self.bn1, xm)
+        idt = xs if self.downsample is None else _down(self.downsample, xs)
+        y = conv_bn_act(self.conv1, self.bn1, xm, handoff=True)  # bn1's output feeds conv2 only
         return conv_bn_act(self.conv2, self.bn2, y, idt, dual=True)
 
 
@@ -74,11 +81,13 @@ class Bottleneck(nn.Module):
             idt, br = xs, None
         else:  # projection shortcut on a second stream, beside the main path (ops/wgrad.py branch)
             with branch(xs) as br:
-                idt = self.downsample(xs)
+                idt = _down(self.downsample, xs)
         # 1x1 conv -> BN pairs: the BN statistics may come from the conv GEMM's epilogue
         # (ops/conv.py conv_bn_act, autotuned; otherwise exactly bn(conv(x)))
-        y = conv_bn_act(self.conv1, self.bn1, xm)
-        y = conv_bn_act(self.conv2, self.bn2, y)
+        # bn1 / bn2 outputs feed exactly one conv each: their backward reductions come from the
+        # consuming conv's data-grad GEMM epilogue (ops/bnact.py BNHandoff)
+        y = conv_bn_act(self.conv1, self.bn1, xm, handoff=True)
+        y = conv_bn_act(self.conv2, self.bn2, y, handoff=True)
         if br is not None:
             idt = br.merge(idt)
         return conv_bn_act(self.conv3, self.bn3, y, idt, dual=True)

@@ -73,10 +73,35 @@ def _kernel_grad(g: Optional[torch.Tensor], like: torch.Tensor) -> Optional[torc
     return g
 
 
+# BN -> conv hand-off: a BN(+ReLU) output consumed by exactly ONE convolution (declared by the
+# model, e.g. bn1 -> conv2 and bn2 -> conv3 of a ResNet bottleneck) carries a BNHandoff.  The
+# consuming conv's data-grad GEMM (ops/conv.py) then also reduces [sum dz | sum dz (x - mean)] in
+# its epilogue (gemm_f32.hip BnBwdEpi) and this BN's backward only folds those partials and runs
+# its dx pass -- the reduction pass over (dy, x) disappears.  Used only when the gradient handed
+# to the BN backward IS the GEMM's output (same storage, no accumulation in between).
+_HANDOFF = __import__("os").environ.get("GRACE_BN_BWD_EPI", "1") == "1"
+
+
+class BNHandoff:
+    __slots__ = ("x", "mask", "save", "part", "tiles", "dz_ptr")
+
+    def __init__(self, x, mask, save):
+        self.x, self.mask, self.save = x, mask, save
+        self.part, self.tiles, self.dz_ptr = None, 0, 0
+
+    def publish(self, part: torch.Tensor, tiles: int, dz: torch.Tensor) -> None:
+        self.part, self.tiles, self.dz_ptr = part, int(tiles), dz.data_ptr()
+
+
+def handoff_of(x: torch.Tensor) -> Optional[BNHandoff]:
+    """The BN hand-off of a conv input (None unless the producing BN declared one)."""
+    return getattr(x, "_grace_bn_handoff", None) if _HANDOFF else None
+
+
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, nbt, momentum, eps, relu, dual,
-                partials=None, tiles=0):
+                partials=None, tiles=0, handoff=False):
         if partials is not None:  # statistics from the producing conv GEMM's epilogue (ops/conv.py)
             y, save, mask = _native.lib().bn_act_fwd_partials(x, residual, partials, int(tiles), weight, bias,
                                                               running_mean, running_var, nbt, float(momentum),
@@ -89,6 +114,10 @@ class _BNActFn(torch.autograd.Function):
         ctx.bn_params = (weight, bias)
         # the backward needs only the ReLU mask (1 bit per element), not the bf16 output
         ctx.save_for_backward(x, mask if relu else None, weight, save)
+        ctx.handoff = None
+        if handoff and not dual and residual is None and x.dtype == torch.float32 and x.shape[1] % 8 == 0:
+            ctx.handoff = BNHandoff(x, mask if relu else None, save)
+            y._grace_bn_handoff = ctx.handoff
         if dual:
             # two aliases of y for two consumers: autograd then hands their gradients to
             # backward() separately and the kernels sum them (no add kernel)
@@ -102,7 +131,18 @@ class _BNActFn(torch.autograd.Function):
         if dy is None:
             dy, dy2 = dy2, None
         if dy is None:
-            return (None,) * 13
+            return (None,) * 14
+        h = ctx.handoff
+        if h is not None and h.part is not None and dy2 is None and dy.data_ptr() == h.dz_ptr \
+                and dy.stride() == x.stride() and not ctx.has_res:
+            part, tiles = h.part, h.tiles
+            h.part = None  # one use per backward
+            want_w = weight is not None and ctx.needs_input_grad[2]
+            tw, tb = _param_targets(ctx, want_w)
+            dx, dw, db = _native.lib().bn_act_bwd_partials(dy, x, mask, weight, save, part, tiles, ctx.relu, want_w,
+                                                           tw, tb)
+            dw, db = _wg.into_target(dw, tw) if want_w else None, _wg.into_target(db, tb) if want_w else None
+            return (dx, None, dw, db if ctx.needs_input_grad[3] else None) + (None,) * 10
         dy = _kernel_grad(dy, x)
         dy2 = _kernel_grad(dy2, x)
         want_w = weight is not None and ctx.needs_input_grad[2]
@@ -116,17 +156,19 @@ class _BNActFn(torch.autograd.Function):
         dw, db = _wg.into_target(dw, tw) if want_w else None, _wg.into_target(db, tb) if want_w else None
         return (dx, dres if ctx.has_res and ctx.needs_input_grad[1] else None,
                 dw, db if ctx.needs_input_grad[3] else None,
-                None, None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None, None)
 
 
 def bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, residual: Optional[torch.Tensor] = None,
-           relu: bool = False, dual: bool = False, partials: Optional[torch.Tensor] = None, tiles: int = 0):
+           relu: bool = False, dual: bool = False, partials: Optional[torch.Tensor] = None, tiles: int = 0,
+           handoff: bool = False):
     """``act(bn(x) + residual)`` with the module's parameters and running statistics.
 
     ``dual=True`` returns ``(y, y_alias)``: two aliases of the output for two consumers (e.g. a
     ResNet block output feeding the next block's conv and its shortcut).  Their gradients reach
     the fused backward separately and are summed inside its kernels instead of by autograd's
-    add kernel (one full read+write pass of the activation saved per block)."""
+    add kernel (one full read+write pass of the activation saved per block).
+    ``handoff=True``: the caller guarantees ONE convolution consumes the output (BNHandoff)."""
     training = bn.training or not bn.track_running_stats
     if training and _fusable(x, bn, residual):
         track = bn.training and bn.track_running_stats
@@ -134,7 +176,7 @@ def bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, residual: Optional[torch.Tensor]
                               bn.running_mean if track else None, bn.running_var if track else None,
                               bn.num_batches_tracked if track else None,
                               bn.momentum if bn.momentum is not None else 0.0, bn.eps, relu, bool(dual),
-                              partials, tiles)
+                              partials, tiles, bool(handoff and _HANDOFF))
     y = nn.BatchNorm2d.forward(bn, x)
     if residual is not None:
         y = y + residual

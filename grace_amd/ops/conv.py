@@ -33,6 +33,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _native
+from . import bnact as _bn
 from . import wgrad as _wg
 
 _TARGET_BLOCKS = 512  # >> 256 CUs
@@ -205,6 +206,26 @@ def _pick(direction: str, x, wt, dy, wshape) -> str:
     return c
 
 
+def _dgrad_handoff(h, x, w, dy, ksize: int):
+    """Data grad on the MFMA GEMM with the producing BN's backward reduction in its epilogue
+    (ops/bnact.py BNHandoff); None when it does not apply.  ksize 1: w is [Cout, Cin] (plain
+    GEMM); 3: the channels_last 3x3 weight (implicit GEMM, stride 1)."""
+    if h is None or h.x.shape != x.shape or not h.x.is_contiguous(memory_format=torch.channels_last):
+        return None
+    nb, cin, hh, ww = x.shape
+    m = nb * hh * ww
+    dx = torch.empty_like(x, memory_format=torch.channels_last)
+    part = torch.empty(((m + 63) // 64) * 2 * cin, device=x.device, dtype=torch.float32)
+    C = _native.lib()
+    if ksize == 1:
+        cout = w.shape[0]
+        t = C.gemm_f32(dy, True, cout, w, False, cin, dx, cin, m, cin, cout, 1, 0, part, h.x, h.mask, h.save)
+    else:
+        t = C.conv3x3_f32(1, dy, w, dx, 1, 1, 0, part, 3, h.x, h.mask, h.save)
+    h.publish(part, t, dx)
+    return dx
+
+
 class _Conv1x1AutoFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight):
@@ -216,6 +237,7 @@ class _Conv1x1AutoFn(torch.autograd.Function):
         ctx.save_for_backward(x, wt)
         ctx.wshape = weight.shape
         ctx.weight = weight
+        ctx.bn_h = _bn.handoff_of(x)
         return y
 
     @staticmethod
@@ -255,7 +277,9 @@ class _Conv1x1AutoFn(torch.autograd.Function):
         if f is not None and _wg._WG_FIRST:
             dw = wg()
         if ctx.needs_input_grad[0]:
-            dx = _run("dgrad", _pick("dgrad", x, wt, dy, ctx.wshape), x, wt, dy, ctx.wshape)
+            dx = _dgrad_handoff(getattr(ctx, "bn_h", None), x, wt, dy, 1)
+            if dx is None:
+                dx = _run("dgrad", _pick("dgrad", x, wt, dy, ctx.wshape), x, wt, dy, ctx.wshape)
         if f is not None and not _wg._WG_FIRST:
             dw = wg()
         return dx, dw
@@ -280,6 +304,7 @@ class _Conv1x1StatsFn(torch.autograd.Function):
         ctx.save_for_backward(x, wt)
         ctx.wshape = weight.shape
         ctx.weight = weight
+        ctx.bn_h = _bn.handoff_of(x)
         ctx.mark_non_differentiable(part)
         # the statistics output never gets a gradient: without this autograd would materialise a
         # zero tensor for it in every backward (one fill kernel per layer on the critical path)
@@ -319,7 +344,7 @@ def _time(fn, reps=5):
 
 def _pick_bn(conv, bn, x, residual, relu) -> str:
     nb, cin, h, w = x.shape
-    k3 = conv.kernel_size == (3, 3)
+    k3 = conv.kernel_size == (3, 3) or conv.stride != (1, 1)  # implicit-GEMM conv (3x3 or strided 1x1)
     s = conv.stride[0]
     key = (nb * h * w, cin, conv.out_channels, bool(relu), residual is not None) + ((3, s) if k3 else ())
     c = _BN_CHOICE.get(key)
@@ -353,7 +378,7 @@ def _pick_bn(conv, bn, x, residual, relu) -> str:
         def fused(tile=tile):
             y = torch.empty((nb, cout, ho, wo), device=x.device, memory_format=torch.channels_last)
             if k3:
-                t = C.conv3x3_f32(0, xd, w4, y, s, 1, tile, part)
+                t = C.conv3x3_f32(0, xd, w4, y, s, 1, tile, part, w4.shape[2])
             else:
                 t = C.gemm_f32(xd, True, cin, wt, True, cin, y, cout, m, cout, cin, 1, tile, part)
             C.bn_act_fwd_partials(y, res, part, t, g, b, rm, rv, nbt, 0.1, 1e-5, bool(relu))
@@ -372,14 +397,15 @@ def bn_autotune_table():
     return [k + (v, dict(_BN_TIMES.get(k, {}))) for k, v in sorted(_BN_CHOICE.items())]
 
 
-def conv_bn_act(conv: nn.Module, bn: nn.Module, x: torch.Tensor, residual=None, dual: bool = False):
+def conv_bn_act(conv: nn.Module, bn: nn.Module, x: torch.Tensor, residual=None, dual: bool = False,
+                handoff: bool = False):
     """``bn(conv(x), residual, dual)`` for a 1x1 stride-1 ``Conv1x1F32`` or a 3x3 implicit-GEMM
     convolution (``conv3x3_ok``) followed by a fused
     ``BatchNormAct2d``: when the autotuner measured it faster (GEMM + statistics epilogue + fold +
     apply vs the best conv backend + the BN statistics and apply passes, each timed whole), the
     conv runs on the MFMA GEMM that also emits the BN statistics, and the BN skips its
     statistics pass over the activation.  Otherwise exactly ``bn(conv(x), residual, dual=dual)``."""
-    from .bnact import _fusable, bn_act
+    from .bnact import BatchNormAct2d, _fusable, bn_act
 
     relu = getattr(bn, "relu", False)
     bn_ok = _BN_FUSE and bn.training and bn.track_running_stats and bn.momentum is not None
@@ -391,7 +417,7 @@ def conv_bn_act(conv: nn.Module, bn: nn.Module, x: torch.Tensor, residual=None, 
             y, part = _Conv1x1StatsFn.apply(x, conv.weight, tile)
             if _fusable(y, bn, residual):
                 m = x.shape[0] * x.shape[2] * x.shape[3]
-                return bn_act(y, bn, residual, relu, dual, partials=part, tiles=_tiles_m(m, tile))
+                return bn_act(y, bn, residual, relu, dual, partials=part, tiles=_tiles_m(m, tile), handoff=handoff)
             return bn(y, residual, dual=dual)
     if bn_ok and isinstance(conv, _wg.Conv2dSplitGrad) and conv3x3_ok(x, conv):
         choice = _pick_bn(conv, bn, x, residual, relu)
@@ -400,8 +426,10 @@ def conv_bn_act(conv: nn.Module, bn: nn.Module, x: torch.Tensor, residual=None, 
             y, part = _Conv3x3StatsFn.apply(x, conv.weight, conv.stride[0], tile)
             if _fusable(y, bn, residual):
                 m = y.shape[0] * y.shape[2] * y.shape[3]
-                return bn_act(y, bn, residual, relu, dual, partials=part, tiles=_tiles_m(m, tile))
+                return bn_act(y, bn, residual, relu, dual, partials=part, tiles=_tiles_m(m, tile), handoff=handoff)
             return bn(y, residual, dual=dual)
+    if handoff and isinstance(bn, BatchNormAct2d):
+        return bn_act(conv(x), bn, residual, relu, dual, handoff=True)
     return bn(conv(x), residual, dual=dual)
 
 
@@ -432,9 +460,10 @@ C3_BACKENDS = ("miopen", "mfma", "mfma_t1", "mfma_t2", "mfma_t3", "mfma_t4")
 _C3_ON = os.environ.get("GRACE_CONV3X3", "1") == "1"
 
 
-def conv3x3_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
+def conv3x3_ok(x: torch.Tensor, conv: nn.Conv2d, bias_ok: bool = False) -> bool:
     """The implicit-GEMM path applies: fp32 channels_last activation and weight, 3x3 / pad 1 /
-    stride 1 or 2, no bias / groups / dilation, channels multiples of 32."""
+    stride 1 or 2, no groups / dilation, no bias (unless the caller adds it: ``bias_ok``),
+    channels multiples of 32."""
     if not (_C3_ON and (_AUTO or _ENABLED)):
         return False
     w = conv.weight
@@ -442,8 +471,11 @@ def conv3x3_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
         return False
     if torch.is_autocast_enabled() or not _native.native_on(x.device):
         return False
-    if conv.kernel_size != (3, 3) or conv.padding != (1, 1) or conv.dilation != (1, 1) or conv.groups != 1 \
-            or conv.bias is not None or conv.stride not in ((1, 1), (2, 2)) or conv.padding_mode != "zeros":
+    k3 = conv.kernel_size == (3, 3) and conv.padding == (1, 1)
+    k1s = conv.kernel_size == (1, 1) and conv.padding == (0, 0) and conv.stride == (2, 2)  # strided 1x1
+    if not (k3 or k1s) or conv.dilation != (1, 1) or conv.groups != 1 \
+            or (conv.bias is not None and not bias_ok) or conv.stride not in ((1, 1), (2, 2)) \
+            or conv.padding_mode != "zeros":
         return False
     if x.dim() != 4 or not x.is_contiguous(memory_format=torch.channels_last) or x.data_ptr() % 16:
         return False
@@ -454,12 +486,15 @@ def conv3x3_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
 
 
 def _run3(direction: str, backend: str, x, w, dy, stride: int, out=None):
-    """One direction of a 3x3 / pad 1 conv on one backend (x, dy, w channels_last)."""
+    """One direction of a 3x3 / pad 1 (or strided 1x1 / pad 0) conv on one backend (x, dy, w
+    channels_last)."""
+    ks = w.shape[2]
+    pad = (ks - 1) // 2
     if backend == "miopen":
         if direction == "fwd":
-            return F.conv2d(x, w, None, stride, 1)
+            return F.conv2d(x, w, None, stride, pad)
         mask = [direction == "dgrad", direction == "wgrad", False]
-        gi, gw, _ = torch.ops.aten.convolution_backward(dy, x, w, None, [stride, stride], [1, 1], [1, 1], False,
+        gi, gw, _ = torch.ops.aten.convolution_backward(dy, x, w, None, [stride, stride], [pad, pad], [1, 1], False,
                                                         [0, 0], 1, mask)
         return gi if direction == "dgrad" else gw
     tile = int(backend[6:]) if backend.startswith("mfma_t") else 0
@@ -469,28 +504,30 @@ def _run3(direction: str, backend: str, x, w, dy, stride: int, out=None):
     if direction == "fwd":
         ho, wo = (h - 1) // stride + 1, (wd - 1) // stride + 1
         y = torch.empty((nb, cout, ho, wo), device=x.device, dtype=torch.float32, memory_format=torch.channels_last)
-        C.conv3x3_f32(0, x, w, y, stride, 1, tile)
+        C.conv3x3_f32(0, x, w, y, stride, 1, tile, None, ks)
         return y
     if direction == "dgrad":
-        if stride != 1:
-            raise ValueError("implicit-GEMM data grad: stride 1 only")
+        if stride != 1 or ks != 3:
+            raise ValueError("implicit-GEMM data grad: 3x3 stride 1 only")
         dx = torch.empty_like(x, memory_format=torch.channels_last)
         C.conv3x3_f32(1, dy, w, dx, 1, 1, tile)
         return dx
     dw = out if (out is not None and out.is_contiguous(memory_format=torch.channels_last)
                  and out.data_ptr() % 16 == 0) else \
-        torch.empty((cout, cin, 3, 3), device=x.device, dtype=torch.float32, memory_format=torch.channels_last)
-    C.conv3x3_f32(2, x, dy, dw, stride, 0, tile)
+        torch.empty((cout, cin, ks, ks), device=x.device, dtype=torch.float32, memory_format=torch.channels_last)
+    C.conv3x3_f32(2, x, dy, dw, stride, 0, tile, None, ks)
     return dw
 
 
 def _pick3(direction: str, x, w, dy, stride: int) -> str:
     nb, cin, h, wd = x.shape
-    key = (direction, nb, h, wd, cin, w.shape[0], stride)
+    key = (direction, nb, h, wd, cin, w.shape[0], stride, w.shape[2])
     c = _C3_CHOICE.get(key)
     if c is not None:
         return c
-    if _ENABLED and not (direction == "dgrad" and stride != 1):
+    if direction == "dgrad" and (stride != 1 or w.shape[2] != 3):
+        return "miopen"
+    if _ENABLED:
         return "mfma"
     if torch.cuda.is_current_stream_capturing():
         return "miopen"  # never time inside a capture
@@ -507,7 +544,7 @@ def _pick3(direction: str, x, w, dy, stride: int) -> str:
 
 
 def conv3x3_autotune_table():
-    """[(direction, N, H, W, Cin, Cout, stride, chosen, {backend: ms})] of every tuned 3x3 direction."""
+    """[(direction, N, H, W, Cin, Cout, stride, ksize, chosen, {backend: ms})] of every tuned direction."""
     return [k + (v, dict(_C3_TIMES.get(k, {}))) for k, v in sorted(_C3_CHOICE.items())]
 
 
@@ -521,6 +558,7 @@ class _Conv3x3Fn(torch.autograd.Function):
         ctx.save_for_backward(x, weight)
         ctx.stride = stride
         ctx.weight = weight
+        ctx.bn_h = _bn.handoff_of(x) if stride == 1 and weight.shape[2] == 3 else None
         return y
 
     @staticmethod
@@ -556,7 +594,9 @@ class _Conv3x3Fn(torch.autograd.Function):
         if f is not None and _wg._WG_FIRST:
             dw = wg()
         if ctx.needs_input_grad[0]:
-            dx = _run3("dgrad", _pick3("dgrad", x, w, dy, stride), x, w, dy, stride)
+            dx = _dgrad_handoff(getattr(ctx, "bn_h", None), x, w, dy, 3)
+            if dx is None:
+                dx = _run3("dgrad", _pick3("dgrad", x, w, dy, stride), x, w, dy, stride)
         if f is not None and not _wg._WG_FIRST:
             dw = wg()
         return dx, dw, None
@@ -570,13 +610,14 @@ class _Conv3x3StatsFn(torch.autograd.Function):
     def forward(ctx, x, weight, stride, tile):
         nb, cin, h, w = x.shape
         cout = weight.shape[0]
-        ho, wo = (h - 1) // stride + 1, (w - 1) // stride + 1
+        ho, wo = (h - 1) // stride + 1, (w - 1) // stride + 1  # 3x3 pad 1 or 1x1 pad 0
         y = torch.empty((nb, cout, ho, wo), device=x.device, dtype=torch.float32, memory_format=torch.channels_last)
         part = torch.empty(((nb * ho * wo + 63) // 64) * 2 * cout, device=x.device, dtype=torch.float32)
-        _native.lib().conv3x3_f32(0, x, weight, y, stride, 1, int(tile), part)
+        _native.lib().conv3x3_f32(0, x, weight, y, stride, 1, int(tile), part, weight.shape[2])
         ctx.save_for_backward(x, weight)
         ctx.stride = stride
         ctx.weight = weight
+        ctx.bn_h = _bn.handoff_of(x) if stride == 1 and weight.shape[2] == 3 else None
         ctx.mark_non_differentiable(part)
         ctx.set_materialize_grads(False)  # no zero tensor for the statistics' gradient
         return y, part

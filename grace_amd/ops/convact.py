@@ -66,7 +66,12 @@ class ConvBiasAct2d(nn.Conv2d):
         self.relu = relu
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        y = self._conv_forward(x, self.weight, None)
+        from . import conv as _conv
+
+        if _conv.conv3x3_ok(x, self, bias_ok=True):  # implicit GEMM on the f32 MFMA kernel, autotuned vs MIOpen
+            y = _conv._Conv3x3Fn.apply(x, self.weight, self.stride[0])
+        else:
+            y = self._conv_forward(x, self.weight, None)
         return bias_act(y, self.bias, self.relu)
 
     def extra_repr(self) -> str:

@@ -359,7 +359,7 @@ class Conv2dSplitGrad(nn.Conv2d):
     on GPU; bias / string padding / non-zero padding modes / CPU fall back to ``nn.Conv2d``."""
 
     def forward(self, x):
-        if self.kernel_size == (3, 3) and x.is_cuda:
+        if (self.kernel_size == (3, 3) or self.stride != (1, 1)) and x.is_cuda:
             from . import conv as _conv  # (conv imports this module)
 
             if _conv.conv3x3_ok(x, self):  # implicit GEMM on the f32 MFMA kernel, autotuned vs MIOpen

@@ -63,6 +63,26 @@ def test_conv3x3_implicit_gemm_directions(shape, tile):
     torch.cuda.synchronize()
 
 
+@pytest.mark.parametrize("shape", [(2, 64, 12, 12, 128), (3, 32, 9, 11, 64), (2, 256, 14, 14, 512)])
+@pytest.mark.parametrize("tile", [0, 2, 4])
+def test_strided_1x1_implicit_gemm(shape, tile):
+    N, Cin, H, W, Cout = shape
+    g = torch.Generator().manual_seed(tile)
+    x = torch.randn(N, Cin, H, W, generator=g, dtype=torch.float64)
+    w = torch.randn(Cout, Cin, 1, 1, generator=g, dtype=torch.float64) / Cin ** 0.5
+    xr, wr = x.clone().requires_grad_(), w.clone().requires_grad_()
+    yr = F.conv2d(xr, wr, None, 2, 0)
+    dy = torch.randn(yr.shape, generator=g, dtype=torch.float64)
+    yr.backward(dy)
+    C = _native.lib()
+    y = torch.empty(yr.shape, device="cuda").contiguous(memory_format=torch.channels_last)
+    C.conv3x3_f32(0, _cl(x), _cl(w), y, 2, 1, tile, None, 1)
+    _close(y, yr.detach(), "fwd")
+    dw = torch.empty(w.shape, device="cuda").contiguous(memory_format=torch.channels_last)
+    C.conv3x3_f32(2, _cl(x), _cl(dy), dw, 2, 0, tile, None, 1)
+    _close(dw, wr.grad, "wgrad")
+
+
 def test_conv3x3_fwd_statistics_epilogue():
     N, Cin, H, W, Cout, s = 4, 64, 14, 14, 96, 1
     x, w, _ = _data(N, Cin, H, W, Cout, s, seed=5)
@@ -114,3 +134,94 @@ def test_conv3x3_rejects_bad_shapes():
     w2 = torch.randn(64, 64, 3, 3, device="cuda").contiguous(memory_format=torch.channels_last)
     with pytest.raises(RuntimeError):
         C.conv3x3_f32(0, x2, w2, y, 1, 1, 0)
+
+
+class _Counting:
+    """Wraps the native module and counts calls of the named entry points."""
+
+    def __init__(self, lib, names):
+        self.lib, self.n = lib, {k: 0 for k in names}
+
+    def __getattr__(self, name):
+        f = getattr(self.lib, name)
+        if name in self.n:
+            def g(*a, **k):
+                self.n[name] += 1
+                return f(*a, **k)
+            return g
+        return f
+
+
+@pytest.mark.parametrize("ksize", [1, 3])
+def test_gemm_bn_backward_epilogue_partials(ksize):
+    """dgrad GEMM epilogue partials == the BN backward reduction of (dy masked by the ReLU, x)."""
+    N, C, H, W, Co = 4, 64, 10, 10, 96
+    g = torch.Generator().manual_seed(7)
+    xb = torch.randn(N, C, H, W, generator=g).cuda().contiguous(memory_format=torch.channels_last)  # BN input
+    y = torch.randn(N, Co, H, W, generator=g).cuda().contiguous(memory_format=torch.channels_last)  # conv dy
+    w = (torch.randn(Co, C, ksize, ksize, generator=g) / C).cuda().contiguous(memory_format=torch.channels_last)
+    mean = xb.mean((0, 2, 3))
+    save = torch.zeros(6 * C, device="cuda")
+    save[:C] = mean
+    relu_mask = (torch.rand(N, C, H, W, generator=g) > 0.4).cuda().contiguous(memory_format=torch.channels_last)
+    bits = relu_mask.permute(0, 2, 3, 1).reshape(-1, 8).to(torch.uint8)
+    mask = (bits * (2 ** torch.arange(8, device="cuda", dtype=torch.uint8))).sum(1).to(torch.uint8).contiguous()
+    C_ = _native.lib()
+    dx = torch.empty(N, C, H, W, device="cuda").contiguous(memory_format=torch.channels_last)
+    M = N * H * W
+    part = torch.empty(((M + 63) // 64) * 2 * C, device="cuda")
+    if ksize == 1:
+        t = C_.gemm_f32(y, True, Co, w.reshape(Co, C), False, C, dx, C, M, C, Co, 1, 0, part, xb, mask, save)
+        ref_dx = torch.nn.functional.conv_transpose2d(y.double().cpu(), w.double().cpu())
+    else:
+        t = C_.conv3x3_f32(1, y, w, dx, 1, 1, 0, part, 3, xb, mask, save)
+        ref_dx = torch.nn.functional.conv_transpose2d(y.double().cpu(), w.double().cpu(), padding=1)
+    _close(dx, ref_dx, "dgrad")
+    p = part[: t * 2 * C].view(t, 2, C).double().sum(0).cpu()
+    dz = dx.double().cpu() * relu_mask.cpu()
+    xh = xb.double().cpu() - mean.double().cpu().view(1, -1, 1, 1)
+    torch.testing.assert_close(p[0], dz.sum((0, 2, 3)), rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(p[1], (dz * xh).sum((0, 2, 3)), rtol=1e-5, atol=1e-4)
+
+
+def test_bn_handoff_chain_matches_unfused():
+    """conv1x1 -> BN+ReLU -> conv3x3 -> BN+ReLU -> conv1x1 (the bottleneck's main path): gradients
+    with the BN reductions in the consumers' dgrad epilogues == the BN's own reduction pass."""
+    from grace_amd.ops import bnact as BN
+    from grace_amd.ops.bnact import BatchNormAct2d
+    from grace_amd.ops.conv import Conv1x1F32, conv_bn_act
+    from grace_amd.ops.wgrad import Conv2dSplitGrad
+
+    torch.manual_seed(3)
+    c1, c2, c3 = Conv1x1F32(64, 64), Conv2dSplitGrad(64, 64, 3, padding=1, bias=False), Conv1x1F32(64, 256)
+    b1, b2 = BatchNormAct2d(64, relu=True), BatchNormAct2d(64, relu=True)
+    mods = torch.nn.ModuleList([c1, c2, c3, b1, b2]).cuda().to(memory_format=torch.channels_last)
+    x0 = torch.randn(8, 64, 14, 14, device="cuda").contiguous(memory_format=torch.channels_last)
+
+    def run():
+        for p in mods.parameters():
+            p.grad = None
+        x = x0.clone().requires_grad_()
+        y = conv_bn_act(c1, b1, x, handoff=True)
+        y = conv_bn_act(c2, b2, y, handoff=True)
+        c3(y).square().mean().backward()
+        torch.cuda.synchronize()
+        return [x.grad.clone()] + [p.grad.clone() for p in mods.parameters()]
+
+    lib = _native.lib()
+    for _ in range(2):
+        run()  # autotune
+    counting = _Counting(lib, ["bn_act_bwd_partials", "bn_act_bwd"])
+    _native._lib = counting
+    try:
+        fused = run()
+        assert counting.n["bn_act_bwd_partials"] == 2, counting.n
+        BN._HANDOFF = False
+        counting.n = {k: 0 for k in counting.n}
+        plain = run()
+        assert counting.n["bn_act_bwd_partials"] == 0 and counting.n["bn_act_bwd"] == 2, counting.n
+    finally:
+        BN._HANDOFF = True
+        _native._lib = lib
+    for a, b in zip(fused, plain):
+        torch.testing.assert_close(a, b, rtol=2e-4, atol=2e-6)
