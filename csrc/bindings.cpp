@@ -735,7 +735,7 @@ static void check_operand(const Tensor& x, bool kc, int64_t ld, int64_t rows, in
 // BN-backward epilogue operands: x [M][N] fp32 dense (the BN input), mask [M*N/8] uint8 (None: no
 // ReLU), save [>= 2N] fp32 (mean, invstd)
 static bool bn_epi(const c10::optional<Tensor>& bx, const c10::optional<Tensor>& bmask,
-                   const c10::optional<Tensor>& bsave, int64_t M, int64_t N, grace::BnBwdEpi* e) {
+                   const c10::optional<Tensor>& bsave, bool relu, int64_t M, int64_t N, grace::BnBwdEpi* e) {
   if (!(bx.has_value() && bx->defined())) return false;
   CHECK_DEV((*bx));
   CHECK_DT((*bx), at::kFloat);
@@ -743,11 +743,12 @@ static bool bn_epi(const c10::optional<Tensor>& bx, const c10::optional<Tensor>&
                   reinterpret_cast<uintptr_t>(bx->data_ptr()) % 16 == 0 && N % 8 == 0,
               "bn epilogue: x must be a dense 16-B aligned [M][N] image, N % 8 == 0");
   TORCH_CHECK(bsave.has_value() && bsave->defined() && bsave->is_cuda() && bsave->scalar_type() == at::kFloat &&
-                  bsave->numel() >= 2 * N && reinterpret_cast<uintptr_t>(bsave->data_ptr()) % 16 == 0,
-              "bn epilogue: save [>= 2N] fp32");
+                  bsave->numel() >= 4 * N && reinterpret_cast<uintptr_t>(bsave->data_ptr()) % 16 == 0,
+              "bn epilogue: save [>= 4N] fp32 (mean, invstd, scale, shift)");
   e->x = bx->data_ptr<float>();
   e->save = bsave->data_ptr<float>();
   e->mask = nullptr;
+  e->relu = relu ? 1 : 0;
   if (bmask.has_value() && bmask->defined()) {
     TORCH_CHECK(bmask->is_cuda() && bmask->scalar_type() == at::kByte && bmask->is_contiguous() &&
                     bmask->numel() == M * N / 8, "bn epilogue: mask [M*N/8] uint8");
@@ -756,10 +757,24 @@ static bool bn_epi(const c10::optional<Tensor>& bx, const c10::optional<Tensor>&
   return true;
 }
 
+// BN-apply prologue operand: save [>= 4C] fp32 (scale at 2C, shift at 3C) of the C-channel BN
+static bool bn_pro(const c10::optional<Tensor>& xsave, int64_t C, bool relu, int op, grace::BnApplyPro* f) {
+  if (!(xsave.has_value() && xsave->defined())) return false;
+  TORCH_CHECK(xsave->is_cuda() && xsave->scalar_type() == at::kFloat && xsave->is_contiguous() &&
+                  xsave->numel() >= 4 * C && reinterpret_cast<uintptr_t>(xsave->data_ptr()) % 16 == 0 && C % 4 == 0,
+              "bn prologue: save [>= 4C] fp32, 16-B aligned, C % 4 == 0");
+  f->save = xsave->data_ptr<float>();
+  f->C = (int)C;
+  f->relu = relu ? 1 : 0;
+  f->op = op;
+  return true;
+}
+
 int64_t gemm_f32(const Tensor& A, bool a_kc, int64_t lda, const Tensor& B, bool b_kc, int64_t ldb, const Tensor& C,
                  int64_t ldc, int64_t M, int64_t N, int64_t K, int64_t splits, int64_t tile,
                  const c10::optional<Tensor>& stats, const c10::optional<Tensor>& bn_x,
-                 const c10::optional<Tensor>& bn_mask, const c10::optional<Tensor>& bn_save) {
+                 const c10::optional<Tensor>& bn_mask, const c10::optional<Tensor>& bn_save, bool bn_relu,
+                 const c10::optional<Tensor>& x_save, bool x_relu, int64_t x_op) {
   check_operand(A, a_kc, lda, M, K, "A");
   check_operand(B, b_kc, ldb, N, K, "B");
   CHECK_DEV(C);
@@ -776,11 +791,18 @@ int64_t gemm_f32(const Tensor& A, bool a_kc, int64_t lda, const Tensor& B, bool 
     st = stats->data_ptr<float>();
   }
   grace::BnBwdEpi epi{};
-  const bool has_epi = bn_epi(bn_x, bn_mask, bn_save, M, N, &epi);
+  const bool has_epi = bn_epi(bn_x, bn_mask, bn_save, bn_relu, M, N, &epi);
   TORCH_CHECK(!has_epi || (st != nullptr && ldc == N), "bn epilogue: needs stats and a dense C");
+  grace::BnApplyPro pro{};
+  TORCH_CHECK(x_op == 1 || x_op == 2, "bn prologue: x_op 1 (A) or 2 (B)");
+  // the transformed operand's channels: A's k (K-contig A) or B's rows (MN-contig B)
+  TORCH_CHECK(!(x_save.has_value() && x_save->defined()) || (x_op == 1 ? a_kc : !b_kc),
+              "bn prologue: the operand's channels must be its contiguous extent (K-contig A / MN-contig B)");
+  const bool has_pro = bn_pro(x_save, x_op == 1 ? K : N, x_relu, (int)x_op, &pro);
   DevGuard guard(C.device());
   return grace::gemm_f32(A.data_ptr<float>(), a_kc, lda, B.data_ptr<float>(), b_kc, ldb, C.data_ptr<float>(), ldc,
-                         (int)M, (int)N, (int)K, (int)splits, cur_stream(), (int)tile, st, has_epi ? &epi : nullptr);
+                         (int)M, (int)N, (int)K, (int)splits, cur_stream(), (int)tile, st, has_epi ? &epi : nullptr,
+                         has_pro ? &pro : nullptr);
 }
 
 // 3x3 / pad 1 implicit-GEMM convolution (gemm_f32.hip).  Activations and the weight are NCHW-shaped
@@ -797,7 +819,8 @@ static void check_cl(const Tensor& t, std::initializer_list<int64_t> shape, cons
 int64_t conv3x3_f32(int64_t dir, const Tensor& act, const Tensor& other, const Tensor& C, int64_t stride,
                     int64_t splits, int64_t tile, const c10::optional<Tensor>& stats, int64_t ksize,
                     const c10::optional<Tensor>& bn_x, const c10::optional<Tensor>& bn_mask,
-                    const c10::optional<Tensor>& bn_save) {
+                    const c10::optional<Tensor>& bn_save, bool bn_relu, const c10::optional<Tensor>& x_save,
+                    bool x_relu) {
   TORCH_CHECK(dir >= 0 && dir <= 2, "conv3x3_f32: dir 0 (fwd) / 1 (dgrad) / 2 (wgrad)");
   TORCH_CHECK(stride == 1 || (stride == 2 && dir != 1), "conv3x3_f32: stride 1, or 2 for fwd / wgrad");
   TORCH_CHECK(ksize == 3 || (ksize == 1 && dir != 1), "conv3x3_f32: 3x3 (pad 1), or 1x1 (pad 0) fwd / wgrad");
@@ -828,7 +851,10 @@ int64_t conv3x3_f32(int64_t dir, const Tensor& act, const Tensor& other, const T
   TORCH_CHECK(N * H * W < (1 << 24), "conv3x3_f32: N*H*W < 2^24 (float pixel division)");
   float* st = nullptr;
   grace::BnBwdEpi epi{};
-  const bool has_epi = dir == 1 && bn_epi(bn_x, bn_mask, bn_save, N * H * W, Cin, &epi);
+  const bool has_epi = dir == 1 && bn_epi(bn_x, bn_mask, bn_save, bn_relu, N * H * W, Cin, &epi);
+  grace::BnApplyPro pro{};
+  TORCH_CHECK(!(x_save.has_value() && x_save->defined()) || dir != 1, "bn prologue: forward / weight grad only");
+  const bool has_pro = dir != 1 && bn_pro(x_save, Cin, x_relu, 0, &pro);
   if (stats.has_value() && stats->defined()) {
     TORCH_CHECK((dir == 0 || has_epi) && splits == 1,
                 "conv3x3_f32: statistics on the forward / the data grad's BN epilogue, splits = 1");
@@ -843,7 +869,7 @@ int64_t conv3x3_f32(int64_t dir, const Tensor& act, const Tensor& other, const T
   DevGuard guard(C.device());
   return grace::conv3x3_f32((int)dir, act.data_ptr<float>(), other.data_ptr<float>(), C.data_ptr<float>(), (int)N,
                             (int)H, (int)W, (int)Cin, (int)Cout, (int)stride, (int)splits, (int)tile, st, cur_stream(), (int)ksize,
-                            has_epi ? &epi : nullptr);
+                            has_epi ? &epi : nullptr, has_pro ? &pro : nullptr);
 }
 
 // ------------------------------------------------------------------------------ segment stats
@@ -1155,11 +1181,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv3x3_f32", &conv3x3_f32, py::arg("dir"), py::arg("act"), py::arg("other"), py::arg("C"),
         py::arg("stride") = 1, py::arg("splits") = 0, py::arg("tile") = 0, py::arg("stats") = py::none(),
         py::arg("ksize") = 3, py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(),
-        py::arg("bn_save") = py::none());
+        py::arg("bn_save") = py::none(), py::arg("bn_relu") = false, py::arg("x_save") = py::none(),
+        py::arg("x_relu") = false);
   m.def("gemm_f32", &gemm_f32, py::arg("A"), py::arg("a_kc"), py::arg("lda"), py::arg("B"), py::arg("b_kc"),
         py::arg("ldb"), py::arg("C"), py::arg("ldc"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("splits"),
         py::arg("tile") = 0, py::arg("stats") = py::none(), py::arg("bn_x") = py::none(),
-        py::arg("bn_mask") = py::none(), py::arg("bn_save") = py::none());
+        py::arg("bn_mask") = py::none(), py::arg("bn_save") = py::none(), py::arg("bn_relu") = false,
+        py::arg("x_save") = py::none(), py::arg("x_relu") = false, py::arg("x_op") = 1);
   m.def("axpby", &axpby);
   m.def("scale_", &scale_);
   m.def("gather_segments", &gather_segments);

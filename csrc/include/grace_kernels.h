@@ -152,12 +152,22 @@ void quantile_select(const ChunkTable& ct, int n_seg, const float* x, int max_sl
 // save (mean, invstd); stats receives [tiles][2][N] = [sum dz | sum dz (x - mean)].
 struct BnBwdEpi {
   const float* x;
-  const uint8_t* mask;
+  const uint8_t* mask;  // null with relu: the ReLU test is recomputed from x and save's scale / shift
   const float* save;
+  int relu;
+};
+// BatchNorm-apply prologue (gemm_f32 / conv3x3_f32 forward and weight grad): the activation
+// operand holds a BN input x of C channels; the GEMM consumes act(scale * x + shift) computed as
+// it loads (scale / shift at save + 2C / + 3C).  op: 1 = A, 2 = B (gemm_f32; conv3x3_f32 picks).
+struct BnApplyPro {
+  const float* save;
+  int C;
+  int relu;
+  int op;
 };
 int gemm_f32(const float* A, bool a_kcontig, int64_t lda, const float* B, bool b_kcontig, int64_t ldb, float* C,
               int64_t ldc, int M, int N, int K, int splits, hipStream_t stream, int tile = 0,
-             float* stats = nullptr, const BnBwdEpi* bnb = nullptr);
+             float* stats = nullptr, const BnBwdEpi* bnb = nullptr, const BnApplyPro* xf = nullptr);
 // 3x3 (pad 1) convolution of NHWC fp32 activations as an implicit GEMM on the same kernel (no
 // im2col).  dir 0: C = y [N,Ho,Wo,Cout] from act = x, other = W [Cout][3][3][Cin] (+ stats as
 // gemm_f32); dir 1 (stride 1): C = dx [N,H,W,Cin] from act = dY, other = W; dir 2: C = dW
@@ -167,7 +177,7 @@ int gemm_f32(const float* A, bool a_kcontig, int64_t lda, const float* B, bool b
 // ksize 1: a strided 1x1 (pad 0) convolution on the same path (one tap).
 int conv3x3_f32(int dir, const float* act, const float* other, float* C, int N, int H, int W, int Cin, int Cout,
                 int stride, int splits, int tile, float* stats, hipStream_t stream, int ksize = 3,
-                const BnBwdEpi* bnb = nullptr);
+                const BnBwdEpi* bnb = nullptr, const BnApplyPro* xf = nullptr);
 
 // ---------------------------------------------------------------- ef.hip (elementwise)
 void axpby(const float* x, const float* y, float* out, int64_t n, float a, float b, hipStream_t stream);
@@ -226,6 +236,10 @@ void bn_act_forward_from_partials(const float* x, const float* res, const float*
                                   const float* gamma, const float* beta, float* running_mean, float* running_var,
                                   int64_t* nbt, float momentum, float eps, bool relu, float* save, float* y,
                                   uint8_t* mask, hipStream_t stream);
+// Statistics only (no apply): the BN output is consumed by a GEMM's BnApplyPro prologue.
+void bn_fold_partials(const float* part, int tiles, int64_t M, int C, const float* gamma, const float* beta,
+                      float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps, float* save,
+                      hipStream_t stream);
 // Backward from the consuming conv's data-grad GEMM epilogue partials (BnBwdEpi): fold + dx pass.
 void bn_act_backward_from_partials(const float* dy, const float* x, const uint8_t* mask, const float* part, int tiles,
                                    int64_t M, int C, const float* gamma, const float* save, bool relu, float* dgamma,

@@ -1926,6 +1926,13 @@ void bn_act_forward_from_partials(const float* x, const float* res, const float*
     hipLaunchKernelGGL((bn_apply_kernel<float, false, false>), dim3(gb), dim3(kB), 0, stream, x, res, save, y, mask, n_vec, C);
 }
 
+void bn_fold_partials(const float* part, int tiles, int64_t M, int C, const float* gamma, const float* beta,
+                      float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps, float* save,
+                      hipStream_t stream) {
+  StatsOut o{gamma, beta, running_mean, running_var, nbt, momentum, eps, save};
+  hipLaunchKernelGGL(bn_stats_fold_kernel, dim3((C + 31) / 32), dim3(kB), 0, stream, part, tiles, M, C, o);
+}
+
 void bn_act_backward_from_partials(const float* dy, const float* x, const uint8_t* mask, const float* part, int tiles,
                                    int64_t M, int C, const float* gamma, const float* save, bool relu, float* dgamma,
                                    float* dbeta, float* coef, float* dx, hipStream_t stream) {
@@ -1937,6 +1944,9 @@ void bn_act_backward_from_partials(const float* dy, const float* x, const uint8_
   if (relu && mask != nullptr)
     hipLaunchKernelGGL((bn_dx_kernel<float, true, false, false>), dim3(gb), dim3(kB), 0, stream, dy, (const float*)nullptr,
                        x, mask, cs, dx, (float*)nullptr, n_vec, C);
+  else if (relu)  // no saved mask (the BN output was never materialised): recomputed from x, scale, shift
+    hipLaunchKernelGGL((bn_dx_kernel<float, true, false, false, true>), dim3(gb), dim3(kB), 0, stream, dy,
+                       (const float*)nullptr, x, (const uint8_t*)nullptr, cs, dx, (float*)nullptr, n_vec, C);
   else
     hipLaunchKernelGGL((bn_dx_kernel<float, false, false, false>), dim3(gb), dim3(kB), 0, stream, dy,
                        (const float*)nullptr, x, (const uint8_t*)nullptr, cs, dx, (float*)nullptr, n_vec, C);

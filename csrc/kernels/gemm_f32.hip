@@ -78,9 +78,22 @@ struct GemmParams {
   // writes per (row tile, column) [sum dz | sum dz * (x - mean)], dz = dy masked by the ReLU --
   // the BN backward's reduction pass over (dy, x) disappears (ops/bnact.py hand-off)
   const float* bx;
-  const uint8_t* bmask;  // null: no ReLU
+  const uint8_t* bmask;  // null: no ReLU mask (brelu: recomputed from x and the save's scale / shift)
   const float* bsave;
+  int brelu;
+  // BatchNorm-apply prologue: the operand `xop` (1 = A, 2 = B) is a BN INPUT x whose output
+  // act(scale[c] * x + shift[c]) (scale / shift at xsave + 2C / + 3C) is what the GEMM multiplies
+  // -- transformed as it is loaded (the image's zero padding stays zero); the BN output is never
+  // written to memory (ops/conv.py _BnActConvFn)
+  const float* xsave;
+  int xC, xrelu, xop;
 };
+
+__device__ __forceinline__ float4 bn_xform(float4 v, float4 sc, float4 sh, int relu) {
+  v = make_float4(fmaf(v.x, sc.x, sh.x), fmaf(v.y, sc.y, sh.y), fmaf(v.z, sc.z, sh.z), fmaf(v.w, sc.w, sh.w));
+  if (relu) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+  return v;
+}
 
 // Operand modes.  0: K-contig rows, 1: MN-contig, 2: implicit conv rows (K-contig gather of
 // shifted pixels), 3: implicit conv MN rows (r = tap * C + c, k = output pixel), 4: a 3x3 weight
@@ -114,8 +127,18 @@ struct Operand {
   // mode 3: this thread's (fixed) row r = tap * C + c
   int rdy, rdx, rc;
   bool rok;
+  bool xf;           // BN-apply prologue on this operand
+  float4 xsc, xsh;   // MN modes: this thread's 4 channels' scale / shift (fixed rows)
 
-  __device__ __forceinline__ void init(const GemmParams& p, int r0, int rmax) {
+  __device__ __forceinline__ void init(const GemmParams& p, int r0, int rmax, int which) {
+    xf = p.xsave != nullptr && p.xop == which;
+    if (xf && !KC) {  // rows are channels (mode 1: r; mode 3: rc), fixed per thread
+      int c = r0 + 4 * (threadIdx.x % TPR);
+      if constexpr (MODE == 3) c = (c < rmax ? c : 0) % p.gC;
+      if (c + 3 >= p.xC) c = 0;
+      xsc = *reinterpret_cast<const float4*>(p.xsave + 2 * p.xC + c);
+      xsh = *reinterpret_cast<const float4*>(p.xsave + 3 * p.xC + c);
+    }
     if constexpr (MODE == 2) {
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
@@ -143,14 +166,31 @@ struct Operand {
       const int tap = k0 / p.gC;  // uniform over the slice (C % BK == 0)
       const int dy = p.gT == 3 ? (tap / 3 - 1) * p.gSign : 0, dx = p.gT == 3 ? (tap % 3 - 1) * p.gSign : 0;
       const int c = k0 - tap * p.gC + 4 * (threadIdx.x % (BK / 4));
+      float4 sc = make_float4(0.f, 0.f, 0.f, 0.f), sh = sc;
+      if (xf) {
+        sc = *reinterpret_cast<const float4*>(p.xsave + 2 * p.xC + c);
+        sh = *reinterpret_cast<const float4*>(p.xsave + 3 * p.xC + c);
+      }
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
         const int iy = sy[i] + dy, ix = sx[i] + dx;
         v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if ((unsigned)iy < (unsigned)p.gHs && (unsigned)ix < (unsigned)p.gWs && k0 < kmax)
+        if ((unsigned)iy < (unsigned)p.gHs && (unsigned)ix < (unsigned)p.gWs && k0 < kmax) {
           v[i] = *reinterpret_cast<const float4*>(x + ((int64_t)(pn[i] + iy) * p.gWs + ix) * p.gC + c);
+          if (xf) v[i] = bn_xform(v[i], sc, sh, p.xrelu);  // outside the image: the padding's 0
+        }
       }
       return;
+    }
+    float4 ksc = make_float4(0.f, 0.f, 0.f, 0.f), ksh = ksc;  // mode 0: channels = k (per slice)
+    if constexpr (MODE == 0) {
+      if (xf) {
+        const int c = k0 + 4 * (threadIdx.x % (BK / 4));
+        if (c + 3 < p.xC) {
+          ksc = *reinterpret_cast<const float4*>(p.xsave + 2 * p.xC + c);
+          ksh = *reinterpret_cast<const float4*>(p.xsave + 3 * p.xC + c);
+        }
+      }
     }
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
@@ -169,8 +209,10 @@ struct Operand {
           const int q = fdivmod(k, p.gWr, p.gInvWr, &ox);
           const int n = fdivmod(q, p.gHr, p.gInvHr, &oy);
           const int iy = oy * p.gS + rdy, ix = ox * p.gS + rdx;
-          if ((unsigned)iy < (unsigned)p.gHs && (unsigned)ix < (unsigned)p.gWs)
+          if ((unsigned)iy < (unsigned)p.gHs && (unsigned)ix < (unsigned)p.gWs) {
             v[i] = *reinterpret_cast<const float4*>(x + ((int64_t)(n * p.gHs + iy) * p.gWs + ix) * p.gC + rc);
+            if (xf) v[i] = bn_xform(v[i], xsc, xsh, p.xrelu);
+          }
         }
       } else if constexpr (MODE == 4) {
         if (r < rmax && k < kmax) {
@@ -180,6 +222,7 @@ struct Operand {
       } else if (r < rmax && k < kmax) {
         v[i] = KC ? *reinterpret_cast<const float4*>(x + (int64_t)r * ld + k)
                   : *reinterpret_cast<const float4*>(x + (int64_t)k * ld + r);
+        if (xf) v[i] = KC ? bn_xform(v[i], ksc, ksh, p.xrelu) : bn_xform(v[i], xsc, xsh, p.xrelu);
       }
     }
   }
@@ -242,8 +285,8 @@ __global__ __launch_bounds__(kGB, 2) void gemm_f32_kernel(GemmParams p) {
 
   OA oa;
   OB ob;
-  oa.init(p, m0, p.M);
-  ob.init(p, n0, p.N);
+  oa.init(p, m0, p.M, 1);
+  ob.init(p, n0, p.N, 2);
   if (kb < ke) {
     oa.load(p, p.A, p.lda, m0, p.M, kb, ke);
     ob.load(p, p.B, p.ldb, n0, p.N, kb, ke);
@@ -297,8 +340,14 @@ __global__ __launch_bounds__(kGB, 2) void gemm_f32_kernel(GemmParams p) {
     const int cq = lane % LPR;
     const int col = n0 + wn * WN + 4 * cq;
     const bool bnb = p.stats != nullptr && p.bx != nullptr;
-    float4 bmean = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (bnb && col + 3 < p.N) bmean = *reinterpret_cast<const float4*>(p.bsave + col);
+    float4 bmean = make_float4(0.f, 0.f, 0.f, 0.f), bsc = bmean, bsh = bmean;
+    if (bnb && col + 3 < p.N) {
+      bmean = *reinterpret_cast<const float4*>(p.bsave + col);
+      if (p.bmask == nullptr && p.brelu) {
+        bsc = *reinterpret_cast<const float4*>(p.bsave + 2 * p.N + col);
+        bsh = *reinterpret_cast<const float4*>(p.bsave + 3 * p.N + col);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
 #pragma unroll
@@ -318,7 +367,13 @@ __global__ __launch_bounds__(kGB, 2) void gemm_f32_kernel(GemmParams p) {
             if (col + 3 < p.N) {
               const int64_t e = (int64_t)row * p.N + col;  // dense [M][N] BN activation (ldc == N)
               const float4 xv = *reinterpret_cast<const float4*>(p.bx + e);
-              const uint32_t mb = p.bmask != nullptr ? (uint32_t)(p.bmask[e >> 3] >> (e & 7)) : 0xfu;
+              uint32_t mb = 0xfu;
+              if (p.bmask != nullptr) {
+                mb = (uint32_t)(p.bmask[e >> 3] >> (e & 7));
+              } else if (p.brelu) {  // the forward's ReLU test, recomputed: scale * x + shift > 0
+                mb = (fmaf(xv.x, bsc.x, bsh.x) > 0.f ? 1u : 0u) | (fmaf(xv.y, bsc.y, bsh.y) > 0.f ? 2u : 0u) |
+                     (fmaf(xv.z, bsc.z, bsh.z) > 0.f ? 4u : 0u) | (fmaf(xv.w, bsc.w, bsh.w) > 0.f ? 8u : 0u);
+              }
               const float d0 = (mb & 1u) ? v.x : 0.f, d1 = (mb & 2u) ? v.y : 0.f;
               const float d2 = (mb & 4u) ? v.z : 0.f, d3 = (mb & 8u) ? v.w : 0.f;
               st_s[0] += d0; st_s[1] += d1; st_s[2] += d2; st_s[3] += d3;
@@ -459,13 +514,20 @@ void set_splits(GemmParams& p, int splits, float* stats, hipStream_t stream) {
 
 int gemm_f32(const float* A, bool a_kcontig, int64_t lda, const float* B, bool b_kcontig, int64_t ldb, float* C,
              int64_t ldc, int M, int N, int K, int splits, hipStream_t stream, int tile, float* stats,
-             const BnBwdEpi* bnb) {
+             const BnBwdEpi* bnb, const BnApplyPro* xf) {
   if (M <= 0 || N <= 0) return 0;
   GemmParams p{};
   if (bnb != nullptr) {
     p.bx = bnb->x;
     p.bmask = bnb->mask;
     p.bsave = bnb->save;
+    p.brelu = bnb->relu;
+  }
+  if (xf != nullptr) {
+    p.xsave = xf->save;
+    p.xC = xf->C;
+    p.xrelu = xf->relu;
+    p.xop = xf->op;
   }
   p.A = A;
   p.B = B;
@@ -485,7 +547,8 @@ int gemm_f32(const float* A, bool a_kcontig, int64_t lda, const float* B, bool b
 }
 
 int conv3x3_f32(int dir, const float* act, const float* other, float* C, int N, int H, int W, int Cin, int Cout,
-                int stride, int splits, int tile, float* stats, hipStream_t stream, int ksize, const BnBwdEpi* bnb) {
+                int stride, int splits, int tile, float* stats, hipStream_t stream, int ksize, const BnBwdEpi* bnb,
+                const BnApplyPro* xf) {
   const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;  // 3x3 pad 1, or 1x1 pad 0
   const int T = ksize * ksize;
   GemmParams p{};
@@ -493,6 +556,13 @@ int conv3x3_f32(int dir, const float* act, const float* other, float* C, int N, 
     p.bx = bnb->x;
     p.bmask = bnb->mask;
     p.bsave = bnb->save;
+    p.brelu = bnb->relu;
+  }
+  if (xf != nullptr && dir != 1) {  // the activation operand: A of the forward, B of the weight grad
+    p.xsave = xf->save;
+    p.xC = xf->C;
+    p.xrelu = xf->relu;
+    p.xop = dir == 0 ? 1 : 2;
   }
   p.C = C;
   if (dir == 0) {  // forward: rows = output pixels, k = (tap, ci)

@@ -107,6 +107,30 @@ std::vector<Tensor> bn_act_fwd_partials(const Tensor& x, const c10::optional<Ten
   return {y, save, mask};
 }
 
+// BN statistics from GEMM partials only: save [6C] (mean, invstd, scale, shift, 0, 0), running
+// statistics and num_batches_tracked updated; the apply runs in the consumer GEMM's prologue
+Tensor bn_fold_partials(const Tensor& part, int64_t tiles, int64_t M, int64_t C, const c10::optional<Tensor>& weight,
+                        const c10::optional<Tensor>& bias, const c10::optional<Tensor>& running_mean,
+                        const c10::optional<Tensor>& running_var, const c10::optional<Tensor>& nbt, double momentum,
+                        double eps) {
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() && tiles >= 1 &&
+                  part.numel() >= tiles * 2 * C && M >= 1 && C >= 1, "partials: fp32 [tiles][2][C]");
+  float* rm = const_cast<float*>(opt_f32(running_mean, C, "running_mean"));
+  float* rv = const_cast<float*>(opt_f32(running_var, C, "running_var"));
+  TORCH_CHECK((rm == nullptr) == (rv == nullptr), "running_mean / running_var: both or neither");
+  int64_t* nb = nullptr;
+  if (nbt.has_value() && nbt->defined()) {
+    TORCH_CHECK(nbt->is_cuda() && nbt->scalar_type() == at::kLong && nbt->numel() == 1, "num_batches_tracked");
+    nb = nbt->data_ptr<int64_t>();
+  }
+  DevGuard guard(part.device());
+  Tensor save = at::empty({6 * C}, part.options());
+  grace::bn_fold_partials(part.data_ptr<float>(), (int)tiles, M, (int)C, opt_f32(weight, C, "weight"),
+                          opt_f32(bias, C, "bias"), rm, rv, nb, (float)momentum, (float)eps, save.data_ptr<float>(),
+                          cur_stream());
+  return save;
+}
+
 // returns (dx, dres (undefined unless want_dres), dweight, dbias)
 std::vector<Tensor> bn_act_bwd(const Tensor& dy, const c10::optional<Tensor>& dy2, const Tensor& x,
                                const c10::optional<Tensor>& mask, const c10::optional<Tensor>& weight,
@@ -166,7 +190,6 @@ std::vector<Tensor> bn_act_bwd_partials(const Tensor& dy, const Tensor& x, const
   same_layout(x, dy, "grad_output");
   TORCH_CHECK(x.scalar_type() == at::kFloat, "bn_act_bwd_partials: fp32 activations");
   const bool has_mask = mask.has_value() && mask->defined();
-  TORCH_CHECK(!relu || has_mask, "bn_act_bwd_partials: a ReLU needs the forward's mask");
   if (has_mask)
     TORCH_CHECK(mask->is_cuda() && mask->scalar_type() == at::kByte && mask->is_contiguous() && mask->numel() == M * C / 8,
                 "mask [M*C/8] uint8");
@@ -188,7 +211,8 @@ std::vector<Tensor> bn_act_bwd_partials(const Tensor& dy, const Tensor& x, const
   Tensor coef = at::empty({3 * C}, f32);
   Tensor dx = at::empty_like(x);
   grace::bn_act_backward_from_partials(dy.data_ptr<float>(), x.data_ptr<float>(),
-                                       relu ? mask->data_ptr<uint8_t>() : nullptr, part.data_ptr<float>(), (int)tiles,
+                                       relu && has_mask ? mask->data_ptr<uint8_t>() : nullptr, part.data_ptr<float>(),
+                                       (int)tiles,
                                        M, (int)C, opt_f32(weight, C, "weight"), save.data_ptr<float>(), relu,
                                        want_dweight ? dg.data_ptr<float>() : nullptr,
                                        want_dweight ? db.data_ptr<float>() : nullptr, coef.data_ptr<float>(),
@@ -367,6 +391,7 @@ void grace_bind_nn(py::module& m) {
   m.def("bn_set_atomic_chunks", [](int64_t n) { grace::bn_set_atomic_chunks((int)n); });
   m.def("bn_atomic_chunks", []() { return (int64_t)grace::bn_atomic_chunks(); });
   m.def("bn_act_fwd_partials", &bn_act_fwd_partials);
+  m.def("bn_fold_partials", &bn_fold_partials);
   m.def("bn_act_bwd_partials", &bn_act_bwd_partials, py::arg("dy"), py::arg("x"), py::arg("mask"), py::arg("weight"),
         py::arg("save"), py::arg("part"), py::arg("tiles"), py::arg("relu"), py::arg("want_dweight"),
         py::arg("dweight_out") = py::none(), py::arg("dbias_out") = py::none());

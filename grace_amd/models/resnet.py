@@ -15,6 +15,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.bnact import BatchNormAct2d, bn_relu_maxpool
+from ..ops.bnconv import bottleneck_main
 from ..ops.conv import Conv1x1F32, conv_bn_act
 from ..ops.pool import GlobalAvgPoolFlat, MaxPool2dNHWC
 from ..ops.wgrad import Conv2dSplitGrad, branch
@@ -82,6 +83,14 @@ class Bottleneck(nn.Module):
         else:  # projection shortcut on a second stream, beside the main path (ops/wgrad.py branch)
             with branch(xs) as br:
                 idt = _down(self.downsample, xs)
+        # the main path with bn1 / bn2 applied inside conv2 / conv3's GEMMs (ops/bnconv.py);
+        # not with the shortcut on its own stream (opt-in branch: merged at the end)
+        if br is None or not br.on:
+            idt = br.merge(idt) if br is not None else idt
+            br = None
+            out = bottleneck_main(self, xm, idt)
+            if out is not None:
+                return out
         # 1x1 conv -> BN pairs: the BN statistics may come from the conv GEMM's epilogue
         # (ops/conv.py conv_bn_act, autotuned; otherwise exactly bn(conv(x)))
         # bn1 / bn2 outputs feed exactly one conv each: their backward reductions come from the

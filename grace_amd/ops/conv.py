@@ -300,7 +300,8 @@ class _Conv1x1StatsFn(torch.autograd.Function):
             wt = wt.contiguous()
         y = torch.empty((nb, cout, h, w), device=x.device, dtype=torch.float32, memory_format=torch.channels_last)
         part = torch.empty(((m + 63) // 64) * 2 * cout, device=x.device, dtype=torch.float32)
-        _native.lib().gemm_f32(x, True, cin, wt, True, cin, y, cout, m, cout, cin, 1, int(tile), part)
+        part._grace_tiles = _native.lib().gemm_f32(x, True, cin, wt, True, cin, y, cout, m, cout, cin, 1, int(tile),
+                                                   part)
         ctx.save_for_backward(x, wt)
         ctx.wshape = weight.shape
         ctx.weight = weight
@@ -613,7 +614,7 @@ class _Conv3x3StatsFn(torch.autograd.Function):
         ho, wo = (h - 1) // stride + 1, (w - 1) // stride + 1  # 3x3 pad 1 or 1x1 pad 0
         y = torch.empty((nb, cout, ho, wo), device=x.device, dtype=torch.float32, memory_format=torch.channels_last)
         part = torch.empty(((nb * ho * wo + 63) // 64) * 2 * cout, device=x.device, dtype=torch.float32)
-        _native.lib().conv3x3_f32(0, x, weight, y, stride, 1, int(tile), part, weight.shape[2])
+        part._grace_tiles = _native.lib().conv3x3_f32(0, x, weight, y, stride, 1, int(tile), part, weight.shape[2])
         ctx.save_for_backward(x, weight)
         ctx.stride = stride
         ctx.weight = weight
