@@ -89,6 +89,8 @@ struct GemmParams {
   int xC, xrelu, xop;
 };
 
+__host__ __device__ constexpr int bnb_slots(int nr) { return nr > 0 ? nr : 1; }
+
 __device__ __forceinline__ float4 bn_xform(float4 v, float4 sc, float4 sh, int relu) {
   v = make_float4(fmaf(v.x, sc.x, sh.x), fmaf(v.y, sc.y, sh.y), fmaf(v.z, sc.z, sh.z), fmaf(v.w, sc.w, sh.w));
   if (relu) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
@@ -128,10 +130,14 @@ struct Operand {
   int rdy, rdx, rc;
   bool rok;
   bool xf;           // BN-apply prologue on this operand
-  float4 xsc, xsh;   // MN modes: this thread's 4 channels' scale / shift (fixed rows)
+  float4 xsc, xsh;   // the channels' scale / shift: fixed rows (MN modes) or this slice's k (KC)
+  uint32_t xok;      // bit i: v[i] was loaded (transformed at store; padding / out of range stays 0)
+  int xrelu;
 
   __device__ __forceinline__ void init(const GemmParams& p, int r0, int rmax, int which) {
     xf = p.xsave != nullptr && p.xop == which;
+    xrelu = p.xrelu;
+    xok = 0;
     if (xf && !KC) {  // rows are channels (mode 1: r; mode 3: rc), fixed per thread
       int c = r0 + 4 * (threadIdx.x % TPR);
       if constexpr (MODE == 3) c = (c < rmax ? c : 0) % p.gC;
@@ -166,10 +172,10 @@ struct Operand {
       const int tap = k0 / p.gC;  // uniform over the slice (C % BK == 0)
       const int dy = p.gT == 3 ? (tap / 3 - 1) * p.gSign : 0, dx = p.gT == 3 ? (tap % 3 - 1) * p.gSign : 0;
       const int c = k0 - tap * p.gC + 4 * (threadIdx.x % (BK / 4));
-      float4 sc = make_float4(0.f, 0.f, 0.f, 0.f), sh = sc;
-      if (xf) {
-        sc = *reinterpret_cast<const float4*>(p.xsave + 2 * p.xC + c);
-        sh = *reinterpret_cast<const float4*>(p.xsave + 3 * p.xC + c);
+      if (xf) {  // consumed at store(): the loads stay in flight across the MFMAs
+        xsc = *reinterpret_cast<const float4*>(p.xsave + 2 * p.xC + c);
+        xsh = *reinterpret_cast<const float4*>(p.xsave + 3 * p.xC + c);
+        xok = 0;
       }
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
@@ -177,21 +183,22 @@ struct Operand {
         v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
         if ((unsigned)iy < (unsigned)p.gHs && (unsigned)ix < (unsigned)p.gWs && k0 < kmax) {
           v[i] = *reinterpret_cast<const float4*>(x + ((int64_t)(pn[i] + iy) * p.gWs + ix) * p.gC + c);
-          if (xf) v[i] = bn_xform(v[i], sc, sh, p.xrelu);  // outside the image: the padding's 0
+          xok |= 1u << i;  // outside the image: the padding's 0, never transformed
         }
       }
       return;
     }
-    float4 ksc = make_float4(0.f, 0.f, 0.f, 0.f), ksh = ksc;  // mode 0: channels = k (per slice)
-    if constexpr (MODE == 0) {
+    if constexpr (MODE == 0) {  // channels = k (per slice)
       if (xf) {
         const int c = k0 + 4 * (threadIdx.x % (BK / 4));
+        xsc = xsh = make_float4(0.f, 0.f, 0.f, 0.f);
         if (c + 3 < p.xC) {
-          ksc = *reinterpret_cast<const float4*>(p.xsave + 2 * p.xC + c);
-          ksh = *reinterpret_cast<const float4*>(p.xsave + 3 * p.xC + c);
+          xsc = *reinterpret_cast<const float4*>(p.xsave + 2 * p.xC + c);
+          xsh = *reinterpret_cast<const float4*>(p.xsave + 3 * p.xC + c);
         }
       }
     }
+    xok = 0;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       int r, k;
@@ -211,7 +218,7 @@ struct Operand {
           const int iy = oy * p.gS + rdy, ix = ox * p.gS + rdx;
           if ((unsigned)iy < (unsigned)p.gHs && (unsigned)ix < (unsigned)p.gWs) {
             v[i] = *reinterpret_cast<const float4*>(x + ((int64_t)(n * p.gHs + iy) * p.gWs + ix) * p.gC + rc);
-            if (xf) v[i] = bn_xform(v[i], xsc, xsh, p.xrelu);
+            xok |= 1u << i;
           }
         }
       } else if constexpr (MODE == 4) {
@@ -222,11 +229,16 @@ struct Operand {
       } else if (r < rmax && k < kmax) {
         v[i] = KC ? *reinterpret_cast<const float4*>(x + (int64_t)r * ld + k)
                   : *reinterpret_cast<const float4*>(x + (int64_t)k * ld + r);
-        if (xf) v[i] = KC ? bn_xform(v[i], ksc, ksh, p.xrelu) : bn_xform(v[i], xsc, xsh, p.xrelu);
+        xok |= 1u << i;
       }
     }
   }
-  __device__ __forceinline__ void store(float* lds) const {
+  __device__ __forceinline__ void store(float* lds) {
+    if (xf) {  // BN-apply prologue, applied here so the stage's global loads overlap the MFMAs
+#pragma unroll
+      for (int i = 0; i < NV; ++i)
+        if ((xok >> i) & 1u) v[i] = bn_xform(v[i], xsc, xsh, xrelu);
+    }
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       if constexpr (KC) {
@@ -348,8 +360,26 @@ __global__ __launch_bounds__(kGB, 2) void gemm_f32_kernel(GemmParams p) {
         bsh = *reinterpret_cast<const float4*>(p.bsave + 3 * p.N + col);
       }
     }
+    constexpr int NR = 32 / RPI;  // staged rows per lane per slab
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
+      // BN-backward epilogue: this slab's x (and mask) loads are issued before the slab is staged,
+      // so their latency overlaps the staging instead of serialising the row loop
+      float4 xpre[bnb_slots(NR)];
+      uint32_t mpre[bnb_slots(NR)];
+      if (bnb) {
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+          const int row = m0 + wm * WM + i * 32 + lane / LPR + j * RPI;
+          xpre[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+          mpre[j] = 0xfu;
+          if (row < p.M && col + 3 < p.N) {
+            const int64_t e = (int64_t)row * p.N + col;  // dense [M][N] BN activation (ldc == N)
+            xpre[j] = *reinterpret_cast<const float4*>(p.bx + e);
+            if (p.bmask != nullptr) mpre[j] = (uint32_t)(p.bmask[e >> 3] >> (e & 7));
+          }
+        }
+      }
 #pragma unroll
       for (int j = 0; j < FN; ++j)
 #pragma unroll
@@ -358,22 +388,19 @@ __global__ __launch_bounds__(kGB, 2) void gemm_f32_kernel(GemmParams p) {
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-      for (int rr = lane / LPR; rr < 32; rr += RPI) {
+      for (int j = 0; j < NR; ++j) {
+        const int rr = lane / LPR + j * RPI;
         const int row = m0 + wm * WM + i * 32 + rr;
         if (row < p.M) {
           const float4 v = *reinterpret_cast<const float4*>(slab + rr * CP + 4 * cq);
           float* dst = p.C + (int64_t)row * p.ldc + col;
           if (bnb) {
             if (col + 3 < p.N) {
-              const int64_t e = (int64_t)row * p.N + col;  // dense [M][N] BN activation (ldc == N)
-              const float4 xv = *reinterpret_cast<const float4*>(p.bx + e);
-              uint32_t mb = 0xfu;
-              if (p.bmask != nullptr) {
-                mb = (uint32_t)(p.bmask[e >> 3] >> (e & 7));
-              } else if (p.brelu) {  // the forward's ReLU test, recomputed: scale * x + shift > 0
+              const float4 xv = xpre[j];
+              uint32_t mb = mpre[j];
+              if (p.bmask == nullptr && p.brelu)  // the forward's ReLU test, recomputed: scale * x + shift > 0
                 mb = (fmaf(xv.x, bsc.x, bsh.x) > 0.f ? 1u : 0u) | (fmaf(xv.y, bsc.y, bsh.y) > 0.f ? 2u : 0u) |
                      (fmaf(xv.z, bsc.z, bsh.z) > 0.f ? 4u : 0u) | (fmaf(xv.w, bsc.w, bsh.w) > 0.f ? 8u : 0u);
-              }
               const float d0 = (mb & 1u) ? v.x : 0.f, d1 = (mb & 2u) ? v.y : 0.f;
               const float d2 = (mb & 4u) ? v.z : 0.f, d3 = (mb & 8u) ? v.w : 0.f;
               st_s[0] += d0; st_s[1] += d1; st_s[2] += d2; st_s[3] += d3;

@@ -15,8 +15,8 @@
 // payloads).  K_r is either fixed or read from the payload's in-band header (capacity payloads,
 // counted into the health words when a payload overflowed).
 //
-// Barrier: an arrival counter (agent scope) per phase; agent-scope release / acquire fences carry
-// the phase's stores across the 8 XCDs' L2s.  The grid is sized to be co-resident (<= 1 workgroup
+// Barrier: an arrival counter (agent scope) per phase; agent-scope release / acquire fences in
+// every wave carry the phase's stores across the 8 XCDs' L2s.  The grid is sized to be co-resident (<= 1 workgroup
 // per CU), and every spin is bounded: a barrier that does not complete raises the health fault
 // and the workgroup proceeds (the step's optimizer update is then skipped), so no wave can hang.
 // The last workgroup to leave resets the counters: the kernel is replayable from a HIP graph.
@@ -36,9 +36,13 @@ struct DecodeArgs {
 };
 
 __device__ __forceinline__ void grid_barrier(int32_t* ctr, int32_t target, uint32_t* health_host, uint32_t* health_dev) {
+  // EVERY wave releases at agent scope: a release only waits for the issuing wave's own stores
+  // (vmcnt) before the L2 write-back, and the workgroup barrier alone does not drain the other
+  // waves' stores to L2 -- with one releasing thread, another wave's phase stores could still be
+  // in flight and miss the write-back, and another XCD would read stale lines.
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int64_t spins = 0;
     while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
@@ -51,9 +55,9 @@ __device__ __forceinline__ void grid_barrier(int32_t* ctr, int32_t target, uint3
         break;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every wave: no stale L1 / L2 line of the phase
 }
 
 __global__ __launch_bounds__(kDB) void sparse_decode_kernel(DecodeArgs a, int W, float* __restrict__ out, int64_t n,

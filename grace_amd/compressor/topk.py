@@ -12,9 +12,9 @@ MI355X kernels (csrc/kernels/topk.hip):
   x = beta*r + gamma*g happens in the first histogram pass and the new residual (x with the
   sent entries zeroed) is written by the compaction pass: the reference's second decompress
   (residual.py:17) disappears.
-* ``decompress_aggregate``: ONE launch zeroes the bucket and scatters the W payloads in rank
-  order behind grid barriers (csrc/kernels/sparse_decode.hip), atomic-free, with the 1/W average
-  folded in -> bitwise identical on every rank.
+* ``decompress_aggregate``: the W payloads scattered in fixed rank order into the zeroed bucket
+  (ops/cappayload.py decode_ranks), atomic-free, with the 1/W average folded in -> bitwise
+  identical on every rank.
 """
 from __future__ import annotations
 
@@ -83,7 +83,7 @@ class TopKCompressor(Compressor):
         out = BucketCompressor.out_buffer(ctx, per_rank[0][0].device) if ctx.dtype == torch.float32 \
             else torch.empty(ctx.numel, dtype=torch.float32, device=per_rank[0][0].device)
         scale = (1.0 / world_size) if self.average else 1.0
-        # zero + every rank's scatter in fixed rank order, one launch -> identical on every rank
+        # zero + every rank's scatter in fixed rank order -> identical on every rank
         P.decode_ranks([p[0] for p in per_rank], [p[1] for p in per_rank], [None] * len(per_rank), out, scale)
         return out.view(ctx.shape).to(ctx.dtype)
 

@@ -15,7 +15,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.bnact import BatchNormAct2d, bn_relu_maxpool
-from ..ops.bnconv import bottleneck_main
+from ..ops.bnconv import basic_main, bottleneck_main
 from ..ops.conv import Conv1x1F32, conv_bn_act
 from ..ops.pool import GlobalAvgPoolFlat, MaxPool2dNHWC
 from ..ops.wgrad import Conv2dSplitGrad, branch
@@ -55,6 +55,9 @@ class BasicBlock(nn.Module):
     def forward(self, x):
         xm, xs = x if isinstance(x, tuple) else (x, x)
         idt = xs if self.downsample is None else _down(self.downsample, xs)
+        out = basic_main(self, xm, idt)  # bn1 applied inside conv2's GEMM (ops/bnconv.py)
+        if out is not None:
+            return out
         y = conv_bn_act(self.conv1, self.bn1, xm, handoff=True)  # bn1's output feeds conv2 only
         return conv_bn_act(self.conv2, self.bn2, y, idt, dual=True)
 

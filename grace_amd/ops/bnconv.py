@@ -15,8 +15,9 @@ the consumer conv reading y back, and in backward a BN reduction pass over (dy, 
 
 Per fused pair: one apply pass, one reduction pass, the y write and the mask write are gone.
 Every direction runs on the f32 MFMA GEMM (exact fp32, no xf32); the 3x3 data grad exists for
-stride 1, so a strided 3x3 consumer keeps the materialised BN output.  ``GRACE_BN_PROLOGUE=0``
-restores the unfused path (ops/conv.py conv_bn_act).  Reference for the layer structure:
+stride 1, so a strided 3x3 consumer keeps the materialised BN output.  Opt-in
+(``GRACE_BN_PROLOGUE=1``): measured slower than the unfused, per-direction autotuned path on
+the fp32 headline (see ``_ON``).  Reference for the layer structure:
 torchvision ResNet v1.5 bottleneck, as the reference harness trains it
 (/root/reference/examples/torch/pytorch_synthetic_benchmark.py:86).
 """
@@ -31,7 +32,11 @@ from . import _native
 from . import wgrad as _wg
 from .bnact import BatchNormAct2d, _fusable, bn_act
 
-_ON = os.environ.get("GRACE_BN_PROLOGUE", "1") == "1"
+# opt-in: measured slower on the fp32 ResNet-50 headline (2072 vs 2722 img/s,
+# profiles/r4_bn_fusion_ab.txt) -- every direction of the fused convolutions must then run on the
+# f32 MFMA GEMM, which trails MIOpen's 3x3 solvers (stages 3-4, all weight grads) by more than the
+# BN passes it removes save
+_ON = os.environ.get("GRACE_BN_PROLOGUE", "0") == "1"
 _TARGETS = os.environ.get("GRACE_BN_GRAD_TARGET", "1") == "1"
 
 
@@ -189,3 +194,29 @@ def bottleneck_main(blk, xm: torch.Tensor, idt: torch.Tensor):
     s2 = bn_fold(b2, p2, p2._grace_tiles, nb * ho * wo)
     y3, p3 = _BnActConvFn.apply(y2, b2.weight, b2.bias, s2, c3.weight, bool(b2.relu), 1, True)
     return bn_act(y3, b3, idt, b3.relu, True, partials=p3, tiles=p3._grace_tiles)
+
+
+def basic_main(blk, xm: torch.Tensor, idt: torch.Tensor):
+    """A basic block's main path conv1 -> bn1 -> conv2 -> bn2(+idt, dual) with bn1 applied inside
+    conv2's implicit GEMM; None when it does not apply (decided before anything runs)."""
+    from . import conv as _conv
+
+    c1, b1, c2, b2 = blk.conv1, blk.bn1, blk.conv2, blk.bn2
+    if not (_ON and xm.is_cuda and xm.dtype == torch.float32 and torch.is_grad_enabled()
+            and not torch.is_autocast_enabled() and _native.native_on(xm.device)):
+        return None
+    if not (isinstance(c1, _wg.Conv2dSplitGrad) and isinstance(c2, _wg.Conv2dSplitGrad)
+            and _conv.conv3x3_ok(xm, c1) and c1.kernel_size == (3, 3)):
+        return None
+    w1, w2 = c1.out_channels, c2.out_channels
+    nb, _, h, w = xm.shape
+    s = c1.stride[0]
+    ho, wo = (h - 1) // s + 1, (w - 1) // s + 1
+    if not (_bn_ok(b1, w1) and _bn_ok(b2, w2) and c2.in_channels == w1 and c2.stride == (1, 1)
+            and c2.kernel_size == (3, 3) and c2.padding == (1, 1) and c2.dilation == (1, 1) and c2.groups == 1
+            and c2.bias is None and c2.padding_mode == "zeros" and w1 % 32 == 0 and w2 % 32 == 0 and _cl(c2.weight)):
+        return None
+    y1, p1 = _conv._Conv3x3StatsFn.apply(xm, c1.weight, s, 0)
+    s1 = bn_fold(b1, p1, p1._grace_tiles, nb * ho * wo)
+    y2, p2 = _BnActConvFn.apply(y1, b1.weight, b1.bias, s1, c2.weight, bool(b1.relu), 3, True)
+    return bn_act(y2, b2, idt, b2.relu, True, partials=p2, tiles=p2._grace_tiles)

@@ -58,6 +58,11 @@ def scatter_capped(hdr: torch.Tensor, vals: torch.Tensor, idx: torch.Tensor, out
 
 MAX_DECODE_RANKS = 32  # csrc/include/grace_kernels.h kDecodeMaxRanks
 _DECODE_CTR = {}
+# opt-in: the one-launch decode measured 2.8-5.6x SLOWER than a zero fill + W scatter launches on
+# a ResNet-50 bucket (65 vs 23 us at W = 1, 480 vs 85 us at W = 8, graph-replayed;
+# profiles/r4_decode_bench.txt): every grid barrier pays an agent-scope L2 write-back of the
+# freshly zeroed bucket plus an invalidate, ~60 us per phase, far above a launch boundary
+ONE_LAUNCH = __import__("os").environ.get("GRACE_DECODE_ONE_LAUNCH", "0") == "1"
 
 
 def _decode_ctr(device) -> torch.Tensor:
@@ -74,21 +79,23 @@ def _decode_ctr(device) -> torch.Tensor:
 def decode_ranks(vals, idxs, counts, out: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
     """``out`` = 0, then ``out[idxs[r]] += vals[r] * scale`` for r = 0..W-1 in rank order --
     bit-identical on every rank.  ``counts[r]``: None (every entry) or the payload's in-band count
-    word (capacity payloads: the first min(count, capacity) entries).  Native path: ONE launch
-    (zero + W rank phases behind grid barriers, csrc/kernels/sparse_decode.hip) instead of a zero
-    fill plus W scatter launches."""
+    word (capacity payloads: the first min(count, capacity) entries).  Default: a zero fill plus W
+    atomic-free scatter launches; ``GRACE_DECODE_ONE_LAUNCH=1``: ONE launch (zero + W rank phases
+    behind grid barriers, csrc/kernels/sparse_decode.hip) -- measured slower, see ONE_LAUNCH."""
     W = len(vals)
-    if _native.use_native(out) and 1 <= W <= MAX_DECODE_RANKS and out.is_contiguous():
+    if ONE_LAUNCH and _native.use_native(out) and 1 <= W <= MAX_DECODE_RANKS and out.is_contiguous():
         _native.lib().sparse_decode_ranks(list(vals), list(idxs), [None if c is None else c[:1] for c in counts],
                                           out, float(scale), _decode_ctr(out.device))
         return out
     out.zero_()
-    for v, i, c in zip(vals, idxs, counts):
-        if c is None:
-            il = i.long()
-            out.index_add_(0, il, v * scale)
-        else:
+    native = _native.use_native(out)
+    for v, i, c in zip(vals, idxs, counts):  # fixed rank order: identical on every rank
+        if c is not None:
             scatter_capped(c, v, i, out, scale, accumulate=True)
+        elif native:
+            _native.lib().sparse_scatter_add(v, i, out, scale, True)
+        else:
+            out.index_add_(0, i.long(), v * scale)
     return out
 
 

@@ -206,7 +206,11 @@ def _pick(direction: str, x, wt, dy, wshape) -> str:
     return c
 
 
-def _dgrad_handoff(h, x, w, dy, ksize: int):
+def _tile_of(backend: str) -> int:
+    return int(backend[6:]) if backend.startswith("mfma_t") else 0
+
+
+def _dgrad_handoff(h, x, w, dy, ksize: int, tile: int = 0):
     """Data grad on the MFMA GEMM with the producing BN's backward reduction in its epilogue
     (ops/bnact.py BNHandoff); None when it does not apply.  ksize 1: w is [Cout, Cin] (plain
     GEMM); 3: the channels_last 3x3 weight (implicit GEMM, stride 1)."""
@@ -219,9 +223,9 @@ def _dgrad_handoff(h, x, w, dy, ksize: int):
     C = _native.lib()
     if ksize == 1:
         cout = w.shape[0]
-        t = C.gemm_f32(dy, True, cout, w, False, cin, dx, cin, m, cin, cout, 1, 0, part, h.x, h.mask, h.save)
+        t = C.gemm_f32(dy, True, cout, w, False, cin, dx, cin, m, cin, cout, 1, tile, part, h.x, h.mask, h.save)
     else:
-        t = C.conv3x3_f32(1, dy, w, dx, 1, 1, 0, part, 3, h.x, h.mask, h.save)
+        t = C.conv3x3_f32(1, dy, w, dx, 1, 1, tile, part, 3, h.x, h.mask, h.save)
     h.publish(part, t, dx)
     return dx
 
@@ -277,9 +281,13 @@ class _Conv1x1AutoFn(torch.autograd.Function):
         if f is not None and _wg._WG_FIRST:
             dw = wg()
         if ctx.needs_input_grad[0]:
-            dx = _dgrad_handoff(getattr(ctx, "bn_h", None), x, wt, dy, 1)
+            be = _pick("dgrad", x, wt, dy, ctx.wshape)
+            # the producing BN's reduction in the epilogue -- only where the MFMA GEMM is already the
+            # measured-fastest data grad (forcing it elsewhere measured slower overall)
+            dx = _dgrad_handoff(getattr(ctx, "bn_h", None), x, wt, dy, 1, _tile_of(be)) \
+                if be.startswith("mfma") else None
             if dx is None:
-                dx = _run("dgrad", _pick("dgrad", x, wt, dy, ctx.wshape), x, wt, dy, ctx.wshape)
+                dx = _run("dgrad", be, x, wt, dy, ctx.wshape)
         if f is not None and not _wg._WG_FIRST:
             dw = wg()
         return dx, dw
@@ -595,9 +603,11 @@ class _Conv3x3Fn(torch.autograd.Function):
         if f is not None and _wg._WG_FIRST:
             dw = wg()
         if ctx.needs_input_grad[0]:
-            dx = _dgrad_handoff(getattr(ctx, "bn_h", None), x, w, dy, 3)
+            be = _pick3("dgrad", x, w, dy, stride)
+            dx = _dgrad_handoff(getattr(ctx, "bn_h", None), x, w, dy, 3, _tile_of(be)) \
+                if be.startswith("mfma") else None
             if dx is None:
-                dx = _run3("dgrad", _pick3("dgrad", x, w, dy, stride), x, w, dy, stride)
+                dx = _run3("dgrad", be, x, w, dy, stride)
         if f is not None and not _wg._WG_FIRST:
             dw = wg()
         return dx, dw, None

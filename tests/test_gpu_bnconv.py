@@ -123,8 +123,9 @@ def test_fused_bottleneck_matches_unfused(stride, cin):
             return y.detach(), x.grad, {n: p.grad.clone() for n, p in model.named_parameters()}, \
                 {n: b.clone() for n, b in model.named_buffers()}
         finally:
-            BC.set_enabled(True)
+            BC.set_enabled(default)
 
+    default = BC._ON
     calls = {"n": 0}
     real = BC._BnActConvFn.apply
 
@@ -145,3 +146,34 @@ def test_fused_bottleneck_matches_unfused(stride, cin):
         torch.testing.assert_close(gf[n], gu[n], rtol=1e-3, atol=1e-5, msg=lambda m, n=n: f"{n}: {m}")
     for n in bu:
         torch.testing.assert_close(bf[n].float(), bu[n].float(), rtol=1e-4, atol=1e-6, msg=lambda m, n=n: f"{n}: {m}")
+
+
+def test_fused_basic_block_matches_unfused():
+    from grace_amd.models.resnet import BasicBlock
+    from grace_amd.ops.bnact import BatchNormAct2d
+
+    torch.manual_seed(6)
+    blk = BasicBlock(64, 64, 1, None).cuda().to(memory_format=torch.channels_last)
+    for m in blk.modules():
+        if isinstance(m, BatchNormAct2d):
+            m.weight.data.uniform_(0.5, 1.5)
+            m.bias.data.uniform_(-0.2, 0.2)
+    ref = copy.deepcopy(blk)
+    x0 = torch.randn(8, 64, 16, 16, device="cuda").contiguous(memory_format=torch.channels_last)
+    res = []
+    default = BC._ON
+    for model, fused in ((blk, True), (ref, False)):
+        BC.set_enabled(fused)
+        try:
+            x = x0.clone().requires_grad_()
+            y = model(x)[0]
+            y.square().mean().backward()
+            torch.cuda.synchronize()
+            res.append((y.detach(), x.grad, [p.grad.clone() for p in model.parameters()]))
+        finally:
+            BC.set_enabled(default)
+    (yf, dxf, gf), (yu, dxu, gu) = res
+    torch.testing.assert_close(yf, yu, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(dxf, dxu, rtol=1e-3, atol=1e-6)
+    for a, b in zip(gf, gu):
+        torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-5)

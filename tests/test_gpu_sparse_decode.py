@@ -38,9 +38,10 @@ def _payloads(W, n, k, seed, counts=False):
 
 def _ref(vals, idxs, cnts, n, scale):
     out = torch.zeros(n)
+    s = torch.tensor(scale, dtype=torch.float32)  # the kernel's fp32 scale (not a double multiply)
     for v, i, c in zip(vals, idxs, cnts):
         K = v.numel() if c is None else min(int(c[0]), v.numel())
-        out.index_add_(0, i[:K].long(), v[:K] * scale)
+        out.index_add_(0, i[:K].long(), v[:K] * s)
     return out
 
 
@@ -48,12 +49,36 @@ def _gpu(xs):
     return [None if x is None else x.cuda() for x in xs]
 
 
+@pytest.fixture(autouse=True)
+def _one_launch():
+    """These tests exercise the opt-in one-launch kernel (the default decode is the rank loop)."""
+    old = P.ONE_LAUNCH
+    P.ONE_LAUNCH = True
+    yield
+    P.ONE_LAUNCH = old
+
+
+def _loop(vals, idxs, cnts, n, scale):
+    """The default GPU decode: zero fill + one native scatter launch per rank."""
+    old = P.ONE_LAUNCH
+    P.ONE_LAUNCH = False
+    try:
+        out = torch.full((n,), 5.0, device="cuda")
+        return P.decode_ranks(_gpu(vals), _gpu(idxs), _gpu(cnts), out, scale)
+    finally:
+        P.ONE_LAUNCH = old
+
+
 @pytest.mark.parametrize("W,n,k", [(1, 1000, 10), (3, 1_000_003, 20_000), (8, 257, 100), (20, 300_001, 3000)])
 def test_decode_matches_rank_loop(W, n, k):
     vals, idxs, cnts = _payloads(W, n, k, seed=W)
     out = torch.full((n,), 7.0, device="cuda")  # garbage: the kernel zeroes
     P.decode_ranks(_gpu(vals), _gpu(idxs), cnts, out, 1.0 / W)
-    assert torch.equal(out.cpu(), _ref(vals, idxs, cnts, n, 1.0 / W))
+    loop = _loop(vals, idxs, cnts, n, 1.0 / W)
+    diff = (out != loop).nonzero().flatten()
+    assert diff.numel() == 0, f"{diff.numel()} entries differ from the rank loop, e.g. {diff[:5].tolist()}"
+    ref = _ref(vals, idxs, cnts, n, 1.0 / W)
+    torch.testing.assert_close(loop.cpu(), ref, rtol=1e-6, atol=1e-7)
 
 
 def test_decode_counts_unaligned_and_overflow():
@@ -67,7 +92,7 @@ def test_decode_counts_unaligned_and_overflow():
     out = big[1:n + 1]  # 4-B aligned, not 16-B aligned
     P.decode_ranks(_gpu(vals), _gpu(idxs), _gpu(cnts), out, 0.5)
     torch.cuda.synchronize()
-    assert torch.equal(out.cpu(), _ref(vals, idxs, cnts, n, 0.5))
+    assert torch.equal(out, _loop(vals, idxs, cnts, n, 0.5))
     assert big[0].item() == -1.0 and big[n + 1].item() == -1.0 and big[n + 2].item() == -1.0
     assert health.overflows() == before + sum(int(c[0]) > k for c in cnts)
     assert health.status()[0] == 0  # every barrier completed
@@ -80,7 +105,7 @@ def test_decode_repeated_and_graph_replay():
     out = torch.empty(n, device="cuda")
     for _ in range(3):  # the counters are left zero by every launch
         P.decode_ranks(gv, gi, cnts, out, 0.25)
-    assert torch.equal(out.cpu(), _ref(vals, idxs, cnts, n, 0.25))
+    assert torch.equal(out, _loop(vals, idxs, cnts, n, 0.25))
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
@@ -97,7 +122,7 @@ def test_decode_repeated_and_graph_replay():
             a.copy_(b)
         graph.replay()
         torch.cuda.synchronize()
-        assert torch.equal(out.cpu(), _ref(vals2, idxs2, cnts, n, 0.25)), step
+        assert torch.equal(out, _loop(vals2, idxs2, cnts, n, 0.25)), step
 
 
 def _w4_body(rank, world):
@@ -122,6 +147,7 @@ def _w4_body(rank, world):
             return getattr(lib, name)
 
     _native._lib = Counting()
+    P.ONE_LAUNCH = True  # (spawned worker: the fixture does not reach it)
     try:
         for comp in ({"compressor": "topk", "compress_ratio": 0.05, "memory": "residual", "communicator": "allgather"},
                      {"compressor": "threshold", "threshold": 0.5, "memory": "residual", "communicator": "allgather"}):

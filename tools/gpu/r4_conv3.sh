@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 4: implicit-GEMM conv + BN hand-off numerics, per-layer A/B vs MIOpen, headline A/B.
-R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; export TMPDIR=/tmp; mkdir -p gpurun_out
+R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; export TMPDIR=/tmp PYTHONPATH=$R; mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_conv3x3.py tests/test_gpu_bnconv.py tests/test_gpu_conv.py > gpurun_out/r4_c3_t.log 2>&1 || { tail -40 gpurun_out/r4_c3_t.log; exit 1; }
 tail -2 gpurun_out/r4_c3_t.log
 timeout -k 10 300 python tools/gpu/conv3_bench.py > gpurun_out/r4_conv3_bench.txt 2>&1 || { tail -20 gpurun_out/r4_conv3_bench.txt; exit 1; }
