@@ -27,6 +27,7 @@ namespace grace {
 namespace {
 
 constexpr int kDB = 256;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 struct DecodeArgs {
   const float* val[kDecodeMaxRanks];
@@ -65,13 +66,28 @@ __global__ __launch_bounds__(kDB) void sparse_decode_kernel(DecodeArgs a, int W,
                                                            uint32_t* health_dev) {
   const int G = gridDim.x;
   const int64_t tid = (int64_t)blockIdx.x * kDB + threadIdx.x, stride = (int64_t)G * kDB;
-  // phase 0: zero (head to the first 16-B boundary, float4 body, tail)
+  // phase 0: zero (head to the first 16-B boundary, float4 body, tail).  Every store of `out`
+  // is write-through and drops its line from this XCD's L2 (sc1), and the rank phases add with
+  // device-coherent atomics (performed past the L2s): the per-XCD L2s are not coherent with each
+  // other, and an agent-scope acquire does not evict them, so a line one XCD kept from an
+  // earlier phase would otherwise be read stale after another XCD changed it.
   const int64_t head = std::min<int64_t>(n, (int64_t)((16 - (reinterpret_cast<uintptr_t>(out) & 15)) & 15) / 4);
-  if (tid < head) out[tid] = 0.f;
-  float4* body = reinterpret_cast<float4*>(out + head);
+  if (tid < head) __hip_atomic_store(out + tid, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int64_t nv = (n - head) / 4;
-  for (int64_t v = tid; v < nv; v += stride) body[v] = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int64_t i = head + 4 * nv + tid; i < n; i += stride) out[i] = 0.f;
+  {
+    float* body = out + head;
+    const int64_t bytes = nv * 16;
+    for (int64_t v0 = 0; v0 < nv; v0 += (int64_t(1) << 26)) {  // buffer descriptors address < 2 GB
+      const int64_t cnt = std::min<int64_t>(nv - v0, int64_t(1) << 26);
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc(body + 4 * v0, 0, (int)std::min<int64_t>(bytes - 16 * v0, 0x7fffffff),
+                                            0x00020000);
+      for (int64_t v = tid; v < cnt; v += stride)
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, rs, (int)(v * 16), 0, 16 /* sc1 */);
+    }
+  }
+  for (int64_t i = head + 4 * nv + tid; i < n; i += stride)
+    __hip_atomic_store(out + i, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // phases 1..W: rank r's entries, in rank order
   for (int r = 0; r < W; ++r) {
     grid_barrier(ctr, (r + 1) * G, health_host, health_dev);
@@ -83,23 +99,13 @@ __global__ __launch_bounds__(kDB) void sparse_decode_kernel(DecodeArgs a, int W,
     }
     const float* __restrict__ val = a.val[r];
     const int32_t* __restrict__ idx = a.idx[r];
-    // 4 entries per thread in flight (the idx -> out loads are dependent: latency-bound);
-    // out + round(val * scale), unfused, as torch's index_add_(v * scale)
-    for (int64_t j0 = tid; j0 < K; j0 += 4 * stride) {
-      int32_t t[4];
-      float v[4], o[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int64_t j = j0 + u * stride;
-        t[u] = j < K ? idx[j] : -1;
-        v[u] = j < K ? val[j] : 0.f;
-        if (t[u] >= n) t[u] = -1;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) o[u] = t[u] >= 0 ? out[t[u]] : 0.f;
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (t[u] >= 0) out[t[u]] = __fadd_rn(o[u], __fmul_rn(v[u], scale));
+    // indices are unique within a payload, so no two adds of a phase meet: the device-coherent
+    // atomic add is just a coherent read-modify-write, in rank order across the phases;
+    // out + round(val * scale), as torch's index_add_(v * scale)
+    for (int64_t j = tid; j < K; j += stride) {
+      const int32_t t = idx[j];
+      if (t >= 0 && t < n)
+        __hip_atomic_fetch_add(out + t, __fmul_rn(val[j], scale), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   // leave: the last workgroup out resets both counters for the next launch / graph replay
