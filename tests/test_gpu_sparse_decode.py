@@ -92,9 +92,9 @@ def test_decode_counts_unaligned_and_overflow():
     out = big[1:n + 1]  # 4-B aligned, not 16-B aligned
     P.decode_ranks(_gpu(vals), _gpu(idxs), _gpu(cnts), out, 0.5)
     torch.cuda.synchronize()
+    assert health.overflows() == before + sum(int(c[0]) > k for c in cnts)
     assert torch.equal(out, _loop(vals, idxs, cnts, n, 0.5))
     assert big[0].item() == -1.0 and big[n + 1].item() == -1.0 and big[n + 2].item() == -1.0
-    assert health.overflows() == before + sum(int(c[0]) > k for c in cnts)
     assert health.status()[0] == 0  # every barrier completed
 
 
