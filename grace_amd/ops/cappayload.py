@@ -58,11 +58,12 @@ def scatter_capped(hdr: torch.Tensor, vals: torch.Tensor, idx: torch.Tensor, out
 
 MAX_DECODE_RANKS = 32  # csrc/include/grace_kernels.h kDecodeMaxRanks
 _DECODE_CTR = {}
-# opt-in: the one-launch decode measured 2.8-5.6x SLOWER than a zero fill + W scatter launches on
-# a ResNet-50 bucket (65 vs 23 us at W = 1, 480 vs 85 us at W = 8, graph-replayed;
-# profiles/r4_decode_bench.txt): every grid barrier pays an agent-scope L2 write-back of the
-# freshly zeroed bucket plus an invalidate, ~60 us per phase, far above a launch boundary
-ONE_LAUNCH = __import__("os").environ.get("GRACE_DECODE_ONE_LAUNCH", "0") == "1"
+# the one-launch decode (default): as fast as a zero fill + W scatter launches on a ResNet-50
+# bucket (23.6 / 32.3 / 50.0 / 85.4 us at W = 1 / 2 / 4 / 8 vs 23.5 / 32.3 / 50.0 / 85.5,
+# graph-replayed, bit-identical; profiles/r4_decode_bench.txt) with 1 launch instead of W + 1.
+# Its first form (plain zero stores, RMW through the L2s) paid an agent-scope write-back of the
+# freshly zeroed bucket at every grid barrier: 65-480 us.  GRACE_DECODE_ONE_LAUNCH=0: the loop.
+ONE_LAUNCH = __import__("os").environ.get("GRACE_DECODE_ONE_LAUNCH", "1") == "1"
 
 
 def _decode_ctr(device) -> torch.Tensor:
@@ -79,9 +80,9 @@ def _decode_ctr(device) -> torch.Tensor:
 def decode_ranks(vals, idxs, counts, out: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
     """``out`` = 0, then ``out[idxs[r]] += vals[r] * scale`` for r = 0..W-1 in rank order --
     bit-identical on every rank.  ``counts[r]``: None (every entry) or the payload's in-band count
-    word (capacity payloads: the first min(count, capacity) entries).  Default: a zero fill plus W
-    atomic-free scatter launches; ``GRACE_DECODE_ONE_LAUNCH=1``: ONE launch (zero + W rank phases
-    behind grid barriers, csrc/kernels/sparse_decode.hip) -- measured slower, see ONE_LAUNCH."""
+    word (capacity payloads: the first min(count, capacity) entries).  Native path: ONE launch
+    (zero + W rank phases behind grid barriers, csrc/kernels/sparse_decode.hip);
+    ``GRACE_DECODE_ONE_LAUNCH=0``: a zero fill plus W scatter launches (same speed, see ONE_LAUNCH)."""
     W = len(vals)
     if ONE_LAUNCH and _native.use_native(out) and 1 <= W <= MAX_DECODE_RANKS and out.is_contiguous():
         _native.lib().sparse_decode_ranks(list(vals), list(idxs), [None if c is None else c[:1] for c in counts],
