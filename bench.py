@@ -54,9 +54,9 @@ def parse():
                          "(pytorch_synthetic_benchmark.py:86,151-160: plain model(data), no autocast, "
                          "TF32/xf32 disabled); bf16 = autocast, an explicitly labelled secondary run")
     ap.add_argument("--overlap", choices=["auto", "on", "off"], default="auto",
-                    help="compress+communicate on a side stream during backward; auto = off under a "
-                         "whole-step HIP graph (a forked capture costs ~0.9 ms/step on ROCm for ResNet-50, "
-                         "more than the overlap can hide), on otherwise")
+                    help="compress+communicate on a side stream during backward; auto = under a "
+                         "whole-step HIP graph on only when the estimated dense exchange exceeds the ~0.9 ms "
+                         "forked-capture cost (never for the compressed pipelines), on otherwise")
     ap.add_argument("--no-overlap", action="store_true", help="same as --overlap off")
     ap.add_argument("--bf16-weights", choices=["on", "off"], default="on",
                     help="fp32 master weights + bf16 working copies of conv/linear weights (autocast "
@@ -219,6 +219,19 @@ def main():
                          "(the exchange on the xGMI one-shot comm); else use --backend nccl")
     if args.no_overlap:
         args.overlap = "off"
+    # --overlap auto under the whole-step graph: on only when the exchange could hide more than a
+    # forked capture costs.  Fork cost: ~0.9 ms/step for ResNet-50 (profiles/r2_overlap_buckets.txt).
+    # Exchange estimate: a dense ring-equivalent 2 (W-1)/W x bytes over the 7 xGMI links per GPU at
+    # ~50 GB/s effective each -- the uncompressed 102 MB ResNet-50 gradient at W = 8 is ~0.5 ms,
+    # every compressed pipeline far less: off.  The W = 2 rehearsal (two ranks SHARING one GPU,
+    # profiles/r4_overlap_w2_rehearsal.txt: on 2986 vs off 2354 img/s Top-K, 2935 vs 2489 None)
+    # measures the shared card -- an early rank's in-line pull kernel spins on the compute stream
+    # the other rank needs -- not separate GPUs, where that spin blocks nothing.
+    if args.overlap == "auto" and mode == "full" and world > 1:
+        dense = w.grace.get("compressor") in ("none", "fp16")
+        grad_bytes = sum(p.numel() for p in model.parameters()) * (2 if w.grace.get("compressor") == "fp16" else 4)
+        est_ms = (2.0 * (world - 1) / world * grad_bytes / (7 * 50e9) * 1e3) if dense else 0.0
+        args.overlap = "on" if est_ms > 0.9 else "off"
     overlap = args.overlap == "on" or (args.overlap == "auto" and mode != "full")
     comm_kind = "local"
     comm_obj = None
