@@ -235,15 +235,17 @@ void bn_act_forward(const void* x, const void* res, bool fp32, int64_t M, int C,
 void bn_act_forward_from_partials(const float* x, const float* res, const float* part, int tiles, int64_t M, int C,
                                   const float* gamma, const float* beta, float* running_mean, float* running_var,
                                   int64_t* nbt, float momentum, float eps, bool relu, float* save, float* y,
-                                  uint8_t* mask, hipStream_t stream);
+                                  uint8_t* mask, hipStream_t stream, double* ws = nullptr);
 // Statistics only (no apply): the BN output is consumed by a GEMM's BnApplyPro prologue.
 void bn_fold_partials(const float* part, int tiles, int64_t M, int C, const float* gamma, const float* beta,
                       float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps, float* save,
-                      hipStream_t stream);
+                      hipStream_t stream, double* ws = nullptr);
 // Backward from the consuming conv's data-grad GEMM epilogue partials (BnBwdEpi): fold + dx pass.
 void bn_act_backward_from_partials(const float* dy, const float* x, const uint8_t* mask, const float* part, int tiles,
                                    int64_t M, int C, const float* gamma, const float* save, bool relu, float* dgamma,
-                                   float* dbeta, float* coef, float* dx, hipStream_t stream);
+                                   float* dbeta, float* coef, float* dx, hipStream_t stream, double* ws = nullptr);
+// doubles of the two-level fold workspace for `tiles` partial rows of C channels
+inline int64_t bn_fold_ws_doubles(int64_t tiles, int64_t C) { return ((tiles + 31) / 32) * 2 * C; }
 // fixed-order tree reductions in every BN backward (run-to-run bitwise reproducible) instead of
 // the default atomic totals (GRACE_BN_DETERMINISTIC=1 at start-up does the same)
 void bn_set_deterministic(bool on);

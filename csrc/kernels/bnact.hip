@@ -1647,11 +1647,44 @@ void forward_2k(const T* x, const T* res, int64_t M, int C, const StatsOut& o, b
     hipLaunchKernelGGL((bn_apply_kernel<T, false, false>), dim3(gb), dim3(kB), 0, stream, x, res, save, y, mask, n_vec, C);
 }
 
+// First level of a two-level fold of GEMM-epilogue partials [tiles][2][C] (fp32) into
+// [S][2][C] fp64 rows: a (C/32) x S grid instead of C/32 workgroups walking every tile -- a
+// ResNet-50 stage-1 layer has 1568 64-row tiles, which one 32-channel workgroup folded in ~28 us.
+// Fixed order inside each slice and across slices (deterministic).
+constexpr int kFoldSlice = 32;  // tiles per first-level workgroup
+__global__ __launch_bounds__(kB) void bn_fold_l1_kernel(const float* __restrict__ part, int tiles, int C,
+                                                        double* __restrict__ out) {
+  const int cl = threadIdx.x & 31, ph = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
+  const int t0 = blockIdx.y * kFoldSlice, t1 = min(tiles, t0 + kFoldSlice);
+  double s1 = 0.0, s2 = 0.0;
+  if (c < C)
+    for (int t = t0 + ph; t < t1; t += 8) {
+      s1 += (double)part[(int64_t)t * 2 * C + c];
+      s2 += (double)part[(int64_t)t * 2 * C + C + c];
+    }
+  __shared__ double l1[8][32], l2[8][32];
+  l1[ph][cl] = s1;
+  l2[ph][cl] = s2;
+  __syncthreads();
+  if (ph == 0 && c < C) {
+    double a = 0.0, b = 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      a += l1[i][cl];
+      b += l2[i][cl];
+    }
+    out[(int64_t)blockIdx.y * 2 * C + c] = a;
+    out[(int64_t)blockIdx.y * 2 * C + C + c] = b;
+  }
+}
+
 // BN statistics from the producing GEMM's epilogue partials (csrc/kernels/gemm_f32.hip p.stats:
 // per (row tile, channel) [sum | sum of squares] of the output as stored): the statistics pass
 // over the activation disappears; this fold reads tiles x 2C floats.  Block = 32 channels x 8
 // tile phases, fp64 accumulation in fixed order (deterministic), finish as bn_stats_kernel.
-__global__ __launch_bounds__(kB) void bn_stats_fold_kernel(const float* __restrict__ part, int tiles, int64_t M,
+template <typename P>
+__global__ __launch_bounds__(kB) void bn_stats_fold_kernel(const P* __restrict__ part, int tiles, int64_t M,
                                                            int C, StatsOut o) {
   const int cl = threadIdx.x & 31, ph = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + cl;
@@ -1698,7 +1731,8 @@ __global__ __launch_bounds__(kB) void bn_stats_fold_kernel(const float* __restri
 // per (row tile, channel) [sum dz | sum dz (x - mean)]): the reduction pass over (dy, x)
 // disappears; this fold reads tiles x 2C floats (fp64, fixed order: deterministic) and writes the
 // dx pass's coefficients and the parameter gradients exactly as bn_reduce_kernel's finisher.
-__global__ __launch_bounds__(kB) void bn_grad_fold_kernel(const float* __restrict__ part, int tiles, int64_t M,
+template <typename P>
+__global__ __launch_bounds__(kB) void bn_grad_fold_kernel(const P* __restrict__ part, int tiles, int64_t M,
                                                           int C, GradOut o) {
   const int cl = threadIdx.x & 31, ph = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + cl;
@@ -1907,13 +1941,26 @@ void bn_act_forward(const void* xv, const void* resv, bool fp32, int64_t M, int 
   forward_2k(x, res, M, C, o, relu, save, ws, y, mask, stream);
 }
 
+// Statistics fold of [tiles][2][C] epilogue partials: one level up to 2 slices, else two (ws:
+// >= ceil(tiles / kFoldSlice) * 2C doubles).
+void fold_stats(const float* part, int tiles, int64_t M, int C, const StatsOut& o, double* ws, hipStream_t stream) {
+  if (tiles > 2 * kFoldSlice && ws != nullptr) {
+    const int S = (tiles + kFoldSlice - 1) / kFoldSlice;
+    hipLaunchKernelGGL(bn_fold_l1_kernel, dim3((C + 31) / 32, S), dim3(kB), 0, stream, part, tiles, C, ws);
+    hipLaunchKernelGGL(bn_stats_fold_kernel<double>, dim3((C + 31) / 32), dim3(kB), 0, stream, (const double*)ws, S,
+                       M, C, o);
+  } else {
+    hipLaunchKernelGGL(bn_stats_fold_kernel<float>, dim3((C + 31) / 32), dim3(kB), 0, stream, part, tiles, M, C, o);
+  }
+}
+
 // Forward from GEMM-epilogue statistics (fp32): fold + apply, no statistics pass over x.
 void bn_act_forward_from_partials(const float* x, const float* res, const float* part, int tiles, int64_t M, int C,
                                   const float* gamma, const float* beta, float* running_mean, float* running_var,
                                   int64_t* nbt, float momentum, float eps, bool relu, float* save, float* y,
-                                  uint8_t* mask, hipStream_t stream) {
+                                  uint8_t* mask, hipStream_t stream, double* ws) {
   StatsOut o{gamma, beta, running_mean, running_var, nbt, momentum, eps, save};
-  hipLaunchKernelGGL(bn_stats_fold_kernel, dim3((C + 31) / 32), dim3(kB), 0, stream, part, tiles, M, C, o);
+  fold_stats(part, tiles, M, C, o, ws, stream);
   const int64_t n_vec = M * C / 8;
   const int gb = apply_grid(n_vec, C);
   if (relu && res)
@@ -1928,16 +1975,23 @@ void bn_act_forward_from_partials(const float* x, const float* res, const float*
 
 void bn_fold_partials(const float* part, int tiles, int64_t M, int C, const float* gamma, const float* beta,
                       float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps, float* save,
-                      hipStream_t stream) {
+                      hipStream_t stream, double* ws) {
   StatsOut o{gamma, beta, running_mean, running_var, nbt, momentum, eps, save};
-  hipLaunchKernelGGL(bn_stats_fold_kernel, dim3((C + 31) / 32), dim3(kB), 0, stream, part, tiles, M, C, o);
+  fold_stats(part, tiles, M, C, o, ws, stream);
 }
 
 void bn_act_backward_from_partials(const float* dy, const float* x, const uint8_t* mask, const float* part, int tiles,
                                    int64_t M, int C, const float* gamma, const float* save, bool relu, float* dgamma,
-                                   float* dbeta, float* coef, float* dx, hipStream_t stream) {
+                                   float* dbeta, float* coef, float* dx, hipStream_t stream, double* ws) {
   GradOut o{gamma, save, dgamma, dbeta, coef};
-  hipLaunchKernelGGL(bn_grad_fold_kernel, dim3((C + 31) / 32), dim3(kB), 0, stream, part, tiles, M, C, o);
+  if (tiles > 2 * kFoldSlice && ws != nullptr) {
+    const int S = (tiles + kFoldSlice - 1) / kFoldSlice;
+    hipLaunchKernelGGL(bn_fold_l1_kernel, dim3((C + 31) / 32, S), dim3(kB), 0, stream, part, tiles, C, ws);
+    hipLaunchKernelGGL(bn_grad_fold_kernel<double>, dim3((C + 31) / 32), dim3(kB), 0, stream, (const double*)ws, S, M,
+                       C, o);
+  } else {
+    hipLaunchKernelGGL(bn_grad_fold_kernel<float>, dim3((C + 31) / 32), dim3(kB), 0, stream, part, tiles, M, C, o);
+  }
   const int64_t n_vec = M * C / 8;
   const int gb = apply_grid(n_vec, C);
   const CoefSrc cs = CoefSrc{coef, save};

@@ -99,11 +99,12 @@ std::vector<Tensor> bn_act_fwd_partials(const Tensor& x, const c10::optional<Ten
   Tensor y = at::empty_like(x);
   Tensor save = at::empty({6 * C}, x.options());
   Tensor mask = relu ? at::empty({M * C / 8}, x.options().dtype(at::kByte)) : Tensor();
+  Tensor fws = at::empty({grace::bn_fold_ws_doubles(tiles, C)}, x.options().dtype(at::kDouble));
   grace::bn_act_forward_from_partials(x.data_ptr<float>(), has_res ? res->data_ptr<float>() : nullptr,
                                       part.data_ptr<float>(), (int)tiles, M, (int)C, opt_f32(weight, C, "weight"),
                                       opt_f32(bias, C, "bias"), rm, rv, nb, (float)momentum, (float)eps, relu,
                                       save.data_ptr<float>(), y.data_ptr<float>(),
-                                      relu ? mask.data_ptr<uint8_t>() : nullptr, cur_stream());
+                                      relu ? mask.data_ptr<uint8_t>() : nullptr, cur_stream(), fws.data_ptr<double>());
   return {y, save, mask};
 }
 
@@ -125,9 +126,10 @@ Tensor bn_fold_partials(const Tensor& part, int64_t tiles, int64_t M, int64_t C,
   }
   DevGuard guard(part.device());
   Tensor save = at::empty({6 * C}, part.options());
+  Tensor fws = at::empty({grace::bn_fold_ws_doubles(tiles, C)}, part.options().dtype(at::kDouble));
   grace::bn_fold_partials(part.data_ptr<float>(), (int)tiles, M, (int)C, opt_f32(weight, C, "weight"),
                           opt_f32(bias, C, "bias"), rm, rv, nb, (float)momentum, (float)eps, save.data_ptr<float>(),
-                          cur_stream());
+                          cur_stream(), fws.data_ptr<double>());
   return save;
 }
 
@@ -210,13 +212,14 @@ std::vector<Tensor> bn_act_bwd_partials(const Tensor& dy, const Tensor& x, const
   Tensor db = want_dweight ? out_or(dbias_out) : Tensor();
   Tensor coef = at::empty({3 * C}, f32);
   Tensor dx = at::empty_like(x);
+  Tensor fws = at::empty({grace::bn_fold_ws_doubles(tiles, C)}, x.options().dtype(at::kDouble));
   grace::bn_act_backward_from_partials(dy.data_ptr<float>(), x.data_ptr<float>(),
                                        relu && has_mask ? mask->data_ptr<uint8_t>() : nullptr, part.data_ptr<float>(),
                                        (int)tiles,
                                        M, (int)C, opt_f32(weight, C, "weight"), save.data_ptr<float>(), relu,
                                        want_dweight ? dg.data_ptr<float>() : nullptr,
                                        want_dweight ? db.data_ptr<float>() : nullptr, coef.data_ptr<float>(),
-                                       dx.data_ptr<float>(), cur_stream());
+                                       dx.data_ptr<float>(), cur_stream(), fws.data_ptr<double>());
   return {dx, dg, db};
 }
 
