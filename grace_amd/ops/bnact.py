@@ -79,7 +79,7 @@ def _kernel_grad(g: Optional[torch.Tensor], like: torch.Tensor) -> Optional[torc
 # its epilogue (gemm_f32.hip BnBwdEpi) and this BN's backward only folds those partials and runs
 # its dx pass -- the reduction pass over (dy, x) disappears.  Used only when the gradient handed
 # to the BN backward IS the GEMM's output (same storage, no accumulation in between).
-_HANDOFF = __import__("os").environ.get("GRACE_BN_BWD_EPI", "1") == "1"
+_HANDOFF = __import__("os").environ.get("GRACE_BN_BWD_EPI", "0") == "1"  # measured neutral: opt-in
 
 
 class BNHandoff:

@@ -217,6 +217,8 @@ def test_bn_handoff_chain_matches_unfused():
     CV._pick3 = lambda d, *a, **k: "mfma" if d == "dgrad" else pick3(d, *a, **k)
     counting = _Counting(lib, ["bn_act_bwd_partials", "bn_act_bwd"])
     _native._lib = counting
+    default = BN._HANDOFF
+    BN._HANDOFF = True  # opt-in (measured neutral): forced on for this test
     try:
         fused = run()
         assert counting.n["bn_act_bwd_partials"] == 2, counting.n
@@ -225,7 +227,7 @@ def test_bn_handoff_chain_matches_unfused():
         plain = run()
         assert counting.n["bn_act_bwd_partials"] == 0 and counting.n["bn_act_bwd"] == 2, counting.n
     finally:
-        BN._HANDOFF = True
+        BN._HANDOFF = default
         _native._lib = lib
         CV._pick, CV._pick3 = pick, pick3
     for a, b in zip(fused, plain):
