@@ -236,6 +236,10 @@ void bn_act_forward_from_partials(const float* x, const float* res, const float*
                                   const float* gamma, const float* beta, float* running_mean, float* running_var,
                                   int64_t* nbt, float momentum, float eps, bool relu, float* save, float* y,
                                   uint8_t* mask, hipStream_t stream, double* ws = nullptr);
+// Statistics pass only (save, running statistics; no apply) over an fp32 [M][C] activation.
+void bn_stats_only(const float* x, int64_t M, int C, const float* gamma, const float* beta, float* running_mean,
+                   float* running_var, int64_t* nbt, float momentum, float eps, float* save, float* ws,
+                   hipStream_t stream);
 // Statistics only (no apply): the BN output is consumed by a GEMM's BnApplyPro prologue.
 void bn_fold_partials(const float* part, int tiles, int64_t M, int C, const float* gamma, const float* beta,
                       float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps, float* save,

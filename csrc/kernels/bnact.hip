@@ -1973,6 +1973,15 @@ void bn_act_forward_from_partials(const float* x, const float* res, const float*
     hipLaunchKernelGGL((bn_apply_kernel<float, false, false>), dim3(gb), dim3(kB), 0, stream, x, res, save, y, mask, n_vec, C);
 }
 
+void bn_stats_only(const float* x, int64_t M, int C, const float* gamma, const float* beta, float* running_mean,
+                   float* running_var, int64_t* nbt, float momentum, float eps, float* save, float* ws,
+                   hipStream_t stream) {
+  StatsOut o{gamma, beta, running_mean, running_var, nbt, momentum, eps, save};
+  Red R = plan(M, C);
+  bind_ws(R, ws, stream, bn_fwd_atomic() && !bn_deterministic_env());
+  hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(R.nchunks, C / R.CT), dim3(kB), 0, stream, x, R, o);
+}
+
 void bn_fold_partials(const float* part, int tiles, int64_t M, int C, const float* gamma, const float* beta,
                       float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps, float* save,
                       hipStream_t stream, double* ws) {

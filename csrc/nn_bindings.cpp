@@ -108,6 +108,30 @@ std::vector<Tensor> bn_act_fwd_partials(const Tensor& x, const c10::optional<Ten
   return {y, save, mask};
 }
 
+// BN statistics pass only (no apply) over an fp32 channels_last activation: save [6C], running
+// statistics updated; the apply runs in the consumer GEMM's prologue
+Tensor bn_stats_only(const Tensor& x, const c10::optional<Tensor>& weight, const c10::optional<Tensor>& bias,
+                     const c10::optional<Tensor>& running_mean, const c10::optional<Tensor>& running_var,
+                     const c10::optional<Tensor>& nbt, double momentum, double eps) {
+  int64_t M, C;
+  check_rows(x, "x", &M, &C);
+  TORCH_CHECK(x.scalar_type() == at::kFloat, "bn_stats_only: fp32 activations");
+  float* rm = const_cast<float*>(opt_f32(running_mean, C, "running_mean"));
+  float* rv = const_cast<float*>(opt_f32(running_var, C, "running_var"));
+  TORCH_CHECK((rm == nullptr) == (rv == nullptr), "running_mean / running_var: both or neither");
+  int64_t* nb = nullptr;
+  if (nbt.has_value() && nbt->defined()) {
+    TORCH_CHECK(nbt->is_cuda() && nbt->scalar_type() == at::kLong && nbt->numel() == 1, "num_batches_tracked");
+    nb = nbt->data_ptr<int64_t>();
+  }
+  DevGuard guard(x.device());
+  Tensor save = at::empty({6 * C}, x.options());
+  Tensor ws = at::empty({grace::bn_workspace_floats(M, (int)C)}, x.options());
+  grace::bn_stats_only(x.data_ptr<float>(), M, (int)C, opt_f32(weight, C, "weight"), opt_f32(bias, C, "bias"), rm, rv,
+                       nb, (float)momentum, (float)eps, save.data_ptr<float>(), ws.data_ptr<float>(), cur_stream());
+  return save;
+}
+
 // BN statistics from GEMM partials only: save [6C] (mean, invstd, scale, shift, 0, 0), running
 // statistics and num_batches_tracked updated; the apply runs in the consumer GEMM's prologue
 Tensor bn_fold_partials(const Tensor& part, int64_t tiles, int64_t M, int64_t C, const c10::optional<Tensor>& weight,
@@ -395,6 +419,7 @@ void grace_bind_nn(py::module& m) {
   m.def("bn_atomic_chunks", []() { return (int64_t)grace::bn_atomic_chunks(); });
   m.def("bn_act_fwd_partials", &bn_act_fwd_partials);
   m.def("bn_fold_partials", &bn_fold_partials);
+  m.def("bn_stats_only", &bn_stats_only);
   m.def("bn_act_bwd_partials", &bn_act_bwd_partials, py::arg("dy"), py::arg("x"), py::arg("mask"), py::arg("weight"),
         py::arg("save"), py::arg("part"), py::arg("tiles"), py::arg("relu"), py::arg("want_dweight"),
         py::arg("dweight_out") = py::none(), py::arg("dbias_out") = py::none());

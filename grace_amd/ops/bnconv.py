@@ -32,17 +32,21 @@ from . import _native
 from . import wgrad as _wg
 from .bnact import BatchNormAct2d, _fusable, bn_act
 
-# opt-in: measured slower on the fp32 ResNet-50 headline (2072 vs 2722 img/s,
-# profiles/r4_bn_fusion_ab.txt) -- every direction of the fused convolutions must then run on the
-# f32 MFMA GEMM, which trails MIOpen's 3x3 solvers (stages 3-4, all weight grads) by more than the
-# BN passes it removes save
-_ON = os.environ.get("GRACE_BN_PROLOGUE", "0") == "1"
+# GRACE_BN_PROLOGUE: 0 = off (default); 1 = bn1 -> conv2 and bn2 -> conv3 fused, measured slower
+# on the fp32 ResNet-50 headline (2072 vs 2722 img/s, profiles/r4_bn_fusion_ab.txt: every
+# direction of the fused convolutions then runs on the f32 MFMA GEMM, which trails MIOpen's 3x3
+# solvers by more than the removed BN passes save); 2 = bn2 -> conv3 only (the 1x1 conv3, where
+# the MFMA GEMM is competitive; conv2 keeps its autotuned backend and bn2 a statistics-only pass)
+_MODE = int(os.environ.get("GRACE_BN_PROLOGUE", "0") or 0)
+_ON = _MODE != 0
 _TARGETS = os.environ.get("GRACE_BN_GRAD_TARGET", "1") == "1"
 
 
-def set_enabled(on: bool) -> None:
-    global _ON
+def set_enabled(on, mode: Optional[int] = None) -> None:
+    """on: the fused bottleneck path (mode 1 unless ``mode`` is given: 1 full, 2 conv3 only)."""
+    global _ON, _MODE
     _ON = bool(on)
+    _MODE = (mode if mode is not None else 1) if _ON else 0
 
 
 def _cl(t: torch.Tensor) -> bool:
@@ -182,6 +186,8 @@ def bottleneck_main(blk, xm: torch.Tensor, idt: torch.Tensor):
         return None
     if (nb * ho * wo) % 4 or c3.out_channels % 4:
         return None
+    if _MODE == 2:
+        return _conv3_only(blk, xm, idt)
     # --- run
     y1, p1 = _Conv1x1StatsFn.apply(xm, c1.weight, 0)
     m1 = nb * h * w
@@ -196,13 +202,48 @@ def bottleneck_main(blk, xm: torch.Tensor, idt: torch.Tensor):
     return bn_act(y3, b3, idt, b3.relu, True, partials=p3, tiles=p3._grace_tiles)
 
 
+def bn_stats(bn: BatchNormAct2d, y: torch.Tensor) -> torch.Tensor:
+    """The BN's statistics by one pass over its input (no apply): save [6C]; running statistics
+    and num_batches_tracked updated as nn.BatchNorm2d does."""
+    track = bn.training and bn.track_running_stats
+    with torch.no_grad():
+        return _native.lib().bn_stats_only(y, bn.weight, bn.bias, bn.running_mean if track else None,
+                                           bn.running_var if track else None,
+                                           bn.num_batches_tracked if track else None,
+                                           float(bn.momentum if bn.momentum is not None else 0.0), float(bn.eps))
+
+
+def _conv3_only(blk, xm: torch.Tensor, idt: torch.Tensor):
+    """Mode 2: conv1 -> bn1 -> conv2 as the plain (autotuned) path; bn2's statistics from conv2's
+    epilogue when the autotuner chose it, else a statistics-only pass; bn2's apply inside conv3's
+    GEMM and its backward reduction in conv3's data-grad epilogue."""
+    from .conv import _Conv3x3StatsFn, _pick_bn, conv3x3_ok, conv_bn_act
+
+    c1, b1, c2, b2, c3, b3 = blk.conv1, blk.bn1, blk.conv2, blk.bn2, blk.conv3, blk.bn3
+    y1 = conv_bn_act(c1, b1, xm)
+    m2 = None
+    if conv3x3_ok(y1, c2):
+        choice = _pick_bn(c2, b2, y1, None, b2.relu)
+        if choice.startswith("stats_t"):
+            y2, p2 = _Conv3x3StatsFn.apply(y1, c2.weight, c2.stride[0], int(choice[7:]))
+            m2 = y2.shape[0] * y2.shape[2] * y2.shape[3]
+            s2 = bn_fold(b2, p2, p2._grace_tiles, m2)
+    if m2 is None:
+        y2 = c2(y1)
+        if not (_cl(y2) and y2.dtype == torch.float32):
+            return bn_act(c3(bn_act(y2, b2, None, b2.relu)), b3, idt, b3.relu, True)
+        s2 = bn_stats(b2, y2)
+    y3, p3 = _BnActConvFn.apply(y2, b2.weight, b2.bias, s2, c3.weight, bool(b2.relu), 1, True)
+    return bn_act(y3, b3, idt, b3.relu, True, partials=p3, tiles=p3._grace_tiles)
+
+
 def basic_main(blk, xm: torch.Tensor, idt: torch.Tensor):
     """A basic block's main path conv1 -> bn1 -> conv2 -> bn2(+idt, dual) with bn1 applied inside
     conv2's implicit GEMM; None when it does not apply (decided before anything runs)."""
     from . import conv as _conv
 
     c1, b1, c2, b2 = blk.conv1, blk.bn1, blk.conv2, blk.bn2
-    if not (_ON and xm.is_cuda and xm.dtype == torch.float32 and torch.is_grad_enabled()
+    if not (_ON and _MODE == 1 and xm.is_cuda and xm.dtype == torch.float32 and torch.is_grad_enabled()
             and not torch.is_autocast_enabled() and _native.native_on(xm.device)):
         return None
     if not (isinstance(c1, _wg.Conv2dSplitGrad) and isinstance(c2, _wg.Conv2dSplitGrad)

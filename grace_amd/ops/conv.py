@@ -189,15 +189,7 @@ def _pick(direction: str, x, wt, dy, wshape) -> str:
     times = {}
     for be in BACKENDS:
         try:
-            for _ in range(2):
-                _run(direction, be, x, wt, dy, wshape)
-            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s.record()
-            for _ in range(5):
-                _run(direction, be, x, wt, dy, wshape)
-            e.record()
-            e.synchronize()
-            times[be] = s.elapsed_time(e) / 5
+            times[be] = _time(lambda be=be: _run(direction, be, x, wt, dy, wshape))
         except Exception:  # a backend that rejects the shape is simply not a candidate
             continue
     c = min(times, key=times.get) if times else "miopen"
@@ -339,16 +331,21 @@ _BN_TIMES = {}
 _BN_FUSE = os.environ.get("GRACE_CONV_BN_STATS", "1") == "1"
 
 
-def _time(fn, reps=5):
+def _time(fn, reps=5, trials=3):
+    """ms per call: the best of ``trials`` runs of ``reps`` calls (near-ties between backends
+    otherwise flip from run to run)."""
     for _ in range(2):
         fn()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(reps):
-        fn()
-    e.record()
-    e.synchronize()
-    return s.elapsed_time(e) / reps
+    best = float("inf")
+    for _ in range(trials):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            fn()
+        e.record()
+        e.synchronize()
+        best = min(best, s.elapsed_time(e) / reps)
+    return best
 
 
 def _pick_bn(conv, bn, x, residual, relu) -> str:

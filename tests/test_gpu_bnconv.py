@@ -92,8 +92,9 @@ def test_epilogue_recomputed_relu(ksize):
     torch.testing.assert_close(p[1], (dz * xh).sum((0, 2, 3)), rtol=1e-5, atol=1e-4)
 
 
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("stride,cin", [(1, 256), (2, 256), (1, 64)])
-def test_fused_bottleneck_matches_unfused(stride, cin):
+def test_fused_bottleneck_matches_unfused(stride, cin, mode):
     from grace_amd.models.resnet import Bottleneck
     from grace_amd.ops.bnact import BatchNormAct2d
 
@@ -113,7 +114,7 @@ def test_fused_bottleneck_matches_unfused(stride, cin):
     x0 = torch.randn(4, cin, 14, 14, device="cuda").contiguous(memory_format=torch.channels_last)
 
     def run(model, fused):
-        BC.set_enabled(fused)
+        BC.set_enabled(fused, mode)
         try:
             x = x0.clone().requires_grad_()
             out = model(x)
@@ -123,9 +124,9 @@ def test_fused_bottleneck_matches_unfused(stride, cin):
             return y.detach(), x.grad, {n: p.grad.clone() for n, p in model.named_parameters()}, \
                 {n: b.clone() for n, b in model.named_buffers()}
         finally:
-            BC.set_enabled(default)
+            BC.set_enabled(default[0], default[1])
 
-    default = BC._ON
+    default = (BC._ON, BC._MODE)
     calls = {"n": 0}
     real = BC._BnActConvFn.apply
 
@@ -138,7 +139,7 @@ def test_fused_bottleneck_matches_unfused(stride, cin):
         yf, dxf, gf, bf = run(blk, True)
     finally:
         BC._BnActConvFn.apply = real
-    assert calls["n"] == (2 if stride == 1 else 1), calls  # bn1 -> conv2 only at stride 1
+    assert calls["n"] == (2 if stride == 1 and mode == 1 else 1), calls  # bn1 -> conv2 only in mode 1, stride 1
     yu, dxu, gu, bu = run(ref, False)
     torch.testing.assert_close(yf, yu, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(dxf, dxu, rtol=1e-3, atol=1e-6)
@@ -161,9 +162,9 @@ def test_fused_basic_block_matches_unfused():
     ref = copy.deepcopy(blk)
     x0 = torch.randn(8, 64, 16, 16, device="cuda").contiguous(memory_format=torch.channels_last)
     res = []
-    default = BC._ON
+    default = (BC._ON, BC._MODE)
     for model, fused in ((blk, True), (ref, False)):
-        BC.set_enabled(fused)
+        BC.set_enabled(fused, 1)
         try:
             x = x0.clone().requires_grad_()
             y = model(x)[0]
@@ -171,7 +172,7 @@ def test_fused_basic_block_matches_unfused():
             torch.cuda.synchronize()
             res.append((y.detach(), x.grad, [p.grad.clone() for p in model.parameters()]))
         finally:
-            BC.set_enabled(default)
+            BC.set_enabled(default[0], default[1])
     (yf, dxf, gf), (yu, dxu, gu) = res
     torch.testing.assert_close(yf, yu, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(dxf, dxu, rtol=1e-3, atol=1e-6)
