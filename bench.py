@@ -299,6 +299,10 @@ def main():
                                                               gradient_as_bucket_view=True, broadcast_buffers=False)
         ddp_state = GraceHookState(grc, model=model)
         model.register_comm_hook(ddp_state, grace_comm_hook)
+        if ddp_stream is not None and hasattr(torch.autograd.graph, "set_warn_on_accumulate_grad_stream_mismatch"):
+            # intentional: DDP's reducer keeps AccumulateGrad nodes created on the capture stream (see
+            # above), so the eager warm-up steps before the capture run them across streams
+            torch.autograd.graph.set_warn_on_accumulate_grad_stream_mismatch(False)
 
         class _DdpOpt:  # the bench loop's optimizer interface over DDP + a plain optimizer
             engine = type("E", (), {"grc": grc})()
