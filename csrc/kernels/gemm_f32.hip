@@ -48,8 +48,11 @@ namespace grace {
 namespace {
 
 constexpr int kGB = 256;  // threads per workgroup (4 waves)
-constexpr int BK = 32;    // k per LDS stage (4 x 8-k groups; BK = 16 with 4 workgroups per CU measured slower)
-constexpr int LDK = 36;   // row pitch (floats) of a K-contig LDS image (conflict-free b128 reads)
+// k per LDS stage: 32 (4 x 8-k groups; BK = 16 with 4 workgroups per CU measured slower), or 64
+// for the 128x64 / 64x128 / 64x64 tiles (tiles 5-7): twice the MFMA work between two barriers, so
+// a small tile's next-slice global loads are hidden (a 64x64 tile's 32-k slice is ~1000 MFMA
+// cycles per wave, less than an HBM round trip)
+constexpr int BK = 32;
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -117,8 +120,9 @@ __device__ __forceinline__ int fdivmod(int m, int d, float inv, int* r) {
   return q;
 }
 
-template <int R, int MODE>
+template <int R, int MODE, int BK = 32>
 struct Operand {
+  static constexpr int LDK = BK + 4;                   // K-contig row pitch (conflict-free b128 reads)
   static constexpr bool KC = mode_kc(MODE);
   static constexpr int NV = R * BK / 4 / kGB;          // float4 per thread per stage
   static constexpr int LDS = KC ? R * LDK : BK * R;    // floats per stage
@@ -263,10 +267,10 @@ struct Operand {
 
 __device__ __forceinline__ float f4get(const float4& v, int s) { return s == 0 ? v.x : s == 1 ? v.y : s == 2 ? v.z : v.w; }
 
-template <int BM, int BN, int AM, int BMD>
+template <int BM, int BN, int AM, int BMD, int BK = 32>
 __global__ __launch_bounds__(kGB, 2) void gemm_f32_kernel(GemmParams p) {
-  using OA = Operand<BM, AM>;
-  using OB = Operand<BN, BMD>;
+  using OA = Operand<BM, AM, BK>;
+  using OB = Operand<BN, BMD, BK>;
   constexpr int STAGE = OA::LDS + OB::LDS;
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 32, FN = WN / 32;
   constexpr int CP = WN + 4;                  // padded row pitch of a wave's staged 32-row C slab
@@ -476,12 +480,12 @@ __global__ __launch_bounds__(kGB, 2) void gemm_f32_kernel(GemmParams p) {
     }
 }
 
-template <int BM, int BN, int AM, int BMD>
+template <int BM, int BN, int AM, int BMD, int BKT = 32>
 int launch_cfg(GemmParams p, hipStream_t stream) {
   p.tiles_m = (p.M + BM - 1) / BM;
   p.tiles_n = (p.N + BN - 1) / BN;
   const int64_t blocks = (int64_t)p.tiles_m * p.tiles_n * p.splits;
-  gemm_f32_kernel<BM, BN, AM, BMD><<<(unsigned)blocks, kGB, 0, stream>>>(p);
+  gemm_f32_kernel<BM, BN, AM, BMD, BKT><<<(unsigned)blocks, kGB, 0, stream>>>(p);
   return p.tiles_m;
 }
 
@@ -503,7 +507,8 @@ int launch_layout(GemmParams p, hipStream_t stream) {
 }  // namespace
 
 namespace {
-// tile: 0 = by the launcher's rule, 1 = 128x128, 2 = 128x64, 3 = 64x128, 4 = 64x64
+// tile: 0 = by the launcher's rule, 1 = 128x128, 2 = 128x64, 3 = 64x128, 4 = 64x64 (32-k slices);
+// 5 = 128x64, 6 = 64x128, 7 = 64x64 with 64-k slices
 template <int AM, int BMD>
 int launch_tile(GemmParams p, int tile, hipStream_t stream) {
   switch (tile) {
@@ -511,6 +516,9 @@ int launch_tile(GemmParams p, int tile, hipStream_t stream) {
     case 2: return launch_cfg<128, 64, AM, BMD>(p, stream);
     case 3: return launch_cfg<64, 128, AM, BMD>(p, stream);
     case 4: return launch_cfg<64, 64, AM, BMD>(p, stream);
+    case 5: return launch_cfg<128, 64, AM, BMD, 64>(p, stream);
+    case 6: return launch_cfg<64, 128, AM, BMD, 64>(p, stream);
+    case 7: return launch_cfg<64, 64, AM, BMD, 64>(p, stream);
     default: return launch_layout<AM, BMD>(p, stream);
   }
 }
@@ -525,10 +533,10 @@ int auto_splits(int M, int N, int K, int64_t ldc) {
 }
 
 // splits -> k per split (multiple of BK), C zeroed for split-K; returns whether atomic
-void set_splits(GemmParams& p, int splits, float* stats, hipStream_t stream) {
+void set_splits(GemmParams& p, int splits, float* stats, hipStream_t stream, int bk = BK) {
   if (splits < 1) splits = 1;
   int kps = (p.K + splits - 1) / splits;
-  kps = (kps + BK - 1) / BK * BK;
+  kps = (kps + bk - 1) / bk * bk;
   splits = p.K > 0 ? (p.K + kps - 1) / kps : 1;
   p.splits = splits;
   p.k_per_split = kps;
@@ -566,7 +574,7 @@ int gemm_f32(const float* A, bool a_kcontig, int64_t lda, const float* B, bool b
   p.ldb = ldb;
   p.ldc = ldc;
   if (splits == 0) splits = auto_splits(M, N, K, ldc);  // host-checked: split-K only with ldc == N
-  set_splits(p, splits, stats, stream);
+  set_splits(p, splits, stats, stream, tile >= 5 ? 64 : BK);
   if (a_kcontig && b_kcontig) return launch_tile<0, 0>(p, tile, stream);
   if (a_kcontig && !b_kcontig) return launch_tile<0, 1>(p, tile, stream);
   if (!a_kcontig && !b_kcontig) return launch_tile<1, 1>(p, tile, stream);
@@ -626,8 +634,10 @@ int conv3x3_f32(int dir, const float* act, const float* other, float* C, int N, 
   p.gInvWr = 1.f / (float)p.gWr;
   p.gInvHr = 1.f / (float)p.gHr;
   if (p.M <= 0 || p.N <= 0) return 0;
+  // 64-k slices need a slice never to straddle a tap: C (mode 2) / Cout (mode 4) % 64 == 0
+  if (tile >= 5 && ((dir != 2 && p.gC % 64 != 0) || (dir == 1 && p.kt % 64 != 0))) tile -= 3;
   if (splits == 0) splits = dir == 2 ? auto_splits(p.M, p.N, p.K, p.ldc) : 1;
-  set_splits(p, splits, (dir == 0 || p.bx != nullptr) ? stats : nullptr, stream);
+  set_splits(p, splits, (dir == 0 || p.bx != nullptr) ? stats : nullptr, stream, tile >= 5 ? 64 : BK);
   if (dir == 0) return launch_tile<2, 0>(p, tile, stream);
   if (dir == 1) return launch_tile<2, 4>(p, tile, stream);
   return launch_tile<1, 3>(p, tile, stream);

@@ -45,6 +45,28 @@ def test_gemm_f32_layouts(a_kc, b_kc, m, n, k, splits):
     assert (err <= bound).all(), err.max()
 
 
+@pytest.mark.parametrize("tile", [5, 6, 7])
+@pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, False), (False, True)])
+@pytest.mark.parametrize("m,n,k,splits", [(200, 132, 68, 1), (64, 256, 1000, 4), (333, 520, 96, 3),
+                                          (1568, 512, 2048, 0)])
+def test_gemm_f32_64k_slices(tile, a_kc, b_kc, m, n, k, splits):
+    """Tiles 5-7 (64-k LDS slices): K not a multiple of 64, split-K, ragged edges."""
+    g = torch.Generator().manual_seed(m * 3 + n + tile)
+    if not a_kc and m % 4:
+        m += 4 - m % 4
+    if not b_kc and n % 4:
+        n += 4 - n % 4
+    A, a, lda = _operand(m, k, a_kc, 4, g)
+    B, b, ldb = _operand(n, k, b_kc, 8, g)
+    c = torch.full((m, n), float("nan"), device="cuda")
+    gemm(a, a_kc, lda, b, b_kc, ldb, c, n, m, n, k, splits, tile)
+    ref = A.float().double() @ B.float().double().t()
+    bound = (A.float().double().abs() @ B.float().double().abs().t()) * 2e-6 + 1e-30
+    err = (c.double().cpu() - ref).abs()
+    assert torch.isfinite(c).all()
+    assert (err <= bound).all(), err.max()
+
+
 @pytest.mark.parametrize("nb,cin,cout,hw", [(4, 64, 256, 14), (2, 256, 64, 7), (3, 128, 512, 5), (2, 512, 128, 9)])
 def test_conv1x1_f32_fwd_bwd(nb, cin, cout, hw):
     torch.manual_seed(0)
