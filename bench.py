@@ -518,6 +518,15 @@ def main():
             "final_loss": round(final_loss, 4),
         }
         print(json.dumps(out), flush=True)
+        if os.environ.get("GRACE_AUTOTUNE_REPORT", "0") == "1":  # the per-layer backend choices, to stderr
+            from grace_amd.ops import conv as _cv
+
+            for row in _cv.autotune_table():
+                print("conv1x1", row[:5], {k: round(v, 4) for k, v in row[5].items()}, file=sys.stderr)
+            for row in _cv.conv3x3_autotune_table():
+                print("conv", row[:9], {k: round(v, 4) for k, v in row[9].items()}, file=sys.stderr)
+            for row in _cv.bn_autotune_table():
+                print("conv_bn", row[:6], {k: round(v, 4) for k, v in row[6].items()}, file=sys.stderr)
     if dist.is_initialized():
         dist.destroy_process_group()
 
