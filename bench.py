@@ -525,8 +525,8 @@ def main():
                 print("conv1x1", row[:5], {k: round(v, 4) for k, v in row[5].items()}, file=sys.stderr)
             for row in _cv.conv3x3_autotune_table():
                 print("conv", row[:9], {k: round(v, 4) for k, v in row[9].items()}, file=sys.stderr)
-            for row in _cv.bn_autotune_table():
-                print("conv_bn", row[:6], {k: round(v, 4) for k, v in row[6].items()}, file=sys.stderr)
+            for row in _cv.bn_autotune_table():  # (key..., choice, {candidate: ms})
+                print("conv_bn", row[:-1], {k: round(v, 4) for k, v in row[-1].items()}, file=sys.stderr)
     if dist.is_initialized():
         dist.destroy_process_group()
 
