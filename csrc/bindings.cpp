@@ -248,6 +248,15 @@ void randk_scatter(const Tensor& vals, int64_t rank_stride, int64_t n_ranks, int
                        opt_i64(step), K, out.data_ptr<float>(), (float)scale, accumulate, cur_stream());
 }
 
+// Bytes of the in-band payload header to clear before a compaction: the whole 16-B
+// [selected, capacity, 0, 0] header when the count word heads one (ops/cappayload.py
+// sparse_payload), so no stale allocator bytes ride on the wire (payload bytes identical on every
+// rank and run); else the count word alone.
+static int header_bytes(const Tensor& counter) {
+  const int64_t avail = (int64_t)counter.storage().nbytes() - counter.storage_offset() * (int64_t)sizeof(int32_t);
+  return avail >= 16 ? 16 : 4;
+}
+
 int64_t threshold_compact(const Tensor& g, const c10::optional<Tensor>& r, int64_t mode, double beta, double gamma,
                           double thr, const Tensor& out_val, const Tensor& out_idx, const Tensor& counter,
                           const c10::optional<Tensor>& resid) {
@@ -271,7 +280,7 @@ int64_t threshold_compact(const Tensor& g, const c10::optional<Tensor>& r, int64
   DevGuard guard(g.device());
   grace::threshold_compact(g.data_ptr<float>(), rp, (int)mode, (float)beta, (float)gamma, g.numel(), (float)thr,
                            out_val.data_ptr<float>(), out_idx.data_ptr<int32_t>(), out_val.numel(),
-                           counter.data_ptr<int32_t>(), wp, cur_stream());
+                           counter.data_ptr<int32_t>(), wp, cur_stream(), header_bytes(counter));
   return 0;
 }
 
@@ -552,7 +561,8 @@ void dgc_compact(const Tensor& x, const Tensor& thr, const Tensor& out_val, cons
   auto ct = make_ct(seg, cb, ce);
   DevGuard guard(x.device());
   grace::dgc_compact(ct, x.data_ptr<float>(), thr.data_ptr<float>(), out_val.data_ptr<float>(),
-                     out_idx.data_ptr<int32_t>(), out_val.numel(), counter.data_ptr<int32_t>(), vp, up, cur_stream());
+                     out_idx.data_ptr<int32_t>(), out_val.numel(), counter.data_ptr<int32_t>(), vp, up, cur_stream(),
+                     header_bytes(counter));
 }
 
 void dgc_compensate(const Tensor& g, const Tensor& u, const Tensor& v, double momentum, bool first) {

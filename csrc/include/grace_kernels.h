@@ -63,7 +63,7 @@ void randk_scatter(const float* vals, int64_t rank_stride, int n_ranks, int n_se
                    float scale, bool accumulate, hipStream_t stream);
 void threshold_compact(const float* g, const float* r, int mode, float beta, float gamma, int64_t n, float thr,
                        float* out_val, int32_t* out_idx, int64_t cap, int32_t* counter, float* resid,
-                       hipStream_t stream);
+                       hipStream_t stream, int header_bytes = 4);
 
 // ---------------------------------------------------------------- signbits.hip
 void sign_pack(const ChunkTable& ct, const int64_t* seg_start, const int64_t* word_off, const float* g,
@@ -107,7 +107,7 @@ void dgc_refine(const ChunkTable& ct, int n_seg, const float* x, const TopkState
                 int max_iters, float* thr, int32_t* count, int32_t* done, float* u, float* v, float momentum,
                 int first, int64_t n, hipStream_t stream);
 void dgc_compact(const ChunkTable& ct, const float* x, const float* thr, float* out_val, int32_t* out_idx,
-                 int64_t cap, int32_t* counter, float* vmask, float* umask, hipStream_t stream);
+                 int64_t cap, int32_t* counter, float* vmask, float* umask, hipStream_t stream, int header_bytes = 4);
 void dgc_compensate(const float* g, float* u, float* v, float momentum, int64_t n, bool first, hipStream_t stream);
 
 // ---------------------------------------------------------------- powersgd.hip

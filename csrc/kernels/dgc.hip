@@ -346,8 +346,8 @@ void dgc_refine(const ChunkTable& ct, int n_seg, const float* x, const TopkState
 }
 
 void dgc_compact(const ChunkTable& ct, const float* x, const float* thr, float* out_val, int32_t* out_idx,
-                 int64_t cap, int32_t* counter, float* vmask, float* umask, hipStream_t stream) {
-  GRACE_HIP_CHECK(hipMemsetAsync(counter, 0, sizeof(int32_t), stream));
+                 int64_t cap, int32_t* counter, float* vmask, float* umask, hipStream_t stream, int header_bytes) {
+  GRACE_HIP_CHECK(hipMemsetAsync(counter, 0, header_bytes, stream));
   if (ct.n_chunks == 0) return;
   dgc_compact_kernel<<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, thr, out_val, out_idx, cap, counter, vmask, umask);
 }

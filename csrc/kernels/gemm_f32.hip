@@ -49,9 +49,9 @@ namespace {
 
 constexpr int kGB = 256;  // threads per workgroup (4 waves)
 // k per LDS stage: 32 (4 x 8-k groups; BK = 16 with 4 workgroups per CU measured slower), or 64
-// for the 128x64 / 64x128 / 64x64 tiles (tiles 5-7): twice the MFMA work between two barriers, so
-// a small tile's next-slice global loads are hidden (a 64x64 tile's 32-k slice is ~1000 MFMA
-// cycles per wave, less than an HBM round trip)
+// for the 64x64 tile 7: twice the MFMA work between two barriers, so a small tile's next-slice
+// global loads are hidden (a 64x64 tile's 32-k slice is ~1000 MFMA cycles per wave, less than an
+// HBM round trip; profiles/r4_conv3x3_implicit_gemm_vs_miopen.txt second table)
 constexpr int BK = 32;
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -508,7 +508,7 @@ int launch_layout(GemmParams p, hipStream_t stream) {
 
 namespace {
 // tile: 0 = by the launcher's rule, 1 = 128x128, 2 = 128x64, 3 = 64x128, 4 = 64x64 (32-k slices);
-// 5 = 128x64, 6 = 64x128, 7 = 64x64 with 64-k slices
+// 7 = 64x64 with 64-k slices (5 / 6 = 2 / 3)
 template <int AM, int BMD>
 int launch_tile(GemmParams p, int tile, hipStream_t stream) {
   switch (tile) {
@@ -516,8 +516,10 @@ int launch_tile(GemmParams p, int tile, hipStream_t stream) {
     case 2: return launch_cfg<128, 64, AM, BMD>(p, stream);
     case 3: return launch_cfg<64, 128, AM, BMD>(p, stream);
     case 4: return launch_cfg<64, 64, AM, BMD>(p, stream);
-    case 5: return launch_cfg<128, 64, AM, BMD, 64>(p, stream);
-    case 6: return launch_cfg<64, 128, AM, BMD, 64>(p, stream);
+    // (the 128x64 / 64x128 64-k-slice tiles need ~100 KB of LDS -- one workgroup per CU -- and never
+    // won a ResNet-50 direction: 5 / 6 map to their 32-k-slice shapes)
+    case 5: return launch_cfg<128, 64, AM, BMD>(p, stream);
+    case 6: return launch_cfg<64, 128, AM, BMD>(p, stream);
     case 7: return launch_cfg<64, 64, AM, BMD, 64>(p, stream);
     default: return launch_layout<AM, BMD>(p, stream);
   }

@@ -158,8 +158,8 @@ void randk_scatter(const float* vals, int64_t rank_stride, int n_ranks, int n_se
 
 void threshold_compact(const float* g, const float* r, int mode, float beta, float gamma, int64_t n, float thr,
                        float* out_val, int32_t* out_idx, int64_t cap, int32_t* counter, float* resid,
-                       hipStream_t stream) {
-  GRACE_HIP_CHECK(hipMemsetAsync(counter, 0, sizeof(int32_t), stream));
+                       hipStream_t stream, int header_bytes) {
+  GRACE_HIP_CHECK(hipMemsetAsync(counter, 0, header_bytes, stream));
   if (n <= 0) return;
   int64_t tiles = (n + kTile - 1) / kTile;
   if (tiles > 2048) tiles = 2048;
