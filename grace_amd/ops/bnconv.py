@@ -230,8 +230,9 @@ def _conv3_only(blk, xm: torch.Tensor, idt: torch.Tensor):
             s2 = bn_fold(b2, p2, p2._grace_tiles, m2)
     if m2 is None:
         y2 = c2(y1)
-        if not (_cl(y2) and y2.dtype == torch.float32):
-            return bn_act(c3(bn_act(y2, b2, None, b2.relu)), b3, idt, b3.relu, True)
+        if not (_cl(y2) and y2.dtype == torch.float32):  # (MIOpen returned another layout: plain path)
+            a2 = bn_act(y2, b2, None, b2.relu)
+            return bn_act(c3(a2), b3, idt, b3.relu, True)
         s2 = bn_stats(b2, y2)
     y3, p3 = _BnActConvFn.apply(y2, b2.weight, b2.bias, s2, c3.weight, bool(b2.relu), 1, True)
     return bn_act(y3, b3, idt, b3.relu, True, partials=p3, tiles=p3._grace_tiles)
