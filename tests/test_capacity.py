@@ -109,3 +109,22 @@ def test_inceptionn_auto_capacity_payload_size():
     d, _ = grace_from_params({"compressor": "inceptionn", "communicator": "allgather"},
                              comm=LocalComm()).compress_step(torch.randn(n) * 0.01, "w")
     assert sum(t.numel() * t.element_size() for t in d) >= 4 * n
+
+
+def test_decode_ranks_cpu_path_rank_order_and_counts():
+    """ops/cappayload.py decode_ranks on the CPU path: the output is zeroed, payloads are added in
+    rank order (the sum order every rank reproduces), in-band counts bound each payload."""
+    from grace_amd.ops import cappayload as P
+
+    g = torch.Generator().manual_seed(4)
+    n = 1000
+    vals = [torch.randn(50, generator=g) for _ in range(3)]
+    idxs = [torch.randperm(120, generator=g)[:50].to(torch.int32) for _ in range(3)]  # overlapping
+    cnts = [None, torch.tensor([20, 50, 0, 0], dtype=torch.int32), torch.tensor([70, 50, 0, 0], dtype=torch.int32)]
+    out = torch.full((n,), 9.0)
+    P.decode_ranks(vals, idxs, cnts, out, 0.5)
+    ref = torch.zeros(n)
+    for v, i, k in zip(vals, idxs, (50, 20, 50)):  # rank 2's count 70 > capacity 50: the first 50
+        for j in range(k):
+            ref[int(i[j])] = ref[int(i[j])] + v[j] * 0.5
+    assert torch.equal(out, ref)
