@@ -12,9 +12,10 @@ MI355X kernels (csrc/kernels/topk.hip):
   x = beta*r + gamma*g happens in the first histogram pass and the new residual (x with the
   sent entries zeroed) is written by the compaction pass: the reference's second decompress
   (residual.py:17) disappears.
-* ``decompress_aggregate``: ONE launch zeroes the bucket and adds the W payloads in fixed rank
-  order behind grid barriers (ops/cappayload.py decode_ranks, csrc/kernels/sparse_decode.hip),
-  with the 1/W average folded in -> bitwise identical on every rank.
+* ``decompress_aggregate``: the W payloads added in fixed rank order into the zeroed bucket
+  (ops/cappayload.py decode_ranks: fill + atomic-free scatters, or one launch with grid barriers
+  under GRACE_DECODE_ONE_LAUNCH=1), with the 1/W average folded in -> bitwise identical on every
+  rank.
 """
 from __future__ import annotations
 

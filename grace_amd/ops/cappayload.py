@@ -58,12 +58,14 @@ def scatter_capped(hdr: torch.Tensor, vals: torch.Tensor, idx: torch.Tensor, out
 
 MAX_DECODE_RANKS = 32  # csrc/include/grace_kernels.h kDecodeMaxRanks
 _DECODE_CTR = {}
-# the one-launch decode (default): as fast as a zero fill + W scatter launches on a ResNet-50
-# bucket (23.6 / 32.3 / 50.0 / 85.4 us at W = 1 / 2 / 4 / 8 vs 23.5 / 32.3 / 50.0 / 85.5,
-# graph-replayed, bit-identical; profiles/r4_decode_bench.txt) with 1 launch instead of W + 1.
-# Its first form (plain zero stores, RMW through the L2s) paid an agent-scope write-back of the
-# freshly zeroed bucket at every grid barrier: 65-480 us.  GRACE_DECODE_ONE_LAUNCH=0: the loop.
-ONE_LAUNCH = __import__("os").environ.get("GRACE_DECODE_ONE_LAUNCH", "1") == "1"
+# the one-launch decode (csrc/kernels/sparse_decode.hip) is opt-in: stand-alone it is as fast as a
+# zero fill + W scatter launches on a ResNet-50 bucket (23.6 / 32.3 / 50.0 / 85.4 us at W = 1 / 2 /
+# 4 / 8 vs 23.5 / 32.3 / 50.0 / 85.5, graph-replayed, bit-identical; profiles/r4_decode_bench.txt),
+# but inside the whole-step graph its grid barriers wait on workgroups that share the chip with the
+# side-stream weight gradients still running: 51 us vs ~28 us for the fill + scatter
+# (profiles/r4_final_headline_graph_kernels.txt).  Its first form (plain zero stores, RMW through
+# the L2s) paid an agent-scope write-back of the zeroed bucket at every barrier: 65-480 us.
+ONE_LAUNCH = __import__("os").environ.get("GRACE_DECODE_ONE_LAUNCH", "0") == "1"
 
 
 def _decode_ctr(device) -> torch.Tensor:
@@ -80,9 +82,9 @@ def _decode_ctr(device) -> torch.Tensor:
 def decode_ranks(vals, idxs, counts, out: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
     """``out`` = 0, then ``out[idxs[r]] += vals[r] * scale`` for r = 0..W-1 in rank order --
     bit-identical on every rank.  ``counts[r]``: None (every entry) or the payload's in-band count
-    word (capacity payloads: the first min(count, capacity) entries).  Native path: ONE launch
-    (zero + W rank phases behind grid barriers, csrc/kernels/sparse_decode.hip);
-    ``GRACE_DECODE_ONE_LAUNCH=0``: a zero fill plus W scatter launches (same speed, see ONE_LAUNCH)."""
+    word (capacity payloads: the first min(count, capacity) entries).  Native path: a zero fill plus
+    W atomic-free scatter launches; ``GRACE_DECODE_ONE_LAUNCH=1``: ONE launch (zero + W rank phases
+    behind grid barriers, csrc/kernels/sparse_decode.hip) -- slower inside the step, see ONE_LAUNCH."""
     W = len(vals)
     if ONE_LAUNCH and _native.use_native(out) and 1 <= W <= MAX_DECODE_RANKS and out.is_contiguous():
         _native.lib().sparse_decode_ranks(list(vals), list(idxs), [None if c is None else c[:1] for c in counts],

@@ -147,7 +147,7 @@ def _w4_body(rank, world):
             return getattr(lib, name)
 
     _native._lib = Counting()
-    P.ONE_LAUNCH = True  # (the default; set explicitly: the fixture does not reach a spawned worker)
+    P.ONE_LAUNCH = True  # opt-in path under test (the fixture does not reach a spawned worker)
     try:
         for comp in ({"compressor": "topk", "compress_ratio": 0.05, "memory": "residual", "communicator": "allgather"},
                      {"compressor": "threshold", "threshold": 0.5, "memory": "residual", "communicator": "allgather"}):
