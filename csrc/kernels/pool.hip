@@ -105,16 +105,42 @@ __global__ __launch_bounds__(kPB) void maxpool_fwd_kernel(const T* __restrict__ 
   }
 }
 
-template <typename T>
+// q = m / d, r = m % d for m < 2^24 (a float multiply and one correction)
+__device__ __forceinline__ int fdiv(int m, int d, float inv, int* r) {
+  int q = (int)((float)m * inv);
+  int rr = m - q * d;
+  if (rr < 0) {
+    --q;
+    rr += d;
+  } else if (rr >= d) {
+    ++q;
+    rr -= d;
+  }
+  *r = rr;
+  return q;
+}
+
+// SMALL: n_vec < 2^24 -- the index decomposition in 32-bit float-reciprocal divmods instead of
+// four 64-bit integer divisions per element (the ResNet-50 stem's backward: 101 us -> see
+// profiles/r4_final_headline_graph_kernels.txt)
+template <typename T, bool SMALL>
 __global__ __launch_bounds__(kPB) void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ code,
                                                           T* __restrict__ dx, PoolGeom g, int64_t n_vec) {
   const int cv = g.C >> 3;
+  const float inv_cv = 1.f / (float)cv, inv_w = 1.f / (float)g.W, inv_h = 1.f / (float)g.H;
   for (int64_t i = (int64_t)blockIdx.x * kPB + threadIdx.x; i < n_vec; i += (int64_t)gridDim.x * kPB) {
-    const int c8 = (int)(i % cv);
-    const int64_t pix = i / cv;
-    const int w = (int)(pix % g.W);
-    const int h = (int)((pix / g.W) % g.H);
-    const int n = (int)(pix / ((int64_t)g.W * g.H));
+    int c8, w, h, n;
+    if constexpr (SMALL) {
+      const int pix = fdiv((int)i, cv, inv_cv, &c8);
+      const int q = fdiv(pix, g.W, inv_w, &w);
+      n = fdiv(q, g.H, inv_h, &h);
+    } else {
+      c8 = (int)(i % cv);
+      const int64_t pix = i / cv;
+      w = (int)(pix % g.W);
+      h = (int)((pix / g.W) % g.H);
+      n = (int)(pix / ((int64_t)g.W * g.H));
+    }
     float acc[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = 0.f;
@@ -198,12 +224,15 @@ void maxpool_backward(const void* dy, const uint8_t* code, bool fp32, int N, int
   const PoolGeom g{N, H, W, C, OH, OW, k, s, pad};
   const int64_t n_vec = (int64_t)N * H * W * (C / 8);
   if (n_vec == 0) return;
-  if (fp32)
-    hipLaunchKernelGGL(maxpool_bwd_kernel<float>, dim3(pool_grid(n_vec)), dim3(kPB), 0, stream,
-                       static_cast<const float*>(dy), code, static_cast<float*>(dx), g, n_vec);
-  else
-    hipLaunchKernelGGL(maxpool_bwd_kernel<uint16_t>, dim3(pool_grid(n_vec)), dim3(kPB), 0, stream,
-                       static_cast<const uint16_t*>(dy), code, static_cast<uint16_t*>(dx), g, n_vec);
+  const bool small = n_vec < (int64_t(1) << 24);
+#define GRACE_POOL_BWD(T, S)                                                                             \
+  hipLaunchKernelGGL((maxpool_bwd_kernel<T, S>), dim3(pool_grid(n_vec)), dim3(kPB), 0, stream,          \
+                     static_cast<const T*>(dy), code, static_cast<T*>(dx), g, n_vec)
+  if (fp32 && small) GRACE_POOL_BWD(float, true);
+  else if (fp32) GRACE_POOL_BWD(float, false);
+  else if (small) GRACE_POOL_BWD(uint16_t, true);
+  else GRACE_POOL_BWD(uint16_t, false);
+#undef GRACE_POOL_BWD
 }
 
 }  // namespace grace
