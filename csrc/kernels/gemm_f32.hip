@@ -48,10 +48,9 @@ namespace grace {
 namespace {
 
 constexpr int kGB = 256;  // threads per workgroup (4 waves)
-// k per LDS stage: 32 (4 x 8-k groups; BK = 16 with 4 workgroups per CU measured slower), or 64
-// for the 64x64 tile 7: twice the MFMA work between two barriers, so a small tile's next-slice
-// global loads are hidden (a 64x64 tile's 32-k slice is ~1000 MFMA cycles per wave, less than an
-// HBM round trip; profiles/r4_conv3x3_implicit_gemm_vs_miopen.txt second table)
+// k per LDS stage: 32 (4 x 8-k groups; BK = 16 with 4 workgroups per CU measured slower).  The
+// kernel is templated on it; 64-k slices (more MFMA work between barriers for small tiles,
+// profiles/r4_conv3x3_implicit_gemm_vs_miopen.txt second table) are not launched (see launch_tile)
 constexpr int BK = 32;
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -507,8 +506,7 @@ int launch_layout(GemmParams p, hipStream_t stream) {
 }  // namespace
 
 namespace {
-// tile: 0 = by the launcher's rule, 1 = 128x128, 2 = 128x64, 3 = 64x128, 4 = 64x64 (32-k slices);
-// 7 = 64x64 with 64-k slices (5 / 6 = 2 / 3)
+// tile: 0 = by the launcher's rule, 1 = 128x128, 2 = 128x64, 3 = 64x128, 4 = 64x64 (5-7 = 2-4)
 template <int AM, int BMD>
 int launch_tile(GemmParams p, int tile, hipStream_t stream) {
   switch (tile) {
@@ -516,11 +514,12 @@ int launch_tile(GemmParams p, int tile, hipStream_t stream) {
     case 2: return launch_cfg<128, 64, AM, BMD>(p, stream);
     case 3: return launch_cfg<64, 128, AM, BMD>(p, stream);
     case 4: return launch_cfg<64, 64, AM, BMD>(p, stream);
-    // (the 128x64 / 64x128 64-k-slice tiles need ~100 KB of LDS -- one workgroup per CU -- and never
-    // won a ResNet-50 direction: 5 / 6 map to their 32-k-slice shapes)
+    // 5-7: the 64-k-slice variants of 2-4.  Their LDS (70-104 KB of static shared memory) coincided
+    // with intermittent aborts inside forked HIP-graph captures on ROCm 7.2, and they won no
+    // direction in situ by more than 1 us (profiles/r4_autotune_decisions.txt): mapped to 2-4
     case 5: return launch_cfg<128, 64, AM, BMD>(p, stream);
     case 6: return launch_cfg<64, 128, AM, BMD>(p, stream);
-    case 7: return launch_cfg<64, 64, AM, BMD, 64>(p, stream);
+    case 7: return launch_cfg<64, 64, AM, BMD>(p, stream);
     default: return launch_layout<AM, BMD>(p, stream);
   }
 }
@@ -576,7 +575,7 @@ int gemm_f32(const float* A, bool a_kcontig, int64_t lda, const float* B, bool b
   p.ldb = ldb;
   p.ldc = ldc;
   if (splits == 0) splits = auto_splits(M, N, K, ldc);  // host-checked: split-K only with ldc == N
-  set_splits(p, splits, stats, stream, tile >= 5 ? 64 : BK);
+  set_splits(p, splits, stats, stream);
   if (a_kcontig && b_kcontig) return launch_tile<0, 0>(p, tile, stream);
   if (a_kcontig && !b_kcontig) return launch_tile<0, 1>(p, tile, stream);
   if (!a_kcontig && !b_kcontig) return launch_tile<1, 1>(p, tile, stream);
@@ -636,10 +635,8 @@ int conv3x3_f32(int dir, const float* act, const float* other, float* C, int N, 
   p.gInvWr = 1.f / (float)p.gWr;
   p.gInvHr = 1.f / (float)p.gHr;
   if (p.M <= 0 || p.N <= 0) return 0;
-  // 64-k slices need a slice never to straddle a tap: C (mode 2) / Cout (mode 4) % 64 == 0
-  if (tile >= 5 && ((dir != 2 && p.gC % 64 != 0) || (dir == 1 && p.kt % 64 != 0))) tile -= 3;
   if (splits == 0) splits = dir == 2 ? auto_splits(p.M, p.N, p.K, p.ldc) : 1;
-  set_splits(p, splits, (dir == 0 || p.bx != nullptr) ? stats : nullptr, stream, tile >= 5 ? 64 : BK);
+  set_splits(p, splits, (dir == 0 || p.bx != nullptr) ? stats : nullptr, stream);
   if (dir == 0) return launch_tile<2, 0>(p, tile, stream);
   if (dir == 1) return launch_tile<2, 4>(p, tile, stream);
   return launch_tile<1, 3>(p, tile, stream);

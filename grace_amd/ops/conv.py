@@ -49,8 +49,7 @@ def _splits(m: int, n: int, k: int) -> int:
 def gemm(a, a_kc, lda, b, b_kc, ldb, c, ldc, m, n, k, splits=1, tile=0):
     """C[m, n] = sum_k A(m, k) B(n, k) (see csrc/kernels/gemm_f32.hip); splits=0: split-K chosen by
     the launcher when the output has too few tiles to fill the chip (needs a dense C); tile:
-    0 = launcher's rule, 1 = 128x128, 2 = 128x64, 3 = 64x128, 4 = 64x64 (32-k slices), 7 = 64x64
-    with 64-k slices."""
+    0 = launcher's rule, 1 = 128x128, 2 = 128x64, 3 = 64x128, 4 = 64x64 (5-7: aliases of 2-4)."""
     _native.lib().gemm_f32(a, a_kc, lda, b, b_kc, ldb, c, ldc, m, n, k, splits, tile)
 
 
@@ -101,7 +100,7 @@ _AUTO = os.environ.get("GRACE_CONV_AUTO", "1") == "1"
 # (direction, M, Cin, Cout) -> backend name; and the measured times (ms) per backend
 _CHOICE = {}
 _TIMES = {}
-BACKENDS = ("miopen", "hipblaslt", "mfma", "mfma_t1", "mfma_t2", "mfma_t3", "mfma_t4", "mfma_t7")
+BACKENDS = ("miopen", "hipblaslt", "mfma", "mfma_t1", "mfma_t2", "mfma_t3", "mfma_t4")
 
 
 def set_enabled(on: bool) -> None:
@@ -323,7 +322,7 @@ class _Conv1x1StatsFn(torch.autograd.Function):
 
 
 def _tiles_m(m: int, tile: int) -> int:
-    return (m + 127) // 128 if tile in (1, 2, 5) else (m + 63) // 64
+    return (m + 127) // 128 if tile in (1, 2, 5) else (m + 63) // 64  # (5-7 alias 2-4)
 
 
 # (M, Cin, Cout, relu, residual) -> "unfused" | "stats_t<tile>" ; measured ms per candidate
@@ -381,7 +380,7 @@ def _pick_bn(conv, bn, x, residual, relu) -> str:
 
     times["unfused"] = _time(unfused)
     part = torch.empty(((m + 63) // 64) * 2 * cout, device=x.device)
-    for tile in (1, 2, 3, 4, 7):
+    for tile in (1, 2, 3, 4):
         def fused(tile=tile):
             y = torch.empty((nb, cout, ho, wo), device=x.device, memory_format=torch.channels_last)
             if k3:
@@ -463,7 +462,7 @@ def fast_ok(x: torch.Tensor, conv: nn.Conv2d, force: bool = False) -> bool:
 # its zero fills) against the implicit GEMM's tile shapes and keeps the fastest.
 _C3_CHOICE = {}
 _C3_TIMES = {}
-C3_BACKENDS = ("miopen", "mfma", "mfma_t1", "mfma_t2", "mfma_t3", "mfma_t4", "mfma_t7")
+C3_BACKENDS = ("miopen", "mfma", "mfma_t1", "mfma_t2", "mfma_t3", "mfma_t4")
 _C3_ON = os.environ.get("GRACE_CONV3X3", "1") == "1"
 
 

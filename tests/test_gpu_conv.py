@@ -50,7 +50,8 @@ def test_gemm_f32_layouts(a_kc, b_kc, m, n, k, splits):
 @pytest.mark.parametrize("m,n,k,splits", [(200, 132, 68, 1), (64, 256, 1000, 4), (333, 520, 96, 3),
                                           (1568, 512, 2048, 0)])
 def test_gemm_f32_64k_slices(tile, a_kc, b_kc, m, n, k, splits):
-    """Tiles 5-7 (64-k LDS slices): K not a multiple of 64, split-K, ragged edges."""
+    """Tile codes 5-7 (the 64-k-slice variants, now launched as tiles 2-4): K not a multiple of 64,
+    split-K, ragged edges."""
     g = torch.Generator().manual_seed(m * 3 + n + tile)
     if not a_kc and m % 4:
         m += 4 - m % 4
