@@ -379,6 +379,11 @@ def test_plain_ddp_resnet_grads_match_inline(nccl_group):
     ref = grads(False)
     got = grads(True)
     torch.cuda.synchronize()
-    for a, b in zip(got, ref):
+    names = [n for n, _ in base.named_parameters()]
+    bad = []
+    for n, a, b in zip(names, got, ref):
         tol = 1e-4 * float(b.abs().max()) + 1e-6
-        assert float((a - b).abs().max()) <= tol
+        err = float((a - b).abs().max())
+        if err > tol:
+            bad.append(f"{n}{tuple(a.shape)}: {err:.3g} > {tol:.3g}")
+    assert not bad, f"{len(bad)} of {len(names)} differ, deepest first: " + "; ".join(bad[::-1])
