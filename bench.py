@@ -402,6 +402,10 @@ def main():
         _chk()
     step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
     final_loss = float(loss.float().item())
+    loss_finite = final_loss == final_loss and abs(final_loss) != float("inf")
+    if not loss_finite:  # a diverged run's throughput is not a measurement of training
+        print(f"[rank {rank}] ERROR: final loss is {final_loss}: the timed steps trained a diverged model; "
+              f"the throughput below is NOT a valid {w.name} number", file=sys.stderr, flush=True)
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -515,7 +519,8 @@ def main():
             "noop_exchange_ms_per_step": None if noop_ms is None else round(noop_ms, 3),
             "exposed_exchange_ms_eager": round(float(ex.item()) * 1e3, 3),
             "host_issue_ms_per_step": round(issue_s / args.steps * 1e3, 3),
-            "final_loss": round(final_loss, 4),
+            "final_loss": round(final_loss, 4) if loss_finite else str(final_loss),
+            "loss_finite": loss_finite,
         }
         print(json.dumps(out), flush=True)
         if os.environ.get("GRACE_AUTOTUNE_REPORT", "0") == "1":  # the per-layer backend choices, to stderr

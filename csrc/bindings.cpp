@@ -152,7 +152,7 @@ void topk_ef(const Tensor& g, const Tensor& x, double beta, double gamma, int64_
 }
 
 void sparse_scatter_add_dev(const Tensor& val, const Tensor& idx, const Tensor& count, const Tensor& out,
-                            double scale, bool accumulate) {
+                            double scale, bool accumulate, bool count_overflow) {
   CHECK_F32(val);
   CHECK_I32(idx);
   CHECK_I32(count);
@@ -160,12 +160,13 @@ void sparse_scatter_add_dev(const Tensor& val, const Tensor& idx, const Tensor& 
   TORCH_CHECK(val.numel() == idx.numel() && count.numel() >= 1, "val/idx size mismatch");
   DevGuard guard(out.device());
   grace::sparse_scatter_add_dev(val.data_ptr<float>(), idx.data_ptr<int32_t>(), count.data_ptr<int32_t>(),
-                                val.numel(), out.data_ptr<float>(), (float)scale, accumulate, cur_stream());
+                                val.numel(), out.data_ptr<float>(), (float)scale, accumulate, cur_stream(),
+                                count_overflow);
 }
 
 void sparse_decode_ranks(const std::vector<Tensor>& vals, const std::vector<Tensor>& idxs,
                          const std::vector<c10::optional<Tensor>>& counts, const Tensor& out, double scale,
-                         const Tensor& ctr) {
+                         const Tensor& ctr, int64_t own) {
   const int W = (int)vals.size();
   TORCH_CHECK(W >= 1 && W <= grace::kDecodeMaxRanks, "sparse_decode_ranks: 1..", grace::kDecodeMaxRanks, " ranks");
   TORCH_CHECK((int)idxs.size() == W && (int)counts.size() == W, "sparse_decode_ranks: per-rank list sizes differ");
@@ -194,7 +195,8 @@ void sparse_decode_ranks(const std::vector<Tensor>& vals, const std::vector<Tens
   }
   DevGuard guard(out.device());
   grace::sparse_decode_ranks(W, v, ix, c, cap, out.data_ptr<float>(), out.numel(), (float)scale,
-                             ctr.data_ptr<int32_t>(), grace::health_dev(out.device().index()), cur_stream());
+                             ctr.data_ptr<int32_t>(), grace::health_dev(out.device().index()), cur_stream(),
+                             (int)own);
 }
 
 void sparse_scatter_add(const Tensor& val, const Tensor& idx, const Tensor& out, double scale,
@@ -1141,8 +1143,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("topk_compact", &topk_compact);
   m.def("topk_ef", &topk_ef);
   m.def("sparse_scatter_add", &sparse_scatter_add);
-  m.def("sparse_scatter_add_dev", &sparse_scatter_add_dev);
-  m.def("sparse_decode_ranks", &sparse_decode_ranks);
+  m.def("sparse_scatter_add_dev", &sparse_scatter_add_dev, py::arg("val"), py::arg("idx"), py::arg("count"),
+        py::arg("out"), py::arg("scale"), py::arg("accumulate"), py::arg("count_overflow") = false);
+  m.def("sparse_decode_ranks", &sparse_decode_ranks, py::arg("vals"), py::arg("idxs"), py::arg("counts"),
+        py::arg("out"), py::arg("scale"), py::arg("ctr"), py::arg("own") = (int64_t)-1);
   m.def("segment_stats", &segment_stats);
   m.def("randk_gather", &randk_gather);
   m.def("randk_scatter", &randk_scatter);

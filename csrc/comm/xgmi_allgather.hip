@@ -168,7 +168,7 @@ __device__ __forceinline__ int64_t range_vecs(const Ranges& R, int i, const char
 __global__ __launch_bounds__(kThreads) void xg_pull(const char* __restrict__ in, Ranges R, Peers peers, int rank,
                                                     int world, int direct, uint32_t spin_limit, int64_t span,
                                                     int64_t slot_bytes,
-                                                    char* __restrict__ out, Local* L, Fault F) {
+                                                    char* __restrict__ out, Local* L, Fault F, uint32_t fillw) {
   __shared__ int64_t nv[kMaxRanges];
   __shared__ int ok;
   __shared__ int64_t src_off;  // peer q's slot, as q published it
@@ -208,9 +208,10 @@ __global__ __launch_bounds__(kThreads) void xg_pull(const char* __restrict__ in,
       uint4* o4 = reinterpret_cast<uint4*>(o + R.off[i]);
       for (int64_t v = tid; v < nv[i]; v += stride) o4[v] = s4[v];
     }
-  } else {  // timed-out peer: its rows read as an empty payload, never as stale bytes
+  } else {  // timed-out peer: its rows read as an empty payload (fill 0) or as NaN (an all-reduce's
+            // rows: a zero would be a silently wrong sum), never as stale bytes
     uint4* o4 = reinterpret_cast<uint4*>(o);
-    for (int64_t v = tid; v < (span >> 4); v += stride) o4[v] = make_uint4(0u, 0u, 0u, 0u);
+    for (int64_t v = tid; v < (span >> 4); v += stride) o4[v] = make_uint4(fillw, fillw, fillw, fillw);
   }
   if (arrive_last(&L->arrive2, gridDim.x * gridDim.y)) {
     // every peer block of this launch has read its peer's slot: tell the peers, then wait until
@@ -292,7 +293,9 @@ class XgmiPeers {
   // out = [W, n] bytes, in = [n] bytes; n % 16 == 0 and n <= capacity (checked).  `ranges`
   // (int64 [k, 8]: off, nbytes, cnt_off, esz0..esz3, unused) describes the variable-length
   // parts (empty = the whole payload fixed).  Issued on the caller's current stream (capturable).
-  void all_gather(const Tensor& out, const Tensor& in, const Tensor& ranges) {
+  // `fill`: the 32-bit word written over a timed-out peer's rows (0: an empty payload for the
+  // Allgather decoders; 0xFFFFFFFF: NaN in fp32 / bf16 / fp16, for the gather-reduce all-reduce)
+  void all_gather(const Tensor& out, const Tensor& in, const Tensor& ranges, int64_t fill) {
     TORCH_CHECK(opened_ || world_ == 1, "xgmi all-gather: open() the peers first");
     TORCH_CHECK(in.is_cuda() && out.is_cuda() && in.is_contiguous() && out.is_contiguous(), "contiguous GPU tensors");
     TORCH_CHECK(in.get_device() == device_ && out.get_device() == device_, "tensor on the wrong device");
@@ -342,7 +345,7 @@ class XgmiPeers {
     Fault F{hw.host_dev, grace::health_dev(device_)};
     hipLaunchKernelGGL(xg_pull, dim3(b2, world_), dim3(kThreads), 0, s, static_cast<const char*>(in.data_ptr()), R,
                        peers_, rank_, world_, direct ? 1 : 0, spin_, n, cap_, static_cast<char*>(out.data_ptr()),
-                       local_, F);
+                       local_, F, (uint32_t)fill);
     XG_HIP(hipGetLastError());
   }
 
@@ -378,7 +381,8 @@ void bind(py::module& m) {
            py::arg("capacity"), py::arg("spin_limit") = (int64_t)1 << 25)
       .def("handle", &XgmiPeers::handle)
       .def("open", &XgmiPeers::open)
-      .def("all_gather", &XgmiPeers::all_gather)
+      .def("all_gather", &XgmiPeers::all_gather, py::arg("out"), py::arg("inp"), py::arg("ranges"),
+           py::arg("fill") = (int64_t)0)
       .def("slot_ptr", &XgmiPeers::slot_ptr)
       .def("slot_tensor", &XgmiPeers::slot_tensor)
       .def("close", &XgmiPeers::close)

@@ -63,7 +63,7 @@ __device__ __forceinline__ void grid_barrier(int32_t* ctr, int32_t target, uint3
 
 __global__ __launch_bounds__(kDB) void sparse_decode_kernel(DecodeArgs a, int W, float* __restrict__ out, int64_t n,
                                                            float scale, int32_t* ctr, uint32_t* health_host,
-                                                           uint32_t* health_dev) {
+                                                           uint32_t* health_dev, int own) {
   const int G = gridDim.x;
   const int64_t tid = (int64_t)blockIdx.x * kDB + threadIdx.x, stride = (int64_t)G * kDB;
   // phase 0: zero (head to the first 16-B boundary, float4 body, tail).  Every store of `out`
@@ -94,7 +94,8 @@ __global__ __launch_bounds__(kDB) void sparse_decode_kernel(DecodeArgs a, int W,
     int64_t K = a.cap[r];
     if (a.count[r] != nullptr) {
       const int64_t c = a.count[r][0];
-      if (c > K && blockIdx.x == 0 && threadIdx.x == 0) health_count_overflow(health_host);
+      // counted once per process: for its OWN payload (every rank decodes every payload)
+      if (r == own && c > K && blockIdx.x == 0 && threadIdx.x == 0) health_count_overflow(health_host);
       K = c < K ? c : K;
     }
     const float* __restrict__ val = a.val[r];
@@ -136,7 +137,7 @@ int decode_grid(int64_t n, int64_t kmax) {
 
 void sparse_decode_ranks(int W, const float* const* val, const int32_t* const* idx, const int32_t* const* count,
                          const int64_t* cap, float* out, int64_t n, float scale, int32_t* ctr,
-                         uint32_t* health_dev, hipStream_t stream) {
+                         uint32_t* health_dev, hipStream_t stream, int own) {
   DecodeArgs a{};
   int64_t kmax = 0;
   for (int r = 0; r < W; ++r) {
@@ -147,7 +148,7 @@ void sparse_decode_ranks(int W, const float* const* val, const int32_t* const* i
     kmax = std::max<int64_t>(kmax, cap[r]);
   }
   const int G = decode_grid(n, kmax);
-  sparse_decode_kernel<<<G, kDB, 0, stream>>>(a, W, out, n, scale, ctr, health_words().host_dev, health_dev);
+  sparse_decode_kernel<<<G, kDB, 0, stream>>>(a, W, out, n, scale, ctr, health_words().host_dev, health_dev, own);
 }
 
 }  // namespace grace

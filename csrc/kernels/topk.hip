@@ -608,7 +608,9 @@ __global__ __launch_bounds__(kBlock) void sparse_scatter_add_dev_kernel(const fl
                                                                         uint32_t* health) {
   const int64_t c = *count;
   const int64_t K = c < cap ? c : cap;
-  if (c > cap && blockIdx.x == 0 && threadIdx.x == 0) health_count_overflow(health);
+  // health == null: not this process's own payload (a peer's, or a memory's zeroing scatter) --
+  // an overflow is counted once, by the decode of the sender's own payload
+  if (health != nullptr && c > cap && blockIdx.x == 0 && threadIdx.x == 0) health_count_overflow(health);
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < K; j += stride) {
     const int32_t t = idx[j];
@@ -667,12 +669,13 @@ void sparse_scatter_add(const float* val, const int32_t* idx, int64_t K, float* 
 }
 
 void sparse_scatter_add_dev(const float* val, const int32_t* idx, const int32_t* count, int64_t cap, float* out,
-                            float scale, bool accumulate, hipStream_t stream) {
+                            float scale, bool accumulate, hipStream_t stream, bool count_overflow) {
   if (cap <= 0) return;
   int64_t blocks = (cap + kBlock - 1) / kBlock;
   if (blocks > 2048) blocks = 2048;
   sparse_scatter_add_dev_kernel<<<(int)blocks, kBlock, 0, stream>>>(val, idx, count, cap, out, scale,
-                                                                    accumulate ? 1 : 0, health_words().host_dev);
+                                                                    accumulate ? 1 : 0,
+                                                                    count_overflow ? health_words().host_dev : nullptr);
 }
 
 }  // namespace grace

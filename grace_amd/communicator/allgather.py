@@ -67,10 +67,12 @@ def allgather_send(comm, compressor, tensors, world_size):
     return (out, buf.numel(), rank_specs, work, buf)
 
 
-def allgather_recv(handles, compressor, ctx, world_size):
+def allgather_recv(handles, compressor, ctx, world_size, rank=None):
     out, span, rank_specs, work, _keep = handles
     if work is not None:
         work.wait()
+    if rank is not None and isinstance(getattr(ctx, "extra", None), dict):
+        ctx.extra["own_rank"] = int(rank)  # the decoders count only this process's payload overflow
     per_rank = [unpack(out[r * span:(r + 1) * span], rank_specs[r]) for r in range(world_size)]
     return compressor.decompress_aggregate(per_rank, ctx, world_size)
 
@@ -84,4 +86,4 @@ class Allgather(Communicator):
             handles[3].wait()
 
     def wait_receive(self, handles, ctx):
-        return allgather_recv(handles, self.compressor, ctx, self.world_size)
+        return allgather_recv(handles, self.compressor, ctx, self.world_size, getattr(self.comm, "rank", None))

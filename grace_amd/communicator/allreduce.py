@@ -73,7 +73,7 @@ class Allreduce(Communicator):
     def wait_receive(self, handles, ctx):
         kind, handles = handles
         if kind == "ag":
-            return allgather_recv(handles, self.compressor, ctx, self.world_size)
+            return allgather_recv(handles, self.compressor, ctx, self.world_size, getattr(self.comm, "rank", None))
         if kind == "rs":
             return self.compressor.rs_receive(self.comm, handles, ctx, self.world_size)
         tensors, works = handles

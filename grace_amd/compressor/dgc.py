@@ -72,7 +72,8 @@ class DgcCompressor(BucketCompressor):
     def decompress_aggregate_impl(self, per_rank, ctx, n_ranks, scale):
         out = self.out_buffer(ctx, per_rank[0][1].device)
         # zero + the W payloads in rank order: identical on every rank
-        P.decode_ranks([p[1] for p in per_rank], [p[2] for p in per_rank], [p[0] for p in per_rank], out, scale)
+        P.decode_ranks([p[1] for p in per_rank], [p[2] for p in per_rank], [p[0] for p in per_rank], out, scale,
+                       own=P.own_rank(ctx))
         return self.finish(out, ctx)
 
 

@@ -115,5 +115,6 @@ class ThresholdCompressor(Compressor):
         out = torch.empty(ctx.numel, dtype=torch.float32, device=per_rank[0][1].device)
         scale = 1.0 / world_size if self.average else 1.0
         # zero + the W payloads in fixed rank order: identical result on every rank
-        P.decode_ranks([p[1] for p in per_rank], [p[2] for p in per_rank], [p[0] for p in per_rank], out, scale)
+        P.decode_ranks([p[1] for p in per_rank], [p[2] for p in per_rank], [p[0] for p in per_rank], out, scale,
+                       own=P.own_rank(ctx))
         return out.view(ctx.shape).to(ctx.dtype)

@@ -42,11 +42,13 @@ def sparse_payload(device, cap: int) -> Tuple[torch.Tensor, torch.Tensor, torch.
 
 
 def scatter_capped(hdr: torch.Tensor, vals: torch.Tensor, idx: torch.Tensor, out: torch.Tensor,
-                   scale: float = 1.0, accumulate: bool = True) -> None:
+                   scale: float = 1.0, accumulate: bool = True, count_overflow: bool = False) -> None:
     """out[idx[j]] (+)= vals[j] * scale for j < min(hdr[0], capacity) -- the count is read on the
-    device on the native path (no host sync)."""
+    device on the native path (no host sync).  ``count_overflow``: this is the decode of the
+    process's OWN payload, so an overflow (hdr[0] > capacity) is counted in health.overflows() --
+    once per overflowing payload, not once per rank that decodes it."""
     if _native.use_native(out):
-        _native.lib().sparse_scatter_add_dev(vals, idx, hdr[:1], out, scale, accumulate)
+        _native.lib().sparse_scatter_add_dev(vals, idx, hdr[:1], out, scale, accumulate, count_overflow)
         return
     k = min(int(hdr[0]), vals.numel())
     il = idx[:k].long()
@@ -79,22 +81,30 @@ def _decode_ctr(device) -> torch.Tensor:
     return c
 
 
-def decode_ranks(vals, idxs, counts, out: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
+def own_rank(ctx):
+    """The decoding process's rank, as the communicator recorded it in ``ctx.extra`` (None: unknown,
+    then no overflow is counted by the decode)."""
+    extra = getattr(ctx, "extra", None)
+    return extra.get("own_rank") if isinstance(extra, dict) else None
+
+
+def decode_ranks(vals, idxs, counts, out: torch.Tensor, scale: float = 1.0, own=None) -> torch.Tensor:
     """``out`` = 0, then ``out[idxs[r]] += vals[r] * scale`` for r = 0..W-1 in rank order --
     bit-identical on every rank.  ``counts[r]``: None (every entry) or the payload's in-band count
     word (capacity payloads: the first min(count, capacity) entries).  Native path: a zero fill plus
     W atomic-free scatter launches; ``GRACE_DECODE_ONE_LAUNCH=1``: ONE launch (zero + W rank phases
-    behind grid barriers, csrc/kernels/sparse_decode.hip) -- slower inside the step, see ONE_LAUNCH."""
+    behind grid barriers, csrc/kernels/sparse_decode.hip) -- slower inside the step, see ONE_LAUNCH.
+    ``own``: this process's rank -- only that payload's overflow is counted (health.overflows())."""
     W = len(vals)
     if ONE_LAUNCH and _native.use_native(out) and 1 <= W <= MAX_DECODE_RANKS and out.is_contiguous():
         _native.lib().sparse_decode_ranks(list(vals), list(idxs), [None if c is None else c[:1] for c in counts],
-                                          out, float(scale), _decode_ctr(out.device))
+                                          out, float(scale), _decode_ctr(out.device), -1 if own is None else int(own))
         return out
     out.zero_()
     native = _native.use_native(out)
-    for v, i, c in zip(vals, idxs, counts):  # fixed rank order: identical on every rank
+    for r, (v, i, c) in enumerate(zip(vals, idxs, counts)):  # fixed rank order: identical on every rank
         if c is not None:
-            scatter_capped(c, v, i, out, scale, accumulate=True)
+            scatter_capped(c, v, i, out, scale, accumulate=True, count_overflow=(r == own))
         elif native:
             _native.lib().sparse_scatter_add(v, i, out, scale, True)
         else:

@@ -24,9 +24,10 @@ csrc/comm/xgmi_allgather.hip has the protocol).  The reference gathers through H
 * construction exchanges HIP IPC handles through the torch.distributed Store and, by default,
   verifies gathers against ``inner`` (every rank must agree, else it raises and the caller
   keeps ``inner``);
-* a peer wait that exceeds the spin limit zero-fills that peer's rows, raises the process-wide
-  fault flag (FusedSGD skips the update; parallel/health.py) and ``check()`` raises -- the
-  device never hangs and no stale bytes reach the weights.
+* a peer wait that exceeds the spin limit fills that peer's rows (zeros = an empty payload for a
+  gather, NaN for the gather-reduce all-reduce), raises the process-wide fault flag (FusedSGD
+  skips the update; parallel/health.py) and ``check()`` raises -- the device never hangs and no
+  stale bytes reach the weights.
 """
 from __future__ import annotations
 
@@ -204,7 +205,7 @@ class XgmiComm(_comm.Comm):
             return self.inner.all_gather_into(out, inp, async_op)
         return self._one_shot(out, inp, ranges)
 
-    def _one_shot(self, out, inp, ranges):
+    def _one_shot(self, out, inp, ranges, fill: int = 0):
         o, i = out, inp
         if not self._aligned(i):  # staged, not a different path: every rank stays on the one-shot
             i = torch.empty(inp.numel() * inp.element_size(), dtype=torch.uint8, device=inp.device)
@@ -213,7 +214,7 @@ class XgmiComm(_comm.Comm):
             o = torch.empty(out.numel() * out.element_size(), dtype=torch.uint8, device=out.device)
         rg = ranges if ranges is not None else _EMPTY_RANGES
         # stream-ordered on the current stream: complete for every later op on it
-        self._x.all_gather(o.reshape(-1).view(torch.uint8), i.reshape(-1).view(torch.uint8), rg)
+        self._x.all_gather(o.reshape(-1).view(torch.uint8), i.reshape(-1).view(torch.uint8), rg, fill)
         if o is not out:
             out.reshape(-1).view(torch.uint8).copy_(o)
         self.one_shot_calls += 1
@@ -243,7 +244,9 @@ class XgmiComm(_comm.Comm):
 
     def _gather_reduce(self, t, op):
         rows = torch.empty((self.world_size, t.numel()), dtype=t.dtype, device=t.device)
-        self._one_shot(rows.view(-1), t.reshape(-1), None)
+        # a timed-out peer's rows come back as NaN (not zeros): the reduced value is visibly
+        # wrong for ANY consumer, not only for FusedSGD's fault-word check
+        self._one_shot(rows.view(-1), t.reshape(-1), None, fill=0xFFFFFFFF)
         if op == "sum":
             torch.sum(rows, 0, out=t.view(-1))
         elif op == "max":
@@ -318,7 +321,9 @@ class XgmiComm(_comm.Comm):
                 inp.copy_(pat)
             got = torch.empty(self.world_size * n, dtype=torch.int32, device=dev)
             ref = torch.empty_like(got)
-            self.all_gather_into(got, inp)
+            # the one-shot path itself, whatever a probe would pick for this size: the
+            # self-check must never compare the inner comm against itself
+            self._one_shot(got, inp, None)
             self.inner.all_gather_into(ref, pat).wait()
             torch.cuda.synchronize(dev)
             ok &= int(torch.equal(got, ref)) & int(_health.status()[1] == 0)

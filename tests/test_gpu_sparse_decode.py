@@ -87,12 +87,18 @@ def test_decode_counts_unaligned_and_overflow():
     W, n, k = 5, 123_457, 4000
     vals, idxs, cnts = _payloads(W, n, k, seed=11, counts=True)
     health.init()
-    before = health.overflows()
+    over = [int(c[0]) > k for c in cnts]
+    assert any(over) and not all(over)
+    # counted exactly once per overflowing payload: only the decoding process's OWN payload
+    # (every rank decodes every payload, so counting each would inflate W-fold)
+    for own in [None] + list(range(W)):
+        before = health.overflows()
+        P.decode_ranks(_gpu(vals), _gpu(idxs), _gpu(cnts), torch.empty(n, device="cuda"), 0.5, own=own)
+        torch.cuda.synchronize()
+        assert health.overflows() == before + (0 if own is None else int(over[own])), own
     big = torch.full((n + 3,), -1.0, device="cuda")
     out = big[1:n + 1]  # 4-B aligned, not 16-B aligned
     P.decode_ranks(_gpu(vals), _gpu(idxs), _gpu(cnts), out, 0.5)
-    torch.cuda.synchronize()
-    assert health.overflows() == before + sum(int(c[0]) > k for c in cnts)
     assert torch.equal(out, _loop(vals, idxs, cnts, n, 0.5))
     assert big[0].item() == -1.0 and big[n + 1].item() == -1.0 and big[n + 2].item() == -1.0
     assert health.status()[0] == 0  # every barrier completed

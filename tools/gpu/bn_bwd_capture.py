@@ -155,7 +155,7 @@ def main():
     g = torch.Generator().manual_seed(7)
     x = torch.randn(8, 3, 16, 16, generator=g)
     y = torch.randint(0, 10, (8,), generator=g)
-    _, ref_g, _ = D.run(copy.deepcopy(base).double(), x.double(), y, torch.device("cpu"), False, False)
+    _, ref_g, ref_m = D.run(copy.deepcopy(base).double(), x.double(), y, torch.device("cpu"), False, False)
     for mode in args.modes.split(","):
         log.clear()
         proxy.kept.clear()
@@ -188,6 +188,11 @@ def main():
                 # the mask the forward should have written: y > 0
                 yr = f["y"].permute(0, 2, 3, 1).reshape(-1, SHAPE[1]).cpu() > 0
                 r["fwd_mask_matches_y"] = bool(torch.equal(unpack_mask(f["mask"].cpu(), *yr.shape), yr))
+            # which layer / is the kernel's dbias what ends up in .grad / were its input gradients right
+            r["db_vs_grad"] = {n: D.rel(b["db"].double().cpu(), gr[n]) for n in ("layer3.0.bn2.bias", "layer3.1.bn2.bias")}
+            r["db_vs_fp64"] = {n: D.rel(b["db"].double().cpu(), ref_g[n]) for n in ("layer3.0.bn2.bias", "layer3.1.bn2.bias")}
+            dsum = (b["dy"].double() + b["dy2"].double()).cpu()
+            r["dy_sum_vs_fp64"] = {k: D.rel(dsum, ref_m[k]) for k in ("layer3.0[full]", "layer3.1[full]") if k in ref_m}
             rep[f"bwd{i}"] = r
         print(json.dumps(rep), flush=True)
     dist.destroy_process_group()
