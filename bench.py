@@ -96,6 +96,11 @@ def parse():
                          "under a whole-step graph without overlap (measured 0.44 ms/step less than torch "
                          "for ResNet-50 Top-K), torch otherwise; xgmi = native-inline plus the one-shot "
                          "peer-memory all-gather for payloads <= 8 MB (parallel/xgmi.py, self-checked at start)")
+    ap.add_argument("--rccl-ctas", default="auto",
+                    help="workgroup (channel) budget of the native RCCL communicator, ncclConfig_t minCTAs/maxCTAs: "
+                         "auto = at W > 1 for a dense all-reduce pipeline (None / FP16 + Allreduce) probe "
+                         "RcclComm.CTA_CANDIDATES on the real bucket size and keep the fastest (MAX over ranks); "
+                         "off = RCCL's default; 'MIN/MAX' = fixed")
     ap.add_argument("--xgmi-capacity-mb", type=float, default=8.0,
                     help="per-rank payload capacity of the xGMI one-shot comm (two slots of this size are exported "
                          "per rank); collectives above it go to RCCL / the inner comm")
@@ -235,6 +240,7 @@ def main():
     overlap = args.overlap == "on" or (args.overlap == "auto" and mode != "full")
     comm_kind = "local"
     comm_obj = None
+    rccl_obj = None
     if dist.is_initialized():
         comm_kind = args.comm
         if comm_kind == "auto":
@@ -256,8 +262,20 @@ def main():
 
                     native = TorchComm()
                 else:
-                    native = RcclComm.from_process_group(
-                        inline=comm_kind in ("native-inline", "xgmi", "auto-probe"))
+                    inl = comm_kind in ("native-inline", "xgmi", "auto-probe")
+                    dense_ar = (w.grace.get("communicator") == "allreduce"
+                                and w.grace.get("compressor") in ("none", "fp16"))
+                    if args.rccl_ctas == "auto" and world > 1 and dense_ar:
+                        # the dense all-reduce's channel budget for the 7-link mesh, measured on the
+                        # real bucket: one ring drives one outbound link per GPU
+                        esz = 2 if w.grace.get("compressor") == "fp16" else 4
+                        nbytes = min(sum(p.numel() for p in model.parameters()) * esz, int(args.bucket_mb * 2 ** 20))
+                        native = RcclComm.tuned(nbytes, inline=inl)
+                    else:
+                        ctas = (0, 0) if args.rccl_ctas in ("auto", "off") else \
+                            tuple(int(v) for v in args.rccl_ctas.split("/"))
+                        native = RcclComm.from_process_group(inline=inl, ctas=ctas)
+                    rccl_obj = native
                 if comm_kind in ("xgmi", "auto-probe"):
                     from grace_amd.parallel.xgmi import XgmiComm
 
@@ -510,6 +528,8 @@ def main():
                                    {"note": "W=1 without a process group: 'comm' is a local device copy, "
                                             "not a collective"})),
             "comm_choice": (list(getattr(comm_obj, "choices", {}).values()) or None) if comm_obj is not None else None,
+            "rccl_ctas": (getattr(rccl_obj, "choice", None) or {"ctas": list(getattr(rccl_obj, "ctas", (0, 0)))})
+            if rccl_obj is not None else None,
             "bn_backward": ("fixed-order fp64 tree (deterministic)" if os.environ.get("GRACE_BN_DETERMINISTIC") == "1"
                             else "atomic fp32 totals (run-to-run order noise ~1e-7 rel.; GRACE_BN_DETERMINISTIC=1 "
                                  "for bitwise reproducibility)"),

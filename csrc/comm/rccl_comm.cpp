@@ -128,13 +128,25 @@ py::bytes unique_id() {
 
 class RcclComm {
  public:
-  RcclComm(int rank, int world, const std::string& id_bytes, int device, bool high_priority)
-      : rank_(rank), world_(world), device_(device) {
+  // min_ctas / max_ctas > 0: the communicator's workgroup (channel) budget through ncclConfig_t --
+  // one ring drives one outbound xGMI link per GPU, so a dense all-reduce over the 7-link mesh
+  // needs several channels; the Python side probes candidates on the real bucket size
+  // (parallel/native_comm.py RcclComm.tuned).  0 / 0 = RCCL's own choice (ncclCommInitRank).
+  RcclComm(int rank, int world, const std::string& id_bytes, int device, bool high_priority, int min_ctas,
+           int max_ctas)
+      : rank_(rank), world_(world), device_(device), min_ctas_(min_ctas), max_ctas_(max_ctas) {
     if ((int)id_bytes.size() != NCCL_UNIQUE_ID_BYTES) throw std::runtime_error("bad unique id size");
     HIP_OK(hipSetDevice(device));
     ncclUniqueId id;
     std::memcpy(id.internal, id_bytes.data(), NCCL_UNIQUE_ID_BYTES);
-    RCCL_CHECK(ncclCommInitRank(&comm_, world, id, rank));
+    if (min_ctas > 0 || max_ctas > 0) {
+      ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+      if (min_ctas > 0) cfg.minCTAs = min_ctas;
+      if (max_ctas > 0) cfg.maxCTAs = max_ctas;
+      RCCL_CHECK(ncclCommInitRankConfig(&comm_, world, id, rank, &cfg));
+    } else {
+      RCCL_CHECK(ncclCommInitRank(&comm_, world, id, rank));
+    }
     int lo = 0, hi = 0;
     HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
     HIP_OK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, high_priority ? hi : lo));
@@ -151,6 +163,8 @@ class RcclComm {
   }
 
   int rank() const { return rank_; }
+  int min_ctas() const { return min_ctas_; }
+  int max_ctas() const { return max_ctas_; }
   int world_size() const { return world_; }
   uintptr_t stream_ptr() const { return reinterpret_cast<uintptr_t>(stream_); }
 
@@ -331,6 +345,7 @@ class RcclComm {
 
  private:
   int rank_, world_, device_;
+  int min_ctas_ = 0, max_ctas_ = 0;
   ncclComm_t comm_ = nullptr;
   hipStream_t stream_ = nullptr;
   std::atomic<bool> inline_{false};
@@ -347,8 +362,11 @@ void bind(py::module& m) {
       .def("is_completed", &Work::is_completed)
       .def("synchronize", &Work::synchronize);
   py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
-      .def(py::init<int, int, const std::string&, int, bool>(), py::arg("rank"), py::arg("world"),
-           py::arg("unique_id"), py::arg("device"), py::arg("high_priority") = true)
+      .def(py::init<int, int, const std::string&, int, bool, int, int>(), py::arg("rank"), py::arg("world"),
+           py::arg("unique_id"), py::arg("device"), py::arg("high_priority") = true, py::arg("min_ctas") = 0,
+           py::arg("max_ctas") = 0)
+      .def_property_readonly("min_ctas", &RcclComm::min_ctas)
+      .def_property_readonly("max_ctas", &RcclComm::max_ctas)
       .def_property_readonly("rank", &RcclComm::rank)
       .def_property_readonly("world_size", &RcclComm::world_size)
       .def_property_readonly("stream_ptr", &RcclComm::stream_ptr)

@@ -165,9 +165,12 @@ __device__ __forceinline__ int64_t range_vecs(const Ranges& R, int i, const char
   return b < mx ? b : mx;
 }
 
+// span: bytes per peer row of `out`; src_shift: byte offset of the pulled part inside every
+// payload (0 for the all-gather; rank * chunk for the all-to-all: each rank pulls ITS chunk of
+// every peer's payload -- one hop per pair, over that pair's own link)
 __global__ __launch_bounds__(kThreads) void xg_pull(const char* __restrict__ in, Ranges R, Peers peers, int rank,
                                                     int world, int direct, uint32_t spin_limit, int64_t span,
-                                                    int64_t slot_bytes,
+                                                    int64_t src_shift, int64_t slot_bytes,
                                                     char* __restrict__ out, Local* L, Fault F, uint32_t fillw) {
   __shared__ int64_t nv[kMaxRanges];
   __shared__ int ok;
@@ -195,11 +198,12 @@ __global__ __launch_bounds__(kThreads) void xg_pull(const char* __restrict__ in,
     }
     src_off = (q != rank && ld_sys(reinterpret_cast<const uint32_t*>(peers.base[q]) + kReadySlotWord) != 0u)
                   ? slot_bytes : 0;
-    const char* s = q == rank ? in : peers.base[q] + kCtrlBytes + src_off;
+    const char* s = (q == rank ? in : peers.base[q] + kCtrlBytes + src_off) + src_shift;
     for (int i = 0; i < R.n; ++i) nv[i] = ok ? range_vecs(R, i, s) : 0;
   }
   __syncthreads();
   if (q != rank) src = peers.base[q] + kCtrlBytes + src_off;
+  src += src_shift;
   char* o = out + (int64_t)q * span;
   const int64_t tid = (int64_t)blockIdx.x * kThreads + threadIdx.x, stride = (int64_t)gridDim.x * kThreads;
   if (ok) {
@@ -344,8 +348,46 @@ class XgmiPeers {
     const auto& hw = grace::health_words();
     Fault F{hw.host_dev, grace::health_dev(device_)};
     hipLaunchKernelGGL(xg_pull, dim3(b2, world_), dim3(kThreads), 0, s, static_cast<const char*>(in.data_ptr()), R,
-                       peers_, rank_, world_, direct ? 1 : 0, spin_, n, cap_, static_cast<char*>(out.data_ptr()),
-                       local_, F, (uint32_t)fill);
+                       peers_, rank_, world_, direct ? 1 : 0, spin_, n, (int64_t)0, cap_,
+                       static_cast<char*>(out.data_ptr()), local_, F, (uint32_t)fill);
+    XG_HIP(hipGetLastError());
+  }
+
+  // out[p] = chunk `rank` of rank p's in (chunk = n / W), the all-to-all of the QSGD compressed-
+  // domain reduce-scatter: the payload is staged / published exactly like an all-gather's and
+  // every rank pulls only its own chunk of each peer's -- (W-1)/W of n over W-1 links at once.
+  // out and in: n bytes each, n % (16 W) == 0, n <= capacity.  A timed-out peer's chunk is NaN-
+  // filled (0xFF words: the int8 codes then decode as -1 levels, so the fault word is what marks
+  // the step; FusedSGD skips it).
+  void all_to_all(const Tensor& out, const Tensor& in) {
+    TORCH_CHECK(opened_ || world_ == 1, "xgmi all-to-all: open() the peers first");
+    TORCH_CHECK(in.is_cuda() && out.is_cuda() && in.is_contiguous() && out.is_contiguous(), "contiguous GPU tensors");
+    TORCH_CHECK(in.get_device() == device_ && out.get_device() == device_, "tensor on the wrong device");
+    const int64_t n = in.numel() * in.element_size();
+    TORCH_CHECK(out.numel() * out.element_size() == n, "all_to_all: out and in must be the same size");
+    TORCH_CHECK(n % (16 * world_) == 0 && n <= cap_, "xgmi all-to-all: 16-B granular chunks, <= capacity");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(in.data_ptr()) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0, "16-B aligned buffers");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(in.data_ptr()) != slot_ptr(), "all_to_all: stage from a tensor, not slot D");
+    if (n == 0) return;
+    const int64_t chunk = n / world_;
+    Ranges R{};
+    R.n = 1;
+    R.off[0] = 0;
+    R.nbytes[0] = chunk;
+    R.cnt_off[0] = -1;
+    c10::hip::HIPGuardMasqueradingAsCUDA guard(device_);
+    hipStream_t s = current_stream();
+    const int64_t per_blk = (int64_t)kThreads * 8;
+    int b1 = (int)std::min<int64_t>(std::max<int64_t>((n / 16 + per_blk - 1) / per_blk, 1), 256);
+    hipLaunchKernelGGL(xg_stage, dim3(b1), dim3(kThreads), 0, s, static_cast<const uint4*>(in.data_ptr()), n / 16,
+                       mine_, cap_, local_);
+    int b2 = (int)std::min<int64_t>(std::max<int64_t>((chunk / 16 + per_blk - 1) / per_blk, 1), 64);
+    const auto& hw = grace::health_words();
+    Fault F{hw.host_dev, grace::health_dev(device_)};
+    hipLaunchKernelGGL(xg_pull, dim3(b2, world_), dim3(kThreads), 0, s, static_cast<const char*>(in.data_ptr()), R,
+                       peers_, rank_, world_, 0, spin_, chunk, (int64_t)rank_ * chunk, cap_,
+                       static_cast<char*>(out.data_ptr()), local_, F, 0xFFFFFFFFu);
     XG_HIP(hipGetLastError());
   }
 
@@ -383,6 +425,7 @@ void bind(py::module& m) {
       .def("open", &XgmiPeers::open)
       .def("all_gather", &XgmiPeers::all_gather, py::arg("out"), py::arg("inp"), py::arg("ranges"),
            py::arg("fill") = (int64_t)0)
+      .def("all_to_all", &XgmiPeers::all_to_all, py::arg("out"), py::arg("inp"))
       .def("slot_ptr", &XgmiPeers::slot_ptr)
       .def("slot_tensor", &XgmiPeers::slot_tensor)
       .def("close", &XgmiPeers::close)

@@ -71,8 +71,9 @@ def allgather_recv(handles, compressor, ctx, world_size, rank=None):
     out, span, rank_specs, work, _keep = handles
     if work is not None:
         work.wait()
-    if rank is not None and isinstance(getattr(ctx, "extra", None), dict):
-        ctx.extra["own_rank"] = int(rank)  # the decoders count only this process's payload overflow
+    from ..ops.cappayload import set_own_rank
+
+    set_own_rank(ctx, rank)  # the decoders count only this process's payload overflow
     per_rank = [unpack(out[r * span:(r + 1) * span], rank_specs[r]) for r in range(world_size)]
     return compressor.decompress_aggregate(per_rank, ctx, world_size)
 

@@ -67,6 +67,7 @@ class Broadcast(Communicator):
             if w is not None:
                 w.wait()
         per_rank = [unpack(b, s) for b, s in zip(bufs, rank_specs)]
-        if isinstance(getattr(ctx, "extra", None), dict) and getattr(self.comm, "rank", None) is not None:
-            ctx.extra["own_rank"] = int(self.comm.rank)  # overflow counted for the own payload only
+        from ..ops.cappayload import set_own_rank
+
+        set_own_rank(ctx, getattr(self.comm, "rank", None))  # overflow counted for the own payload only
         return self.compressor.decompress_aggregate(per_rank, ctx, self.world_size)

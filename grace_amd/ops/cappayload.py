@@ -81,11 +81,21 @@ def _decode_ctr(device) -> torch.Tensor:
     return c
 
 
+def set_own_rank(ctx, rank) -> None:
+    """Record the decoding process's rank on a compress ctx (the communicators do, before the
+    decode): the decoders count capacity overflows for that payload only."""
+    if rank is None:
+        return
+    try:
+        ctx.own_rank = int(rank)
+    except (AttributeError, TypeError):  # a ctx that takes no attributes (tuple / slots): not counted
+        pass
+
+
 def own_rank(ctx):
-    """The decoding process's rank, as the communicator recorded it in ``ctx.extra`` (None: unknown,
-    then no overflow is counted by the decode)."""
-    extra = getattr(ctx, "extra", None)
-    return extra.get("own_rank") if isinstance(extra, dict) else None
+    """The decoding process's rank recorded by ``set_own_rank`` (None: unknown, then no overflow
+    is counted by the decode)."""
+    return getattr(ctx, "own_rank", None)
 
 
 def decode_ranks(vals, idxs, counts, out: torch.Tensor, scale: float = 1.0, own=None) -> torch.Tensor:

@@ -11,6 +11,12 @@ runtime's own high-priority HIP stream, ordered after the caller's current strea
 CURRENT stream instead: no event fork/join, which is what a whole-step HIP graph with the
 exchange on the main stream wants (bench.py picks it for ``--graph full`` without overlap; the
 forked torch/ProcessGroupNCCL path measured 0.44 ms/step slower for ResNet-50 Top-K).
+
+``RcclComm.tuned(nbytes)`` sizes the communicator's workgroup budget for the 7-link xGMI mesh
+(one ring drives one outbound link per GPU, so a dense all-reduce needs several
+channels): it builds one communicator per ``ncclConfig_t`` (minCTAs, maxCTAs) candidate, times an
+all-reduce of the REAL bucket size on each, takes the MAX over ranks and keeps the fastest
+(``choice`` records every candidate's time).
 """
 from __future__ import annotations
 
@@ -47,19 +53,65 @@ def _agree(ok: bool, group) -> None:
 
 
 class RcclComm(_comm.Comm):
+    #: (minCTAs, maxCTAs) candidates of ``tuned``; (0, 0) = RCCL's own choice
+    CTA_CANDIDATES = ((0, 0), (8, 8), (16, 16), (32, 32), (64, 64))
+
     def __init__(self, rank: int, world: int, unique_id: bytes, device: int, high_priority: bool = True,
-                 inline: bool = False):
+                 inline: bool = False, ctas=(0, 0)):
         C = _native.lib()
         _hook_exit()
-        self._c = C.RcclComm(rank, world, unique_id, device, high_priority)
+        self._c = C.RcclComm(rank, world, unique_id, device, high_priority, int(ctas[0]), int(ctas[1]))
+        self.ctas = (int(ctas[0]), int(ctas[1]))
+        self.choice = None
         self._c.inline = bool(inline)
         self.inline = bool(inline)
         self.rank, self.world_size, self.device = rank, world, device
         self._stream = torch.cuda.ExternalStream(self._c.stream_ptr, device=torch.device("cuda", device))
 
     @classmethod
+    def tuned(cls, nbytes: int, group=None, candidates=None, iters: int = 10, inline: bool = False,
+              high_priority: bool = True, dtype=torch.float32) -> "RcclComm":
+        """The communicator whose (minCTAs, maxCTAs) budget all-reduces ``nbytes`` (the real dense
+        bucket) fastest: every candidate is built (collectively), verified, timed on ``iters``
+        all-reduces of that size (wall time around synchronised issue, MAX over ranks: the
+        slowest rank sets each candidate's time), and all but the winner are destroyed.  Every
+        rank takes the same decision.  ``choice`` = {"collective", "bytes", "ctas", "us": {cand: us}}."""
+        import time
+
+        cands = [tuple(c) for c in (candidates if candidates is not None else cls.CTA_CANDIDATES)]
+        dev = torch.device("cuda", torch.cuda.current_device())
+        n = max(1, int(nbytes) // torch.empty((), dtype=dtype).element_size())
+        buf = torch.ones(n, dtype=dtype, device=dev)
+        times, comms = {}, {}
+        for cand in cands:
+            c = cls.from_process_group(group, high_priority=high_priority, inline=False, ctas=cand)
+            w = c._c.all_reduce(buf, "sum")  # warm: RCCL builds its channels / buffers lazily
+            w.synchronize()
+            c.barrier()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                w = c._c.all_reduce(buf, "sum")
+            w.synchronize()
+            torch.cuda.synchronize(dev)
+            t = torch.tensor([(time.perf_counter() - t0) * 1e6 / iters], dtype=torch.float64, device=dev)
+            c._c.all_reduce(t, "max").synchronize()
+            times[cand] = float(t.item())
+            comms[cand] = c
+        best = min(cands, key=lambda k: times[k])  # identical on every rank (MAX-reduced times)
+        for cand, c in comms.items():
+            if cand != best:
+                c.close()
+        win = comms[best]
+        win._c.inline = bool(inline)
+        win.inline = bool(inline)
+        win.choice = {"collective": "all_reduce", "bytes": int(n * buf.element_size()),
+                      "ctas": list(best), "us": {f"{a}/{b}": round(v, 2) for (a, b), v in times.items()}}
+        return win
+
+    @classmethod
     def from_process_group(cls, group=None, high_priority: bool = True, inline: bool = False,
-                           verify: bool = True, timeout_s: float = 120.0) -> "RcclComm":
+                           verify: bool = True, timeout_s: float = 120.0, ctas=(0, 0)) -> "RcclComm":
         """Bootstrap the runtime from the torch.distributed Store; with ``verify`` (default) the
         new communicator passes :meth:`verify` on every rank before it is returned (all ranks
         raise together otherwise, so the caller can fall back to ``TorchComm``)."""
@@ -77,7 +129,7 @@ class RcclComm(_comm.Comm):
         err = None
         c = None
         try:
-            c = cls(rank, world, bytes(uid), torch.cuda.current_device(), high_priority, inline)
+            c = cls(rank, world, bytes(uid), torch.cuda.current_device(), high_priority, inline, ctas)
         except Exception as e:  # every rank must learn it (the peers would wait in verify)
             err = e
         if verify:

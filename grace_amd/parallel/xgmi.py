@@ -41,6 +41,10 @@ from . import health as _health
 from ..ops import _native
 
 _UID = itertools.count()
+
+
+def n_bytes(t: torch.Tensor) -> int:
+    return t.numel() * t.element_size()
 _EMPTY_RANGES = torch.empty(0, 8, dtype=torch.int64)
 
 
@@ -226,10 +230,13 @@ class XgmiComm(_comm.Comm):
         """Small all-reduces as a one-shot gather + a rank-ordered local reduction (the same bytes
         summed in the same order on every rank: bit-identical results); larger ones -- or when
         ``select="probe"`` measured ``inner`` faster for this size -- go to ``inner``."""
-        if (op not in ("sum", "max", "min") or not t.is_contiguous() or not t.is_floating_point()
-                or not self._fits(t)):
-            return self.inner.all_reduce(t, op, async_op)
         n = t.numel() * t.element_size()
+        # sizes that are not 16-B granular (PowerSGD's P / Q: rows x rank fp32) are padded, not
+        # sent to the inner comm: the path must not depend on the byte size's alignment (a gloo
+        # inner cannot be captured, and every rank must take the same path)
+        if (op not in ("sum", "max", "min") or not t.is_contiguous() or not t.is_floating_point()
+                or not t.is_cuda or n == 0 or -(-n // 16) * 16 > self.capacity):
+            return self.inner.all_reduce(t, op, async_op)
         if self.select == "probe":
             c = self.choices.get(("ar", n))
             if c is None:
@@ -243,10 +250,18 @@ class XgmiComm(_comm.Comm):
         return _comm.Work()
 
     def _gather_reduce(self, t, op):
-        rows = torch.empty((self.world_size, t.numel()), dtype=t.dtype, device=t.device)
+        n, esz = t.numel(), t.element_size()
+        npad = -(-(n * esz) // 16) * 16 // esz  # 16-B granular row
+        src = t.reshape(-1)
+        if npad != n:
+            src = torch.zeros(npad, dtype=t.dtype, device=t.device)
+            src[:n].copy_(t.reshape(-1))
+        rows = torch.empty((self.world_size, npad), dtype=t.dtype, device=t.device)
         # a timed-out peer's rows come back as NaN (not zeros): the reduced value is visibly
         # wrong for ANY consumer, not only for FusedSGD's fault-word check
-        self._one_shot(rows.view(-1), t.reshape(-1), None, fill=0xFFFFFFFF)
+        self._one_shot(rows.view(-1), src, None, fill=0xFFFFFFFF)
+        if npad != n:
+            rows = rows[:, :n]
         if op == "sum":
             torch.sum(rows, 0, out=t.view(-1))
         elif op == "max":
@@ -288,7 +303,60 @@ class XgmiComm(_comm.Comm):
         return self.inner.broadcast(t, src, async_op)
 
     def all_to_all(self, out, inp, async_op=False):
-        return self.inner.all_to_all(out, inp, async_op)
+        """out[p] = chunk ``rank`` of rank p's ``inp`` (QSGD's compressed-domain reduce-scatter):
+        each rank pulls only its own chunk of every peer's staged payload, all links at once
+        (graph-capturable); sizes past the capacity / not 16-B x W granular -- or, with
+        ``select="probe"``, sizes where ``inner`` measured faster -- go to ``inner``."""
+        n = inp.numel() * inp.element_size()
+        if not (inp.is_cuda and 0 < n <= self.capacity and n % (16 * self.world_size) == 0
+                and out.numel() * out.element_size() == n):
+            return self.inner.all_to_all(out, inp, async_op)
+        if self.select == "probe":
+            c = self.choices.get(("a2a", n))
+            if c is None:
+                if torch.cuda.is_current_stream_capturing():
+                    c = {"path": "xgmi"}
+                else:
+                    c = self.choices[("a2a", n)] = self._probe_a2a(out, inp)
+            if c["path"] != "xgmi":
+                return self.inner.all_to_all(out, inp, async_op)
+        self._a2a(out, inp)
+        return _comm.Work()
+
+    def _a2a(self, out, inp):
+        i = inp if self._aligned(inp) else inp.contiguous().clone()
+        o = out if self._aligned(out) else torch.empty(out.numel() * out.element_size(), dtype=torch.uint8,
+                                                       device=out.device)
+        self._x.all_to_all(o.reshape(-1).view(torch.uint8), i.reshape(-1).view(torch.uint8))
+        if o is not out:
+            out.reshape(-1).view(torch.uint8).copy_(o)
+        self.one_shot_calls += 1
+
+    def _probe_a2a(self, out, inp, iters: int = 8) -> dict:
+        import time
+
+        dev = torch.device("cuda", self.device)
+        o = torch.empty_like(out)
+        i = inp.detach().clone()
+        times = []
+        for path in ("xgmi", "inner"):
+            fn = (lambda: self._a2a(o, i)) if path == "xgmi" else (lambda: self.inner.all_to_all(o, i, False).wait())
+            fn()
+            torch.cuda.synchronize(dev)
+            self.inner.barrier()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                fn()
+            torch.cuda.synchronize(dev)
+            times.append((time.perf_counter() - t0) * 1e6 / iters)
+        tt = torch.tensor(times, dtype=torch.float64, device=dev)
+        self.inner.all_reduce(tt, "max").wait()
+        torch.cuda.synchronize(dev)
+        xg, inn = (float(v) for v in tt.tolist())
+        self.one_shot_calls -= iters + 1
+        return {"path": "xgmi" if xg <= inn else "inner", "xgmi_us": round(xg, 2), "inner_us": round(inn, 2),
+                "bytes": int(n_bytes(inp)), "collective": "all_to_all"}
 
     def reduce_scatter(self, out, inp, op="sum", async_op=False):
         return self.inner.reduce_scatter(out, inp, op, async_op)
@@ -327,7 +395,16 @@ class XgmiComm(_comm.Comm):
             self.inner.all_gather_into(ref, pat).wait()
             torch.cuda.synchronize(dev)
             ok &= int(torch.equal(got, ref)) & int(_health.status()[1] == 0)
-        self._agree(bool(ok), "xGMI one-shot all-gather failed its self-check against the inner comm")
+        # the one-shot all-to-all (QSGD's compressed-domain reduce-scatter) against the inner comm
+        if self.world_size > 1:
+            m = 16 * self.world_size * 131  # int32 words: W chunks of 16-B granular size
+            pat = torch.arange(m, device=dev, dtype=torch.int32) * (self.rank + 5) + 11
+            got, ref = torch.empty_like(pat), torch.empty_like(pat)
+            self._a2a(got, pat)
+            self.inner.all_to_all(ref, pat).wait()
+            torch.cuda.synchronize(dev)
+            ok &= int(torch.equal(got, ref)) & int(_health.status()[1] == 0)
+        self._agree(bool(ok), "xGMI one-shot collectives failed their self-check against the inner comm")
         self.one_shot_calls = self.direct_calls = 0
 
     def _all(self, flag: bool) -> bool:

@@ -30,6 +30,25 @@ def nccl_group():
     # leave the group up for the rest of the session (destroying + re-initialising RCCL is slow)
 
 
+def test_rccl_cta_probe_single_rank(nccl_group):
+    """RcclComm.tuned: one communicator per ncclConfig_t (minCTAs, maxCTAs) candidate, each timed
+    on an all-reduce of the given size (MAX over ranks), the fastest kept and working (W = 1 runs
+    the whole probe path; the choice itself only matters on the 8-GPU mesh)."""
+    from grace_amd.parallel.native_comm import RcclComm
+
+    cands = ((0, 0), (8, 8), (16, 32))
+    c = RcclComm.tuned(1 << 20, candidates=cands, iters=2, inline=True)
+    assert tuple(c.choice["ctas"]) in cands and c.ctas == tuple(c.choice["ctas"])
+    assert set(c.choice["us"]) == {f"{a}/{b}" for a, b in cands} and c.choice["bytes"] == 1 << 20
+    assert c.inline and c.verify()
+    t = torch.arange(1000, dtype=torch.float32, device="cuda")
+    c.all_reduce(t)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(t, torch.arange(1000, dtype=torch.float32, device="cuda"))
+    fixed = RcclComm.from_process_group(ctas=(4, 4))
+    assert fixed._c.min_ctas == 4 and fixed._c.max_ctas == 4 and fixed.verify()
+
+
 def _net():
     torch.manual_seed(0)
     return nn.Sequential(nn.Conv2d(3, 16, 3, padding=1), nn.BatchNorm2d(16), nn.ReLU(), nn.AdaptiveAvgPool2d(1),

@@ -327,3 +327,90 @@ def _xgmi_whole_step_graph_body(rank, world):
 
 def test_xgmi_whole_step_graph_two_ranks():
     run_distributed(_xgmi_whole_step_graph_body, 2, timeout=300)
+
+
+# The five BASELINE pipelines (BASELINE.json configs 2-5 + DGC): each one's W = 2 exchange captured
+# in a whole-step HIP graph on the one-shot xGMI comm (gathers, the gather-reduce all-reduce of
+# PowerSGD's P / Q and DGC's clipping norm, QSGD's one-shot all-to-all), replayed, and compared
+# with an EAGER W = 2 run of the same steps through the gloo comm -- not only across ranks
+# (an exchange wrong identically on every rank must fail here).
+REHEARSAL = {
+    "topk": {"compressor": "topk", "compress_ratio": 0.01, "memory": "residual", "communicator": "allgather"},
+    "dgc": {"compressor": "dgc", "compress_ratio": 0.01, "memory": "dgc", "communicator": "allgather"},
+    "powersgd": {"compressor": "powersgd", "compress_rank": 4, "memory": "powersgd", "communicator": "allreduce"},
+    "efsignsgd": {"compressor": "efsignsgd", "lr": 0.1, "memory": "efsignsgd", "communicator": "allreduce"},
+    "qsgd": {"compressor": "qsgd", "quantum_num": 127, "memory": "none", "communicator": "allreduce"},
+}
+
+
+def _mlp():
+    import torch.nn as nn
+
+    torch.manual_seed(0)
+    return nn.Sequential(nn.Linear(256, 512), nn.ReLU(), nn.Linear(512, 384), nn.ReLU(), nn.Linear(384, 10))
+
+
+def _rehearsal_body(rank, world, name, replays):
+    import torch.nn.functional as F
+
+    from grace_amd import grace_from_params
+    from grace_amd.parallel import DistributedOptimizer, FusedSGD, broadcast_parameters
+    from grace_amd.parallel.comm import TorchComm
+    from grace_amd.parallel.graph import GraphedStep
+    from grace_amd.parallel.xgmi import XgmiComm
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    comm = XgmiComm(TorchComm(), capacity_mb=8.0, select="size")
+    params = dict(REHEARSAL[name], world_size=world)
+    g = torch.Generator().manual_seed(100 + rank)  # different data per rank
+    x = torch.randn(64, 256, generator=g).to(dev)
+    y = torch.randint(0, 10, (64,), generator=g).to(dev)
+
+    def build(c):
+        model = _mlp().to(dev)
+        broadcast_parameters(model.state_dict(), root_rank=0)
+        grc = grace_from_params(params, comm=c)
+        opt = DistributedOptimizer(FusedSGD(list(model.parameters()), lr=0.05, momentum=0.5), grc,
+                                   named_parameters=list(model.named_parameters()), overlap=False)
+        return model, opt
+
+    def stepper(model, opt):
+        def step():
+            opt.zero_grad(set_to_none=True)
+            loss = F.cross_entropy(model(x), y)
+            loss.backward()
+            opt.step()
+            return loss
+        return step
+
+    try:
+        m1, o1 = build(comm)
+        run = GraphedStep(stepper(m1, o1), warmup=3, capture_error_mode="thread_local")
+        calls = comm.one_shot_calls
+        assert calls > 0, "the eager warm-up must have used the one-shot comm"
+        for _ in range(replays):
+            run()
+        torch.cuda.synchronize()
+        assert comm.one_shot_calls == calls  # the replays ran without Python
+        comm.check()
+        m2, o2 = build(TorchComm())
+        step2 = stepper(m2, o2)
+        for _ in range(3 + replays):  # the warm-up steps are real steps too
+            step2()
+        torch.cuda.synchronize()
+        for (n, a), b in zip(m1.named_parameters(), m2.parameters()):
+            ref = a.detach().clone()
+            dist.broadcast(ref, 0)
+            assert torch.equal(ref, a.detach()), f"{name}: {n} differs across ranks"
+            assert torch.equal(a.detach(), b.detach()), \
+                f"{name}: {n} graphed one-shot exchange != eager gloo exchange (max diff {(a - b).abs().max():.3g})"
+        dist.barrier()
+        torch.cuda.synchronize()
+    finally:
+        comm.close()
+
+
+@pytest.mark.parametrize("name", sorted(REHEARSAL))
+def test_pipeline_whole_step_graph_two_ranks_matches_eager(name):
+    run_distributed(_rehearsal_body, 2, name, 6, timeout=300)

@@ -25,7 +25,10 @@ def main():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--modes", default="eager_torch,eager_fused,graph_fused")
     ap.add_argument("--dropout", type=float, default=None, help="override the model's dropout")
+    ap.add_argument("--benchmark", action="store_true", help="torch.backends.cudnn.benchmark = True (as bench.py)")
+    ap.add_argument("--cap-warm", type=int, default=3)
     args = ap.parse_args()
+    torch.backends.cudnn.benchmark = args.benchmark
     dev = torch.device("cuda", 0)
     torch.backends.cuda.matmul.allow_tf32 = False
     w = WORKLOADS[args.workload]
@@ -58,8 +61,8 @@ def main():
 
         losses = []
         if mode.startswith("graph"):
-            run = GraphedStep(step, warmup=3)
-            for _ in range(args.steps - 3):
+            run = GraphedStep(step, warmup=args.cap_warm)
+            for _ in range(args.steps - args.cap_warm):
                 losses.append(float(run().item()))
         else:
             for i in range(args.steps):

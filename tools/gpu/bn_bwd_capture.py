@@ -44,6 +44,14 @@ class Proxy:
         h.copy_(t, non_blocking=True)
         return h
 
+    def conv3x3_f32(self, dir, act, other, C, *a, **k):
+        t = self._real.conv3x3_f32(dir, act, other, C, *a, **k)
+        if VARIANT == "pinned" and dir == 1 and tuple(act.shape) == SHAPE:
+            # the data gradient that feeds layer3.0's output: inputs + output, device-allocation free
+            self._log.append(("dgrad", {"dy": self._pin(act), "w": self._pin(other), "dx": self._pin(C),
+                                        "dx_ptr": C.data_ptr(), "args": [repr(v) for v in a]}))
+        return t
+
     def bn_act_fwd(self, x, res, *a):
         out = self._real.bn_act_fwd(x, res, *a)
         if VARIANT == "pinned" and tuple(x.shape) == SHAPE and res is not None:
@@ -155,7 +163,12 @@ def main():
     g = torch.Generator().manual_seed(7)
     x = torch.randn(8, 3, 16, 16, generator=g)
     y = torch.randint(0, 10, (8,), generator=g)
-    _, ref_g, ref_m = D.run(copy.deepcopy(base).double(), x.double(), y, torch.device("cpu"), False, False)
+    ref_model = copy.deepcopy(base).double()
+    ref_act = {}
+    for nm in ("layer3.0", "layer3.1"):  # fp64 forward outputs (the block output's ReLU pattern)
+        dict(ref_model.named_modules())[nm].register_forward_hook(
+            lambda mod, i, o, nm=nm: ref_act.__setitem__(nm, (o[0] if isinstance(o, tuple) else o).detach().clone()))
+    _, ref_g, ref_m = D.run(ref_model, x.double(), y, torch.device("cpu"), False, False)
     for mode in args.modes.split(","):
         log.clear()
         proxy.kept.clear()
@@ -172,6 +185,9 @@ def main():
             rep[f"kept{i}"] = {"dx_rel": D.rel(rows(kk["dx"]), dx), "db_rel": D.rel(kk["db"].double().cpu(), db),
                                "dw_rel": D.rel(kk["dw"].double().cpu(), dw),
                                "dres_rel": None if kk["dres"] is None else D.rel(rows(kk["dres"]), dz)}
+        for i, dg in enumerate([d for k, d in log if k == "dgrad"]):
+            ref = torch.nn.grad.conv2d_input((8, 256, 4, 4), dg["w"].double(), dg["dy"].double(), padding=1)
+            rep[f"dgrad{i}"] = {"rel": D.rel(dg["dx"].double(), ref), "args": dg["args"]}
         for i, b in enumerate(bw):
             f = [d for d in fw if d["save_ptr"] == b["save_ptr"]]
             f = f[-1] if f else None
@@ -193,6 +209,13 @@ def main():
             r["db_vs_fp64"] = {n: D.rel(b["db"].double().cpu(), ref_g[n]) for n in ("layer3.0.bn2.bias", "layer3.1.bn2.bias")}
             dsum = (b["dy"].double() + b["dy2"].double()).cpu()
             r["dy_sum_vs_fp64"] = {k: D.rel(dsum, ref_m[k]) for k in ("layer3.0[full]", "layer3.1[full]") if k in ref_m}
+            m_cap = unpack_mask(b["mask"].cpu(), 128, 256)
+            for nm, ya in ref_act.items():
+                yr = ya.permute(0, 2, 3, 1).reshape(128, 256) > 0
+                r[f"mask_vs_fp64_{nm}"] = int((m_cap != yr).sum())  # disagreeing ReLU bits
+            if f is not None:
+                yg = f["y"].permute(0, 2, 3, 1).reshape(128, 256).double()
+                r["fwd_y_vs_fp64"] = {nm: D.rel(yg, ya.permute(0, 2, 3, 1).reshape(128, 256)) for nm, ya in ref_act.items()}
             rep[f"bwd{i}"] = r
         print(json.dumps(rep), flush=True)
     dist.destroy_process_group()
