@@ -392,8 +392,11 @@ def main():
             else:
                 dist.barrier(device_ids=[local])
 
-    for _ in range(args.warmup):
-        run()
+    trace_loss = os.environ.get("GRACE_BENCH_LOSS_TRACE", "0") == "1"  # debug: per-step loss to stderr
+    for i in range(args.warmup):
+        lw = run()
+        if trace_loss:
+            print(f"[bench] warmup step {i} loss {float(lw.float().item()):.5f}", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -405,6 +408,8 @@ def main():
     for i in range(args.steps):
         loss = run()
         evs[i + 1].record()
+        if trace_loss:
+            print(f"[bench] timed step {i} loss {float(loss.float().item()):.5f}", file=sys.stderr, flush=True)
     issue_s = time.perf_counter() - t0  # host time to issue the steps (graph replays) before the wait
     torch.cuda.synchronize()
     barrier()

@@ -162,7 +162,7 @@ def _run(direction: str, backend: str, x, wt, dy, wshape, out=None):
             return torch.mm(_x2d(dy).t(), _x2d(x), out=out)
         return torch.mm(_x2d(dy).t(), _x2d(x))
     # mfma[_tN]: csrc/kernels/gemm_f32.hip with the launcher's tile rule or a forced tile
-    tile = int(backend[6:]) if backend.startswith("mfma_t") else 0
+    tile = _tile_of(backend)
     if direction == "fwd":
         y = torch.empty((nb, cout, h, w), device=x.device, dtype=torch.float32, memory_format=torch.channels_last)
         gemm(x, True, cin, wt, True, cin, y, cout, m, cout, cin, 0, tile)
@@ -199,7 +199,19 @@ def _pick(direction: str, x, wt, dy, wshape) -> str:
 
 
 def _tile_of(backend: str) -> int:
-    return int(backend[6:]) if backend.startswith("mfma_t") else 0
+    return _mfma_cfg(backend)[0]
+
+
+def _mfma_cfg(backend: str):
+    """(tile, splits) of an "mfma[_tN][_sK]" backend name (tile 0 = the launcher's rule; splits 0 =
+    the caller's default)."""
+    tile = splits = 0
+    for tok in backend.split("_")[1:]:
+        if tok.startswith("t"):
+            tile = int(tok[1:])
+        elif tok.startswith("s"):
+            splits = int(tok[1:])
+    return tile, splits
 
 
 def _dgrad_handoff(h, x, w, dy, ksize: int, tile: int = 0):
@@ -463,6 +475,26 @@ def fast_ok(x: torch.Tensor, conv: nn.Conv2d, force: bool = False) -> bool:
 _C3_CHOICE = {}
 _C3_TIMES = {}
 C3_BACKENDS = ("miopen", "mfma", "mfma_t1", "mfma_t2", "mfma_t3", "mfma_t4")
+# split-K variants for the forward / data grad of the small-M layers (14x14 / 7x7 at batch 32:
+# M = N*H*W of 6272 / 1568 leaves most of the 256 CUs idle with whole-K tiles, and a 64x64 tile
+# is latency bound -- 32 k per LDS stage is too little MFMA work to cover a global load); every
+# split accumulates with f32 atomics into a zeroed output.  Only candidates whose whole-K tiling
+# leaves CUs idle are timed (_c3_candidates).
+C3_SPLIT_BACKENDS = ("mfma_t1_s2", "mfma_t1_s4", "mfma_t2_s2", "mfma_t2_s4", "mfma_t3_s2", "mfma_t3_s4",
+                     "mfma_t4_s2")
+_TILE_MN = {1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64)}
+
+
+def _c3_candidates(direction: str, m: int, n: int):
+    if direction == "wgrad":
+        return C3_BACKENDS  # split-K by the launcher's own rule (K = output pixels)
+    out = list(C3_BACKENDS)
+    for be in C3_SPLIT_BACKENDS:
+        t, s = _mfma_cfg(be)
+        bm, bn = _TILE_MN[t]
+        if -(-m // bm) * -(-n // bn) * s <= 2 * 256 * 2 and -(-m // bm) * -(-n // bn) < 256:
+            out.append(be)
+    return tuple(out)
 _C3_ON = os.environ.get("GRACE_CONV3X3", "1") == "1"
 
 
@@ -503,20 +535,21 @@ def _run3(direction: str, backend: str, x, w, dy, stride: int, out=None):
         gi, gw, _ = torch.ops.aten.convolution_backward(dy, x, w, None, [stride, stride], [pad, pad], [1, 1], False,
                                                         [0, 0], 1, mask)
         return gi if direction == "dgrad" else gw
-    tile = int(backend[6:]) if backend.startswith("mfma_t") else 0
+    tile, splits = _mfma_cfg(backend)
+    splits = max(1, splits)  # forward / data grad: whole-K tiles unless the backend splits K
     C = _native.lib()
     nb, cin, h, wd = x.shape
     cout = w.shape[0]
     if direction == "fwd":
         ho, wo = (h - 1) // stride + 1, (wd - 1) // stride + 1
         y = torch.empty((nb, cout, ho, wo), device=x.device, dtype=torch.float32, memory_format=torch.channels_last)
-        C.conv3x3_f32(0, x, w, y, stride, 1, tile, None, ks)
+        C.conv3x3_f32(0, x, w, y, stride, splits, tile, None, ks)
         return y
     if direction == "dgrad":
         if stride != 1 or ks != 3:
             raise ValueError("implicit-GEMM data grad: 3x3 stride 1 only")
         dx = torch.empty_like(x, memory_format=torch.channels_last)
-        C.conv3x3_f32(1, dy, w, dx, 1, 1, tile)
+        C.conv3x3_f32(1, dy, w, dx, 1, splits, tile)
         return dx
     dw = out if (out is not None and out.is_contiguous(memory_format=torch.channels_last)
                  and out.data_ptr() % 16 == 0) else \
@@ -538,7 +571,9 @@ def _pick3(direction: str, x, w, dy, stride: int) -> str:
     if torch.cuda.is_current_stream_capturing():
         return "miopen"  # never time inside a capture
     times = {}
-    for be in C3_BACKENDS:
+    ho, wo = (h - 1) // stride + 1, (wd - 1) // stride + 1
+    m, n = (nb * h * wd, cin) if direction == "dgrad" else (nb * ho * wo, w.shape[0])
+    for be in _c3_candidates(direction, m, n):
         try:
             times[be] = _time(lambda be=be: _run3(direction, be, x, w, dy, stride))
         except Exception:  # a backend that rejects the shape is simply not a candidate
@@ -602,7 +637,7 @@ class _Conv3x3Fn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             be = _pick3("dgrad", x, w, dy, stride)
             dx = _dgrad_handoff(getattr(ctx, "bn_h", None), x, w, dy, 3, _tile_of(be)) \
-                if be.startswith("mfma") else None
+                if be.startswith("mfma") and _mfma_cfg(be)[1] <= 1 else None
             if dx is None:
                 dx = _run3("dgrad", be, x, w, dy, stride)
         if f is not None and not _wg._WG_FIRST:

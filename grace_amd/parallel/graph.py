@@ -27,6 +27,8 @@ import torch
 
 from . import health as _health
 
+_SYNC_EACH = __import__("os").environ.get("GRACE_GRAPH_SYNC_EACH", "0") == "1"
+
 #: stochastic codecs whose native kernels read a device step counter
 _DEVICE_STEPPED = ("RandomKCompressor", "QSGDCompressor", "TernGradCompressor", "NaturalCompressor",
                    "PowerSGDCompressor", "DgcCompressor", "AdaqCompressor")
@@ -127,6 +129,8 @@ class GraphedStep:
             cur.wait_stream(self.stream)
         else:
             self.graphs[i].replay()
+        if _SYNC_EACH:  # debug A/B: no replay overlaps the host issue of the next one
+            torch.cuda.synchronize()
         self.loss = self.losses[i]
         return self.loss
 

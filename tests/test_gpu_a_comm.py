@@ -364,45 +364,111 @@ def test_ddp_hook_graph_capture(nccl_group):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
 
 
-def test_plain_ddp_resnet_grads_match_inline(nccl_group):
+def _masked_reference(recorded):
+    """A bn_act for the float64 CPU reference that applies the GPU run's ReLU decisions: y =
+    (bn(x) + residual) * M_gpu, so the reference differentiates the SAME piecewise-linear function
+    the GPU run did.  (A ReLU input within fp32 rounding of 0 legitimately flips between two fp32
+    runs that sum in different orders -- and then that one element's gradient, |dy| there, shows up
+    in every BN bias / conv weight gradient below it: that, not a race, was the r4 "intermittent
+    plain-DDP mismatch", one flipped bit of 32768 in layer3.0.bn2, tools/gpu/bn_bwd_capture.py.)"""
+    import torch.nn as nn
+
+    it = iter(recorded)
+
+    def bn_act(x, bn, residual=None, relu=False, dual=False, **_):
+        y = nn.BatchNorm2d.forward(bn, x)
+        if residual is not None:
+            y = y + residual
+        if relu:
+            y = y * next(it).to(y.dtype)
+        return (y, y) if dual else y
+    return bn_act
+
+
+def _record_masks(store):
+    from grace_amd.ops import bnact
+
+    real = bnact.bn_act
+
+    def bn_act(x, bn, residual=None, relu=False, dual=False, *a, **k):
+        out = real(x, bn, residual, relu, dual, *a, **k)
+        if relu:
+            y = out[0] if isinstance(out, tuple) else out
+            store.append((y.detach() > 0).cpu())
+        return out
+    return bn_act
+
+
+@pytest.fixture(params=[None, "mfma_t2"], ids=["autotuned", "forced-dgrad-mfma_t2"])
+def dgrad_choice(request):
+    """The second case pins every 3x3 data gradient to the 128x64 MFMA tile: the configuration
+    that flipped layer3.0.bn2's ReLU bit in (almost) every process with the r4 GPU-vs-GPU test."""
+    from grace_amd.ops import conv
+
+    if request.param is None:
+        yield None
+        return
+    real = conv._pick3
+    conv._pick3 = lambda d, x, w, dy, s: (request.param if d == "dgrad" and s == 1 and w.shape[2] == 3
+                                          else real(d, x, w, dy, s))
+    try:
+        yield request.param
+    finally:
+        conv._pick3 = real
+
+
+def test_plain_ddp_resnet_grads_match_fp64(nccl_group, dgrad_choice):
     """grace_amd.models.resnet under PLAIN DDP (no GRACE hook, no engine): its parameters are not
     tagged joinable, so every weight gradient is computed in line and the reducer's mid-backward
-    reads see finished gradients -- equal to the GRACE_WGRAD_STREAM=0 run"""
+    reads see finished gradients.  Both the side-stream-switch-off and -on runs are compared with
+    a float64 CPU reference of the same weights and input that takes each run's ReLU decisions
+    (``_masked_reference``); the tolerance is fp32 summation over the reductions feeding each
+    gradient (<= 4096 terms: 2e-4 of the tensor's max).  A race -- a gradient read before its
+    producer finished -- would be off by O(1), not by rounding (ADVICE r3 high / VERDICT r4 #1)."""
     import copy
 
     from grace_amd.models import resnet18_cifar
-    from grace_amd.ops import wgrad
+    from grace_amd.ops import bnact, bnconv, wgrad
 
     torch.manual_seed(0)
-    base = resnet18_cifar().cuda().to(memory_format=torch.channels_last)
+    base = resnet18_cifar()  # CPU fp32: the source of both the GPU runs and the fp64 reference
     g = torch.Generator().manual_seed(7)
-    x = torch.randn(8, 3, 16, 16, generator=g).cuda().contiguous(memory_format=torch.channels_last)
-    y = torch.randint(0, 10, (8,), generator=g).cuda()
-
-    def grads(stream_on):
-        m = copy.deepcopy(base)
+    x = torch.randn(8, 3, 16, 16, generator=g)
+    y = torch.randint(0, 10, (8,), generator=g)
+    names = [n for n, _ in base.named_parameters()]
+    real = bnact.bn_act
+    for stream_on in (False, True):
+        masks = []
+        m = copy.deepcopy(base).cuda().to(memory_format=torch.channels_last)
         ddp = nn.parallel.DistributedDataParallel(m, device_ids=[0], broadcast_buffers=False)
         wgrad.set_enabled(stream_on)
         try:
-            out = []
-            for _ in range(2):
+            for it in range(2):
                 for p in m.parameters():
                     p.grad = None
-                F.cross_entropy(ddp(x), y).backward()
-                out = [p.grad.detach().clone() for p in m.parameters()]
+                masks.clear()
+                if it == 1:
+                    bnact.bn_act = bnconv.bn_act = _record_masks(masks)
+                try:
+                    F.cross_entropy(ddp(x.cuda().contiguous(memory_format=torch.channels_last)), y.cuda()).backward()
+                finally:
+                    bnact.bn_act = bnconv.bn_act = real
         finally:
             wgrad.set_enabled(True)
         assert not any(wgrad.joinable(p) for p in m.parameters())
-        return out
-
-    ref = grads(False)
-    got = grads(True)
-    torch.cuda.synchronize()
-    names = [n for n, _ in base.named_parameters()]
-    bad = []
-    for n, a, b in zip(names, got, ref):
-        tol = 1e-4 * float(b.abs().max()) + 1e-6
-        err = float((a - b).abs().max())
-        if err > tol:
-            bad.append(f"{n}{tuple(a.shape)}: {err:.3g} > {tol:.3g}")
-    assert not bad, f"{len(bad)} of {len(names)} differ, deepest first: " + "; ".join(bad[::-1])
+        torch.cuda.synchronize()
+        got = [p.grad.detach().double().cpu() for p in m.parameters()]
+        ref_m = copy.deepcopy(base).double()
+        bnact.bn_act = bnconv.bn_act = _masked_reference(masks)
+        try:
+            F.cross_entropy(ref_m(x.double()), y).backward()
+        finally:
+            bnact.bn_act = bnconv.bn_act = real
+        bad = []
+        for n, a, p in zip(names, got, ref_m.parameters()):
+            b = p.grad
+            err, tol = float((a - b).abs().max()), 2e-4 * float(b.abs().max()) + 1e-9
+            if err > tol:
+                bad.append(f"{n}{tuple(a.shape)}: {err:.3g} > {tol:.3g}")
+        assert not bad, f"stream {'on' if stream_on else 'off'}: {len(bad)} of {len(names)} differ from fp64, " \
+                        "deepest first: " + "; ".join(bad[::-1])

@@ -84,12 +84,22 @@ def test_conv3x3_no_oob_writes(shape):
         C.conv3x3_f32(2, x, dy, dw, s, 0, tile, None, k)
         torch.cuda.synchronize()
         _check_guards(buf, dw.numel(), f"wgrad tile {tile}")
-        # data gradient (3x3 stride 1 only)
-        if s == 1 and k == 3:
-            buf, dx = _guarded_cl(n, cin, h, w)
-            C.conv3x3_f32(1, dy, wt, dx, 1, 1, tile)
+        # split-K forward (f32 atomics into a zeroed output: the autotuner's mfma_tN_sK)
+        for splits in (2, 4):
+            buf, y = _guarded_cl(n, cout, ho, wo)
+            C.conv3x3_f32(0, x, wt, y, s, splits, tile, None, k)
             torch.cuda.synchronize()
-            _check_guards(buf, dx.numel(), f"dgrad tile {tile}")
+            _check_guards(buf, y.numel(), f"fwd tile {tile} splits {splits}")
+            torch.testing.assert_close(y, torch.nn.functional.conv2d(x, wt, None, s, (k - 1) // 2), rtol=1e-4, atol=1e-3)
+        # data gradient (3x3 stride 1 only), whole-K and split-K
+        if s == 1 and k == 3:
+            ref = torch.nn.grad.conv2d_input((n, cin, h, w), wt, dy, padding=1)
+            for splits in (1, 2, 4):
+                buf, dx = _guarded_cl(n, cin, h, w)
+                C.conv3x3_f32(1, dy, wt, dx, 1, splits, tile)
+                torch.cuda.synchronize()
+                _check_guards(buf, dx.numel(), f"dgrad tile {tile} splits {splits}")
+                torch.testing.assert_close(dx, ref, rtol=1e-4, atol=1e-3)
     assert torch.equal(x, x0) and torch.equal(wt, w0) and torch.equal(dy, dy0), "an input operand was written"
 
 

@@ -403,8 +403,12 @@ def _rehearsal_body(rank, world, name, replays):
             ref = a.detach().clone()
             dist.broadcast(ref, 0)
             assert torch.equal(ref, a.detach()), f"{name}: {n} differs across ranks"
-            assert torch.equal(a.detach(), b.detach()), \
-                f"{name}: {n} graphed one-shot exchange != eager gloo exchange (max diff {(a - b).abs().max():.3g})"
+            if name == "powersgd":  # P / Q are float SUMS: gloo's ring vs the rank-ordered gather-reduce
+                torch.testing.assert_close(a.detach(), b.detach(), rtol=1e-5, atol=1e-7,
+                                           msg=lambda m: f"{name}: {n} graphed != eager: {m}")
+            else:  # gathered payloads decoded in rank order / integer sums: bit-identical
+                assert torch.equal(a.detach(), b.detach()), \
+                    f"{name}: {n} graphed one-shot exchange != eager gloo exchange (max diff {(a - b).abs().max():.3g})"
         dist.barrier()
         torch.cuda.synchronize()
     finally:
