@@ -393,8 +393,13 @@ def main():
                 dist.barrier(device_ids=[local])
 
     trace_loss = os.environ.get("GRACE_BENCH_LOSS_TRACE", "0") == "1"  # debug: per-step loss to stderr
+    # debug: every step's loss copied on the device (no host sync between steps), printed at the end
+    rec = torch.empty(args.warmup + args.steps, device=dev) \
+        if os.environ.get("GRACE_BENCH_LOSS_RECORD", "0") == "1" else None
     for i in range(args.warmup):
         lw = run()
+        if rec is not None:
+            rec[i].copy_(lw.float().reshape(()))
         if trace_loss:
             print(f"[bench] warmup step {i} loss {float(lw.float().item()):.5f}", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
@@ -408,6 +413,8 @@ def main():
     for i in range(args.steps):
         loss = run()
         evs[i + 1].record()
+        if rec is not None:
+            rec[args.warmup + i].copy_(loss.float().reshape(()))
         if trace_loss:
             print(f"[bench] timed step {i} loss {float(loss.float().item()):.5f}", file=sys.stderr, flush=True)
     issue_s = time.perf_counter() - t0  # host time to issue the steps (graph replays) before the wait
@@ -424,6 +431,8 @@ def main():
     if callable(_chk):
         _chk()
     step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
+    if rec is not None:
+        print("[bench] losses " + " ".join(f"{v:.4f}" for v in rec.tolist()), file=sys.stderr, flush=True)
     final_loss = float(loss.float().item())
     loss_finite = final_loss == final_loss and abs(final_loss) != float("inf")
     if not loss_finite:  # a diverged run's throughput is not a measurement of training

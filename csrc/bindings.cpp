@@ -793,6 +793,7 @@ int64_t gemm_f32(const Tensor& A, bool a_kc, int64_t lda, const Tensor& B, bool 
   CHECK_DT(C, at::kFloat);
   TORCH_CHECK(C.numel() >= (M - 1) * ldc + N && ldc >= N, "C too small");
   TORCH_CHECK(splits == 0 || splits == 1 || ldc == N, "split-K needs a dense C");
+  TORCH_CHECK(tile >= 0 && tile <= 4, "gemm_f32: tile 0 (launcher rule) or 1-4");
   TORCH_CHECK(M < (1LL << 31) && N < (1LL << 31) && K < (1LL << 31), "GEMM dims must fit int32");
   float* st = nullptr;
   if (stats.has_value() && stats->defined()) {
@@ -834,6 +835,7 @@ int64_t conv3x3_f32(int64_t dir, const Tensor& act, const Tensor& other, const T
                     const c10::optional<Tensor>& bn_save, bool bn_relu, const c10::optional<Tensor>& x_save,
                     bool x_relu) {
   TORCH_CHECK(dir >= 0 && dir <= 2, "conv3x3_f32: dir 0 (fwd) / 1 (dgrad) / 2 (wgrad)");
+  TORCH_CHECK(tile >= 0 && tile <= 4, "conv3x3_f32: tile 0 (launcher rule) or 1-4");
   TORCH_CHECK(stride == 1 || (stride == 2 && dir != 1), "conv3x3_f32: stride 1, or 2 for fwd / wgrad");
   TORCH_CHECK(ksize == 3 || (ksize == 1 && dir != 1), "conv3x3_f32: 3x3 (pad 1), or 1x1 (pad 0) fwd / wgrad");
   const int64_t K = ksize;

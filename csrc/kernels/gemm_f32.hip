@@ -49,8 +49,10 @@ namespace {
 
 constexpr int kGB = 256;  // threads per workgroup (4 waves)
 // k per LDS stage: 32 (4 x 8-k groups; BK = 16 with 4 workgroups per CU measured slower).  The
-// kernel is templated on it; 64-k slices (more MFMA work between barriers for small tiles,
-// profiles/r4_conv3x3_implicit_gemm_vs_miopen.txt second table) are not launched (see launch_tile)
+// round-4 64-k-slice variant (tile codes 5-7, 70-104 KB of static LDS) is gone: it won no
+// direction in situ by more than 1 us (profiles/r4_autotune_decisions.txt) and coincided with
+// aborts in forked captures that were never root-caused; the small-M layers get their extra
+// workgroups from split-K instead (ops/conv.py C3_SPLIT_BACKENDS).
 constexpr int BK = 32;
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -119,7 +121,7 @@ __device__ __forceinline__ int fdivmod(int m, int d, float inv, int* r) {
   return q;
 }
 
-template <int R, int MODE, int BK = 32>
+template <int R, int MODE>
 struct Operand {
   static constexpr int LDK = BK + 4;                   // K-contig row pitch (conflict-free b128 reads)
   static constexpr bool KC = mode_kc(MODE);
@@ -266,10 +268,10 @@ struct Operand {
 
 __device__ __forceinline__ float f4get(const float4& v, int s) { return s == 0 ? v.x : s == 1 ? v.y : s == 2 ? v.z : v.w; }
 
-template <int BM, int BN, int AM, int BMD, int BK = 32>
+template <int BM, int BN, int AM, int BMD>
 __global__ __launch_bounds__(kGB, 2) void gemm_f32_kernel(GemmParams p) {
-  using OA = Operand<BM, AM, BK>;
-  using OB = Operand<BN, BMD, BK>;
+  using OA = Operand<BM, AM>;
+  using OB = Operand<BN, BMD>;
   constexpr int STAGE = OA::LDS + OB::LDS;
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 32, FN = WN / 32;
   constexpr int CP = WN + 4;                  // padded row pitch of a wave's staged 32-row C slab
@@ -479,12 +481,12 @@ __global__ __launch_bounds__(kGB, 2) void gemm_f32_kernel(GemmParams p) {
     }
 }
 
-template <int BM, int BN, int AM, int BMD, int BKT = 32>
+template <int BM, int BN, int AM, int BMD>
 int launch_cfg(GemmParams p, hipStream_t stream) {
   p.tiles_m = (p.M + BM - 1) / BM;
   p.tiles_n = (p.N + BN - 1) / BN;
   const int64_t blocks = (int64_t)p.tiles_m * p.tiles_n * p.splits;
-  gemm_f32_kernel<BM, BN, AM, BMD, BKT><<<(unsigned)blocks, kGB, 0, stream>>>(p);
+  gemm_f32_kernel<BM, BN, AM, BMD><<<(unsigned)blocks, kGB, 0, stream>>>(p);
   return p.tiles_m;
 }
 
@@ -506,7 +508,8 @@ int launch_layout(GemmParams p, hipStream_t stream) {
 }  // namespace
 
 namespace {
-// tile: 0 = by the launcher's rule, 1 = 128x128, 2 = 128x64, 3 = 64x128, 4 = 64x64 (5-7 = 2-4)
+// tile: 0 = by the launcher's rule, 1 = 128x128, 2 = 128x64, 3 = 64x128, 4 = 64x64 (the bindings
+// reject anything else)
 template <int AM, int BMD>
 int launch_tile(GemmParams p, int tile, hipStream_t stream) {
   switch (tile) {
@@ -514,12 +517,6 @@ int launch_tile(GemmParams p, int tile, hipStream_t stream) {
     case 2: return launch_cfg<128, 64, AM, BMD>(p, stream);
     case 3: return launch_cfg<64, 128, AM, BMD>(p, stream);
     case 4: return launch_cfg<64, 64, AM, BMD>(p, stream);
-    // 5-7: the 64-k-slice variants of 2-4.  Their LDS (70-104 KB of static shared memory) coincided
-    // with intermittent aborts inside forked HIP-graph captures on ROCm 7.2, and they won no
-    // direction in situ by more than 1 us (profiles/r4_autotune_decisions.txt): mapped to 2-4
-    case 5: return launch_cfg<128, 64, AM, BMD>(p, stream);
-    case 6: return launch_cfg<64, 128, AM, BMD>(p, stream);
-    case 7: return launch_cfg<64, 64, AM, BMD>(p, stream);
     default: return launch_layout<AM, BMD>(p, stream);
   }
 }
@@ -534,10 +531,10 @@ int auto_splits(int M, int N, int K, int64_t ldc) {
 }
 
 // splits -> k per split (multiple of BK), C zeroed for split-K; returns whether atomic
-void set_splits(GemmParams& p, int splits, float* stats, hipStream_t stream, int bk = BK) {
+void set_splits(GemmParams& p, int splits, float* stats, hipStream_t stream) {
   if (splits < 1) splits = 1;
   int kps = (p.K + splits - 1) / splits;
-  kps = (kps + bk - 1) / bk * bk;
+  kps = (kps + BK - 1) / BK * BK;
   splits = p.K > 0 ? (p.K + kps - 1) / kps : 1;
   p.splits = splits;
   p.k_per_split = kps;

@@ -2,7 +2,13 @@
 
 Devlin et al. (2019): 12 layers, hidden 768, 12 heads, FFN 3072, vocab 30,522, max positions
 512, GELU, post-LayerNorm, MLM head tied to the word embeddings (110M parameters).
-Attention uses ``F.scaled_dot_product_attention`` (fused flash kernels on ROCm).
+Attention: ``F.scaled_dot_product_attention`` without dropout (eval / p = 0); in training with
+attention dropout the explicit softmax -> dropout -> matmul form.  The fused fp32 SDPA kernel's
+dropout on this ROCm build is not safe under HIP-graph replay: once the host has synchronised with
+the device at any point, the 12th replay onwards regenerates a backward dropout mask that differs
+from the forward's, and training diverges to NaN within ~8 steps (bench.py's bert rows of round 4;
+tools/gpu/bert_graph_nosync.py isolates it: attention dropout only, hidden dropouts fine, the math
+form fine; profiles/r5_bert_graph_dropout.txt).
 """
 import math
 
@@ -26,7 +32,13 @@ class Layer(nn.Module):
     def forward(self, x, mask=None):
         B, T, D = x.shape
         q, k, v = self.qkv(x).view(B, T, 3, self.h, D // self.h).permute(2, 0, 3, 1, 4)
-        a = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, dropout_p=self.p if self.training else 0.0)
+        if self.training and self.p > 0:
+            s = torch.matmul(q, k.transpose(-2, -1)) * (1.0 / math.sqrt(D // self.h))
+            if mask is not None:
+                s = s + mask
+            a = torch.matmul(F.dropout(torch.softmax(s, dim=-1), self.p, True), v)
+        else:
+            a = F.scaled_dot_product_attention(q, k, v, attn_mask=mask)
         a = a.transpose(1, 2).reshape(B, T, D)
         x = self.ln1(x + F.dropout(self.o(a), self.p, self.training))
         y = self.ff2(F.dropout(F.gelu(self.ff1(x)), 0.0, self.training))

@@ -334,7 +334,7 @@ class _Conv1x1StatsFn(torch.autograd.Function):
 
 
 def _tiles_m(m: int, tile: int) -> int:
-    return (m + 127) // 128 if tile in (1, 2, 5) else (m + 63) // 64  # (5-7 alias 2-4)
+    return (m + 127) // 128 if tile in (1, 2) else (m + 63) // 64
 
 
 # (M, Cin, Cout, relu, residual) -> "unfused" | "stats_t<tile>" ; measured ms per candidate

@@ -45,13 +45,12 @@ def test_gemm_f32_layouts(a_kc, b_kc, m, n, k, splits):
     assert (err <= bound).all(), err.max()
 
 
-@pytest.mark.parametrize("tile", [5, 6, 7])
+@pytest.mark.parametrize("tile", [1, 2, 3, 4])
 @pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, False), (False, True)])
 @pytest.mark.parametrize("m,n,k,splits", [(200, 132, 68, 1), (64, 256, 1000, 4), (333, 520, 96, 3),
                                           (1568, 512, 2048, 0)])
-def test_gemm_f32_64k_slices(tile, a_kc, b_kc, m, n, k, splits):
-    """Tile codes 5-7 (the 64-k-slice variants, now launched as tiles 2-4): K not a multiple of 64,
-    split-K, ragged edges."""
+def test_gemm_f32_forced_tiles(tile, a_kc, b_kc, m, n, k, splits):
+    """Every forced tile shape: K not a multiple of the 32-k slice, split-K, ragged edges."""
     g = torch.Generator().manual_seed(m * 3 + n + tile)
     if not a_kc and m % 4:
         m += 4 - m % 4
@@ -66,6 +65,15 @@ def test_gemm_f32_64k_slices(tile, a_kc, b_kc, m, n, k, splits):
     err = (c.double().cpu() - ref).abs()
     assert torch.isfinite(c).all()
     assert (err <= bound).all(), err.max()
+
+
+def test_gemm_f32_rejects_removed_tile_codes():
+    """The 64-k-slice tile codes 5-7 were deleted (round 5): the binding refuses them."""
+    a = torch.randn(64, 64, device="cuda")
+    c = torch.empty(64, 64, device="cuda")
+    for tile in (5, 7, -1):
+        with pytest.raises(RuntimeError, match="tile"):
+            gemm(a, True, 64, a, True, 64, c, 64, 64, 64, 64, 1, tile)
 
 
 @pytest.mark.parametrize("nb,cin,cout,hw", [(4, 64, 256, 14), (2, 256, 64, 7), (3, 128, 512, 5), (2, 512, 128, 9)])

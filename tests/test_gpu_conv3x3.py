@@ -41,7 +41,7 @@ def _close(got, ref, what):
 
 
 @pytest.mark.parametrize("shape", SHAPES)
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4])
 def test_conv3x3_implicit_gemm_directions(shape, tile):
     N, Cin, H, W, Cout, s = shape
     x, w, dy = _data(*shape, seed=tile)
