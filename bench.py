@@ -201,12 +201,12 @@ def main():
     # a gloo group cannot capture its collectives, but an ALL-GATHER-only pipeline's exchange can
     # run on the xGMI one-shot comm (peer memory, gloo only bootstraps it): that is the W > 1
     # whole-step-graph rehearsal on a 1-GPU box (ranks share the card)
-    # (all-gather pipelines, and linear codecs under Allreduce: XgmiComm's one-shot gather + local
-    # rank-ordered reduction when the bucket fits --xgmi-capacity-mb)
+    # (every Allgather / Allreduce pipeline: XgmiComm gathers one-shot, all-reduces by a one-shot
+    # gather + rank-ordered local reduction -- PowerSGD's P / Q, DGC's clipping norm, the dense
+    # buckets -- and runs QSGD's compressed-domain all-to-all one-shot, all while the payload fits
+    # --xgmi-capacity-mb; tests/test_gpu_xgmi.py checks each against an eager W = 2 run)
     gloo_graph = (gloo and world > 1 and args.comm in ("xgmi", "auto") and args.surface == "engine"
-                  and (w.grace.get("communicator") == "allgather"
-                       or (w.grace.get("communicator") == "allreduce" and w.grace.get("compressor") in ("none", "fp16")))
-                  and w.grace.get("compressor") not in ("powersgd",) and w.grace.get("memory") != "dgc")
+                  and w.grace.get("communicator") in ("allgather", "allreduce"))
     if args.surface == "ddp" and mode == "auto":
         # the whole DDP step (reducer + comm hook) captures: 2341 vs 2309 img/s eager
         # (profiles/r3_ddp_surface.txt); a failed capture falls back to eager below
@@ -226,16 +226,27 @@ def main():
         args.overlap = "off"
     # --overlap auto under the whole-step graph: on only when the exchange could hide more than a
     # forked capture costs.  Fork cost: ~0.9 ms/step for ResNet-50 (profiles/r2_overlap_buckets.txt).
-    # Exchange estimate: a dense ring-equivalent 2 (W-1)/W x bytes over the 7 xGMI links per GPU at
-    # ~50 GB/s effective each -- the uncompressed 102 MB ResNet-50 gradient at W = 8 is ~0.5 ms,
-    # every compressed pipeline far less: off.  The W = 2 rehearsal (two ranks SHARING one GPU,
-    # profiles/r4_overlap_w2_rehearsal.txt: on 2986 vs off 2354 img/s Top-K, 2935 vs 2489 None)
-    # measures the shared card -- an early rank's in-line pull kernel spins on the compute stream
-    # the other rank needs -- not separate GPUs, where that spin blocks nothing.
+    # Exchange time: MEASURED for the dense pipelines -- the RCCL channel-budget probe
+    # (RcclComm.tuned, run here ahead of the decision) all-reduces the real bucket on the real links
+    # and its best time (MAX over ranks) is the exchange the fork could hide; every compressed
+    # pipeline's exchange is a few-MB gather: off.  (The W = 2 rehearsal with two ranks SHARING one
+    # GPU, profiles/r4_overlap_w2_rehearsal.txt, measures the shared card, not links.)
+    dense_ar = w.grace.get("communicator") == "allreduce" and w.grace.get("compressor") in ("none", "fp16")
+    rccl_pre = None
+    overlap_note = None
+    if (world > 1 and not gloo and dense_ar and args.rccl_ctas == "auto" and args.surface == "engine"
+            and mode == "full" and args.comm in ("auto", "native", "native-inline", "xgmi")):
+        from grace_amd.parallel.native_comm import RcclComm
+
+        esz = 2 if w.grace.get("compressor") == "fp16" else 4
+        nbytes = min(sum(p.numel() for p in model.parameters()) * esz, int(args.bucket_mb * 2 ** 20))
+        rccl_pre = RcclComm.tuned(nbytes)  # collective: every rank builds / probes the candidates
     if args.overlap == "auto" and mode == "full" and world > 1:
-        dense = w.grace.get("compressor") in ("none", "fp16")
-        grad_bytes = sum(p.numel() for p in model.parameters()) * (2 if w.grace.get("compressor") == "fp16" else 4)
-        est_ms = (2.0 * (world - 1) / world * grad_bytes / (7 * 50e9) * 1e3) if dense else 0.0
+        est_ms = 0.0
+        if rccl_pre is not None:
+            n_buckets = max(1, -(-sum(p.numel() for p in model.parameters()) * 4 // int(args.bucket_mb * 2 ** 20)))
+            est_ms = min(rccl_pre.choice["us"].values()) * n_buckets / 1e3
+            overlap_note = f"measured dense all-reduce {est_ms:.3f} ms/step vs ~0.9 ms forked-capture cost"
         args.overlap = "on" if est_ms > 0.9 else "off"
     overlap = args.overlap == "on" or (args.overlap == "auto" and mode != "full")
     comm_kind = "local"
@@ -263,9 +274,10 @@ def main():
                     native = TorchComm()
                 else:
                     inl = comm_kind in ("native-inline", "xgmi", "auto-probe")
-                    dense_ar = (w.grace.get("communicator") == "allreduce"
-                                and w.grace.get("compressor") in ("none", "fp16"))
-                    if args.rccl_ctas == "auto" and world > 1 and dense_ar:
+                    if rccl_pre is not None:  # probed above (the overlap decision used its time)
+                        rccl_pre.set_inline(inl)
+                        native = rccl_pre
+                    elif args.rccl_ctas == "auto" and world > 1 and dense_ar:
                         # the dense all-reduce's channel budget for the 7-link mesh, measured on the
                         # real bucket: one ring drives one outbound link per GPU
                         esz = 2 if w.grace.get("compressor") == "fp16" else 4
@@ -527,6 +539,7 @@ def main():
                 "grace": w.grace,
                 "bucket_mb": args.bucket_mb,
                 "overlap": overlap,
+                **({"overlap_rule": overlap_note} if overlap_note else {}),
                 "hip_graph": graph_note,
                 "comm": comm_kind,
                 "grad_mode": args.grad_mode,

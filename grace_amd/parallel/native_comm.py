@@ -183,6 +183,11 @@ class RcclComm(_comm.Comm):
             _agree(ok, None)
         return bool(ok)
 
+    def set_inline(self, on: bool) -> None:
+        """Issue on the caller's current stream (True) or the comm stream (False) from now on."""
+        self._c.inline = bool(on)
+        self.inline = bool(on)
+
     @property
     def stream(self) -> torch.cuda.Stream:
         return self._stream

@@ -8,6 +8,13 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+# the suite runs the BN backward on the fixed-order fp64 tree (bitwise reproducible, VERDICT r4
+# hygiene): fixtures that test the atomic-totals path switch it on for their own duration only
+os.environ.setdefault("GRACE_BN_DETERMINISTIC", "1")
+
+
+def bn_det_default() -> bool:
+    return os.environ.get("GRACE_BN_DETERMINISTIC") == "1"
 
 
 def pytest_configure(config):

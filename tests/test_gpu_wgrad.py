@@ -1,6 +1,7 @@
 """GPU: weight gradients on the side stream (grace_amd/ops/wgrad.py) give the same gradients as the
 in-line backward -- eagerly, through the GRACE engine's bucket gather, and inside a captured
 whole-step HIP graph (the fork is a parallel graph branch)."""
+import os
 import pytest
 import torch
 import torch.nn.functional as F
@@ -30,7 +31,7 @@ def bn_deterministic():
 
     _native.lib().bn_set_deterministic(True)
     yield
-    _native.lib().bn_set_deterministic(False)
+    _native.lib().bn_set_deterministic(os.environ.get("GRACE_BN_DETERMINISTIC") == "1")
 
 
 def _grads(model, x, y):
