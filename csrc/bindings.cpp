@@ -164,41 +164,6 @@ void sparse_scatter_add_dev(const Tensor& val, const Tensor& idx, const Tensor& 
                                 count_overflow);
 }
 
-void sparse_decode_ranks(const std::vector<Tensor>& vals, const std::vector<Tensor>& idxs,
-                         const std::vector<c10::optional<Tensor>>& counts, const Tensor& out, double scale,
-                         const Tensor& ctr, int64_t own) {
-  const int W = (int)vals.size();
-  TORCH_CHECK(W >= 1 && W <= grace::kDecodeMaxRanks, "sparse_decode_ranks: 1..", grace::kDecodeMaxRanks, " ranks");
-  TORCH_CHECK((int)idxs.size() == W && (int)counts.size() == W, "sparse_decode_ranks: per-rank list sizes differ");
-  CHECK_F32(out);
-  CHECK_I32(ctr);
-  TORCH_CHECK(ctr.numel() >= 2 && ctr.device() == out.device(), "sparse_decode_ranks: ctr");
-  TORCH_CHECK(out.numel() < (int64_t(1) << 31), "sparse_decode_ranks: int32 indices");
-  const float* v[grace::kDecodeMaxRanks];
-  const int32_t* ix[grace::kDecodeMaxRanks];
-  const int32_t* c[grace::kDecodeMaxRanks];
-  int64_t cap[grace::kDecodeMaxRanks];
-  for (int r = 0; r < W; ++r) {
-    CHECK_F32(vals[r]);
-    CHECK_I32(idxs[r]);
-    TORCH_CHECK(vals[r].numel() == idxs[r].numel(), "sparse_decode_ranks: val/idx size mismatch at rank ", r);
-    TORCH_CHECK(vals[r].device() == out.device() && idxs[r].device() == out.device(), "sparse_decode_ranks: device");
-    v[r] = vals[r].data_ptr<float>();
-    ix[r] = idxs[r].data_ptr<int32_t>();
-    cap[r] = vals[r].numel();
-    c[r] = nullptr;
-    if (counts[r].has_value()) {
-      CHECK_I32((*counts[r]));
-      TORCH_CHECK(counts[r]->numel() >= 1 && counts[r]->device() == out.device(), "sparse_decode_ranks: count");
-      c[r] = counts[r]->data_ptr<int32_t>();
-    }
-  }
-  DevGuard guard(out.device());
-  grace::sparse_decode_ranks(W, v, ix, c, cap, out.data_ptr<float>(), out.numel(), (float)scale,
-                             ctr.data_ptr<int32_t>(), grace::health_dev(out.device().index()), cur_stream(),
-                             (int)own);
-}
-
 void sparse_scatter_add(const Tensor& val, const Tensor& idx, const Tensor& out, double scale,
                         bool accumulate) {
   CHECK_F32(val);
@@ -1147,8 +1112,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sparse_scatter_add", &sparse_scatter_add);
   m.def("sparse_scatter_add_dev", &sparse_scatter_add_dev, py::arg("val"), py::arg("idx"), py::arg("count"),
         py::arg("out"), py::arg("scale"), py::arg("accumulate"), py::arg("count_overflow") = false);
-  m.def("sparse_decode_ranks", &sparse_decode_ranks, py::arg("vals"), py::arg("idxs"), py::arg("counts"),
-        py::arg("out"), py::arg("scale"), py::arg("ctr"), py::arg("own") = (int64_t)-1);
   m.def("segment_stats", &segment_stats);
   m.def("randk_gather", &randk_gather);
   m.def("randk_scatter", &randk_scatter);

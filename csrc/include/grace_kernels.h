@@ -38,15 +38,6 @@ void sparse_scatter_add(const float* val, const int32_t* idx, int64_t K, float* 
 // count_overflow: count *count > cap in the health words (the decode of this process's OWN payload)
 void sparse_scatter_add_dev(const float* val, const int32_t* idx, const int32_t* count, int64_t cap, float* out,
                             float scale, bool accumulate, hipStream_t stream, bool count_overflow);
-// One launch: out = 0, then out[idx_r[j]] += scale * val_r[j] for r = 0..W-1 in rank order
-// (grid barriers between ranks; bit-identical to the sequential per-rank loop).  count[r] may be
-// null (K = cap[r]) or an in-band count (K = min(*count[r], cap[r])).  ctr: 2 int32 of device
-// memory, zero before the first launch, left zero by every launch (stream-ordered reuse).
-constexpr int kDecodeMaxRanks = 32;
-void sparse_decode_ranks(int W, const float* const* val, const int32_t* const* idx, const int32_t* const* count,
-                         const int64_t* cap, float* out, int64_t n, float scale, int32_t* ctr,
-                         uint32_t* health_dev, hipStream_t stream, int own);  // own: the rank whose
-                                                                                // overflow is counted (-1: none)
 
 // ---------------------------------------------------------------- segstats.hip
 // per segment: [sum, sumsq, max|x|, sum|x|, sum(x<0), count(x<0)]

@@ -13,9 +13,8 @@ MI355X kernels (csrc/kernels/topk.hip):
   sent entries zeroed) is written by the compaction pass: the reference's second decompress
   (residual.py:17) disappears.
 * ``decompress_aggregate``: the W payloads added in fixed rank order into the zeroed bucket
-  (ops/cappayload.py decode_ranks: fill + atomic-free scatters, or one launch with grid barriers
-  under GRACE_DECODE_ONE_LAUNCH=1), with the 1/W average folded in -> bitwise identical on every
-  rank.
+  (ops/cappayload.py decode_ranks: fill + atomic-free scatters), with the 1/W average folded in
+  -> bitwise identical on every rank.
 """
 from __future__ import annotations
 

@@ -58,29 +58,6 @@ def scatter_capped(hdr: torch.Tensor, vals: torch.Tensor, idx: torch.Tensor, out
         out[il] = vals[:k] * scale
 
 
-MAX_DECODE_RANKS = 32  # csrc/include/grace_kernels.h kDecodeMaxRanks
-_DECODE_CTR = {}
-# the one-launch decode (csrc/kernels/sparse_decode.hip) is opt-in: stand-alone it is as fast as a
-# zero fill + W scatter launches on a ResNet-50 bucket (23.6 / 32.3 / 50.0 / 85.4 us at W = 1 / 2 /
-# 4 / 8 vs 23.5 / 32.3 / 50.0 / 85.5, graph-replayed, bit-identical; profiles/r4_decode_bench.txt),
-# but inside the whole-step graph its grid barriers wait on workgroups that share the chip with the
-# side-stream weight gradients still running: 51 us vs ~28 us for the fill + scatter
-# (profiles/r4_final_headline_graph_kernels.txt).  Its first form (plain zero stores, RMW through
-# the L2s) paid an agent-scope write-back of the zeroed bucket at every barrier: 65-480 us.
-ONE_LAUNCH = __import__("os").environ.get("GRACE_DECODE_ONE_LAUNCH", "0") == "1"
-
-
-def _decode_ctr(device) -> torch.Tensor:
-    """The decode kernel's barrier counters, one pair per (device, stream): launches on one stream
-    are ordered and each leaves its counters zero, so they can share them."""
-    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
-    c = _DECODE_CTR.get(key)
-    if c is None:
-        c = torch.zeros(2, dtype=torch.int32, device=device)
-        _DECODE_CTR[key] = c
-    return c
-
-
 def set_own_rank(ctx, rank) -> None:
     """Record the decoding process's rank on a compress ctx (the communicators do, before the
     decode): the decoders count capacity overflows for that payload only."""
@@ -102,14 +79,10 @@ def decode_ranks(vals, idxs, counts, out: torch.Tensor, scale: float = 1.0, own=
     """``out`` = 0, then ``out[idxs[r]] += vals[r] * scale`` for r = 0..W-1 in rank order --
     bit-identical on every rank.  ``counts[r]``: None (every entry) or the payload's in-band count
     word (capacity payloads: the first min(count, capacity) entries).  Native path: a zero fill plus
-    W atomic-free scatter launches; ``GRACE_DECODE_ONE_LAUNCH=1``: ONE launch (zero + W rank phases
-    behind grid barriers, csrc/kernels/sparse_decode.hip) -- slower inside the step, see ONE_LAUNCH.
+    W atomic-free scatter launches.  (A one-launch form -- zero + W rank phases behind grid barriers
+    -- was measured in round 4: as fast stand-alone, 51 vs ~28 us inside the whole-step graph where
+    its barriers wait on workgroups sharing the chip with side-stream weight gradients; deleted.)
     ``own``: this process's rank -- only that payload's overflow is counted (health.overflows())."""
-    W = len(vals)
-    if ONE_LAUNCH and _native.use_native(out) and 1 <= W <= MAX_DECODE_RANKS and out.is_contiguous():
-        _native.lib().sparse_decode_ranks(list(vals), list(idxs), [None if c is None else c[:1] for c in counts],
-                                          out, float(scale), _decode_ctr(out.device), -1 if own is None else int(own))
-        return out
     out.zero_()
     native = _native.use_native(out)
     for r, (v, i, c) in enumerate(zip(vals, idxs, counts)):  # fixed rank order: identical on every rank

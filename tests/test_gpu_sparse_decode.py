@@ -1,15 +1,18 @@
-"""GPU numerics: the one-launch rank-ordered sparse decode (csrc/kernels/sparse_decode.hip) against
-the plain fp32 PyTorch loop ``out = 0; out.index_add_(0, idx_r, v_r * s)`` for r = 0..W-1 --
-bit-identical, including overlapping indices across ranks, in-band counts (capacity payloads),
-unaligned outputs, repeated launches and HIP-graph replay; and a W = 4 exchange (4 ranks on one
-GPU over gloo) whose Top-K / Threshold decodes are single launches, identical on every rank."""
+"""GPU numerics: the rank-ordered sparse decode (``cappayload.decode_ranks``: a zero fill plus one
+native scatter launch per rank) against the plain fp32 PyTorch loop
+``out = 0; out.index_add_(0, idx_r, v_r * s)`` for r = 0..W-1 -- including overlapping indices
+across ranks, in-band counts (capacity payloads, overflow counted for the own payload only),
+unaligned outputs and HIP-graph replay; and a W = 4 exchange (4 ranks on one GPU over gloo) whose
+Top-K / Threshold decodes leave identical weights on every rank.
+
+(The round-4 one-launch grid-barrier decode was deleted in round 5: it never beat this path inside
+the whole-step graph, profiles/r4_final_headline_graph_kernels.txt.)"""
 import os
 import sys
 
 import pytest
 import torch
 
-from grace_amd.ops import _native
 from grace_amd.ops import cappayload as P
 
 sys.path.insert(0, os.path.dirname(__file__))
@@ -49,36 +52,15 @@ def _gpu(xs):
     return [None if x is None else x.cuda() for x in xs]
 
 
-@pytest.fixture(autouse=True)
-def _one_launch():
-    """These tests exercise the opt-in one-launch kernel (the default decode is the rank loop)."""
-    old = P.ONE_LAUNCH
-    P.ONE_LAUNCH = True
-    yield
-    P.ONE_LAUNCH = old
-
-
-def _loop(vals, idxs, cnts, n, scale):
-    """The default GPU decode: zero fill + one native scatter launch per rank."""
-    old = P.ONE_LAUNCH
-    P.ONE_LAUNCH = False
-    try:
-        out = torch.full((n,), 5.0, device="cuda")
-        return P.decode_ranks(_gpu(vals), _gpu(idxs), _gpu(cnts), out, scale)
-    finally:
-        P.ONE_LAUNCH = old
-
-
 @pytest.mark.parametrize("W,n,k", [(1, 1000, 10), (3, 1_000_003, 20_000), (8, 257, 100), (20, 300_001, 3000)])
-def test_decode_matches_rank_loop(W, n, k):
+def test_decode_matches_fp32_reference(W, n, k):
     vals, idxs, cnts = _payloads(W, n, k, seed=W)
-    out = torch.full((n,), 7.0, device="cuda")  # garbage: the kernel zeroes
+    out = torch.full((n,), 7.0, device="cuda")  # garbage: the decode zeroes
     P.decode_ranks(_gpu(vals), _gpu(idxs), cnts, out, 1.0 / W)
-    loop = _loop(vals, idxs, cnts, n, 1.0 / W)
-    diff = (out != loop).nonzero().flatten()
-    assert diff.numel() == 0, f"{diff.numel()} entries differ from the rank loop, e.g. {diff[:5].tolist()}"
-    ref = _ref(vals, idxs, cnts, n, 1.0 / W)
-    torch.testing.assert_close(loop.cpu(), ref, rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(out.cpu(), _ref(vals, idxs, cnts, n, 1.0 / W), rtol=1e-6, atol=1e-7)
+    again = torch.full((n,), -3.0, device="cuda")
+    P.decode_ranks(_gpu(vals), _gpu(idxs), cnts, again, 1.0 / W)
+    assert torch.equal(out, again)  # rank-ordered, atomic-free: the same bits on every call (and rank)
 
 
 def test_decode_counts_unaligned_and_overflow():
@@ -99,23 +81,19 @@ def test_decode_counts_unaligned_and_overflow():
     big = torch.full((n + 3,), -1.0, device="cuda")
     out = big[1:n + 1]  # 4-B aligned, not 16-B aligned
     P.decode_ranks(_gpu(vals), _gpu(idxs), _gpu(cnts), out, 0.5)
-    assert torch.equal(out, _loop(vals, idxs, cnts, n, 0.5))
+    torch.testing.assert_close(out.cpu(), _ref(vals, idxs, cnts, n, 0.5), rtol=1e-6, atol=1e-7)
     assert big[0].item() == -1.0 and big[n + 1].item() == -1.0 and big[n + 2].item() == -1.0
-    assert health.status()[0] == 0  # every barrier completed
 
 
-def test_decode_repeated_and_graph_replay():
+def test_decode_graph_replay():
     W, n, k = 4, 200_000, 5000
     vals, idxs, cnts = _payloads(W, n, k, seed=3)
     gv, gi = _gpu(vals), _gpu(idxs)
     out = torch.empty(n, device="cuda")
-    for _ in range(3):  # the counters are left zero by every launch
-        P.decode_ranks(gv, gi, cnts, out, 0.25)
-    assert torch.equal(out, _loop(vals, idxs, cnts, n, 0.25))
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
-        P.decode_ranks(gv, gi, cnts, out, 0.25)  # counters for the capture stream, allocated eagerly
+        P.decode_ranks(gv, gi, cnts, out, 0.25)
     torch.cuda.current_stream().wait_stream(s)
     graph = torch.cuda.CUDAGraph()
     with torch.cuda.graph(graph, stream=s):
@@ -128,7 +106,7 @@ def test_decode_repeated_and_graph_replay():
             a.copy_(b)
         graph.replay()
         torch.cuda.synchronize()
-        assert torch.equal(out, _loop(vals2, idxs2, cnts, n, 0.25)), step
+        torch.testing.assert_close(out.cpu(), _ref(vals2, idxs2, cnts, n, 0.25), rtol=1e-6, atol=1e-7)
 
 
 def _w4_body(rank, world):
@@ -137,47 +115,25 @@ def _w4_body(rank, world):
     from test_distributed_gloo import _same_on_all_ranks
 
     dev = torch.device("cuda", 0)
-    calls = {"n": 0}
-    lib = _native.lib()
-    real = lib.sparse_decode_ranks
-
-    class Counting:  # count the one-launch decodes; the per-rank scatter must not run
-        def __getattr__(self, name):
-            if name == "sparse_decode_ranks":
-                def f(*a):
-                    calls["n"] += 1
-                    return real(*a)
-                return f
-            if name in ("sparse_scatter_add", "sparse_scatter_add_dev"):
-                raise AssertionError("per-rank scatter launched")
-            return getattr(lib, name)
-
-    _native._lib = Counting()
-    P.ONE_LAUNCH = True  # opt-in path under test (the fixture does not reach a spawned worker)
-    try:
-        for comp in ({"compressor": "topk", "compress_ratio": 0.05, "memory": "residual", "communicator": "allgather"},
-                     {"compressor": "threshold", "threshold": 0.5, "memory": "residual", "communicator": "allgather"}):
-            torch.manual_seed(0)
-            net = torch.nn.Sequential(torch.nn.Linear(64, 256), torch.nn.ReLU(), torch.nn.Linear(256, 10)).to(dev)
-            grc = grace_from_params(dict(comp, world_size=world))
-            params = list(net.parameters())
-            opt = DistributedOptimizer(FusedSGD(params, lr=0.1, momentum=0.5), grc,
-                                       named_parameters=list(net.named_parameters()), bucket_cap_mb=0.05)
-            g = torch.Generator().manual_seed(100 + rank)  # rank-specific data
-            calls["n"] = 0
-            for _ in range(3):
-                x = torch.randn(16, 64, generator=g).to(dev)
-                opt.zero_grad()
-                net(x).square().mean().backward()
-                opt.step()
-            torch.cuda.synchronize()
-            assert calls["n"] == 3 * len(opt.engine.buckets), (comp["compressor"], calls["n"])
-            for p in params:
-                _same_on_all_ranks(p)
-            opt.engine.remove()
-    finally:
-        _native._lib = lib
+    for comp in ({"compressor": "topk", "compress_ratio": 0.05, "memory": "residual", "communicator": "allgather"},
+                 {"compressor": "threshold", "threshold": 0.5, "memory": "residual", "communicator": "allgather"}):
+        torch.manual_seed(0)
+        net = torch.nn.Sequential(torch.nn.Linear(64, 256), torch.nn.ReLU(), torch.nn.Linear(256, 10)).to(dev)
+        grc = grace_from_params(dict(comp, world_size=world))
+        params = list(net.parameters())
+        opt = DistributedOptimizer(FusedSGD(params, lr=0.1, momentum=0.5), grc,
+                                   named_parameters=list(net.named_parameters()), bucket_cap_mb=0.05)
+        g = torch.Generator().manual_seed(100 + rank)  # rank-specific data
+        for _ in range(3):
+            x = torch.randn(16, 64, generator=g).to(dev)
+            opt.zero_grad()
+            net(x).square().mean().backward()
+            opt.step()
+        torch.cuda.synchronize()
+        for p in params:
+            _same_on_all_ranks(p)
+        opt.engine.remove()
 
 
-def test_four_ranks_one_decode_launch_identical():
+def test_four_ranks_decode_identical():
     run_distributed(_w4_body, 4)

@@ -216,16 +216,24 @@ def test_projection_branch_stream_matches_inline():
         (y * y).sum().backward()
         return [y.detach().clone(), xi.grad.clone()] + [p.grad.clone() for p in blk.parameters()]
 
+    # the parameters' AccumulateGrad nodes were created by the in-line runs on the current stream;
+    # with the branch on, the shortcut's gradients arrive from the branch stream -- the cross-stream
+    # hand-off this opt-in mode pays for (wgrad.py ``branch``), so autograd's mismatch note is expected
+    warn = getattr(torch.autograd.graph, "set_warn_on_accumulate_grad_stream_mismatch", None)
     wgrad._BRANCH = False
     try:
         run()
         ref = run()
         wgrad._BRANCH = True
+        if warn is not None:
+            warn(False)
         for _ in range(2):
             for a, b in zip(run(), ref):
                 _close(a, b)
     finally:
         wgrad._BRANCH = False
+        if warn is not None:
+            warn(True)
 
 
 def test_deferred_wgrad_engine_graph(bn_deterministic):
