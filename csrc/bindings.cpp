@@ -21,18 +21,25 @@ using DevGuard = c10::hip::HIPGuardMasqueradingAsCUDA;
 #define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
 #define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
 #define CHECK_DT(t, dt) TORCH_CHECK((t).scalar_type() == (dt), #t " must be " #dt)
-#define CHECK_F32(t) \
-  CHECK_DEV(t);      \
-  CHECK_CONTIG(t);   \
-  CHECK_DT(t, at::kFloat)
-#define CHECK_I32(t) \
-  CHECK_DEV(t);      \
-  CHECK_CONTIG(t);   \
-  CHECK_DT(t, at::kInt)
-#define CHECK_I64(t) \
-  CHECK_DEV(t);      \
-  CHECK_CONTIG(t);   \
-  CHECK_DT(t, at::kLong)
+// one statement each (safe under an unbraced `if`)
+#define CHECK_F32(t)         \
+  do {                       \
+    CHECK_DEV(t);            \
+    CHECK_CONTIG(t);         \
+    CHECK_DT(t, at::kFloat); \
+  } while (0)
+#define CHECK_I32(t)       \
+  do {                     \
+    CHECK_DEV(t);          \
+    CHECK_CONTIG(t);       \
+    CHECK_DT(t, at::kInt); \
+  } while (0)
+#define CHECK_I64(t)        \
+  do {                      \
+    CHECK_DEV(t);           \
+    CHECK_CONTIG(t);        \
+    CHECK_DT(t, at::kLong); \
+  } while (0)
 
 inline const int64_t* opt_i64(const c10::optional<Tensor>& t) {
   if (!t.has_value()) return nullptr;
@@ -547,7 +554,8 @@ void dgc_compensate(const Tensor& g, const Tensor& u, const Tensor& v, double mo
 // ------------------------------------------------------------------------------ PowerSGD
 void powersgd_mq(const Tensor& x, const Tensor& small, const Tensor& out, const Tensor& mats, const Tensor& tiles,
                  int64_t mode, const c10::optional<Tensor>& comp_r, double beta, double gamma,
-                 const c10::optional<Tensor>& xout, int64_t max_r) {
+                 const c10::optional<Tensor>& xout, int64_t max_r, const c10::optional<Tensor>& lazy_p,
+                 const c10::optional<Tensor>& lazy_q, double lazy_scale) {
   CHECK_F32(x);
   CHECK_F32(small);
   CHECK_F32(out);
@@ -557,10 +565,20 @@ void powersgd_mq(const Tensor& x, const Tensor& small, const Tensor& out, const 
   if (comp_r.has_value()) TORCH_CHECK(xout.has_value(), "comp_r needs xout");
   if (xout.has_value()) TORCH_CHECK(xout->numel() == x.numel(), "xout size");
   if (comp_r.has_value()) TORCH_CHECK(comp_r->numel() == x.numel(), "comp_r size");
+  TORCH_CHECK(lazy_p.has_value() == lazy_q.has_value(), "lazy_p and lazy_q go together");
+  if (lazy_p.has_value()) {
+    TORCH_CHECK(comp_r.has_value(), "the deferred residual needs comp_r (the previous M)");
+    CHECK_F32((*lazy_p));
+    CHECK_F32((*lazy_q));
+    // the previous P / Q share this plan's layout: P [p_total] = out's size, Q [q_total] = small's
+    TORCH_CHECK(lazy_p->numel() == out.numel() && lazy_q->numel() == small.numel(), "lazy P / Q sizes");
+    TORCH_CHECK(lazy_p->data_ptr() != out.data_ptr(), "lazy P must not alias the P being written");
+  }
   DevGuard guard(x.device());
   grace::powersgd_mq(x.data_ptr<float>(), small.data_ptr<float>(), out.data_ptr<float>(), out.numel(),
                      mats.data_ptr<int64_t>(), tiles.data_ptr<int32_t>(), (int)(tiles.numel() / 3), (int)mode,
-                     opt_f32(comp_r), (float)beta, (float)gamma, opt_f32_mut(xout), (int)max_r, cur_stream());
+                     opt_f32(comp_r), (float)beta, (float)gamma, opt_f32_mut(xout), (int)max_r, cur_stream(),
+                     opt_f32(lazy_p), opt_f32(lazy_q), (float)lazy_scale);
 }
 
 void gram_orthonormalize(const Tensor& buf, const Tensor& mats, int64_t which, int64_t n_mat, const Tensor& gtiles,
@@ -579,16 +597,18 @@ void gram_orthonormalize(const Tensor& buf, const Tensor& mats, int64_t which, i
                              part.data_ptr<double>(), T.data_ptr<float>(), (int)passes, (int)max_r, cur_stream());
 }
 
-void powersgd_pqt(const Tensor& P, const Tensor& Q, const Tensor& out, const Tensor& mats, const Tensor& tiles,
-                  const c10::optional<Tensor>& resid, int64_t max_r, double scale) {
+void powersgd_pqt(const Tensor& P, const Tensor& Q, const c10::optional<Tensor>& out, const Tensor& mats,
+                  const Tensor& tiles, const c10::optional<Tensor>& resid, int64_t max_r, double scale) {
   CHECK_F32(P);
   CHECK_F32(Q);
-  CHECK_F32(out);
   CHECK_I64(mats);
   CHECK_I32(tiles);
-  if (resid.has_value()) TORCH_CHECK(resid->numel() == out.numel(), "resid size");
-  DevGuard guard(out.device());
-  grace::powersgd_pqt(P.data_ptr<float>(), Q.data_ptr<float>(), out.data_ptr<float>(), mats.data_ptr<int64_t>(),
+  TORCH_CHECK(out.has_value() || resid.has_value(), "powersgd_pqt: nothing to write");
+  if (out.has_value()) CHECK_F32((*out));
+  if (resid.has_value()) CHECK_F32((*resid));
+  if (resid.has_value() && out.has_value()) TORCH_CHECK(resid->numel() == out->numel(), "resid size");
+  DevGuard guard(P.device());
+  grace::powersgd_pqt(P.data_ptr<float>(), Q.data_ptr<float>(), opt_f32_mut(out), mats.data_ptr<int64_t>(),
                       tiles.data_ptr<int32_t>(), (int)(tiles.numel() / 3), opt_f32_mut(resid), (float)scale,
                       (int)max_r, cur_stream());
 }
@@ -1137,7 +1157,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("u") = py::none(), py::arg("v") = py::none(), py::arg("momentum") = 0.0, py::arg("first") = false);
   m.def("dgc_compact", &dgc_compact);
   m.def("dgc_compensate", &dgc_compensate);
-  m.def("powersgd_mq", &powersgd_mq);
+  m.def("powersgd_mq", &powersgd_mq, py::arg("x"), py::arg("small"), py::arg("out"), py::arg("mats"), py::arg("tiles"),
+        py::arg("mode"), py::arg("comp_r"), py::arg("beta"), py::arg("gamma"), py::arg("xout"), py::arg("max_r"),
+        py::arg("lazy_p") = py::none(), py::arg("lazy_q") = py::none(), py::arg("lazy_scale") = 0.0);
   m.def("gram_orthonormalize", &gram_orthonormalize);
   m.def("adaq_sample", &adaq_sample);
   m.def("adaq_prepare", &adaq_prepare);

@@ -107,13 +107,15 @@ void dgc_compensate(const float* g, float* u, float* v, float momentum, int64_t 
 // mats: int64 [n_mat][6] = (x_off, n, m, r, p_off, q_off); tiles: int32 [n_tiles][3]
 void powersgd_mq(const float* x, const float* small, float* out, int64_t out_len, const int64_t* mats,
                  const int32_t* tiles, int n_tiles, int mode, const float* comp_r, float beta, float gamma,
-                 float* xout, int max_r, hipStream_t stream);
+                 float* xout, int max_r, hipStream_t stream, const float* lazy_p = nullptr,
+                 const float* lazy_q = nullptr, float lazy_scale = 0.f);  // lazy_*: deferred residual (mode 0
+                                                                          // with comp_r): r = comp_r - s P Q^T
 // max_r: largest rank r of the matrices (<= 4 selects the one-launch, one-workgroup-per-matrix form)
 void gram_orthonormalize(float* buf, const int64_t* mats, int n_mat, int which, const int32_t* gtiles,
                          int n_gtiles, const int32_t* gtile_begin, double* partials, float* T, int passes,
                          int max_r, hipStream_t stream);
 void powersgd_pqt(const float* P, const float* Q, float* out, const int64_t* mats, const int32_t* tiles, int n_tiles,
-                  float* resid, float scale, int max_r, hipStream_t stream);
+                  float* resid, float scale, int max_r, hipStream_t stream);  // out may be null (resid only)
 void philox_normal(float* out, int64_t n, SeedArg seed, hipStream_t stream);
 
 // ---------------------------------------------------------------- cast_sketch.hip

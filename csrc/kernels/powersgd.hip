@@ -74,11 +74,20 @@ __device__ __forceinline__ void load_small_row(const float* __restrict__ S, int6
   }
 }
 
+// COMP 3 (deferred residual): cr holds the previous step's compensated M, and the residual
+// r = cr - ls * Pp Qp^T of that step (Pp / Qp: its final P and summed Q, ls = 1/W) is formed here,
+// with the float ops of ps_pqt's residual update, instead of being written by ps_pqt and read back.
+struct Lazy {
+  const float* p;
+  const float* q;
+  float s;
+};
+
 template <int R, int COMP>
 __global__ __launch_bounds__(kBlock) void ps_mq_kernel(const float* __restrict__ x, const float* __restrict__ Qall,
                                                        float* __restrict__ Pall, const int64_t* __restrict__ mats,
                                                        const int32_t* __restrict__ tiles, const float* cr, float beta,
-                                                       float gamma, float* xout) {
+                                                       float gamma, float* xout, Lazy lz) {
   const int* tl = tiles + 3 * blockIdx.x;
   const Mat mt = load_mat(mats, tl[0]);
   const int64_t n = mt.n, m = mt.m;
@@ -93,6 +102,24 @@ __global__ __launch_bounds__(kBlock) void ps_mq_kernel(const float* __restrict__
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int j = 0; j < R; ++j) acc[a][j] = 0.f;
+  float lp[COMP == 3 ? 4 : 1][R];  // the previous P rows of this wave's 4 rows (wave-uniform)
+  if constexpr (COMP == 3) {
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      if (row0 + rr < n)
+        load_small_row<R>(lz.p + mt.p_off, row0 + rr, r, lp[rr]);
+      else
+#pragma unroll
+        for (int j = 0; j < R; ++j) lp[rr][j] = 0.f;
+    }
+  }
+  // residual of the previous step at (row rr, column c + t): cr - ls * sum_j Pp[row, j] Qp[c + t, j]
+  auto lazy_o = [&](int rr, const float (&lq)[R]) -> float {
+    float v = 0.f;
+#pragma unroll
+    for (int j = 0; j < R; ++j) v = fmaf(lp[rr][j], lq[j], v);
+    return v * lz.s;
+  };
   if (mat_vec(mt)) {
     constexpr int kCU = 2;  // column chunks per iteration: 4 rows x 2 chunks (x2 with COMP 2) loads in flight
     for (int64_t cb = c0 + 4 * lane; cb < c1; cb += 4 * kWave * kCU) {
@@ -107,7 +134,7 @@ __global__ __launch_bounds__(kBlock) void ps_mq_kernel(const float* __restrict__
           if (row < n && c < c1) {
             const int64_t gi = mt.x_off + row * m + c;
             mv[k][rr] = *reinterpret_cast<const float4*>(x + gi);
-            if (COMP == 2) rv[k][rr] = *reinterpret_cast<const float4*>(cr + gi);
+            if (COMP >= 2) rv[k][rr] = *reinterpret_cast<const float4*>(cr + gi);
           }
         }
 #pragma unroll
@@ -117,10 +144,21 @@ __global__ __launch_bounds__(kBlock) void ps_mq_kernel(const float* __restrict__
         float q[4][R];
 #pragma unroll
         for (int t = 0; t < 4; ++t) load_small_row<R>(Q, c + t, r, q[t]);
+        if constexpr (COMP == 3) {
+          float lq[4][R];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) load_small_row<R>(lz.q + mt.q_off, c + t, r, lq[t]);
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) {
+            float4& rv4 = rv[k][rr];
+            rv4 = make_float4(rv4.x - lazy_o(rr, lq[0]), rv4.y - lazy_o(rr, lq[1]), rv4.z - lazy_o(rr, lq[2]),
+                              rv4.w - lazy_o(rr, lq[3]));
+          }
+        }
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
           float4 v = mv[k][rr];
-          if (COMP == 2)
+          if (COMP >= 2)
             v = make_float4(fmaf(beta, rv[k][rr].x, gamma * v.x), fmaf(beta, rv[k][rr].y, gamma * v.y),
                             fmaf(beta, rv[k][rr].z, gamma * v.z), fmaf(beta, rv[k][rr].w, gamma * v.w));
           const int64_t row = row0 + rr;
@@ -135,8 +173,9 @@ __global__ __launch_bounds__(kBlock) void ps_mq_kernel(const float* __restrict__
     }
   } else {
     for (int64_t c = c0 + lane; c < c1; c += kWave) {
-      float q[R];
+      float q[R], lq[R];
       load_small_row<R>(Q, c, r, q);
+      if constexpr (COMP == 3) load_small_row<R>(lz.q + mt.q_off, c, r, lq);
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int64_t row = row0 + rr;
@@ -144,6 +183,7 @@ __global__ __launch_bounds__(kBlock) void ps_mq_kernel(const float* __restrict__
           const int64_t gi = mt.x_off + row * m + c;
           float v = x[gi];
           if (COMP == 2) v = fmaf(beta, cr[gi], gamma * v);
+          if constexpr (COMP == 3) v = fmaf(beta, cr[gi] - lazy_o(rr, lq), gamma * v);
           if (COMP != 0) xout[gi] = v;
 #pragma unroll
           for (int j = 0; j < R; ++j) acc[rr][j] = fmaf(v, q[j], acc[rr][j]);
@@ -243,9 +283,9 @@ __global__ __launch_bounds__(kBlock) void ps_mtp_kernel(const float* __restrict_
 
 template <int R>
 __global__ __launch_bounds__(kBlock) void ps_pqt_kernel(const float* __restrict__ Pall, const float* __restrict__ Qall,
-                                                        float* __restrict__ out, const int64_t* __restrict__ mats,
+                                                        float* out, const int64_t* __restrict__ mats,
                                                         const int32_t* __restrict__ tiles, float* __restrict__ resid,
-                                                        float scale) {
+                                                        float scale) {  // out == nullptr: residual update only
   const int* tl = tiles + 3 * blockIdx.x;
   const Mat mt = load_mat(mats, tl[0]);
   const int64_t n = mt.n, m = mt.m;
@@ -282,7 +322,7 @@ __global__ __launch_bounds__(kBlock) void ps_pqt_kernel(const float* __restrict_
           o[t] = v * scale;
         }
         const int64_t gi = mt.x_off + row * m + c;
-        *reinterpret_cast<float4*>(out + gi) = make_float4(o[0], o[1], o[2], o[3]);
+        if (out != nullptr) *reinterpret_cast<float4*>(out + gi) = make_float4(o[0], o[1], o[2], o[3]);
         if (resid != nullptr)
           *reinterpret_cast<float4*>(resid + gi) =
               make_float4(rv[u].x - o[0], rv[u].y - o[1], rv[u].z - o[2], rv[u].w - o[3]);
@@ -301,7 +341,7 @@ __global__ __launch_bounds__(kBlock) void ps_pqt_kernel(const float* __restrict_
       for (int j = 0; j < R; ++j) v = fmaf(p[j], q[j], v);
       v *= scale;
       const int64_t gi = mt.x_off + row * m + c;
-      out[gi] = v;
+      if (out != nullptr) out[gi] = v;
       if (resid != nullptr) resid[gi] -= v;
     }
   }
@@ -610,27 +650,32 @@ __global__ __launch_bounds__(kBlock) void philox_normal_kernel(float* __restrict
 
 template <int R>
 void launch_mq(const float* x, const float* small, float* out, const int64_t* mats, const int32_t* tiles, int n_tiles,
-               int mode, const float* comp_r, float beta, float gamma, float* xout, hipStream_t stream) {
+               int mode, const float* comp_r, float beta, float gamma, float* xout, Lazy lz, hipStream_t stream) {
+  const Lazy none{nullptr, nullptr, 0.f};
   if (mode == 1)
     ps_mtp_kernel<R><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles);
   else if (xout == nullptr)
-    ps_mq_kernel<R, 0><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles, nullptr, 0.f, 0.f, nullptr);
+    ps_mq_kernel<R, 0><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles, nullptr, 0.f, 0.f, nullptr, none);
   else if (comp_r == nullptr)
-    ps_mq_kernel<R, 1><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles, nullptr, 0.f, 0.f, xout);
+    ps_mq_kernel<R, 1><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles, nullptr, 0.f, 0.f, xout, none);
+  else if (lz.p == nullptr)
+    ps_mq_kernel<R, 2><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles, comp_r, beta, gamma, xout, none);
   else
-    ps_mq_kernel<R, 2><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles, comp_r, beta, gamma, xout);
+    ps_mq_kernel<R, 3><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles, comp_r, beta, gamma, xout, lz);
 }
 
 void powersgd_mq(const float* x, const float* small, float* out, int64_t out_len, const int64_t* mats,
                  const int32_t* tiles, int n_tiles, int mode, const float* comp_r, float beta, float gamma,
-                 float* xout, int max_r, hipStream_t stream) {
+                 float* xout, int max_r, hipStream_t stream, const float* lazy_p, const float* lazy_q,
+                 float lazy_scale) {
   GRACE_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(float) * out_len, stream));
   if (n_tiles <= 0) return;
-  if (max_r <= 1) launch_mq<1>(x, small, out, mats, tiles, n_tiles, mode, comp_r, beta, gamma, xout, stream);
-  else if (max_r <= 2) launch_mq<2>(x, small, out, mats, tiles, n_tiles, mode, comp_r, beta, gamma, xout, stream);
-  else if (max_r <= 4) launch_mq<4>(x, small, out, mats, tiles, n_tiles, mode, comp_r, beta, gamma, xout, stream);
-  else if (max_r <= 8) launch_mq<8>(x, small, out, mats, tiles, n_tiles, mode, comp_r, beta, gamma, xout, stream);
-  else launch_mq<16>(x, small, out, mats, tiles, n_tiles, mode, comp_r, beta, gamma, xout, stream);
+  const Lazy lz{lazy_p, lazy_q, lazy_scale};
+  if (max_r <= 1) launch_mq<1>(x, small, out, mats, tiles, n_tiles, mode, comp_r, beta, gamma, xout, lz, stream);
+  else if (max_r <= 2) launch_mq<2>(x, small, out, mats, tiles, n_tiles, mode, comp_r, beta, gamma, xout, lz, stream);
+  else if (max_r <= 4) launch_mq<4>(x, small, out, mats, tiles, n_tiles, mode, comp_r, beta, gamma, xout, lz, stream);
+  else if (max_r <= 8) launch_mq<8>(x, small, out, mats, tiles, n_tiles, mode, comp_r, beta, gamma, xout, lz, stream);
+  else launch_mq<16>(x, small, out, mats, tiles, n_tiles, mode, comp_r, beta, gamma, xout, lz, stream);
 }
 
 void gram_orthonormalize(float* buf, const int64_t* mats, int n_mat, int which, const int32_t* gtiles,

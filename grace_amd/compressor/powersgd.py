@@ -41,6 +41,10 @@ from ..ops import powersgd as PS
 from ..ops.randomk import fnv1a64, mix_step
 from ._base import BucketCompressor, Ctx
 
+# GRACE_POWERSGD_DEFER_RESID=0: the residual update r = x - P Q^T stays in the decompress pass
+# (reads and rewrites the residual); default: deferred into the next step's P = M Q pass
+_DEFER_RESID = __import__("os").environ.get("GRACE_POWERSGD_DEFER_RESID", "1") == "1"
+
 
 class PowerSGDCompressor(BucketCompressor):
     allreduce_compatible = True
@@ -60,6 +64,7 @@ class PowerSGDCompressor(BucketCompressor):
         self._pending = []
         self._arena = None
         self.matrix_collectives = 0  # matrix all-reduces issued (tests / monitoring)
+        self._pq_prev = {}  # name -> [P | Q] of the last step (deferred residual), persistent
 
     def enable_step_level(self, on: bool = True):
         """Defer the P/Q exchange of every bucket to :meth:`step_flush` (called by the engine)."""
@@ -106,9 +111,16 @@ class PowerSGDCompressor(BucketCompressor):
             rs = torch.zeros(tensor.shape, dtype=torch.float32, device=g.device)
             memory.residuals[name] = rs
         r = rs.view(-1)
+        # deferred residual of the previous step (r holds its M): formed inside this P = M Q pass
+        lz = memory.lazy.pop(name, None)
+        lazy = (lz[0], lz[1], lz[2]) if (lz is not None and valid and lz[3] is plan) else None
         # x (matrix segments) lands in r; 1-D segments of x equal g (their residual is zero)
-        vec = self._power(g, r, name, ctx, plan, comp_r=r if valid else None, xout=r, defer=self.step_level)
+        vec = self._power(g, r, name, ctx, plan, comp_r=r if valid else None, xout=r, defer=self.step_level,
+                          lazy=lazy)
         ctx.extra["resid"] = r
+        if _DEFER_RESID and g.is_cuda:
+            ctx.extra["lazy_mem"] = memory
+            ctx.extra["name"] = name
         return vec, ctx
 
     def _arena_slice(self, name, plan):
@@ -120,7 +132,7 @@ class PowerSGDCompressor(BucketCompressor):
             return None
         return a["p"][po:po + plan.p_total]
 
-    def _power(self, x, x_after, name, ctx, plan, comp_r=None, xout=None, defer=False):
+    def _power(self, x, x_after, name, ctx, plan, comp_r=None, xout=None, defer=False, lazy=None):
         """P = M Q for every matrix of the bucket (into the step-level P arena when batching);
         the P/Q collectives run now (manual path) or in :meth:`step_flush`.  ``x`` feeds the
         first product (compensated on the fly when ``xout`` is given, which then holds x);
@@ -140,7 +152,7 @@ class PowerSGDCompressor(BucketCompressor):
             # well conditioned).  Skipped: it was a 400 KB single-workgroup pass per step for
             # VGG-16's 25088 x 4 Q.  (A warm-start Q is used as is, as in the reference.)
         p_out = self._arena_slice(name, plan) if defer else None
-        p = PS.mq(x, q, plan, comp_r=comp_r, xout=xout, out=p_out)  # P = M Q for every matrix (one launch)
+        p = PS.mq(x, q, plan, comp_r=comp_r, xout=xout, out=p_out, lazy=lazy)  # P = M Q, every matrix, one launch
         ctx.extra.update(plan=plan, p=p)
         vec = PS.gather_vectors(x, plan)  # 1-D segments, sent through the communicator
         entry = (name, x_after, ctx)
@@ -214,11 +226,29 @@ class PowerSGDCompressor(BucketCompressor):
             out = v * vec_scale if vec_scale != 1.0 else v
             return self.finish(out.reshape(-1), ctx)
         out = self.out_buffer(ctx, dev)
-        # fused path: the residual buffer holds x; this pass also leaves r = x - P Q^T there
         if "q" not in ctx.extra:
             raise RuntimeError("PowerSGD: decompress before the step's P/Q exchange (call step_flush())")
-        PS.pqt(ctx.extra["p"], ctx.extra["q"], plan, out, resid=ctx.extra.pop("resid", None),
-               scale=ctx.extra.get("q_scale", 1.0))
+        resid = ctx.extra.pop("resid", None)
+        mem = ctx.extra.pop("lazy_mem", None)
+        scale = ctx.extra.get("q_scale", 1.0)
+        if mem is not None and resid is not None:
+            # deferred residual: the residual buffer keeps x, and (P, Q, scale) go to the memory
+            # for the next step's P = M Q pass -- as copies in persistent per-name buffers: the
+            # next P = M Q pass rewrites the step-level P arena slice while reading the previous P,
+            # and a HIP graph replays fixed pointers (the manual path's P / Q are fresh tensors)
+            PS.pqt(ctx.extra["p"], ctx.extra["q"], plan, out, resid=None, scale=scale)
+            name = ctx.extra["name"]
+            prev = self._pq_prev.get(name)
+            dev = ctx.extra["p"].device
+            if prev is None or prev.numel() != plan.p_total + plan.q_total or prev.device != dev:
+                prev = self._pq_prev[name] = torch.empty(plan.p_total + plan.q_total, dtype=torch.float32, device=dev)
+            pp, qp = prev[:plan.p_total], prev[plan.p_total:]
+            pp.copy_(ctx.extra["p"])
+            qp.copy_(ctx.extra["q"])
+            mem.lazy[name] = (pp, qp, scale, plan)
+        else:
+            # fused eager form / unfused: the residual buffer holds x; this pass leaves r = x - P Q^T
+            PS.pqt(ctx.extra["p"], ctx.extra["q"], plan, out, resid=resid, scale=scale)
         if tensors:
             PS.scatter_vectors(tensors[0], plan, out, vec_scale)
         return self.finish(out, ctx)

@@ -166,21 +166,34 @@ def orthogonalize(buf: torch.Tensor, plan: Plan, which: str) -> None:
 
 
 def mq(x: torch.Tensor, q: torch.Tensor, plan: Plan, comp_r: Optional[torch.Tensor] = None, beta: float = 1.0,
-       gamma: float = 1.0, xout: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+       gamma: float = 1.0, xout: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+       lazy: Optional[Tuple[torch.Tensor, torch.Tensor, float]] = None) -> torch.Tensor:
     """P_i = M_i Q_i for every matrix (flat P buffer; ``out``: a caller-owned [p_total] view,
     e.g. this bucket's slice of the step-level P arena).
 
     With ``xout``: M = beta*comp_r + gamma*x (or M = x without ``comp_r``) is also stored into
-    ``xout`` for the matrix segments -- the error-feedback compensate fused into this pass."""
+    ``xout`` for the matrix segments -- the error-feedback compensate fused into this pass.
+    ``lazy = (P', Q', s)``: ``comp_r`` holds the previous step's M and the residual is
+    comp_r - s P' Q'^T (the previous step's final P and summed Q; the deferred residual update,
+    formed here with ``pqt``'s float ops instead of written by it and read back)."""
     p = out if out is not None else torch.empty(plan.p_total, dtype=torch.float32, device=x.device)
+    if lazy is not None and comp_r is None:
+        raise ValueError("a deferred residual needs comp_r (the previous M)")
     if _native.use_native(x):
         t = plan.tables(x.device)
-        _native.lib().powersgd_mq(x, q, p, t["mat"], t["tiles0"], 0, comp_r, beta, gamma, xout, plan.rank)
+        lp, lq, ls = lazy if lazy is not None else (None, None, 0.0)
+        _native.lib().powersgd_mq(x, q, p, t["mat"], t["tiles0"], 0, comp_r, beta, gamma, xout, plan.rank,
+                                  lazy_p=lp, lazy_q=lq, lazy_scale=float(ls))
         return p
     for (xo, n, m, r, po, qo) in plan.mats:
         mx = x[xo:xo + n * m]
         if xout is not None:
-            v = beta * comp_r[xo:xo + n * m] + gamma * mx if comp_r is not None else mx
+            cr = comp_r[xo:xo + n * m] if comp_r is not None else None
+            if lazy is not None:
+                lp, lq, ls = lazy
+                o = torch.mm(lp[po:po + n * r].view(n, r), lq[qo:qo + m * r].view(m, r).t()).view(-1)
+                cr = cr - (o * ls if ls != 1.0 else o)
+            v = beta * cr + gamma * mx if cr is not None else mx
             xout[xo:xo + n * m].copy_(v)
             mx = xout[xo:xo + n * m]
         torch.mm(mx.view(n, m), q[qo:qo + m * r].view(m, r), out=p[po:po + n * r].view(n, r))
@@ -199,20 +212,23 @@ def mtp(x: torch.Tensor, p: torch.Tensor, plan: Plan, out: Optional[torch.Tensor
     return q
 
 
-def pqt(p: torch.Tensor, q: torch.Tensor, plan: Plan, out: torch.Tensor, resid: Optional[torch.Tensor] = None,
+def pqt(p: torch.Tensor, q: torch.Tensor, plan: Plan, out: Optional[torch.Tensor], resid: Optional[torch.Tensor] = None,
         scale: float = 1.0) -> None:
     """out[matrix i] = scale * P_i Q_i^T (vector segments untouched); with ``resid`` (holding x)
     also resid[matrix i] -= out in the same pass (PowerSGD residual update).  ``scale`` = 1/W
-    folds the average of the summed Q into this pass (no separate division kernel)."""
-    if _native.use_native(out):
-        t = plan.tables(out.device)
+    folds the average of the summed Q into this pass (no separate division kernel).
+    ``out=None``: only the residual update (materialising a deferred residual)."""
+    ref = out if out is not None else resid
+    if _native.use_native(ref):
+        t = plan.tables(ref.device)
         _native.lib().powersgd_pqt(p, q, out, t["mat"], t["tilesp"], resid, plan.rank, float(scale))
         return
     for (xo, n, m, r, po, qo) in plan.mats:
-        o = out[xo:xo + n * m].view(n, m)
-        torch.mm(p[po:po + n * r].view(n, r), q[qo:qo + m * r].view(m, r).t(), out=o)
+        o = torch.mm(p[po:po + n * r].view(n, r), q[qo:qo + m * r].view(m, r).t())
         if scale != 1.0:
             o.mul_(scale)
+        if out is not None:
+            out[xo:xo + n * m].view(n, m).copy_(o)
         if resid is not None:
             resid[xo:xo + n * m].view(n, m).sub_(o)
 

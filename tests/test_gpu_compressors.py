@@ -4,6 +4,7 @@ Deterministic codecs must match the CPU/PyTorch path (bit-exact or to fp32 round
 stochastic ones (QSGD, TernGrad, Natural) are checked for their error bounds and
 unbiasedness, on the GPU path that runs the HIP kernels.
 """
+import math
 import os
 import sys
 
@@ -257,7 +258,10 @@ def test_powersgd_fused_memory_gpu_matches_cpu_unfused(monkeypatch):
             gen = torch.Generator().manual_seed(s)
             x = torch.cat([torch.randn(*sh, generator=gen).flatten() for sh in shapes])
             res.append(grc.step(x.to(dev), "psgd_gpu").cpu())
+        sd = mem.state_dict()["residuals"]["psgd_gpu"].reshape(-1).cpu()  # materialised copy
+        mem.materialize()  # the GPU memory defers its residual update (PowerSGDMemory.lazy)
         res.append(mem.residuals["psgd_gpu"].reshape(-1).cpu())
+        assert torch.equal(sd, res[-1])
         outs[dev] = res
     for a, b in zip(outs["cuda"], outs["cpu"]):  # 3 decoded steps + the final residual
         torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-4)
@@ -514,3 +518,59 @@ def test_dgc_fused_compensate_equals_compensate_then_select():
         assert torch.equal(pa[1][:k].cpu()[oa], pb[1][:k].cpu()[ob]), step
         ua, va, _ = mem_a.state_buffers("dgc_fuse", g)
         assert torch.equal(ua, u) and torch.equal(va, v), step
+
+
+@pytest.mark.parametrize("graphed", [False, True])
+def test_powersgd_deferred_residual_bit_identical(graphed):
+    """The deferred residual (r = M - s P Q^T formed inside the next P = M Q pass, with the float
+    ops of the eager update) matches the eager residual update inside the decompress pass, step
+    after step -- eager and HIP-graph-replayed -- and a mid-run state_dict (materialised copy)
+    leaves the live deferred state untouched.  Not bitwise across the two runs: Q = M^T P sums its
+    row strips with float atomics, so P / Q themselves differ in the last bit run to run."""
+    import grace_amd.compressor.powersgd as CP
+    from grace_amd.core import register_layout
+
+    shapes = [(512, 300), (64,), (32, 16, 3, 3), (10,), (1000, 36)]
+    register_layout("psgd_def", SegmentLayout.from_tensors([torch.empty(s) for s in shapes]))
+    n = sum(math.prod(s) for s in shapes)
+    xs = [torch.randn(n, generator=torch.Generator().manual_seed(s)).cuda() for s in range(6)]
+    outs = {}
+    for defer in (False, True):
+        old = CP._DEFER_RESID
+        CP._DEFER_RESID = defer
+        try:
+            mem = M.PowerSGDMemory(compress_rank=4)
+            grc = Allreduce(Z.PowerSGDCompressor(rank=4), mem, comm=LocalComm())
+            res = []
+            if not graphed:
+                for s, x in enumerate(xs):
+                    res.append(grc.step(x, "psgd_def").clone())
+                    if s == 2 and defer:
+                        before = mem.residuals["psgd_def"].clone()
+                        mem.state_dict()
+                        assert torch.equal(before, mem.residuals["psgd_def"])
+            else:
+                buf = xs[0].clone()
+                out = torch.empty_like(buf)
+                st = torch.cuda.Stream()
+                st.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(st):
+                    for x in xs[:2]:  # warm-up: allocates residual / P-prev / arenas
+                        buf.copy_(x)
+                        out.copy_(grc.step(buf, "psgd_def"))
+                        res.append(out.clone())
+                torch.cuda.current_stream().wait_stream(st)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=st):
+                    out.copy_(grc.step(buf, "psgd_def"))
+                for x in xs[2:]:
+                    buf.copy_(x)
+                    g.replay()
+                    res.append(out.clone())
+            mem.materialize()
+            res.append(mem.residuals["psgd_def"].reshape(-1).clone())
+            outs[defer] = res
+        finally:
+            CP._DEFER_RESID = old
+    for i, (a, b) in enumerate(zip(outs[False], outs[True])):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5, msg=lambda m, i=i: f"step {i}: {m}")
