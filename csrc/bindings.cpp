@@ -482,7 +482,8 @@ void dgc_sample(const Tensor& x, const Tensor& seg_off, const Tensor& samp_off, 
 // place (u = m u + g; v = v + u; first: u = v = g) and later passes read v
 void dgc_refine(const Tensor& x, const Tensor& state, const Tensor& target, int64_t max_iters, const Tensor& thr,
                 const Tensor& count, const Tensor& done, const Tensor& seg, const Tensor& cb, const Tensor& ce,
-                const c10::optional<Tensor>& u, const c10::optional<Tensor>& v, double momentum, bool first) {
+                const Tensor& ccnt, const Tensor& fnode, const c10::optional<Tensor>& u,
+                const c10::optional<Tensor>& v, double momentum, bool first, bool init) {
   CHECK_F32(x);
   CHECK_I32(state);
   CHECK_F32(target);
@@ -492,6 +493,9 @@ void dgc_refine(const Tensor& x, const Tensor& state, const Tensor& target, int6
   const int n_seg = (int)target.numel();
   TORCH_CHECK(thr.numel() == n_seg && count.numel() >= 32 * n_seg && done.numel() == n_seg && state.numel() >= 2 * n_seg,
               "per-segment tables (count: 32 words per segment)");
+  CHECK_I32(ccnt);
+  CHECK_I32(fnode);
+  TORCH_CHECK(ccnt.numel() >= 32 * seg.numel() && fnode.numel() >= n_seg, "dgc_refine: ccnt [32 n_chunks] / fnode [n_seg]");
   const bool comp = u.has_value() && u->defined();
   if (comp) {
     CHECK_F32(*u);
@@ -506,12 +510,34 @@ void dgc_refine(const Tensor& x, const Tensor& state, const Tensor& target, int6
   grace::dgc_refine(ct, n_seg, x.data_ptr<float>(), reinterpret_cast<const grace::TopkState*>(state.data_ptr<int32_t>()),
                     target.data_ptr<float>(), (int)max_iters, thr.data_ptr<float>(), count.data_ptr<int32_t>(),
                     done.data_ptr<int32_t>(), comp ? u->data_ptr<float>() : nullptr,
-                    comp ? v->data_ptr<float>() : nullptr, (float)momentum, first ? 1 : 0, x.numel(), cur_stream());
+                    comp ? v->data_ptr<float>() : nullptr, (float)momentum, first ? 1 : 0, x.numel(),
+                    ccnt.data_ptr<int32_t>(), fnode.data_ptr<int32_t>(), init, cur_stream());
+}
+
+void dgc_select_init(const Tensor& samples, const Tensor& samp_off, const Tensor& kseg, const Tensor& state,
+                     const Tensor& thr, const Tensor& count, const Tensor& done, const Tensor& fnode) {
+  CHECK_F32(samples);
+  CHECK_I64(samp_off);
+  CHECK_I32(kseg);
+  CHECK_I32(state);
+  CHECK_F32(thr);
+  CHECK_I32(count);
+  CHECK_I32(done);
+  CHECK_I32(fnode);
+  const int n_seg = (int)kseg.numel();
+  TORCH_CHECK(samp_off.numel() == n_seg + 1 && state.numel() >= 2 * n_seg && thr.numel() == n_seg &&
+                  count.numel() >= 32 * n_seg && done.numel() == n_seg && fnode.numel() >= n_seg,
+              "dgc_select_init: per-segment tables");
+  DevGuard guard(samples.device());
+  grace::dgc_select_init(n_seg, samples.data_ptr<float>(), samp_off.data_ptr<int64_t>(), kseg.data_ptr<int32_t>(),
+                         reinterpret_cast<grace::TopkState*>(state.data_ptr<int32_t>()), thr.data_ptr<float>(),
+                         count.data_ptr<int32_t>(), done.data_ptr<int32_t>(), fnode.data_ptr<int32_t>(), cur_stream());
 }
 
 // capacity = out_val.numel(); vmask/umask (optional, DgcMemory fused): zeroed where sent
 void dgc_compact(const Tensor& x, const Tensor& thr, const Tensor& out_val, const Tensor& out_idx,
                  const Tensor& counter, const Tensor& seg, const Tensor& cb, const Tensor& ce,
+                 const Tensor& ccnt, const Tensor& fnode, const Tensor& coff,
                  const c10::optional<Tensor>& vmask, const c10::optional<Tensor>& umask) {
   CHECK_F32(x);
   CHECK_F32(thr);
@@ -532,10 +558,16 @@ void dgc_compact(const Tensor& x, const Tensor& thr, const Tensor& out_val, cons
     TORCH_CHECK(umask->numel() == x.numel(), "umask size");
     up = umask->data_ptr<float>();
   }
+  CHECK_I32(ccnt);
+  CHECK_I32(fnode);
+  CHECK_I32(coff);
+  TORCH_CHECK(ccnt.numel() >= 32 * seg.numel() && coff.numel() >= seg.numel() && fnode.numel() >= thr.numel(),
+              "dgc_compact: ccnt [32 n_chunks] / coff [n_chunks] / fnode [n_seg]");
   auto ct = make_ct(seg, cb, ce);
   DevGuard guard(x.device());
   grace::dgc_compact(ct, x.data_ptr<float>(), thr.data_ptr<float>(), out_val.data_ptr<float>(),
-                     out_idx.data_ptr<int32_t>(), out_val.numel(), counter.data_ptr<int32_t>(), vp, up, cur_stream(),
+                     out_idx.data_ptr<int32_t>(), out_val.numel(), counter.data_ptr<int32_t>(), vp, up,
+                     ccnt.data_ptr<int32_t>(), fnode.data_ptr<int32_t>(), coff.data_ptr<int32_t>(), cur_stream(),
                      header_bytes(counter));
 }
 
@@ -1154,8 +1186,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("momentum") = 0.0, py::arg("first") = false);
   m.def("dgc_refine", &dgc_refine, py::arg("x"), py::arg("state"), py::arg("target"), py::arg("max_iters"),
         py::arg("thr"), py::arg("count"), py::arg("done"), py::arg("seg"), py::arg("cb"), py::arg("ce"),
-        py::arg("u") = py::none(), py::arg("v") = py::none(), py::arg("momentum") = 0.0, py::arg("first") = false);
-  m.def("dgc_compact", &dgc_compact);
+        py::arg("ccnt"), py::arg("fnode"), py::arg("u") = py::none(), py::arg("v") = py::none(),
+        py::arg("momentum") = 0.0, py::arg("first") = false, py::arg("init") = true);
+  m.def("dgc_select_init", &dgc_select_init, py::arg("samples"), py::arg("samp_off"), py::arg("kseg"),
+        py::arg("state"), py::arg("thr"), py::arg("count"), py::arg("done"), py::arg("fnode"));
+  m.def("dgc_compact", &dgc_compact, py::arg("x"), py::arg("thr"), py::arg("out_val"), py::arg("out_idx"),
+        py::arg("counter"), py::arg("seg"), py::arg("cb"), py::arg("ce"), py::arg("ccnt"), py::arg("fnode"),
+        py::arg("coff"), py::arg("vmask") = py::none(), py::arg("umask") = py::none());
   m.def("dgc_compensate", &dgc_compensate);
   m.def("powersgd_mq", &powersgd_mq, py::arg("x"), py::arg("small"), py::arg("out"), py::arg("mats"), py::arg("tiles"),
         py::arg("mode"), py::arg("comp_r"), py::arg("beta"), py::arg("gamma"), py::arg("xout"), py::arg("max_r"),

@@ -96,11 +96,18 @@ void u8_aggregate(const ChunkTable& ct, const uint8_t* base, int64_t rank_stride
 void dgc_sample(const float* x, int n_seg, const int64_t* seg_off, const int64_t* samp_off, int64_t n_samples,
                 SeedArg seed, float* samples, const float* u, const float* v, float momentum, int first,
                 hipStream_t stream);
+// ccnt: int32 [32 n_chunks] per-chunk tree counts; fnode: int32 [n_seg] final counted tree node
+// (-1: uncounted) -- consumed by dgc_compact (coff: int32 [n_chunks] scratch)
 void dgc_refine(const ChunkTable& ct, int n_seg, const float* x, const TopkState* st, const float* target,
                 int max_iters, float* thr, int32_t* count, int32_t* done, float* u, float* v, float momentum,
-                int first, int64_t n, hipStream_t stream);
+                int first, int64_t n, int32_t* ccnt, int32_t* fnode, bool init, hipStream_t stream);
+// exact k'-th largest |sample| per segment (one workgroup each) + the refinement state of
+// dgc_refine (thr, count, done, fnode) -- dgc_refine(init = false) then skips its own init
+void dgc_select_init(int n_seg, const float* samples, const int64_t* samp_off, const int32_t* kseg, TopkState* st,
+                     float* thr, int32_t* count, int32_t* done, int32_t* fnode, hipStream_t stream);
 void dgc_compact(const ChunkTable& ct, const float* x, const float* thr, float* out_val, int32_t* out_idx,
-                 int64_t cap, int32_t* counter, float* vmask, float* umask, hipStream_t stream, int header_bytes = 4);
+                 int64_t cap, int32_t* counter, float* vmask, float* umask, const int32_t* ccnt,
+                 const int32_t* fnode, int32_t* coff, hipStream_t stream, int header_bytes = 4);
 void dgc_compensate(const float* g, float* u, float* v, float momentum, int64_t n, bool first, hipStream_t stream);
 
 // ---------------------------------------------------------------- powersgd.hip

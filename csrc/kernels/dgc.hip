@@ -12,10 +12,12 @@
 //                  workgroup and threshold
 //   dgc_adjust_tree: per segment, the reference's rule walked 3 steps down the counted tree;
 //                  marks converged segments done
-//   dgc_compact  : ballot compaction of |x| >= thr[seg] into (value, flat index)
-//   dgc_compact  : capacity-bounded (the payload has a fixed capacity and an in-band count, so
-//                  the exchange needs no host sync and is graph-capturable), DgcMemory's u / v
-//                  masking fused in
+//   dgc_scan     : output offset of every chunk = prefix sum of the chunk counts the last count
+//                  pass already formed at the final threshold (one workgroup)
+//   dgc_compact  : compaction of |x| >= thr[seg] into (value, flat index) at those offsets --
+//                  no atomics, deterministic slots; capacity-bounded (the payload has a fixed
+//                  capacity and an in-band count, so the exchange needs no host sync and is
+//                  graph-capturable), DgcMemory's u / v masking fused in
 //   dgc_compensate: DgcMemory's momentum correction + accumulation in one pass
 #include "grace_common.h"
 #include "grace_kernels.h"
@@ -72,14 +74,97 @@ __global__ __launch_bounds__(kBlock) void dgc_sample_kernel(const float* __restr
   }
 }
 
-// thr[s] <- float(prefix of the k'-th largest sample key); count[s] = 0; done[s] = 0
+constexpr int kCntStride = 32;
+
+// The k'-th largest |sample| of every segment, exactly (3-digit radix select: bits 30..20,
+// 19..9, 8..0 of the |x| key, as topk.hip's segmented select), ONE workgroup per segment with the
+// samples cached in LDS -- and the refinement state initialised in the same launch: thr[s] = that
+// value, the 32 count words = 0, done = 0, fnode = -1.  Replaces 3 histogram + 3 select launches
+// over the (tiny) sample set plus the init launch: ~40 us of launch latency per DGC step.
+constexpr int kSelBlock = 1024;
+constexpr int kSelLds = 24576;  // samples cached in LDS (96 KB); a larger segment re-reads them
+
+__global__ __launch_bounds__(kSelBlock) void dgc_select_init_kernel(
+    const float* __restrict__ samples, const int64_t* __restrict__ samp_off, const int32_t* __restrict__ kseg,
+    TopkState* __restrict__ st, float* __restrict__ thr, int32_t* __restrict__ count, int32_t* __restrict__ done,
+    int32_t* __restrict__ fnode) {
+  __shared__ uint32_t keys[kSelLds];
+  __shared__ int32_t hist[2048];
+  __shared__ int part[kSelBlock / kWave];
+  __shared__ uint32_t s_prefix;
+  __shared__ int32_t s_krem;
+  const int s = blockIdx.x;
+  const int64_t so = samp_off[s], ns = samp_off[s + 1] - so;
+  const bool in_lds = ns <= kSelLds;
+  if (in_lds)
+    for (int64_t i = threadIdx.x; i < ns; i += kSelBlock) keys[i] = abs_key(samples[so + i]);
+  if (threadIdx.x == 0) {
+    s_prefix = 0u;
+    s_krem = kseg[s];
+  }
+  __syncthreads();
+  constexpr int kShift[3] = {20, 9, 0};
+  constexpr int kBits[3] = {11, 11, 9};
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    const int shift = kShift[d], nbins = 1 << kBits[d];
+    for (int i = threadIdx.x; i < nbins; i += kSelBlock) hist[i] = 0;
+    __syncthreads();
+    const uint32_t want = d == 0 ? 0u : s_prefix >> (shift + kBits[d]);
+    const int32_t krem = s_krem;
+    for (int64_t i = threadIdx.x; i < ns; i += kSelBlock) {
+      const uint32_t key = in_lds ? keys[i] : abs_key(samples[so + i]);
+      if (d == 0 || (key >> (shift + kBits[d])) == want) atomicAdd(&hist[(key >> shift) & (nbins - 1)], 1);
+    }
+    __syncthreads();
+    // descending bins: thread t owns positions [2t, 2t + 2) (bin = nbins - 1 - position)
+    int32_t loc[2] = {0, 0};
+    int32_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int j = 2 * (int)threadIdx.x + q;
+      if (j < nbins) loc[q] = hist[nbins - 1 - j];
+      sum += loc[q];
+    }
+    int tot = 0;
+    const int32_t excl = block_exclusive_scan<kSelBlock>(sum, part, &tot);
+    if (excl < krem && krem <= excl + sum) {
+      int32_t run = excl;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        if (run + loc[q] >= krem) {
+          const uint32_t bin = (uint32_t)(nbins - 1 - (2 * (int)threadIdx.x + q));
+          s_prefix = (d == 0 ? 0u : s_prefix) | (bin << shift);
+          s_krem = krem - run;
+          break;
+        }
+        run += loc[q];
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    st[s].prefix = s_prefix;
+    st[s].krem = s_krem;
+    thr[s] = __uint_as_float(s_prefix);
+    done[s] = 0;
+    fnode[s] = -1;
+  }
+  if (threadIdx.x < kCntStride) count[s * kCntStride + threadIdx.x] = 0;
+}
+
+// thr[s] <- float(prefix of the k'-th largest sample key); the segment's 32 count words = 0;
+// done[s] = 0; fnode[s] = -1 (no counted final threshold yet)
 __global__ void dgc_init_kernel(int n_seg, const TopkState* __restrict__ st, float* __restrict__ thr,
-                                int32_t* __restrict__ count, int32_t* __restrict__ done) {
+                                int32_t* __restrict__ count, int32_t* __restrict__ done,
+                                int32_t* __restrict__ fnode) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n_seg) return;
   thr[s] = __uint_as_float(st[s].prefix);
-  count[s] = 0;
+#pragma unroll
+  for (int k = 0; k < kCntStride; ++k) count[s * kCntStride + k] = 0;
   done[s] = 0;
+  fnode[s] = -1;
 }
 
 // Speculative refinement: the reference's loop (count at thr; x1.3 when too many, x0.7 when too
@@ -94,7 +179,6 @@ __global__ void dgc_init_kernel(int n_seg, const TopkState* __restrict__ st, flo
 // needed 4 passes over the bucket.)
 constexpr int kDepth = 5;
 constexpr int kTree = (1 << kDepth) - 1;  // 31
-constexpr int kCntStride = 32;
 
 __device__ __forceinline__ void tree_thresholds(float root, float* t) {
   t[0] = root;
@@ -113,7 +197,8 @@ __global__ __launch_bounds__(kBlock) void dgc_count_tree_kernel(ChunkTable ct, c
                                                                 const float* __restrict__ thr,
                                                                 const int32_t* __restrict__ done,
                                                                 int32_t* __restrict__ count, float* __restrict__ uu,
-                                                                float* __restrict__ vv, float m, int first) {
+                                                                float* __restrict__ vv, float m, int first,
+                                                                int32_t* __restrict__ ccnt) {
   const int c = blockIdx.x;
   const int s = ct.seg[c];
   if (!FUSE && done[s]) return;  // (the fused pass runs before any segment converged)
@@ -181,12 +266,19 @@ __global__ __launch_bounds__(kBlock) void dgc_count_tree_kernel(ChunkTable ct, c
     unsigned tot = 0;
     for (int w = 0; w < kBlock / kWave; ++w) tot += red[w][threadIdx.x];
     if (tot) atomicAdd(&count[s * kCntStride + threadIdx.x], (int32_t)tot);
+    // this chunk's count at every tree threshold: the compaction's offset at the final one (a
+    // segment that converged keeps the counts of the pass it converged in: later passes exit above)
+    ccnt[(int64_t)c * kCntStride + threadIdx.x] = (int32_t)tot;
   }
 }
 
 // walk up to kDepth adjustments down the counted tree; the node reached becomes the next root
+// fnode[s]: the tree node of the final threshold when the segment converges -- counted by this
+// pass (node < kTree) -- or -1 when the walk ended one level below the counted tree (the
+// compaction then reserves that segment's slots with atomics)
 __global__ void dgc_adjust_tree_kernel(int n_seg, const float* __restrict__ target, float* __restrict__ thr,
-                                       int32_t* __restrict__ count, int32_t* __restrict__ done, int max_iters) {
+                                       int32_t* __restrict__ count, int32_t* __restrict__ done, int max_iters,
+                                       int32_t* __restrict__ fnode) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n_seg || done[s]) return;
   int32_t* cs = count + s * kCntStride;
@@ -213,15 +305,51 @@ __global__ void dgc_adjust_tree_kernel(int n_seg, const float* __restrict__ targ
     }
   }
   thr[s] = t;
-  if (fin || it >= max_iters) done[s] = 1;
+  if (fin || it >= max_iters) {
+    done[s] = 1;
+    fnode[s] = node < kTree ? node : -1;
+  }
   for (int k = 0; k < kTree; ++k) cs[k] = 0;  // recounted by the next pass
   cs[kTree] = it;
 }
 
-constexpr int kPer = 32;
-constexpr int kTile = kBlock * kPer;
+constexpr int kV = 8;                     // float4 per thread per tile
+constexpr int kTileV = kBlock * kV * 4;   // 8192 elements
+constexpr int kScanBlock = 1024;
 
-// |x| >= thr[seg] -> (value, flat index); one atomic per 256x32 tile (grace_scan.h)
+// Chunk output offsets: an exclusive prefix sum over chunks of the count the last count pass
+// formed at the segment's final threshold (ccnt[c][fnode[seg]]; chunks of a segment whose final
+// threshold was not counted contribute 0 and reserve their slots with atomics after the total).
+// Also writes the payload header: word 0 = that total (the atomics add to it), words 1.. = 0.
+__global__ __launch_bounds__(kScanBlock) void dgc_scan_kernel(const int32_t* __restrict__ seg, int n_chunks,
+                                                              const int32_t* __restrict__ ccnt,
+                                                              const int32_t* __restrict__ fnode,
+                                                              int32_t* __restrict__ coff, int32_t* counter,
+                                                              int header_words) {
+  __shared__ int lds[kScanBlock / kWave];
+  int carry = 0;
+  for (int c0 = 0; c0 < n_chunks; c0 += kScanBlock) {
+    const int c = c0 + threadIdx.x;
+    int v = 0;
+    if (c < n_chunks) {
+      const int f = fnode[seg[c]];
+      v = f >= 0 ? ccnt[(int64_t)c * kCntStride + f] : 0;
+    }
+    int tot = 0;
+    const int pre = block_exclusive_scan<kScanBlock>(v, lds, &tot);
+    if (c < n_chunks) coff[c] = carry + pre;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) counter[0] = carry;
+  if (threadIdx.x > 0 && threadIdx.x < header_words) counter[threadIdx.x] = 0;
+}
+
+// |x| >= thr[seg] -> (value, flat index) at the chunk's scanned offset (the selection repeats the
+// count pass's comparison bit for bit, so the chunk fills exactly its range; chunk order, thread-
+// major inside a 256 x 8 x float4 tile: the same payload bytes on every run); chunks of an
+// uncounted final threshold reserve one atomic per tile.  No same-address atomics otherwise: the round-4 kernel
+// took one per tile on the payload counter from every workgroup of the bucket (~2000 on ONE word,
+// serialised at the memory side: 44 us for a 16.6 M-element bucket, 1.5 TB/s).
 // cap: payload capacity -- entries selected past it are not sent (and, with the fused DgcMemory
 // masking, keep their u / v, so they are sent by a later step: spill instead of loss).
 // vmask / umask (optional): DgcMemory.update fused in -- v and u are zeroed where sent.
@@ -230,45 +358,81 @@ __global__ __launch_bounds__(kBlock) void dgc_compact_kernel(ChunkTable ct, cons
                                                              float* __restrict__ out_val,
                                                              int32_t* __restrict__ out_idx, int64_t cap,
                                                              int32_t* __restrict__ counter, float* vmask,
-                                                             float* __restrict__ umask) {
+                                                             float* __restrict__ umask,
+                                                             const int32_t* __restrict__ fnode,
+                                                             const int32_t* __restrict__ coff) {
   __shared__ int lds[kBlock / kWave];
   __shared__ int bcast;
   const int c = blockIdx.x;
   const int s = ct.seg[c];
   const int64_t b = ct.begin[c], e = ct.end[c];
   const float t = thr[s];
-  for (int64_t tb = b; tb < e; tb += kTile) {
-    float v[kPer];
+  const bool scanned = fnode[s] >= 0;
+  int64_t base = scanned ? coff[c] : 0;
+  // 16-B body [a0, a1) in float4 loads (4-B loads ran the pass at ~1.5 TB/s); the <= 3 + 3 head /
+  // tail elements of a misaligned chunk ride along with the first tile (threads 0..5)
+  const int64_t mis = (int64_t)((reinterpret_cast<uintptr_t>(x) >> 2) & 3);
+  int64_t a0 = b + ((4 - ((b + mis) & 3)) & 3);
+  if (a0 > e) a0 = e;
+  const int64_t a1 = a0 + ((e - a0) & ~(int64_t)3);
+  const int nh = (int)(a0 - b), nt = (int)(e - a1);
+  bool first = true;
+  for (int64_t tb = a0; first || tb < a1; tb += kTileV) {
+    float4 v[kV];
     uint32_t take = 0;
 #pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-      const int64_t i = tb + (int64_t)j * kBlock + threadIdx.x;
-      v[j] = 0.f;
-      if (i < e) {
-        v[j] = x[i];
-        take |= (fabsf(v[j]) >= t ? 1u : 0u) << j;
+    for (int j = 0; j < kV; ++j) {
+      const int64_t i = tb + 4 * ((int64_t)j * kBlock + threadIdx.x);
+      v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < a1) {
+        v[j] = *reinterpret_cast<const float4*>(x + i);
+        take |= ((fabsf(v[j].x) >= t ? 1u : 0u) | (fabsf(v[j].y) >= t ? 2u : 0u) | (fabsf(v[j].z) >= t ? 4u : 0u) |
+                 (fabsf(v[j].w) >= t ? 8u : 0u)) << (4 * j);
+      }
+    }
+    float xe = 0.f;
+    int64_t ie = -1;
+    if (first) {
+      const int th = (int)threadIdx.x;
+      ie = th < nh ? b + th : (th < nh + nt ? a1 + (th - nh) : -1);
+      if (ie >= 0) {
+        xe = x[ie];
+        if (!(fabsf(xe) >= t)) ie = -1;
       }
     }
     int tot = 0;
-    const int pre = block_exclusive_scan<kBlock>(__popc(take), lds, &tot);
+    const int pre = block_exclusive_scan<kBlock>(__popc(take) + (ie >= 0 ? 1 : 0), lds, &tot);
     if (tot > 0) {
-      if (threadIdx.x == 0) bcast = atomicAdd(counter, tot);
-      __syncthreads();
-      int64_t p = (int64_t)bcast + pre;
+      if (!scanned) {
+        if (threadIdx.x == 0) bcast = atomicAdd(counter, tot);
+        __syncthreads();
+        base = bcast;
+      }
+      int64_t p = base + pre;
+      auto emit = [&](float val, int64_t i) {
+        if (p < cap) {
+          out_val[p] = val;
+          out_idx[p] = (int32_t)i;
+          if (vmask != nullptr) vmask[i] = 0.f;
+          if (umask != nullptr) umask[i] = 0.f;
+        }
+        ++p;
+      };
 #pragma unroll
-      for (int j = 0; j < kPer; ++j) {
-        if ((take >> j) & 1u) {
-          if (p < cap) {
-            const int64_t i = tb + (int64_t)j * kBlock + threadIdx.x;
-            out_val[p] = v[j];
-            out_idx[p] = (int32_t)i;
-            if (vmask != nullptr) vmask[i] = 0.f;
-            if (umask != nullptr) umask[i] = 0.f;
-          }
-          ++p;
+      for (int j = 0; j < kV; ++j) {
+        const uint32_t tj = (take >> (4 * j)) & 15u;
+        if (tj) {
+          const int64_t i = tb + 4 * ((int64_t)j * kBlock + threadIdx.x);
+          if (tj & 1u) emit(v[j].x, i);
+          if (tj & 2u) emit(v[j].y, i + 1);
+          if (tj & 4u) emit(v[j].z, i + 2);
+          if (tj & 8u) emit(v[j].w, i + 3);
         }
       }
+      if (ie >= 0) emit(xe, ie);
+      if (scanned) base += tot;
     }
+    first = false;
     __syncthreads();
   }
 }
@@ -323,10 +487,9 @@ void dgc_sample(const float* x, int n_seg, const int64_t* seg_off, const int64_t
 
 void dgc_refine(const ChunkTable& ct, int n_seg, const float* x, const TopkState* st, const float* target,
                 int max_iters, float* thr, int32_t* count, int32_t* done, float* u, float* v, float momentum,
-                int first, int64_t n, hipStream_t stream) {
+                int first, int64_t n, int32_t* ccnt, int32_t* fnode, bool init, hipStream_t stream) {
   const int g = (n_seg + 255) / 256;
-  dgc_init_kernel<<<g, 256, 0, stream>>>(n_seg, st, thr, count, done);
-  GRACE_HIP_CHECK(hipMemsetAsync(count, 0, sizeof(int32_t) * (size_t)n_seg * kCntStride, stream));
+  if (init) dgc_init_kernel<<<g, 256, 0, stream>>>(n_seg, st, thr, count, done, fnode);
   const bool fuse = u != nullptr;
   if (fuse && max_iters <= 0) {  // no count pass to carry the compensate: run it alone
     dgc_compensate(x, u, v, momentum, n, first != 0, stream);
@@ -337,19 +500,28 @@ void dgc_refine(const ChunkTable& ct, int n_seg, const float* x, const TopkState
   // (writing u, v); later passes (and the compaction) read v.
   for (int it = 0; it < max_iters; it += kDepth) {
     if (fuse && it == 0)
-      dgc_count_tree_kernel<true><<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, thr, done, count, u, v, momentum, first);
+      dgc_count_tree_kernel<true><<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, thr, done, count, u, v, momentum, first,
+                                                                      ccnt);
     else
       dgc_count_tree_kernel<false><<<ct.n_chunks, kBlock, 0, stream>>>(ct, fuse ? v : x, thr, done, count, nullptr,
-                                                                       nullptr, 0.f, 0);
-    dgc_adjust_tree_kernel<<<g, 256, 0, stream>>>(n_seg, target, thr, count, done, max_iters);
+                                                                       nullptr, 0.f, 0, ccnt);
+    dgc_adjust_tree_kernel<<<g, 256, 0, stream>>>(n_seg, target, thr, count, done, max_iters, fnode);
   }
 }
 
+void dgc_select_init(int n_seg, const float* samples, const int64_t* samp_off, const int32_t* kseg, TopkState* st,
+                     float* thr, int32_t* count, int32_t* done, int32_t* fnode, hipStream_t stream) {
+  if (n_seg <= 0) return;
+  dgc_select_init_kernel<<<n_seg, kSelBlock, 0, stream>>>(samples, samp_off, kseg, st, thr, count, done, fnode);
+}
+
 void dgc_compact(const ChunkTable& ct, const float* x, const float* thr, float* out_val, int32_t* out_idx,
-                 int64_t cap, int32_t* counter, float* vmask, float* umask, hipStream_t stream, int header_bytes) {
-  GRACE_HIP_CHECK(hipMemsetAsync(counter, 0, header_bytes, stream));
+                 int64_t cap, int32_t* counter, float* vmask, float* umask, const int32_t* ccnt,
+                 const int32_t* fnode, int32_t* coff, hipStream_t stream, int header_bytes) {
+  dgc_scan_kernel<<<1, kScanBlock, 0, stream>>>(ct.seg, ct.n_chunks, ccnt, fnode, coff, counter, header_bytes / 4);
   if (ct.n_chunks == 0) return;
-  dgc_compact_kernel<<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, thr, out_val, out_idx, cap, counter, vmask, umask);
+  dgc_compact_kernel<<<ct.n_chunks, kBlock, 0, stream>>>(ct, x, thr, out_val, out_idx, cap, counter, vmask, umask,
+                                                         fnode, coff);
 }
 
 void dgc_compensate(const float* g, float* u, float* v, float momentum, int64_t n, bool first, hipStream_t stream) {

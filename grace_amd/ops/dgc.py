@@ -45,7 +45,6 @@ def dgc_select(x: torch.Tensor, layout: SegmentLayout, ratio: float, sample_rati
         C = _native.lib()
         slay = layout.cached(dev, f"dgc_sample_layout:{sample_ratio}",
                              lambda: SegmentLayout(ns, tuple((s,) for s in ns)))
-        st = slay.device_tables(dev)
         t = layout.device_tables(dev)
 
         def build():
@@ -55,6 +54,11 @@ def dgc_select(x: torch.Tensor, layout: SegmentLayout, ratio: float, sample_rati
                 "thr": torch.empty(layout.n_seg, dtype=torch.float32, device=dev),
                 "count": torch.empty(32 * layout.n_seg, dtype=torch.int32, device=dev),  # tree counts + steps
                 "done": torch.empty(layout.n_seg, dtype=torch.int32, device=dev),
+                # per-chunk tree counts, final counted node per segment, chunk output offsets: the
+                # compaction places every chunk at a scanned offset (no payload-counter atomics)
+                "ccnt": torch.empty(32 * max(1, t["n_chunks"]), dtype=torch.int32, device=dev),
+                "fnode": torch.empty(layout.n_seg, dtype=torch.int32, device=dev),
+                "coff": torch.empty(max(1, t["n_chunks"]), dtype=torch.int32, device=dev),
                 "samples": torch.empty(max(1, slay.total), dtype=torch.float32, device=dev),
             }
 
@@ -67,12 +71,14 @@ def dgc_select(x: torch.Tensor, layout: SegmentLayout, ratio: float, sample_rati
         mom, first = compensate if fuse else (0.0, False)
         C.dgc_sample(x, t["offsets"], ws["samp_off"], sd, step, samples, cu, cv, float(mom), bool(first))
         tw = _topk_ws(slay, ks, dev)
-        C.topk_select(samples, None, samples, 1.0, 1.0, 0, st["seg"], st["begin"], st["end"], tw["kseg"],
-                      tw["state"], tw["hist"])
+        # exact k'-th largest |sample| per segment + the refinement state, one launch
+        C.dgc_select_init(samples, ws["samp_off"], tw["kseg"], tw["state"], ws["thr"], ws["count"], ws["done"],
+                          ws["fnode"])
         C.dgc_refine(x, tw["state"], ws["target"], max_iters, ws["thr"], ws["count"], ws["done"], t["seg"],
-                     t["begin"], t["end"], cu, cv, float(mom), bool(first))
+                     t["begin"], t["end"], ws["ccnt"], ws["fnode"], cu, cv, float(mom), bool(first), init=False)
         sel = vmask if fuse else x  # after the fused refinement v holds the compensated values
-        C.dgc_compact(sel, ws["thr"], v, i, hdr[:1], t["seg"], t["begin"], t["end"], vmask, umask)
+        C.dgc_compact(sel, ws["thr"], v, i, hdr[:1], t["seg"], t["begin"], t["end"], ws["ccnt"], ws["fnode"],
+                      ws["coff"], vmask, umask)
         return hdr, v, i
     if compensate is not None:
         raise ValueError("fused compensate needs the native path")

@@ -574,3 +574,62 @@ def test_powersgd_deferred_residual_bit_identical(graphed):
             CP._DEFER_RESID = old
     for i, (a, b) in enumerate(zip(outs[False], outs[True])):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5, msg=lambda m, i=i: f"step {i}: {m}")
+
+
+@pytest.mark.parametrize("max_iters", [0, 2, 5, 7, 10])
+def test_dgc_scanned_compaction_exact(max_iters):
+    """The DGC compaction places every chunk at a prefix-summed offset of the count pass's per-chunk
+    counts (segments whose final threshold was never counted -- max_iters 0, or a walk that ended
+    below the counted tree -- reserve slots with atomics after them): the payload holds exactly the
+    entries |x| >= thr[segment], each once, the header counts them, and a too-small capacity keeps
+    a duplicate-free subset with the full count in the header."""
+    from grace_amd.ops import dgc as D
+
+    flat, lay = _bucket()
+    x = flat.cuda() * torch.linspace(0.2, 3.0, flat.numel(), device="cuda")
+    dev = x.device
+    seg_of = torch.repeat_interleave(torch.arange(lay.n_seg), torch.tensor(lay.numels))
+    for capf in (2.0, 0.3):
+        cap = D.dgc_capacity(lay, 0.01, capf)
+        hdr, v, i = D.dgc_select(x, lay, 0.01, 0.01, max_iters, 7, cap)
+        torch.cuda.synchronize()
+        ws = lay.cached(dev, "dgc_ws:0.01:0.01", lambda: None)
+        thr = ws["thr"].cpu()
+        xa = x.cpu()
+        sel = (xa.abs() >= thr[seg_of]).nonzero().flatten()
+        count = int(hdr[0])
+        assert count == sel.numel(), (capf, count, sel.numel())
+        k = min(count, cap)
+        got = i[:k].cpu().long()
+        assert got.unique().numel() == k, "duplicate slots"
+        assert torch.equal(xa[got], v[:k].cpu()), "value / index mismatch"
+        if k == count:
+            assert torch.equal(got.sort().values, sel), "selected set differs"
+        else:
+            assert bool(torch.isin(got, sel).all()), "entry below its threshold sent"
+        if max_iters == 0:
+            assert bool((ws["fnode"] < 0).all())
+
+
+def test_dgc_sample_select_is_exact_kth_largest():
+    """The one-launch sample select (one workgroup per segment, samples in LDS up to 24576 and
+    re-read from memory beyond) starts the refinement at exactly the k'-th largest |sample| of
+    every segment -- the reference's torch.topk(samples, k').values.min() (dgc.py:21-24)."""
+    from grace_amd.ops import dgc as D
+    from grace_amd.ops.dgc import _sizes
+
+    shapes = [(3000, 1000), (512, 300), (1000,), (64, 3, 3, 3), (7,), (2, 2)]
+    lay = SegmentLayout.from_tensors([torch.empty(s) for s in shapes])
+    x = torch.randn(lay.total, generator=torch.Generator().manual_seed(4)).cuda()
+    D.dgc_select(x, lay, 0.01, 0.01, 0, 11, D.dgc_capacity(lay, 0.01, 2.0))
+    torch.cuda.synchronize()
+    ws = lay.cached(x.device, "dgc_ws:0.01:0.01", lambda: None)
+    ns, ks = _sizes(lay, 0.01, 0.01)
+    assert max(ns) > 24576  # the memory-resident path runs too
+    samp = ws["samples"].cpu()
+    thr = ws["thr"].cpu()
+    o = 0
+    for s, (n_s, k) in enumerate(zip(ns, ks)):
+        ref = torch.topk(samp[o:o + n_s].abs(), k).values.min()
+        assert torch.equal(thr[s], ref), (s, float(thr[s]), float(ref))
+        o += n_s
