@@ -95,8 +95,11 @@ __global__ __launch_bounds__(kBlock) void ps_mq_kernel(const float* __restrict__
   const float* Q = Qall + mt.q_off;
   const int lane = lane_id(), w = wave_id();
   const int64_t row0 = (int64_t)tl[1] * kRB0 + 4 * w;
-  const int64_t c0 = (int64_t)tl[2] * kCS0;
-  const int64_t c1 = c0 + kCS0 < m ? c0 + kCS0 : m;
+  // tl[2] = strip index | log2(strip columns) << 24 (0: kCS0) -- the strip length is a host choice
+  const int lg = tl[2] >> 24;
+  const int64_t cs = lg ? (int64_t(1) << lg) : kCS0;
+  const int64_t c0 = (int64_t)(tl[2] & 0xffffff) * cs;
+  const int64_t c1 = c0 + cs < m ? c0 + cs : m;
   float acc[4][R];
 #pragma unroll
   for (int a = 0; a < 4; ++a)

@@ -7,6 +7,7 @@ plus the 1-D segments that bypass the low-rank path.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
@@ -14,6 +15,14 @@ import torch
 
 from . import _native
 from .layout import SegmentLayout
+
+
+# ps_mq column strip (power of two, 512..65536) and the ps_mtp workgroup target per matrix
+# (row strips x 1024-column blocks): tuning knobs, GRACE_PS_MQ_COLS / GRACE_PS_MTP_WG
+_MQ_COLS = int(os.environ.get("GRACE_PS_MQ_COLS", "2048"))
+_MTP_WG = int(os.environ.get("GRACE_PS_MTP_WG", "1024"))
+if _MQ_COLS < 512 or _MQ_COLS > 65536 or _MQ_COLS & (_MQ_COLS - 1):
+    raise ValueError("GRACE_PS_MQ_COLS must be a power of two in [512, 65536]")
 
 
 @dataclass
@@ -37,17 +46,19 @@ class Plan:
             # work tables of csrc/kernels/powersgd.hip (ps_mq: 16 rows x 2048 columns; ps_mtp:
             # 1024 / 256 columns x per-matrix row strips; ps_pqt: 32 rows x 1024 / 256 columns)
             t0, t1, tp = [], [], []
+            cs = _MQ_COLS
+            lg = cs.bit_length() - 1
             for i, (xo, n, m, r, po, qo) in enumerate(self.mats):
                 cb = 1024 if (xo % 4 == 0 and m % 4 == 0) else 256
                 for rb in range((n + 15) // 16):
-                    for sidx in range((m + 2047) // 2048):
-                        t0.append((i, rb, sidx))
+                    for sidx in range((m + cs - 1) // cs):
+                        t0.append((i, rb, sidx | (lg << 24)))
                 # ps_mtp: 1024 (16-B path) / 256 (4-B path) column blocks; rows split into strips of a
                 # multiple of 32 rows so that the matrix yields >= ~1024 workgroups (too few waves
                 # left the product latency bound)
                 ncb = (m + cb - 1) // cb
                 n32 = (n + 31) // 32
-                strips = max(1, min(n32, -(-1024 // ncb)))
+                strips = max(1, min(n32, -(-_MTP_WG // ncb)))
                 per = -(-n32 // strips)
                 for c in range(ncb):
                     for s0 in range(0, n32, per):
