@@ -134,15 +134,27 @@ struct Operand {
   // mode 3: this thread's (fixed) row r = tap * C + c
   int rdy, rdx, rc;
   bool rok;
+  // modes 2 / 4: (tap, offset inside the tap) of the NEXT k-slice to load, advanced by BK per load
+  // (slices are loaded strictly in order) -- no per-stage integer division: a division by a
+  // runtime value is ~40 scalar instructions, and two per stage made the 3x3 implicit GEMMs issue
+  // 4x the scalar instructions of MIOpen's solvers (profiles/r5_c3_pmc.txt)
+  int ltap, lc, lty, ltx;
   bool xf;           // BN-apply prologue on this operand
   float4 xsc, xsh;   // the channels' scale / shift: fixed rows (MN modes) or this slice's k (KC)
   uint32_t xok;      // bit i: v[i] was loaded (transformed at store; padding / out of range stays 0)
   int xrelu;
 
-  __device__ __forceinline__ void init(const GemmParams& p, int r0, int rmax, int which) {
+  __device__ __forceinline__ void init(const GemmParams& p, int r0, int rmax, int which, int kb) {
     xf = p.xsave != nullptr && p.xop == which;
     xrelu = p.xrelu;
     xok = 0;
+    if constexpr (MODE == 2 || MODE == 4) {  // one division per workgroup (the split's first slice)
+      const int per = MODE == 2 ? p.gC : p.kt;
+      ltap = kb / per;
+      lc = kb - ltap * per;
+      lty = ltap / 3;
+      ltx = ltap - 3 * lty;
+    }
     if (xf && !KC) {  // rows are channels (mode 1: r; mode 3: rc), fixed per thread
       int c = r0 + 4 * (threadIdx.x % TPR);
       if constexpr (MODE == 3) c = (c < rmax ? c : 0) % p.gC;
@@ -174,9 +186,10 @@ struct Operand {
   __device__ __forceinline__ void load(const GemmParams& p, const float* __restrict__ x, int64_t ld, int r0, int rmax,
                                        int k0, int kmax) {
     if constexpr (MODE == 2) {
-      const int tap = k0 / p.gC;  // uniform over the slice (C % BK == 0)
-      const int dy = p.gT == 3 ? (tap / 3 - 1) * p.gSign : 0, dx = p.gT == 3 ? (tap % 3 - 1) * p.gSign : 0;
-      const int c = k0 - tap * p.gC + 4 * (threadIdx.x % (BK / 4));
+      // tap (uniform over the slice: C % BK == 0) from the running state, then advance it
+      const int dy = p.gT == 3 ? (lty - 1) * p.gSign : 0, dx = p.gT == 3 ? (ltx - 1) * p.gSign : 0;
+      const int c = lc + 4 * (threadIdx.x % (BK / 4));
+      advance(p.gC);
       if (xf) {  // consumed at store(): the loads stay in flight across the MFMAs
         xsc = *reinterpret_cast<const float4*>(p.xsave + 2 * p.xC + c);
         xsh = *reinterpret_cast<const float4*>(p.xsave + 3 * p.xC + c);
@@ -227,14 +240,24 @@ struct Operand {
           }
         }
       } else if constexpr (MODE == 4) {
-        if (r < rmax && k < kmax) {
-          const int tap = k0 / p.kt;  // uniform over the slice (kt % BK == 0)
-          v[i] = *reinterpret_cast<const float4*>(x + tap * p.tap_off + (int64_t)(k - tap * p.kt) * ld + r);
-        }
+        if (r < rmax && k < kmax)  // tap uniform over the slice (kt % BK == 0): the running state
+          v[i] = *reinterpret_cast<const float4*>(x + ltap * p.tap_off + (int64_t)(lc + (k - k0)) * ld + r);
       } else if (r < rmax && k < kmax) {
         v[i] = KC ? *reinterpret_cast<const float4*>(x + (int64_t)r * ld + k)
                   : *reinterpret_cast<const float4*>(x + (int64_t)k * ld + r);
         xok |= 1u << i;
+      }
+    }
+    if constexpr (MODE == 4) advance(p.kt);
+  }
+  __device__ __forceinline__ void advance(int per) {
+    lc += BK;
+    if (lc >= per) {
+      lc -= per;
+      ++ltap;
+      if (++ltx == 3) {
+        ltx = 0;
+        ++lty;
       }
     }
   }
@@ -302,8 +325,8 @@ __global__ __launch_bounds__(kGB, 2) void gemm_f32_kernel(GemmParams p) {
 
   OA oa;
   OB ob;
-  oa.init(p, m0, p.M, 1);
-  ob.init(p, n0, p.N, 2);
+  oa.init(p, m0, p.M, 1, kb);
+  ob.init(p, n0, p.N, 2, kb);
   if (kb < ke) {
     oa.load(p, p.A, p.lda, m0, p.M, kb, ke);
     ob.load(p, p.B, p.ldb, n0, p.N, kb, ke);
