@@ -132,6 +132,105 @@ __global__ __launch_bounds__(kBlock) void threshold_compact_kernel(const float* 
   }
 }
 
+// The same with float4 loads / stores (g, r and resid 16-B aligned: the host checks), 8 float4 per
+// thread per 8192-element tile; the <= 3 trailing elements ride along with block 0's first tile.
+// (The 4-B form moved a ResNet-50 bucket at ~1.5 TB/s: 32 dword loads per thread per tile.)
+constexpr int kV = 8;
+constexpr int kTileV = kBlock * kV * 4;
+
+__global__ __launch_bounds__(kBlock) void threshold_compact_v4_kernel(const float* g, const float* r, int mode,
+                                                                      float beta, float gamma, int64_t n,
+                                                                      float thr, float* __restrict__ out_val,
+                                                                      int32_t* __restrict__ out_idx, int64_t cap,
+                                                                      int32_t* __restrict__ counter,
+                                                                      float* resid) {
+  __shared__ int lds[kBlock / kWave];
+  __shared__ int bcast;
+  const int64_t n4 = n & ~(int64_t)3;
+  const int nt = (int)(n - n4);
+  bool first = blockIdx.x == 0;
+  for (int64_t tb = (int64_t)blockIdx.x * kTileV; first || tb < n4; tb += (int64_t)gridDim.x * kTileV) {
+    float4 v[kV];
+    uint32_t take = 0;
+#pragma unroll
+    for (int j = 0; j < kV; ++j) {
+      const int64_t i = tb + 4 * ((int64_t)j * kBlock + threadIdx.x);
+      v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < n4) {
+        float4 x = *reinterpret_cast<const float4*>(g + i);
+        if (mode == 1) {
+          const float4 rr = *reinterpret_cast<const float4*>(r + i);
+          x = make_float4(fmaf(beta, rr.x, gamma * x.x), fmaf(beta, rr.y, gamma * x.y), fmaf(beta, rr.z, gamma * x.z),
+                          fmaf(beta, rr.w, gamma * x.w));
+        }
+        v[j] = x;
+        take |= ((fabsf(x.x) > thr ? 1u : 0u) | (fabsf(x.y) > thr ? 2u : 0u) | (fabsf(x.z) > thr ? 4u : 0u) |
+                 (fabsf(x.w) > thr ? 8u : 0u)) << (4 * j);
+      }
+    }
+    float xe = 0.f;
+    int64_t ie = -1;
+    bool te = false;
+    if (first && (int)threadIdx.x < nt) {
+      ie = n4 + threadIdx.x;
+      xe = g[ie];
+      if (mode == 1) xe = fmaf(beta, r[ie], gamma * xe);
+      te = fabsf(xe) > thr;
+    }
+    int tot = 0;
+    const int pre = block_exclusive_scan<kBlock>(__popc(take) + (te ? 1 : 0), lds, &tot);
+    uint32_t sent = 0;
+    bool sente = false;
+    if (tot > 0) {
+      if (threadIdx.x == 0) bcast = atomicAdd(counter, tot);
+      __syncthreads();
+      int64_t p = (int64_t)bcast + pre;
+#pragma unroll
+      for (int j = 0; j < kV; ++j) {
+        const uint32_t tj = (take >> (4 * j)) & 15u;
+        if (tj) {
+          const int64_t i = tb + 4 * ((int64_t)j * kBlock + threadIdx.x);
+          const float e[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if ((tj >> q) & 1u) {
+              if (p < cap) {
+                out_val[p] = e[q];
+                out_idx[p] = (int32_t)(i + q);
+                sent |= 1u << (4 * j + q);
+              }
+              ++p;
+            }
+          }
+        }
+      }
+      if (te) {
+        if (p < cap) {
+          out_val[p] = xe;
+          out_idx[p] = (int32_t)ie;
+          sente = true;
+        }
+        ++p;
+      }
+    }
+    if (resid != nullptr) {  // spilled (selected past the capacity) entries stay in the residual
+#pragma unroll
+      for (int j = 0; j < kV; ++j) {
+        const int64_t i = tb + 4 * ((int64_t)j * kBlock + threadIdx.x);
+        if (i < n4) {
+          const uint32_t sj = (sent >> (4 * j)) & 15u;
+          *reinterpret_cast<float4*>(resid + i) =
+              make_float4((sj & 1u) ? 0.f : v[j].x, (sj & 2u) ? 0.f : v[j].y, (sj & 4u) ? 0.f : v[j].z,
+                          (sj & 8u) ? 0.f : v[j].w);
+        }
+      }
+      if (ie >= 0) resid[ie] = sente ? 0.f : xe;
+    }
+    first = false;
+    __syncthreads();
+  }
+}
+
 inline int grid_for(int64_t n) {
   int64_t b = (n + kBlock - 1) / kBlock;
   if (b > 2048) b = 2048;
@@ -161,6 +260,14 @@ void threshold_compact(const float* g, const float* r, int mode, float beta, flo
                        hipStream_t stream, int header_bytes) {
   GRACE_HIP_CHECK(hipMemsetAsync(counter, 0, header_bytes, stream));
   if (n <= 0) return;
+  auto a16 = [](const void* q) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  if (a16(g) && (mode != 1 || a16(r)) && a16(resid)) {
+    int64_t tiles = (n + kTileV - 1) / kTileV;
+    if (tiles > 2048) tiles = 2048;
+    threshold_compact_v4_kernel<<<(int)tiles, kBlock, 0, stream>>>(g, r, mode, beta, gamma, n, thr, out_val,
+                                                                   out_idx, cap, counter, resid);
+    return;
+  }
   int64_t tiles = (n + kTile - 1) / kTile;
   if (tiles > 2048) tiles = 2048;
   threshold_compact_kernel<<<(int)tiles, kBlock, 0, stream>>>(g, r, mode, beta, gamma, n, thr, out_val, out_idx,

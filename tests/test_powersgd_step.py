@@ -125,3 +125,62 @@ def test_powersgd_pqt_scale_folds_average():
     PS.pqt(p, q, plan, a)
     PS.pqt(p, q, plan, b, scale=0.25)
     torch.testing.assert_close(b, a * 0.25)
+
+
+def test_deferred_residual_ops_match_eager_update_cpu():
+    """ops.powersgd: the deferred residual -- mq(comp_r=M_prev, lazy=(P, Q, s)) -- compensates with
+    exactly the residual the eager pqt(resid=...) update would have left (same float ops on the
+    PyTorch path), and pqt(out=None, resid=...) materialises it."""
+    from grace_amd.ops import powersgd as PS
+    from grace_amd.ops.layout import SegmentLayout
+
+    g = torch.Generator().manual_seed(0)
+    shapes = [(30, 20), (7,), (8, 3, 3, 3)]
+    lay = SegmentLayout.from_tensors([torch.empty(s) for s in shapes])
+    plan = PS.plan_for(lay, 2)
+    m_prev = torch.randn(lay.total, generator=g)
+    p = torch.randn(plan.p_total, generator=g)
+    q = torch.randn(plan.q_total, generator=g)
+    s = 0.25
+    # eager: r = M_prev - s P Q^T on the matrix segments (pqt), then M = 0.9 r + 1.0 x
+    r_eager = m_prev.clone()
+    PS.pqt(p, q, plan, torch.empty(lay.total), resid=r_eager, scale=s)
+    x = torch.randn(lay.total, generator=g)
+    q_new = torch.randn(plan.q_total, generator=g)
+    out_e = r_eager.clone()
+    p_e = PS.mq(x, q_new, plan, comp_r=r_eager.clone(), beta=0.9, gamma=1.0, xout=out_e)
+    out_d = m_prev.clone()
+    p_d = PS.mq(x, q_new, plan, comp_r=m_prev.clone(), beta=0.9, gamma=1.0, xout=out_d, lazy=(p, q, s))
+    for (xo, n, mm, rr, po, qo) in plan.mats:
+        assert torch.equal(out_e[xo:xo + n * mm], out_d[xo:xo + n * mm])
+    assert torch.equal(p_e, p_d)
+    r_mat = m_prev.clone()
+    PS.pqt(p, q, plan, None, resid=r_mat, scale=s)  # materialise only
+    assert torch.equal(r_mat, r_eager)
+
+
+def test_powersgd_memory_state_dict_materialises_copy_cpu():
+    """PowerSGDMemory with a deferred entry: state_dict() returns M - s P Q^T and leaves the live
+    buffer (M) untouched; materialize() applies it in place; load_state_dict clears the deferral."""
+    from grace_amd.memory.powersgd import PowerSGDMemory
+    from grace_amd.ops import powersgd as PS
+    from grace_amd.ops.layout import SegmentLayout
+
+    g = torch.Generator().manual_seed(1)
+    lay = SegmentLayout.from_tensors([torch.empty(12, 5), torch.empty(3)])
+    plan = PS.plan_for(lay, 2)
+    mem = PowerSGDMemory(compress_rank=2)
+    m = torch.randn(lay.total, generator=g)
+    mem.residuals["b"] = m.clone()
+    p, q = torch.randn(plan.p_total, generator=g), torch.randn(plan.q_total, generator=g)
+    mem.lazy["b"] = (p, q, 0.5, plan)
+    want = m.clone()
+    PS.pqt(p, q, plan, None, resid=want, scale=0.5)
+    sd = mem.state_dict()
+    assert torch.equal(sd["residuals"]["b"], want)
+    assert torch.equal(mem.residuals["b"], m) and "b" in mem.lazy
+    mem.materialize()
+    assert torch.equal(mem.residuals["b"], want) and not mem.lazy
+    mem.lazy["b"] = (p, q, 0.5, plan)
+    mem.load_state_dict(sd)
+    assert not mem.lazy and torch.equal(mem.residuals["b"], want)

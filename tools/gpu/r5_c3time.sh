@@ -9,3 +9,7 @@ for cfg in "32 256 14 14 1 4 1" "32 256 14 14 1 2 1" "32 256 14 14 1 -1 1" "32 5
 done
 timeout -k 10 400 python -u tools/gpu/conv3_bench.py > $D/conv3_bench.txt 2>&1 || exit 1
 grep -v amdgpu.ids $D/conv3_bench.txt | cut -c1-250
+timeout -k 10 300 python -u -m pytest tests/test_gpu_compressors.py tests/test_gpu_capacity_graph.py -x -q -k "threshold or capacity" \
+  --timeout 250 --timeout-method thread > $D/thr_tests.log 2>&1 || { tail -20 $D/thr_tests.log; exit 1; }
+grep -E "passed|failed" $D/thr_tests.log | tail -1
+timeout -k 10 200 python -u benchmarks/grace_kernels.py --pipeline threshold --iters 30 --bucket-mb 128 2>&1 | grep -v amdgpu.ids | tail -2
