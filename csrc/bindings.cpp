@@ -880,6 +880,8 @@ int64_t conv3x3_f32(int64_t dir, const Tensor& act, const Tensor& other, const T
     check_cl(act, {N, Cin, H, W}, "x");
   }
   TORCH_CHECK(N * H * W < (1 << 24), "conv3x3_f32: N*H*W < 2^24 (float pixel division)");
+  TORCH_CHECK(act.numel() < (int64_t(1) << 31) && other.numel() < (int64_t(1) << 31) && C.numel() < (int64_t(1) << 31),
+              "conv3x3_f32: operands of < 2^31 elements (32-bit gather indices)");
   float* st = nullptr;
   grace::BnBwdEpi epi{};
   const bool has_epi = dir == 1 && bn_epi(bn_x, bn_mask, bn_save, bn_relu, N * H * W, Cin, &epi);

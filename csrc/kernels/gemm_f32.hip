@@ -139,6 +139,10 @@ struct Operand {
   // runtime value is ~40 scalar instructions, and two per stage made the 3x3 implicit GEMMs issue
   // 4x the scalar instructions of MIOpen's solvers (profiles/r5_c3_pmc.txt)
   int ltap, lc, lty, ltx;
+  // mode 3: output pixel (n, oy, ox) of each of this thread's k rows of the NEXT slice, advanced by
+  // BK = (dn, doy, dox) pixels per load with one conditional carry each (no per-element division)
+  int kn[MODE == 3 ? NV : 1], koy[MODE == 3 ? NV : 1], kox[MODE == 3 ? NV : 1];
+  int dn, doy, dox;
   bool xf;           // BN-apply prologue on this operand
   float4 xsc, xsh;   // the channels' scale / shift: fixed rows (MN modes) or this slice's k (KC)
   uint32_t xok;      // bit i: v[i] was loaded (transformed at store; padding / out of range stays 0)
@@ -174,6 +178,19 @@ struct Operand {
         pn[i] = n * p.gHs;
       }
     } else if constexpr (MODE == 3) {
+      const int hw = p.gHr * p.gWr;
+      dn = BK / hw;
+      doy = (BK - dn * hw) / p.gWr;
+      dox = BK - dn * hw - doy * p.gWr;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int k = kb + threadIdx.x / TPR + (kGB / TPR) * i;
+        int ox, oy;
+        const int q = fdivmod(k, p.gWr, p.gInvWr, &ox);
+        kn[i] = fdivmod(q, p.gHr, p.gInvHr, &oy);
+        koy[i] = oy;
+        kox[i] = ox;
+      }
       const int r = r0 + 4 * (threadIdx.x % TPR);
       rok = r < rmax;
       const int tap = r / p.gC;
@@ -200,7 +217,8 @@ struct Operand {
         const int iy = sy[i] + dy, ix = sx[i] + dx;
         v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
         if ((unsigned)iy < (unsigned)p.gHs && (unsigned)ix < (unsigned)p.gWs && k0 < kmax) {
-          v[i] = *reinterpret_cast<const float4*>(x + ((int64_t)(pn[i] + iy) * p.gWs + ix) * p.gC + c);
+          // 32-bit element index (the binding checks every operand has < 2^31 elements)
+          v[i] = *reinterpret_cast<const float4*>(x + (uint32_t)(((pn[i] + iy) * p.gWs + ix) * p.gC + c));
           xok |= 1u << i;  // outside the image: the padding's 0, never transformed
         }
       }
@@ -229,19 +247,31 @@ struct Operand {
       }
       v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
       if constexpr (MODE == 3) {
+        const int n = kn[i], oy = koy[i], ox = kox[i];
+        {  // advance this k row to the next slice: + BK pixels
+          int nx = ox + dox, ny = oy + doy, nn = n + dn;
+          if (nx >= p.gWr) {
+            nx -= p.gWr;
+            ++ny;
+          }
+          if (ny >= p.gHr) {
+            ny -= p.gHr;
+            ++nn;
+          }
+          kn[i] = nn;
+          koy[i] = ny;
+          kox[i] = nx;
+        }
         if (rok && k < kmax) {
-          int ox, oy;
-          const int q = fdivmod(k, p.gWr, p.gInvWr, &ox);
-          const int n = fdivmod(q, p.gHr, p.gInvHr, &oy);
           const int iy = oy * p.gS + rdy, ix = ox * p.gS + rdx;
           if ((unsigned)iy < (unsigned)p.gHs && (unsigned)ix < (unsigned)p.gWs) {
-            v[i] = *reinterpret_cast<const float4*>(x + ((int64_t)(n * p.gHs + iy) * p.gWs + ix) * p.gC + rc);
+            v[i] = *reinterpret_cast<const float4*>(x + (uint32_t)(((n * p.gHs + iy) * p.gWs + ix) * p.gC + rc));
             xok |= 1u << i;
           }
         }
       } else if constexpr (MODE == 4) {
         if (r < rmax && k < kmax)  // tap uniform over the slice (kt % BK == 0): the running state
-          v[i] = *reinterpret_cast<const float4*>(x + ltap * p.tap_off + (int64_t)(lc + (k - k0)) * ld + r);
+          v[i] = *reinterpret_cast<const float4*>(x + (uint32_t)(ltap * (int)p.tap_off + (lc + (k - k0)) * (int)ld + r));
       } else if (r < rmax && k < kmax) {
         v[i] = KC ? *reinterpret_cast<const float4*>(x + (int64_t)r * ld + k)
                   : *reinterpret_cast<const float4*>(x + (int64_t)k * ld + r);
