@@ -240,7 +240,16 @@ def main():
 
         esz = 2 if w.grace.get("compressor") == "fp16" else 4
         nbytes = min(sum(p.numel() for p in model.parameters()) * esz, int(args.bucket_mb * 2 ** 20))
-        rccl_pre = RcclComm.tuned(nbytes)  # collective: every rank builds / probes the candidates
+        try:
+            rccl_pre = RcclComm.tuned(nbytes)  # collective: every rank builds / probes the candidates
+        except Exception as e:  # noqa: BLE001 -- e.g. no ncclConfig support: keep the default comm
+            print(f"[rank {rank}] RCCL CTA probe failed ({type(e).__name__}: {str(e)[:120]}); default channels",
+                  file=sys.stderr, flush=True)
+            rccl_pre = None
+        ok_t = torch.tensor([0 if rccl_pre is None else 1], device=dev)
+        dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)  # every rank keeps the probe, or none does
+        if ok_t.item() == 0:
+            rccl_pre = None
     if args.overlap == "auto" and mode == "full" and world > 1:
         est_ms = 0.0
         if rccl_pre is not None:
