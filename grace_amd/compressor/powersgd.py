@@ -31,10 +31,6 @@ r > 4, register-resident MGS for r <= 4, and decompress P Q^T fused with the res
 """
 from __future__ import annotations
 
-import math
-from dataclasses import dataclass
-from typing import List, Tuple
-
 import torch
 
 from ..ops import powersgd as PS

@@ -6,7 +6,6 @@ plus the 1-D segments that bypass the low-rank path.
 """
 from __future__ import annotations
 
-import math
 import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
