@@ -123,9 +123,21 @@ __global__ __launch_bounds__(kBlock) void ps_mq_kernel(const float* __restrict__
     for (int j = 0; j < R; ++j) v = fmaf(lp[rr][j], lq[j], v);
     return v * lz.s;
   };
+  // r = 4 (the BASELINE rank): the iteration's 512 Q (and Q') rows are staged through LDS by the
+  // whole block -- coalesced 16-B loads, transposed to [j][column] so each lane then takes its 4
+  // columns' values with one conflict-free ds_read_b128 per j.  Direct per-lane loads of those
+  // rows (4 x 16 B at a 64-B lane stride, the same rows re-fetched by all 4 waves) were half of
+  // the kernel's vector loads and left it latency-bound (profiles/r5_powersgd_pmc.txt).
+  constexpr int kStage = 512;  // columns per iteration (kCU * 4 * kWave)
+  __shared__ __align__(16) float sq[(R == 4) ? (COMP == 3 ? 2 : 1) * 4 * kStage : 1];
+  const bool staged = R == 4 && r == 4 && (reinterpret_cast<uintptr_t>(Q) & 15) == 0 &&
+                      (COMP != 3 || (reinterpret_cast<uintptr_t>(lz.q + mt.q_off) & 15) == 0);
   if (mat_vec(mt)) {
     constexpr int kCU = 2;  // column chunks per iteration: 4 rows x 2 chunks (x2 with COMP 2) loads in flight
-    for (int64_t cb = c0 + 4 * lane; cb < c1; cb += 4 * kWave * kCU) {
+    // the trip count is block-uniform (iterations step the uniform chunk start; lanes past the
+    // strip's end load nothing): the staged path's barriers are reached by every thread
+    for (int64_t base = c0; base < c1; base += 4 * kWave * kCU) {
+      const int64_t cb = base + 4 * lane;
       float4 mv[kCU][4], rv[kCU][4];
 #pragma unroll
       for (int k = 0; k < kCU; ++k)
@@ -140,17 +152,58 @@ __global__ __launch_bounds__(kBlock) void ps_mq_kernel(const float* __restrict__
             if (COMP >= 2) rv[k][rr] = *reinterpret_cast<const float4*>(cr + gi);
           }
         }
+      if constexpr (R == 4) {
+        if (staged) {
+          const float* lqg = COMP == 3 ? lz.q + mt.q_off : nullptr;
+          for (int u = threadIdx.x; u < kStage; u += kBlock) {
+            const int64_t col = base + u;
+            float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+            if (col < c1) {
+              a = *reinterpret_cast<const float4*>(Q + col * 4);
+              if (COMP == 3) b = *reinterpret_cast<const float4*>(lqg + col * 4);
+            }
+            sq[0 * kStage + u] = a.x;
+            sq[1 * kStage + u] = a.y;
+            sq[2 * kStage + u] = a.z;
+            sq[3 * kStage + u] = a.w;
+            if (COMP == 3) {
+              sq[4 * kStage + u] = b.x;
+              sq[5 * kStage + u] = b.y;
+              sq[6 * kStage + u] = b.z;
+              sq[7 * kStage + u] = b.w;
+            }
+          }
+          __syncthreads();
+        }
+      }
 #pragma unroll
       for (int k = 0; k < kCU; ++k) {
         const int64_t c = cb + (int64_t)k * 4 * kWave;
         if (c >= c1) break;
         float q[4][R];
+        // the 4 columns' rows: from the LDS image (staged, r = 4) or straight from memory
+        auto rows4 = [&](int which, const float* g, float (&o)[4][R]) {
+          if constexpr (R == 4) {
+            if (staged) {
+              const int u = (int)(c - base);
 #pragma unroll
-        for (int t = 0; t < 4; ++t) load_small_row<R>(Q, c + t, r, q[t]);
+              for (int j = 0; j < 4; ++j) {
+                const float4 w4 = *reinterpret_cast<const float4*>(sq + (which * 4 + j) * kStage + u);
+                o[0][j] = w4.x;
+                o[1][j] = w4.y;
+                o[2][j] = w4.z;
+                o[3][j] = w4.w;
+              }
+              return;
+            }
+          }
+#pragma unroll
+          for (int t = 0; t < 4; ++t) load_small_row<R>(g, c + t, r, o[t]);
+        };
+        rows4(0, Q, q);
         if constexpr (COMP == 3) {
           float lq[4][R];
-#pragma unroll
-          for (int t = 0; t < 4; ++t) load_small_row<R>(lz.q + mt.q_off, c + t, r, lq[t]);
+          rows4(1, lz.q + mt.q_off, lq);
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) {
             float4& rv4 = rv[k][rr];
@@ -172,6 +225,9 @@ __global__ __launch_bounds__(kBlock) void ps_mq_kernel(const float* __restrict__
 #pragma unroll
             for (int j = 0; j < R; ++j) acc[rr][j] = fmaf(e[t], q[t][j], acc[rr][j]);
         }
+      }
+      if constexpr (R == 4) {
+        if (staged) __syncthreads();  // the next iteration rewrites the LDS image
       }
     }
   } else {
