@@ -57,6 +57,7 @@ constexpr int kCBV = 1024, kCBS = 256;    // ps_mtp / ps_pqt: columns per block 
 constexpr int kRSP = 32;                  // rows per strip: ps_pqt (ps_mtp: per-matrix, from the tile table)
 constexpr int kPB = 8;                    // rows per batch: independent 16-B loads in flight per thread
 
+
 __device__ __forceinline__ bool mat_vec(const Mat& mt) { return ((mt.x_off | mt.m) & 3) == 0; }
 
 template <int R>
@@ -271,7 +272,7 @@ __global__ __launch_bounds__(kBlock) void ps_mq_kernel(const float* __restrict__
 // loads in flight, the block's partial Q is transposed through LDS into address order, and the
 // strip's atomics go out as contiguous wave-wide runs (per-lane atomics 64 B apart measured 1.8
 // TB/s for VGG-16 fc6; a block covering only 1 KB of each row read slower than one covering 4 KB).
-template <int R>
+template <int R, int kPBm>  // kPBm: rows per batch (independent 16-B loads in flight per thread)
 __global__ __launch_bounds__(kBlock) void ps_mtp_kernel(const float* __restrict__ x, const float* __restrict__ Pall,
                                                         float* __restrict__ Qall, const int64_t* __restrict__ mats,
                                                         const int32_t* __restrict__ tiles) {
@@ -294,14 +295,14 @@ __global__ __launch_bounds__(kBlock) void ps_mtp_kernel(const float* __restrict_
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int j = 0; j < R; ++j) acc[t][j] = 0.f;
-    for (int64_t rb = r0; rb < r1; rb += kPB) {
-      float4 mv[kPB];
+    for (int64_t rb = r0; rb < r1; rb += kPBm) {
+      float4 mv[kPBm];
 #pragma unroll
-      for (int u = 0; u < kPB; ++u)
+      for (int u = 0; u < kPBm; ++u)
         mv[u] = (act && rb + u < r1) ? *reinterpret_cast<const float4*>(x + mt.x_off + (rb + u) * m + c)
                                      : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-      for (int u = 0; u < kPB; ++u) {
+      for (int u = 0; u < kPBm; ++u) {
         if (rb + u >= r1) break;
         float p[R];
         load_small_row<R>(P, rb + u, r, p);
@@ -711,8 +712,8 @@ template <int R>
 void launch_mq(const float* x, const float* small, float* out, const int64_t* mats, const int32_t* tiles, int n_tiles,
                int mode, const float* comp_r, float beta, float gamma, float* xout, Lazy lz, hipStream_t stream) {
   const Lazy none{nullptr, nullptr, 0.f};
-  if (mode == 1)
-    ps_mtp_kernel<R><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles);
+  if (mode == 1)  // (16 rows per batch measured slower: 0.855 vs 0.755 ms VGG-16 exchange)
+    ps_mtp_kernel<R, kPB><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles);
   else if (xout == nullptr)
     ps_mq_kernel<R, 0><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles, nullptr, 0.f, 0.f, nullptr, none);
   else if (comp_r == nullptr)

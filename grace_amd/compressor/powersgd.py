@@ -174,8 +174,16 @@ class PowerSGDCompressor(BucketCompressor):
             po += plan.p_total
             qo += plan.q_total
         key = tuple((name, ctx.extra["plan"].p_total, ctx.extra["plan"].q_total) for name, _, ctx in entries)
+        # every bucket's matrices over the whole P arena: ONE orthonormalisation launch per step
+        # (one per bucket cost ~10-20 us each of single-workgroup-per-matrix latency)
+        mats = []
+        for name, _, ctx in entries:
+            bpo, bqo = off[name]
+            plan = ctx.extra["plan"]
+            mats += [(xo, n, m, r, mpo + bpo, mqo + bqo) for (xo, n, m, r, mpo, mqo) in plan.mats]
+        orth = PS.Plan(self.rank_r, mats, [], po, qo, 0)
         self._arena = {"key": key, "off": off, "p": torch.empty(po, dtype=torch.float32, device=dev),
-                       "q": torch.empty(qo, dtype=torch.float32, device=dev)}
+                       "q": torch.empty(qo, dtype=torch.float32, device=dev), "orth": orth}
 
     def _exchange(self, entries, arena: bool = False):
         W = self.world_size or 1
@@ -202,8 +210,11 @@ class PowerSGDCompressor(BucketCompressor):
         if comm is not None:
             comm.all_reduce(p_all)  # SUM over ranks: the orthonormalisation is scale invariant
             self.matrix_collectives += 1
-        for _, _, ctx in entries:
-            PS.orthogonalize(ctx.extra["p"], ctx.extra["plan"], which="p")
+        if arena:
+            PS.orthogonalize(p_all, self._arena["orth"], which="p")  # all buckets, one launch
+        else:
+            for _, _, ctx in entries:
+                PS.orthogonalize(ctx.extra["p"], ctx.extra["plan"], which="p")
         for _, x_after, ctx in entries:
             PS.mtp(x_after, ctx.extra["p"], ctx.extra["plan"], out=ctx.extra["q"])  # Q = M^T P
         if comm is not None:
