@@ -280,6 +280,8 @@ class _Conv1x1AutoFn(torch.autograd.Function):
                     _wg.tag(dy, s)
                     _wg.tag(x, s)
                     _wg.tag(d, f.main)
+                elif tgt is None:
+                    d = _wg.ddp_batched(d, ctx.weight)  # DDP: one batched copy instead of the reducer's
             return d
 
         if f is not None and _wg._WG_FIRST:
@@ -630,6 +632,8 @@ class _Conv3x3Fn(torch.autograd.Function):
                     _wg.tag(dy, s)
                     _wg.tag(x, s)
                     _wg.tag(d, f.main)
+                elif tgt is None:
+                    d = _wg.ddp_batched(d, ctx.weight)  # DDP: one batched copy instead of the reducer's
             return d
 
         if f is not None and _wg._WG_FIRST:

@@ -291,7 +291,8 @@ def _split_net(seed=0):
                          nn.AdaptiveAvgPool2d(1), nn.Flatten(), nn.Linear(32, 10)).cuda()
 
 
-def test_ddp_hook_split_grad_convs_match_plain_model(nccl_group):
+@pytest.mark.parametrize("batch_copy", [False, True])
+def test_ddp_hook_split_grad_convs_match_plain_model(nccl_group, batch_copy):
     """DDP + hook over split-gradient convs (ops/wgrad.py): the reducer reads gradients mid-backward,
     so DDP-managed weights compute their gradients in line, and (gradient_as_bucket_view) straight
     into the bucket once the hook has seen it -- gradients equal a plain model's, every step."""
@@ -303,8 +304,12 @@ def test_ddp_hook_split_grad_convs_match_plain_model(nccl_group):
                                               broadcast_buffers=False)
     ddp.register_comm_hook(GraceHookState(grace_from_params({"compressor": "none", "communicator": "allreduce"}),
                                           model=ddp), grace_comm_hook)
+    from grace_amd.ops import wgrad as _wg
+
+    old_batch = _wg._DDP_BATCH
+    _wg._DDP_BATCH = batch_copy
     g = torch.Generator().manual_seed(3)
-    for step in range(4):
+    for step in range(6):  # steps >= 3: MIOpen weight gradients take the batched-copy path when on
         x = torch.randn(16, 3, 24, 24, generator=g).cuda()
         y = torch.randint(0, 10, (16,), generator=g).cuda()
         for p in list(m.parameters()) + list(ref.parameters()):
@@ -316,6 +321,7 @@ def test_ddp_hook_split_grad_convs_match_plain_model(nccl_group):
             assert a._grace_ddp
             tol = 1e-4 * float(b.grad.abs().max()) + 1e-6
             assert float((a.grad - b.grad).abs().max()) <= tol, step
+    _wg._DDP_BATCH = old_batch
     conv_w = [mod.weight for mod in m if hasattr(mod, "kernel_size")]
     for w in conv_w:  # the gradient IS the bucket view the hook marked (no reducer copy)
         assert w._grace_grad_view.data_ptr() == w.grad.data_ptr()

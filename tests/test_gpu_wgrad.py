@@ -359,3 +359,27 @@ def test_second_capture_after_eager_steps(bn_deterministic):
         loss = g2()
     torch.cuda.synchronize()
     assert torch.isfinite(loss).item()
+
+
+def test_strided_copy_batched_matches_copy():
+    """csrc/kernels/ef.hip strided_copy: channels_last / permuted / sliced fp32 sources of <= 4
+    dims into contiguous destinations, 45 tensors (two launches of 40), equal to Tensor.copy_."""
+    from grace_amd.ops import _native
+
+    g = torch.Generator(device="cuda").manual_seed(4)
+    srcs, dsts, refs = [], [], []
+    for i in range(45):
+        shape = [(64, 64, 3, 3), (256, 64, 1, 1), (7, 5, 3), (1000, 33), (17,)][i % 5]
+        t = torch.randn(*shape, device="cuda", generator=g)
+        if len(shape) == 4 and i % 2 == 0:
+            t = t.contiguous(memory_format=torch.channels_last)
+        elif len(shape) == 2:
+            t = torch.randn(shape[1], shape[0], device="cuda", generator=g).t()  # transposed view
+        elif len(shape) == 3:
+            t = torch.randn(*shape, 2, device="cuda", generator=g)[..., 1]  # strided slice
+        srcs.append(t)
+        dsts.append(torch.full(shape, -7.0, device="cuda"))
+        refs.append(t.contiguous())
+    _native.lib().strided_copy(srcs, dsts)
+    for d, r in zip(dsts, refs):
+        assert torch.equal(d, r)
