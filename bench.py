@@ -386,7 +386,7 @@ def main():
             # first 10 iterations: capture only after those
             cap_warm = max(3, args.warmup // 2) if args.surface == "engine" else max(11, args.warmup)
             run = GraphedStep(step, warmup=cap_warm, stream=ddp_stream,
-                              capture_error_mode="thread_local" if world > 1 else "global")
+                              capture_error_mode="thread_local" if world > 1 else None)
             graph_note = "full"
         elif mode == "compute":
             with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp, cache_enabled=False):

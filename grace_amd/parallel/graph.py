@@ -56,6 +56,17 @@ def graph_safe(grc, allow_static_seeds: bool = False) -> Optional[str]:
     return None
 
 
+def _nccl_group_up() -> bool:
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    try:
+        return dist.get_backend() == "nccl"
+    except Exception:  # noqa: BLE001 -- a group without a default backend: no watchdog to race
+        return False
+
+
 class GraphedStep:
     """``step = GraphedStep(fn)``; ``step()`` replays the captured ``fn``.
 
@@ -64,8 +75,10 @@ class GraphedStep:
 
     ``capture_error_mode`` is passed to ``torch.cuda.graph``.  With collectives inside the
     step (W > 1) use ``"thread_local"``: RCCL's proxy thread makes HIP calls of its own while
-    the training thread captures, and under the default ``"global"`` mode such a call from
-    ANY thread invalidates the capture.
+    the training thread captures, and under ``"global"`` mode such a call from ANY thread
+    invalidates the capture.  The default (None) picks ``"thread_local"`` whenever a
+    ``torch.distributed`` NCCL (RCCL) group is up -- its watchdog thread queries the events of
+    work in flight, which is also such a call -- and ``"global"`` otherwise.
 
     Every replay first checks the process-wide communication health words (a host-mapped read,
     no device sync): a device-side fault of an earlier replay (an xGMI peer wait that timed out;
@@ -73,11 +86,13 @@ class GraphedStep:
     """
 
     def __init__(self, fn: Callable[[], torch.Tensor], warmup: int = 3, pool=None,
-                 capture_error_mode: str = "global", copies: Optional[int] = None,
+                 capture_error_mode: Optional[str] = None, copies: Optional[int] = None,
                  stream: Optional[torch.cuda.Stream] = None):
         import os
 
         self.fn = fn
+        if capture_error_mode is None:
+            capture_error_mode = "thread_local" if _nccl_group_up() else "global"
         # ``stream``: warm up, capture and replay on this stream.  Needed when long-lived autograd
         # nodes were created under it -- DDP's reducer keeps the parameters' AccumulateGrad nodes,
         # which run on the stream current at DDP's construction; a capture on any other stream

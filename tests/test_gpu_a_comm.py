@@ -27,7 +27,11 @@ def nccl_group():
         os.environ["MASTER_PORT"] = str(_free_port())
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     yield
-    # leave the group up for the rest of the session (destroying + re-initialising RCCL is slow)
+    # no later module uses the group; tear it down so its watchdog thread (which queries the
+    # events of RCCL work in flight) cannot race a later module's global-mode graph capture
+    if dist.is_initialized():
+        torch.cuda.synchronize()
+        dist.destroy_process_group()
 
 
 def test_rccl_cta_probe_single_rank(nccl_group):
