@@ -37,9 +37,12 @@ def main(argv=None):
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--gaps", type=int, default=0, help="also list the N largest idle gaps (kernel pairs)")
     ap.add_argument("--gap-min-us", type=float, default=5.0)
+    ap.add_argument("--grid-match", default="", help="also list per-(kernel, grid) times of kernels matching this")
     args = ap.parse_args(argv)
     rows = list(csv.DictReader(open(args.trace)))
     ks = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows))
+    grids = {(int(r["Start_Timestamp"]), r["Kernel_Name"]): (r.get("Grid_Size_X", "?"), r.get("Grid_Size_Y", "?"))
+             for r in rows}
     marks = [i for i, k in enumerate(ks) if args.marker in k[2]]
     if not marks:
         sys.exit(f"marker {args.marker!r} not found")
@@ -73,6 +76,17 @@ def main(argv=None):
     print(f"window: {steps} steps, wall {wall / 1e6 / steps:.3f} ms/step, GPU busy {busy / 1e6 / steps:.3f} ms/step "
           f"({100 * busy / max(1, wall):.1f}%), kernels {len(win) / steps:.0f}/step, sum of kernel time "
           f"{total / 1e6 / steps:.3f} ms/step")
+    if args.grid_match:
+        by = collections.defaultdict(list)
+        for s_, e, n in win:
+            if args.grid_match in n:
+                t = re.sub(r"\(.*", "", n.replace("(anonymous namespace)::", "").replace("void ", ""))[:58]
+                by[(t, grids.get((s_, n), ("?", "?")))].append((e - s_) / 1e3)
+        print(f"per (kernel, grid), kernels matching {args.grid_match!r}:")
+        print(f"{'us/step':>8} {'n/step':>6} {'mean_us':>8}  grid  kernel")
+        for (t, g), v in sorted(by.items(), key=lambda kv: -sum(kv[1])):
+            print(f"{sum(v) / steps:8.1f} {len(v) / steps:6.1f} {sum(v) / len(v):8.2f}  {g[0]}x{g[1]}  {t}")
+        print()
     grace = sum(v[0] for k, v in agg.items() if k.startswith("grace::") or "grace" in k)
     print(f"grace_amd kernels: {grace / 1e6 / steps:.3f} ms/step ({100 * grace / max(1, total):.1f}% of kernel time)")
     print(f"{'ms/step':>8} {'calls/step':>10}  kernel")
