@@ -254,3 +254,19 @@ def test_native_library_loads_on_cpu_host():
         pytest.skip("extension not built")
     assert _native.available(), _native._err
     assert "gfx950" in _native.lib().build_info()
+
+
+def _capture_mode_rank(rank, world):
+    from grace_amd.parallel.graph import _nccl_group_up
+
+    assert dist.is_initialized() and dist.get_backend() == "gloo"
+    assert not _nccl_group_up()  # gloo has no watchdog querying HIP events: global capture is fine
+
+
+def test_graphed_step_capture_mode_follows_the_process_group():
+    """GraphedStep(capture_error_mode=None) captures thread-locally only under an RCCL ("nccl")
+    group, whose watchdog thread queries HIP events while the training thread captures."""
+    from grace_amd.parallel.graph import _nccl_group_up
+
+    assert not dist.is_initialized() and not _nccl_group_up()
+    run_distributed(_capture_mode_rank, 1)
