@@ -8,8 +8,15 @@ ResidualMemory + Allgather, SGD(lr = 0.01 * W, momentum 0.5) -- the reference ha
 random-init weights (no datasets / checkpoints offline).
 
     python bench.py --gpus 1 --steps 20 --warmup 10
+    python bench.py --gpus 8 --steps 20 --warmup 10          # launches its own 8 ranks
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
         --master-port 29500 bench.py --gpus 8 --steps 20 --warmup 10
+
+``--gpus N > 1`` without torchrun's ``WORLD_SIZE``: the script re-launches itself as N ranks
+through grace_amd/launcher.py (the ``horovodrun -np N`` role, /root/reference/TRAINING.md:69-73):
+fresh child processes started BEFORE this process imports torch (the parent never touches the
+GPU), env:// rendezvous on 127.0.0.1 and a free port, rank 0's JSON line relayed once, any
+failing rank ends the whole launch non-zero.
 
 Weak scaling: the per-GPU batch is fixed, ``value`` is the WHOLE-JOB throughput (all ranks);
 the timed region is bracketed by a barrier + device synchronize on both sides and the
@@ -24,12 +31,35 @@ import os
 import sys
 import time
 
-import torch
-import torch.distributed as dist
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+
+
+def _maybe_self_launch() -> None:
+    """``--gpus N > 1`` outside torchrun: run N ranks of this script and exit with their verdict.
+    Runs before ``import torch``; the launcher module is loaded by path so that the grace_amd
+    package (which imports torch) is not imported in the parent either."""
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("--gpus", type=int, default=1)
+    pre.add_argument("--launch-timeout", type=float, default=3000.0)
+    a, _ = pre.parse_known_args()
+    if a.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("_grace_launcher", os.path.join(ROOT, "grace_amd", "launcher.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    cmd = [sys.executable, "-u", os.path.abspath(__file__), *sys.argv[1:]]
+    sys.exit(mod.launch(cmd, a.gpus, timeout_s=a.launch_timeout))
+
+
+if __name__ == "__main__":
+    _maybe_self_launch()
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 HEADLINE_METRIC = "images/sec (whole node) ResNet-50 Top-K 1% @ 1/2/4/8 MI355X; comm wall-time"
 
@@ -41,7 +71,10 @@ REFERENCE_VALUE = {"resnet9_dawn": 24 * 50000 / 74.0}
 
 def parse():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); N > 1 without torchrun's WORLD_SIZE self-launches N ranks")
+    ap.add_argument("--launch-timeout", type=float, default=3000.0,
+                    help="self-launch only: kill every rank after this many seconds (exit 124)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="resnet50_topk")
@@ -82,9 +115,10 @@ def parse():
                          "several ranks share one GPU (multi-rank rehearsal on a 1-GPU box; --comm torch, no "
                          "whole-step graph: gloo collectives are not capturable)")
     ap.add_argument("--grace-split", choices=["on", "off"], default="on",
-                    help="after the timed region, time the SAME whole-step graph with the GRACE exchange replaced "
-                         "by a no-op (None compressor, local comm: a copy) and report the difference as "
-                         "grace_ms_per_step (compress + collective + decode as the measured step pays it)")
+                    help="after the timed region, replay the measured whole-step graph interleaved with the same "
+                         "step whose GRACE exchange is a no-op (None compressor, local comm: a copy) and report "
+                         "the mean paired difference +- 95 %% CI as grace_ms_per_step (compress + collective + "
+                         "decode as the measured step pays it)")
     ap.add_argument("--surface", choices=["engine", "ddp"], default="engine",
                     help="engine: grace_amd DistributedOptimizer (bucketed GRACE engine, the default); ddp: "
                          "torch DistributedDataParallel + grace_comm_hook (the DDP comm-hook surface; DDP owns "
@@ -101,16 +135,24 @@ def parse():
                          "auto = at W > 1 for a dense all-reduce pipeline (None / FP16 + Allreduce) probe "
                          "RcclComm.CTA_CANDIDATES on the real bucket size and keep the fastest (MAX over ranks); "
                          "off = RCCL's default; 'MIN/MAX' = fixed")
+    ap.add_argument("--deterministic", action="store_true",
+                    help="bitwise-reproducible BN backward (fixed-order fp64 tree instead of atomic fp32 "
+                         "totals; GRACE_BN_DETERMINISTIC=1)")
     ap.add_argument("--xgmi-capacity-mb", type=float, default=8.0,
                     help="per-rank payload capacity of the xGMI one-shot comm (two slots of this size are exported "
                          "per rank); collectives above it go to RCCL / the inner comm")
     return ap.parse_args()
 
 
-def _noop_graph_ms(args, opt, base_opt, named, weights, w, model, data, amp, set_to_none, world, dev, barrier):
-    """ms/step of the same whole-step graph with the GRACE exchange replaced by a no-op (None +
-    local comm = one copy per bucket), timed like the measured steps: the difference is compress +
-    collective (+ wait) + decode as the graphed step pays it."""
+def _grace_split(args, run, opt, base_opt, named, weights, w, model, data, amp, set_to_none, world, dev):
+    """GRACE's cost inside the measured whole-step graph, MEASURED by interleaving: the same step
+    is captured a second time with the GRACE exchange replaced by a no-op (None compressor + a
+    local comm = one copy per bucket), and the two graphs are replayed ALTERNATELY, each replay
+    bracketed by device events on the stream.  Every pair (measured_i, no-op_i) runs under the
+    same clocks / thermals, so the paired difference d_i = measured_i - no-op_i is the exchange's
+    cost (compress + collective + decode as the graphed step pays it) without the box-drift noise
+    of two separately timed runs.  Returns (mean d, 95 % CI half-width,
+    mean no-op ms, pairs); MAX over ranks for W > 1."""
     from grace_amd import grace_from_params
     from grace_amd.parallel import DistributedOptimizer
     from grace_amd.parallel.comm import LocalComm
@@ -132,20 +174,55 @@ def _noop_graph_ms(args, opt, base_opt, named, weights, w, model, data, amp, set
 
     run2 = GraphedStep(noop_step, warmup=3)
     for _ in range(3):
-        run2()
+        run(), run2()
     torch.cuda.synchronize()
-    barrier()
-    t2 = time.perf_counter()
-    for _ in range(args.steps):
+    pairs = max(10, 2 * args.steps)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * pairs + 1)]
+    ev[0].record()
+    for i in range(pairs):
+        run()
+        ev[2 * i + 1].record()
         run2()
+        ev[2 * i + 2].record()
     torch.cuda.synchronize()
-    e2 = torch.tensor([time.perf_counter() - t2], dtype=torch.float64, device=dev)
+    a = [ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(pairs)]
+    b = [ev[2 * i + 1].elapsed_time(ev[2 * i + 2]) for i in range(pairs)]
+    d = [x - y for x, y in zip(a, b)]
+    mean = sum(d) / pairs
+    sd = (sum((v - mean) ** 2 for v in d) / max(1, pairs - 1)) ** 0.5
+    ci = 1.96 * sd / pairs ** 0.5
+    t = torch.tensor([mean, ci, sum(b) / pairs], dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(e2, op=dist.ReduceOp.MAX)
-    return float(e2.item()) / args.steps * 1e3
+        if args.backend == "gloo":
+            t = t.cpu()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    mean, ci, noop_ms = (float(v) for v in t.tolist())
+    return mean, ci, noop_ms, pairs
 
 
-def main():
+def _dense_bucket_payload(w, model, bucket_mb: float) -> int:
+    """Bytes one dense bucket puts on the wire: the engine fills fp32 buckets of ``bucket_mb``
+    (the last one partial), the FP16 compressor then halves each bucket's payload (ADVICE r5:
+    probe and bucket count in the same units)."""
+    esz = 2 if w.grace.get("compressor") == "fp16" else 4
+    fp32_bucket = min(sum(p.numel() for p in model.parameters()) * 4, int(bucket_mb * 2 ** 20))
+    return fp32_bucket * esz // 4
+
+
+def _rccl_nranks(rccl_obj, world_seen: int, gloo: bool):
+    """What the communicators report: the native RCCL runtime's own ncclCommCount (and the device
+    RCCL bound) when GRACE traffic runs on it, the torch process group's size otherwise."""
+    out = {"process_group": world_seen if not gloo else None}
+    if rccl_obj is not None:
+        try:
+            out["native_rccl"] = rccl_obj.nranks
+            out["native_rccl_device"] = rccl_obj.comm_device
+        except Exception as e:  # noqa: BLE001 -- reporting only
+            out["native_rccl"] = f"unavailable: {type(e).__name__}"
+    return out
+
+
+def main() -> int:
     args = parse()
     from grace_amd import grace_from_params
     from grace_amd.parallel import DistributedOptimizer, broadcast_parameters
@@ -155,12 +232,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: a torchrun launch must pass --gpus WORLD_SIZE")
+    if args.deterministic:
+        os.environ["GRACE_BN_DETERMINISTIC"] = "1"  # read when the BN ops are first used
+    ndev = torch.cuda.device_count()  # counting devices does not initialise the GPU
+    gloo = args.backend == "gloo"
+    if not gloo and local >= ndev:
+        raise SystemExit(f"rank {rank}: LOCAL_RANK {local} but only {ndev} visible GPU(s); RCCL needs one GPU per "
+                         f"rank (--backend gloo lets ranks share a GPU for a rehearsal)")
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU")
-    gloo = args.backend == "gloo"
     if gloo:  # ranks may share GPUs
-        local = local % torch.cuda.device_count()
+        local = local % ndev
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if args.surface == "ddp":
@@ -238,8 +321,7 @@ def main():
             and mode == "full" and args.comm in ("auto", "native", "native-inline", "xgmi")):
         from grace_amd.parallel.native_comm import RcclComm
 
-        esz = 2 if w.grace.get("compressor") == "fp16" else 4
-        nbytes = min(sum(p.numel() for p in model.parameters()) * esz, int(args.bucket_mb * 2 ** 20))
+        nbytes = _dense_bucket_payload(w, model, args.bucket_mb)
         try:
             rccl_pre = RcclComm.tuned(nbytes)  # collective: every rank builds / probes the candidates
         except Exception as e:  # noqa: BLE001 -- e.g. no ncclConfig support: keep the default comm
@@ -261,6 +343,7 @@ def main():
     comm_kind = "local"
     comm_obj = None
     rccl_obj = None
+    xgmi_note = None
     if dist.is_initialized():
         comm_kind = args.comm
         if comm_kind == "auto":
@@ -289,9 +372,7 @@ def main():
                     elif args.rccl_ctas == "auto" and world > 1 and dense_ar:
                         # the dense all-reduce's channel budget for the 7-link mesh, measured on the
                         # real bucket: one ring drives one outbound link per GPU
-                        esz = 2 if w.grace.get("compressor") == "fp16" else 4
-                        nbytes = min(sum(p.numel() for p in model.parameters()) * esz, int(args.bucket_mb * 2 ** 20))
-                        native = RcclComm.tuned(nbytes, inline=inl)
+                        native = RcclComm.tuned(_dense_bucket_payload(w, model, args.bucket_mb), inline=inl)
                     else:
                         ctas = (0, 0) if args.rccl_ctas in ("auto", "off") else \
                             tuple(int(v) for v in args.rccl_ctas.split("/"))
@@ -301,14 +382,20 @@ def main():
                     from grace_amd.parallel.xgmi import XgmiComm
 
                     try:
+                        # construction verifies the one-shot gather (staged and from the exported
+                        # slot) and all-to-all bit-exactly against the inner comm on every rank
                         native = XgmiComm(native, capacity_mb=args.xgmi_capacity_mb,
                                           select="probe" if comm_kind == "auto-probe" else "size")
+                        xgmi_note = {"verified_vs_inner": True, "inner": type(native.inner).__name__,
+                                     "direct_slot": bool(native._direct_ok)}
                     except Exception as e:  # every rank raised together (XgmiComm agrees)
                         if comm_kind == "xgmi" or gloo:
                             raise
                         print(f"[rank {rank}] xGMI one-shot comm unavailable ({str(e)[:120]}); RCCL only",
                               file=sys.stderr, flush=True)
                         comm_kind = "native-inline (xgmi setup failed)"
+                        xgmi_note = {"verified_vs_inner": False, "fallback": "RCCL on every rank",
+                                     "error": str(e)[:200]}
                 comm_obj = native
                 ok = 1
             except Exception as e:  # every rank must agree before the first GRACE collective
@@ -459,10 +546,16 @@ def main():
     if not loss_finite:  # a diverged run's throughput is not a measurement of training
         print(f"[rank {rank}] ERROR: final loss is {final_loss}: the timed steps trained a diverged model; "
               f"the throughput below is NOT a valid {w.name} number", file=sys.stderr, flush=True)
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    # every rank's own timed-region wall time (the spread shows a straggler); the MAX is the job's
+    per_rank_s = [elapsed]
     if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
+        el_dev = torch.device("cpu") if gloo else dev
+        mine = torch.tensor([elapsed], dtype=torch.float64, device=el_dev)
+        allr = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        per_rank_s = [float(t.item()) for t in allr]
+    elapsed = max(per_rank_s)
+    world_seen = dist.get_world_size() if dist.is_initialized() else 1
 
     # untimed: the reference harness's "comm wall-time" split (pytorch_synthetic_benchmark.py:
     # 166-167) -- eager steps with the GraceProfiler attached: compress (compensate + compress +
@@ -498,17 +591,17 @@ def main():
     if world > 1:
         dist.all_reduce(ex, op=dist.ReduceOp.MAX)
 
-    # GRACE's cost inside the measured path: the same whole-step graph with the exchange replaced by
-    # a no-op (None + local comm = one copy per bucket), timed the same way; the difference is
-    # compress + collective (+ wait) + decode as the graphed step pays it
-    grace_ms = noop_ms = None
+    # GRACE's cost inside the measured path: paired, interleaved replays of the measured graph and
+    # the same step with a no-op exchange (_grace_split); diagnostics only, after the timed region
+    grace_ms = grace_ci = grace_raw = noop_ms = grace_pairs = None
     grace_split_note = None
     if args.grace_split == "on" and graph_note == "full" and args.surface == "engine":
-        # diagnostics only (after the timed region): a failure here must not cost the measured line
-        try:
-            noop_ms = _noop_graph_ms(args, opt, base_opt, named, weights, w, model, data, amp, set_to_none,
-                                     world, dev, barrier)
-            grace_ms = elapsed / args.steps * 1e3 - noop_ms
+        try:  # a failure here must not cost the measured line
+            grace_raw, grace_ci, noop_ms, grace_pairs = _grace_split(
+                args, run, opt, base_opt, named, weights, w, model, data, amp, set_to_none, world, dev)
+            # a cost is not negative: a pipeline whose exchange IS the no-op (None at W = 1) reads
+            # 0 within its CI; grace_ms_raw keeps the signed mean
+            grace_ms = max(0.0, grace_raw)
         except Exception as e:  # noqa: BLE001
             grace_split_note = f"no-op graph failed: {type(e).__name__}: {str(e)[:100]}"
             print(f"[rank {rank}] grace split skipped ({grace_split_note})", file=sys.stderr, flush=True)
@@ -518,7 +611,7 @@ def main():
                 pass
 
     samples = w.samples_per_batch(batch) * world * args.steps
-    value = samples / elapsed
+    value = samples / elapsed if loss_finite else None  # a diverged run reports no throughput
     per_gpu = [w.samples_per_batch(batch) / (ms * 1e-3) for ms in step_ms if ms > 0]
     mean_pg = sum(per_gpu) / max(1, len(per_gpu))
     std_pg = (sum((v - mean_pg) ** 2 for v in per_gpu) / max(1, len(per_gpu))) ** 0.5
@@ -526,7 +619,7 @@ def main():
         metric = HEADLINE_METRIC if w.name == "resnet50_topk" else f"{w.unit}/sec (whole node) {w.name}"
         out = {
             "metric": metric,
-            "value": round(value, 2),
+            "value": None if value is None else round(value, 2),
             "unit": f"{w.unit}/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -534,7 +627,8 @@ def main():
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(value / REFERENCE_VALUE[w.name], 3) if w.name in REFERENCE_VALUE else None,
+            "vs_baseline": round(value / REFERENCE_VALUE[w.name], 3)
+            if (w.name in REFERENCE_VALUE and value is not None) else None,
             "dtype": args.dtype,
             "data": "synthetic (random-init weights)",
             "config": {
@@ -564,6 +658,12 @@ def main():
                                    {"note": "W=1 without a process group: 'comm' is a local device copy, "
                                             "not a collective"})),
             "comm_choice": (list(getattr(comm_obj, "choices", {}).values()) or None) if comm_obj is not None else None,
+            "world_seen": world_seen,
+            "rccl_nranks": _rccl_nranks(rccl_obj, world_seen, gloo),
+            "per_rank_ms_per_step": {"min": round(min(per_rank_s) / args.steps * 1e3, 3),
+                                     "max": round(max(per_rank_s) / args.steps * 1e3, 3),
+                                     "ranks": len(per_rank_s)},
+            "xgmi": xgmi_note,
             "rccl_ctas": (getattr(rccl_obj, "choice", None) or {"ctas": list(getattr(rccl_obj, "ctas", (0, 0)))})
             if rccl_obj is not None else None,
             "bn_backward": ("fixed-order fp64 tree (deterministic)" if os.environ.get("GRACE_BN_DETERMINISTIC") == "1"
@@ -571,6 +671,11 @@ def main():
                                  "for bitwise reproducibility)"),
             "bytes_on_wire_per_rank": int(split.get("bytes_per_step", 0)),
             "grace_ms_per_step": None if grace_ms is None else round(grace_ms, 3),
+            "grace_ms_ci95": None if grace_ci is None else round(grace_ci, 3),
+            "grace_ms_raw": None if grace_raw is None else round(grace_raw, 4),
+            "grace_split": None if grace_pairs is None else
+            f"mean of {grace_pairs} paired differences (measured graph replay - no-op-exchange graph replay, "
+            f"interleaved, device events), +- 95 % CI; MAX over ranks",
             **({"grace_split_note": grace_split_note} if grace_split_note else {}),
             "noop_exchange_ms_per_step": None if noop_ms is None else round(noop_ms, 3),
             "exposed_exchange_ms_eager": round(float(ex.item()) * 1e3, 3),
@@ -590,7 +695,8 @@ def main():
                 print("conv_bn", row[:-1], {k: round(v, 4) for k, v in row[-1].items()}, file=sys.stderr)
     if dist.is_initialized():
         dist.destroy_process_group()
+    return 0 if loss_finite else 3  # a diverged run fails the launch (no throughput recorded)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

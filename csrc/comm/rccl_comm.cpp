@@ -166,6 +166,18 @@ class RcclComm {
   int min_ctas() const { return min_ctas_; }
   int max_ctas() const { return max_ctas_; }
   int world_size() const { return world_; }
+  // what RCCL itself reports for the communicator (ncclCommCount / ncclCommCuDevice): the bench
+  // JSON carries it so a driver can check "RCCL saw N ranks" independently of the env
+  int nranks() const {
+    int n = 0;
+    RCCL_CHECK(ncclCommCount(comm_, &n));
+    return n;
+  }
+  int comm_device() const {
+    int d = -1;
+    RCCL_CHECK(ncclCommCuDevice(comm_, &d));
+    return d;
+  }
   uintptr_t stream_ptr() const { return reinterpret_cast<uintptr_t>(stream_); }
 
   std::shared_ptr<Work> all_gather(const Tensor& out, const Tensor& in) {
@@ -369,6 +381,8 @@ void bind(py::module& m) {
       .def_property_readonly("max_ctas", &RcclComm::max_ctas)
       .def_property_readonly("rank", &RcclComm::rank)
       .def_property_readonly("world_size", &RcclComm::world_size)
+      .def_property_readonly("nranks", &RcclComm::nranks)
+      .def_property_readonly("comm_device", &RcclComm::comm_device)
       .def_property_readonly("stream_ptr", &RcclComm::stream_ptr)
       .def("all_gather", &RcclComm::all_gather)
       .def("all_reduce", &RcclComm::all_reduce, py::arg("t"), py::arg("op") = "sum")

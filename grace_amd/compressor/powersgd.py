@@ -108,8 +108,19 @@ class PowerSGDCompressor(BucketCompressor):
             memory.residuals[name] = rs
         r = rs.view(-1)
         # deferred residual of the previous step (r holds its M): formed inside this P = M Q pass
-        lz = memory.lazy.pop(name, None)
-        lazy = (lz[0], lz[1], lz[2]) if (lz is not None and valid and lz[3] is plan) else None
+        lz = memory.lazy.get(name)
+        lazy = None
+        if lz is not None and valid and lz[3] is plan:
+            lazy = (lz[0], lz[1], lz[2])
+            del memory.lazy[name]
+        elif lz is not None:
+            # cannot be fused into this pass (re-planned layout, same numel): apply it now, so r
+            # is the true residual M - s P Q^T and not the previous M; a residual
+            # that is being reset (not valid) drops it with the buffer
+            if valid:
+                memory.materialize(name)
+            else:
+                del memory.lazy[name]
         # x (matrix segments) lands in r; 1-D segments of x equal g (their residual is zero)
         vec = self._power(g, r, name, ctx, plan, comp_r=r if valid else None, xout=r, defer=self.step_level,
                           lazy=lazy)

@@ -56,15 +56,36 @@ def graph_safe(grc, allow_static_seeds: bool = False) -> Optional[str]:
     return None
 
 
+def _is_rccl_backend(name) -> bool:
+    """True for any backend string that includes RCCL: "nccl", and the per-device forms such as
+    "cpu:gloo,cuda:nccl" (what ``init_process_group()`` without a backend reports on a GPU box)."""
+    return "nccl" in str(name).lower()
+
+
 def _nccl_group_up() -> bool:
+    """Whether any RCCL communicator -- whose threads (the ProcessGroupNCCL watchdog, RCCL's proxy)
+    make HIP calls while the training thread captures -- is up in this process: the default
+    group, ANY subgroup (a step may run on an NCCL subgroup over a gloo default group), or a live
+    native RcclComm (csrc/comm/rccl_comm.cpp)."""
     import torch.distributed as dist
 
+    from . import native_comm
+
+    if native_comm.live_count() > 0:
+        return True
     if not (dist.is_available() and dist.is_initialized()):
         return False
     try:
-        return dist.get_backend() == "nccl"
-    except Exception:  # noqa: BLE001 -- a group without a default backend: no watchdog to race
-        return False
+        groups = list(dist.distributed_c10d._world.pg_map.keys())
+    except Exception:  # noqa: BLE001 -- private registry moved: the default group alone
+        groups = []
+    for g in [None] + groups:
+        try:
+            if _is_rccl_backend(dist.get_backend(g)):
+                return True
+        except Exception:  # noqa: BLE001 -- a group without a backend: no watchdog to race
+            continue
+    return False
 
 
 class GraphedStep:

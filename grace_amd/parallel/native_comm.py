@@ -21,6 +21,7 @@ all-reduce of the REAL bucket size on each, takes the MAX over ranks and keeps t
 from __future__ import annotations
 
 import itertools
+import weakref
 
 import torch
 import torch.distributed as dist
@@ -30,6 +31,12 @@ from ..ops import _native
 
 _UID_COUNTER = itertools.count()
 _EXIT_HOOKED = False
+_LIVE = weakref.WeakSet()  # open RcclComm instances (graph.py picks thread-local capture while any is)
+
+
+def live_count() -> int:
+    """Open native RCCL communicators in this process."""
+    return sum(1 for c in list(_LIVE) if c._c is not None)
 
 
 def _hook_exit():
@@ -67,6 +74,7 @@ class RcclComm(_comm.Comm):
         self.inline = bool(inline)
         self.rank, self.world_size, self.device = rank, world, device
         self._stream = torch.cuda.ExternalStream(self._c.stream_ptr, device=torch.device("cuda", device))
+        _LIVE.add(self)
 
     @classmethod
     def tuned(cls, nbytes: int, group=None, candidates=None, iters: int = 10, inline: bool = False,
@@ -182,6 +190,16 @@ class RcclComm(_comm.Comm):
         if agree:
             _agree(ok, None)
         return bool(ok)
+
+    @property
+    def nranks(self) -> int:
+        """Ranks in the communicator as RCCL reports them (ncclCommCount)."""
+        return int(self._c.nranks)
+
+    @property
+    def comm_device(self) -> int:
+        """The device RCCL bound this rank's communicator to (ncclCommCuDevice)."""
+        return int(self._c.comm_device)
 
     def set_inline(self, on: bool) -> None:
         """Issue on the caller's current stream (True) or the comm stream (False) from now on."""

@@ -270,3 +270,48 @@ def test_graphed_step_capture_mode_follows_the_process_group():
 
     assert not dist.is_initialized() and not _nccl_group_up()
     run_distributed(_capture_mode_rank, 1)
+
+
+def test_rccl_backend_string_forms():
+    """Backend strings that include RCCL in any form select the thread-local capture."""
+    from grace_amd.parallel.graph import _is_rccl_backend
+
+    assert _is_rccl_backend("nccl") and _is_rccl_backend("cpu:gloo,cuda:nccl")
+    assert _is_rccl_backend("cuda:nccl") and not _is_rccl_backend("gloo") and not _is_rccl_backend(None)
+
+
+def _capture_mode_mixed_rank(rank, world):
+    import torch.distributed.distributed_c10d as c10d
+
+    from grace_amd.parallel import graph as G
+    from grace_amd.parallel import native_comm
+
+    real = dist.get_backend
+    assert not G._nccl_group_up()
+    # 1. the default group created without a backend on a GPU box reports a mixed string
+    dist.get_backend = lambda g=None: "cpu:gloo,cuda:nccl" if g is None else real(g)
+    c10d.get_backend = dist.get_backend
+    try:
+        assert G._nccl_group_up()
+    finally:
+        dist.get_backend = c10d.get_backend = real
+    # 2. an NCCL SUBGROUP over a gloo default group (the step's own group is what matters)
+    sub = dist.new_group(ranks=list(range(world)), backend="gloo")
+    dist.get_backend = lambda g=None: "nccl" if g is sub else real(g)
+    c10d.get_backend = dist.get_backend
+    try:
+        assert G._nccl_group_up()
+    finally:
+        dist.get_backend = c10d.get_backend = real
+    assert not G._nccl_group_up()
+    # 3. a live native RCCL communicator (its proxy thread makes HIP calls) also counts
+    orig = native_comm.live_count
+    native_comm.live_count = lambda: 1
+    try:
+        assert G._nccl_group_up()
+    finally:
+        native_comm.live_count = orig
+
+
+def test_capture_mode_sees_mixed_backends_and_subgroups():
+    run_distributed(_capture_mode_mixed_rank, 2)
