@@ -135,6 +135,11 @@ def parse():
                          "auto = at W > 1 for a dense all-reduce pipeline (None / FP16 + Allreduce) probe "
                          "RcclComm.CTA_CANDIDATES on the real bucket size and keep the fastest (MAX over ranks); "
                          "off = RCCL's default; 'MIN/MAX' = fixed")
+    ap.add_argument("--graph-split", choices=["auto", "on", "off"], default="auto",
+                    help="whole-step graph as two LINEAR graphs (critical stream / weight-gradient side stream, "
+                         "external event nodes between them) plus the post-join graph, instead of one forked "
+                         "graph (parallel/graph.py GraphedStep split); engine surface without overlap only; "
+                         "auto = GRACE_GRAPH_SPLIT")
     ap.add_argument("--deterministic", action="store_true",
                     help="bitwise-reproducible BN backward (fixed-order fp64 tree instead of atomic fp32 "
                          "totals; GRACE_BN_DETERMINISTIC=1)")
@@ -172,7 +177,7 @@ def _grace_split(args, run, opt, base_opt, named, weights, w, model, data, amp, 
         noop.step()
         return l3
 
-    run2 = GraphedStep(noop_step, warmup=3)
+    run2 = GraphedStep(noop_step, warmup=3, split=getattr(run, "split", False))
     for _ in range(3):
         run(), run2()
     torch.cuda.synchronize()
@@ -472,9 +477,12 @@ def main() -> int:
             # DDP records runtime-logging events (and reads them back with a host sync) in its
             # first 10 iterations: capture only after those
             cap_warm = max(3, args.warmup // 2) if args.surface == "engine" else max(11, args.warmup)
+            split = None if args.graph_split == "auto" else args.graph_split == "on"
+            if args.surface != "engine" or overlap:
+                split = False
             run = GraphedStep(step, warmup=cap_warm, stream=ddp_stream,
-                              capture_error_mode="thread_local" if world > 1 else None)
-            graph_note = "full"
+                              capture_error_mode="thread_local" if world > 1 else None, split=split)
+            graph_note = "full (split: A / side B / A2)" if run.split else "full"
         elif mode == "compute":
             with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp, cache_enabled=False):
                 fwd_model = graph_compute(model, data[0], engine=opt.engine)
@@ -539,6 +547,9 @@ def main() -> int:
     if callable(_chk):
         _chk()
     step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
+    if os.environ.get("GRACE_SPLIT_TRACE", "0") == "1" and getattr(run, "split", False):
+        for row in run._sc.timeline():  # (fork, A signalled us, B's wait returned us, lag us)
+            print("[split-trace] fork %3d  A %9.1f  B %9.1f  lag %8.1f" % row, file=sys.stderr)
     if rec is not None:
         print("[bench] losses " + " ".join(f"{v:.4f}" for v in rec.tolist()), file=sys.stderr, flush=True)
     final_loss = float(loss.float().item())
@@ -595,7 +606,7 @@ def main() -> int:
     # the same step with a no-op exchange (_grace_split); diagnostics only, after the timed region
     grace_ms = grace_ci = grace_raw = noop_ms = grace_pairs = None
     grace_split_note = None
-    if args.grace_split == "on" and graph_note == "full" and args.surface == "engine":
+    if args.grace_split == "on" and graph_note.startswith("full") and args.surface == "engine":
         try:  # a failure here must not cost the measured line
             grace_raw, grace_ci, noop_ms, grace_pairs = _grace_split(
                 args, run, opt, base_opt, named, weights, w, model, data, amp, set_to_none, world, dev)

@@ -1045,6 +1045,7 @@ void grace_bind_comm(py::module& m);  // csrc/comm/rccl_comm.cpp
 void grace_bind_nn(py::module& m);    // csrc/nn_bindings.cpp
 void grace_bind_xgmi(py::module& m);  // csrc/comm/xgmi_allgather.hip
 void grace_bind_health(py::module& m);  // csrc/comm/health.cpp
+void grace_bind_runtime(py::module& m);  // csrc/runtime/graph_split.cpp
 
 // ------------------------------------------------------------------------------ Adaq
 void adaq_sample(const Tensor& x, const Tensor& seg_off, const Tensor& samp_off, int64_t seed,
@@ -1187,6 +1188,7 @@ void inceptionn_decode(const Tensor& base, int64_t rank_stride, int64_t stream_o
 }
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  grace_bind_runtime(m);
   grace_bind_comm(m);
   grace_bind_nn(m);
   grace_bind_xgmi(m);

@@ -58,6 +58,22 @@ def enabled() -> bool:
     return _ENABLED
 
 
+def side_cu_mask(spec: str, n_cu: int):
+    """CU-mask words for GRACE_SIDE_CUS: "k/m" keeps k of every m consecutive CUs (spread over
+    every XCD / shader engine), e.g. "3/4" = 192 of 256 CUs; "" or "all" = no mask."""
+    spec = (spec or "").strip()
+    if spec in ("", "all"):
+        return []
+    k, m = (int(v) for v in spec.split("/"))
+    if not (0 < k <= m):
+        raise ValueError(f"GRACE_SIDE_CUS={spec!r}: need 0 < k <= m")
+    words = [0] * ((n_cu + 31) // 32)
+    for cu in range(n_cu):
+        if cu % m < k:
+            words[cu // 32] |= 1 << (cu % 32)
+    return words
+
+
 def _side(device: torch.device) -> "torch.cuda.Stream":
     idx = device.index if device.index is not None else torch.cuda.current_device()
     s = _streams.get(idx)
@@ -65,14 +81,135 @@ def _side(device: torch.device) -> "torch.cuda.Stream":
         with _lock:
             s = _streams.get(idx)
             if s is None:
-                with torch.cuda.device(idx):
-                    s = torch.cuda.Stream()  # a high-priority side stream measured 20 ms/step (r3_graph_fork_knobs)
+                mask = side_cu_mask(os.environ.get("GRACE_SIDE_CUS", ""),
+                                    torch.cuda.get_device_properties(idx).multi_processor_count)
+                if mask:  # the side GEMMs may not take the CUs the critical chain needs
+                    from . import _native
+
+                    ptr = _native.lib().create_stream(idx, 0, mask)
+                    s = torch.cuda.ExternalStream(ptr, device=torch.device("cuda", idx))
+                else:
+                    with torch.cuda.device(idx):
+                        s = torch.cuda.Stream()  # a high-priority side stream measured 20 ms/step (r3_graph_fork_knobs)
                 _streams[idx] = s
     return s
 
 
 def _final_join():
+    if _split:  # a split capture joins at its split point (the engine's launch), not here
+        return
     join()
+
+
+# ---------------------------------------------------------------- split-stream capture
+# GraphedStep(split=True) (parallel/graph.py) captures a step as TWO linear graphs instead of one
+# forked graph: the critical stream's work (A) and this module's side stream (B), joined by
+# external event nodes (csrc/runtime/graph_split.cpp ExtEvent).  While such a capture is active
+# on a device, ``fork`` records an ExtEvent on the critical stream and the side stream waits on it
+# (one event per fork point: the graphs keep referring to them), the end-of-backward join is
+# skipped, and the FIRST ``join`` on the critical stream -- the GRACE engine's bucket launch,
+# deferred to ``synchronize`` while a split capture runs -- ends both captures and starts the
+# critical stream's second graph (A2: the exchange + optimizer).  Replay runs A on the critical
+# stream, B on the side stream, joins them eagerly and replays A2.  Each graph is a single
+# chain, which the HIP runtime launches as one packet batch; a forked graph is launched node by
+# node.
+class SplitCapture:
+    """State of one split capture on one device.  ``sync`` picks how graph B waits for graph A at
+    a fork point: "flags" (default) = one-thread kernels -- A publishes its generation into a flag
+    word, B spins on it (bounded) -- so both graphs are pure kernel chains; "events" = external
+    event record / wait nodes (measured: every event-record node on the critical stream costs a
+    ~60 us gap, profiles/r6_graph_split.txt)."""
+
+    MAX_FORKS = 1024
+
+    def __init__(self, device_idx: int, main: "torch.cuda.Stream", side: "torch.cuda.Stream", on_split,
+                 sync: str = "flags", spin_limit: int = 1 << 24):
+        from . import _native
+
+        if sync not in ("flags", "events"):
+            raise ValueError(f"sync must be 'flags' or 'events', not {sync!r}")
+        self.idx = device_idx
+        self.main = main
+        self.side = side
+        self.on_split = on_split   # ends the A / B captures, begins A2 on ``main``
+        self.sync = sync
+        self.spin_limit = int(spin_limit)
+        self.events = []           # fork-point tokens (ExtEvents stay alive as long as the graphs)
+        self.split_done = False
+        self._lib = _native.lib()
+        dev = torch.device("cuda", device_idx)
+        self.flags = torch.zeros(self.MAX_FORKS, dtype=torch.int64, device=dev)
+        self.gen = torch.zeros(2, dtype=torch.int64, device=dev)  # [A's generation, B's generation]
+        # GRACE_SPLIT_TRACE=1: per fork point, the device clock when A signalled it and when B's
+        # wait returned (``timeline()``): the two graphs' overlap without a profiler
+        self.times = torch.zeros(2 * self.MAX_FORKS, dtype=torch.int64, device=dev) \
+            if os.environ.get("GRACE_SPLIT_TRACE", "0") == "1" else None
+
+    def begin_main(self) -> None:
+        """First node of graph A (and of every eager use): A's generation += 1."""
+        if self.sync == "flags":
+            self._lib.xs_bump(self.gen[0:1], self.main.cuda_stream)
+
+    def begin_side(self) -> None:
+        """First node of graph B: B's generation += 1 (B waits for flags reaching it)."""
+        if self.sync == "flags":
+            self._lib.xs_bump(self.gen[1:2], self.side.cuda_stream)
+
+    def signal(self, stream: "torch.cuda.Stream"):
+        """Fork point on the critical stream: side work issued after ``wait(token)`` may start."""
+        i = len(self.events)
+        if self.sync == "events":
+            tok = self._lib.ExtEvent(self.idx)
+            tok.record(stream.cuda_stream)
+        else:
+            if i >= self.MAX_FORKS:
+                raise RuntimeError(f"split capture: more than {self.MAX_FORKS} fork points")
+            self._lib.xs_signal(self.flags, i, self.gen[0:1], stream.cuda_stream, self.times)
+            tok = i
+        self.events.append(tok)
+        return tok
+
+    def wait(self, tok, stream: "torch.cuda.Stream") -> None:
+        if self.sync == "events":
+            tok.wait(stream.cuda_stream)
+        else:
+            self._lib.xs_wait(self.flags, tok, self.gen[1:2], self.spin_limit, stream.cuda_stream, self.times)
+
+    def timeline(self):
+        """[(fork, A signalled (us, from fork 0), B's wait returned (us), B lag (us))] of the last
+        replay (GRACE_SPLIT_TRACE=1; the device clock runs at 100 MHz)."""
+        if self.times is None:
+            return []
+        n = len(self.events)
+        t = self.times[: 2 * n].view(n, 2).cpu().tolist()
+        base = t[0][0]
+        return [(i, (a - base) / 100.0, (b - base) / 100.0, (b - a) / 100.0) for i, (a, b) in enumerate(t)]
+
+    def split(self):
+        if not self.split_done:
+            self.split_done = True
+            self.on_split()
+
+
+_split: Dict[int, SplitCapture] = {}
+
+
+def begin_split(sc: SplitCapture) -> None:
+    _split[sc.idx] = sc
+
+
+def end_split(idx: int) -> Optional[SplitCapture]:
+    _pending[idx] = False
+    return _split.pop(idx, None)
+
+
+def split_active(device) -> bool:
+    """A split capture runs on ``device`` and has not reached its join yet."""
+    if not _split:
+        return False
+    idx = device.index if isinstance(device, torch.device) else device
+    sc = _split.get(idx)
+    return sc is not None and not sc.split_done
 
 
 def mark_joinable(params, on: bool = True) -> None:
@@ -147,21 +284,36 @@ class fork:
         # on the current stream right after this backward returns: in line as well.  So does a
         # parameter whose gradient a DistributedDataParallel reducer consumes (parallel/ddp_hook.py
         # clears the tag: the reducer reads it from its AccumulateGrad hook, mid-backward).
+        self.sc = None
         if (_ENABLED and t.is_cuda and param is not None and param.grad is None and joinable(param)):
+            sc = _split.get(t.device.index)
+            if sc is not None and sc.split_done:
+                return  # after the split's join (A2): nothing may fork any more, stay in line
             self.main = torch.cuda.current_stream(t.device)
-            self.ev = torch.cuda.Event()
-            self.ev.record(self.main)
+            if sc is not None:  # split capture: a fork point graph B waits on (flag word / event node)
+                if self.main.cuda_stream != sc.main.cuda_stream:
+                    return
+                self.sc = sc
+                self.ev = sc.signal(self.main)
+            else:
+                self.ev = torch.cuda.Event()
+                self.ev.record(self.main)
 
     def __enter__(self) -> bool:
         if self.ev is None:
             return False
         t = self.t
         side = _side(t.device)
-        side.wait_event(self.ev)
+        if self.sc is not None:
+            self.sc.wait(self.ev, side)
+        else:
+            side.wait_event(self.ev)
         self.ctx = torch.cuda.stream(side)
         self.ctx.__enter__()
         idx = t.device.index
-        if not _pending.get(idx):
+        if self.sc is not None:  # the split's join (``join`` on the critical stream) ends it
+            _pending[idx] = True
+        elif not _pending.get(idx):
             _pending[idx] = True
             # one final callback per backward pass: join before backward() returns
             try:
@@ -277,6 +429,17 @@ def join(stream: Optional["torch.cuda.Stream"] = None, device=None) -> None:
     else:
         devs = [torch.cuda.current_device()]
     for idx in devs:
+        sc = _split.get(idx)
+        if sc is not None and not sc.split_done:
+            if not _pending.get(idx):
+                continue
+            cur = stream if stream is not None else torch.cuda.current_stream(idx)
+            if cur.cuda_stream != sc.main.cuda_stream:
+                raise RuntimeError("split capture: side-stream weight gradients must be joined on the capture "
+                                   "stream (the engine's bucket launch; no overlap stream, no DDP reducer)")
+            sc.split()  # ends graphs A and B, A2 captures from here; the replay joins B into A2
+            _pending[idx] = False
+            continue
         if _deferred.get(idx):
             if stream is not None:
                 with torch.cuda.stream(stream):

@@ -80,6 +80,7 @@ class Bucket:
         self.pending = len(params)
         self.fired = [False] * len(params)
         self.stolen: List[Optional[torch.Tensor]] = [None] * len(params)  # fresh grads awaiting the gather
+        self.copy_later = set()  # stolen grads that need a layout copy, not the gather kernel
         self.handles = None
         self.ctx = None
 
@@ -87,6 +88,7 @@ class Bucket:
         self.pending = len(self.params)
         self.fired = [False] * len(self.params)
         self.stolen = [None] * len(self.params)
+        self.copy_later = set()
         self.handles = None
         self.ctx = None
 
@@ -228,6 +230,10 @@ class GraceEngine:
             # bucket by ONE gather launch when the bucket is complete (native); else copied here.
             if self._gatherable(p.grad, view):
                 b.stolen[idx] = p.grad
+            elif _wgrad.split_active(p.grad.device):
+                # a split capture joins the side stream only at the bucket launch: copy then
+                b.stolen[idx] = p.grad
+                b.copy_later.add(idx)
             else:
                 if p.grad.is_cuda:
                     _wgrad.join(torch.cuda.current_stream(p.grad.device))
@@ -240,8 +246,8 @@ class GraceEngine:
                                "increase backward_passes_per_step or call synchronize()")
         b.fired[idx] = True
         b.pending -= 1
-        if b.pending == 0:
-            self._launch(b)
+        if b.pending == 0 and not (self.device.type == "cuda" and _wgrad.split_active(self.device)):
+            self._launch(b)  # (a split capture launches every bucket from synchronize, after its join)
 
     @staticmethod
     def _gatherable(g: torch.Tensor, view: torch.Tensor) -> bool:
@@ -259,8 +265,11 @@ class GraceEngine:
         idx = [i for i, g in enumerate(b.stolen) if g is not None]
         if not idx:
             return
+        for i in idx:
+            if i in b.copy_later:
+                b.views[i].copy_(b.stolen[i])
         for dt in (torch.float32, torch.bfloat16):
-            sel = [i for i in idx if b.stolen[i].dtype == dt]
+            sel = [i for i in idx if b.stolen[i].dtype == dt and i not in b.copy_later]
             if sel:
                 _native.lib().gather_segments([b.stolen[i] for i in sel], [b.layout.offsets[i] for i in sel], b.flat)
         for i in idx:

@@ -108,12 +108,18 @@ class GraphedStep:
 
     def __init__(self, fn: Callable[[], torch.Tensor], warmup: int = 3, pool=None,
                  capture_error_mode: Optional[str] = None, copies: Optional[int] = None,
-                 stream: Optional[torch.cuda.Stream] = None):
+                 stream: Optional[torch.cuda.Stream] = None, split: Optional[bool] = None):
         import os
 
         self.fn = fn
         if capture_error_mode is None:
             capture_error_mode = "thread_local" if _nccl_group_up() else "global"
+        # split: capture the critical stream and the weight-gradient side stream as separate
+        # linear graphs joined by external event nodes (ops/wgrad.py SplitCapture); the step must
+        # join the side stream only through the GRACE engine (no DDP reducer, no overlap stream)
+        if split is None:
+            split = os.environ.get("GRACE_GRAPH_SPLIT", "0") == "1"
+        self.split = bool(split) and stream is None
         # ``stream``: warm up, capture and replay on this stream.  Needed when long-lived autograd
         # nodes were created under it -- DDP's reducer keeps the parameters' AccumulateGrad nodes,
         # which run on the stream current at DDP's construction; a capture on any other stream
@@ -130,6 +136,10 @@ class GraphedStep:
         # graph (parallel branches) is launched node by node by the HIP runtime, and a graph
         # cannot be re-submitted while its previous launch still runs; alternating copies lets
         # the host submit step N+1 while step N executes.
+        self.g_side = self.g_a2 = None
+        if self.split:
+            self._capture_split(fn, pool, capture_error_mode)
+            return
         copies = int(os.environ.get("GRACE_GRAPH_COPIES", "1")) if copies is None else int(copies)
         # GRACE_GRAPH_PRIORITY=-1: capture and replay on a high-priority stream (the compute
         # stream of the step then outranks the side streams it forks)
@@ -153,8 +163,102 @@ class GraphedStep:
         self.loss = self.losses[0]
         self._next = 0
 
+    def _capture_split(self, fn, pool, mode):
+        """Graph A (critical stream, until the engine's join), graph B (the wgrad side stream,
+        captured at the same time), graph A2 (critical stream, from the join on)."""
+        import os
+
+        from ..ops import wgrad as _wg
+
+        dev = torch.cuda.current_device()
+        # GRACE_SPLIT_MAIN_PRIO=-1: the critical chain's queue outranks the side queue in the
+        # command processor's dispatch arbitration
+        main = torch.cuda.Stream(dev, priority=int(os.environ.get("GRACE_SPLIT_MAIN_PRIO", "0")))
+        side = _wg._side(torch.device("cuda", dev))
+        ga, gb, ga2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        open_ = {"a": False, "b": False, "a2": False}
+
+        def end(g, st, key):
+            with torch.cuda.stream(st):
+                g.capture_end()
+            open_[key] = False
+
+        def on_split():
+            end(gb, side, "b")
+            end(ga, main, "a")
+            with torch.cuda.stream(main):
+                ga2.capture_begin(pool=ga.pool(), capture_error_mode=mode)
+            open_["a2"] = True
+
+        _health.init()  # the flag waits' timeout raises the process-wide fault words
+        sc = _wg.SplitCapture(dev, main, side, on_split, sync=os.environ.get("GRACE_GRAPH_SPLIT_SYNC", "flags"))
+        main.wait_stream(torch.cuda.current_stream())
+        side.wait_stream(torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        try:
+            with torch.cuda.stream(main):
+                ga.capture_begin(pool=pool, capture_error_mode=mode)
+            open_["a"] = True
+            sc.begin_main()
+            with torch.cuda.stream(side):
+                gb.capture_begin(capture_error_mode=mode)  # its own pool: A and B replay concurrently
+            open_["b"] = True
+            sc.begin_side()
+            _wg.begin_split(sc)
+            try:
+                with torch.cuda.stream(main):
+                    loss = fn()
+            finally:
+                _wg.end_split(dev)
+            if open_["a2"]:
+                end(ga2, main, "a2")
+            else:  # no join on the critical stream: A and B only
+                end(gb, side, "b")
+                end(ga, main, "a")
+        except BaseException:
+            for key, g, st in (("a2", ga2, main), ("b", gb, side), ("a", ga, main)):
+                if open_[key]:
+                    try:
+                        end(g, st, key)
+                    except Exception:  # noqa: BLE001 -- already failing; a live capture aborts at exit
+                        pass
+            raise
+        torch.cuda.synchronize()
+        self._sc = sc  # keeps the ExtEvents the graphs' nodes refer to
+        self.s_main, self.s_side = main, side
+        self.graphs = [ga]
+        self.g_side = gb if sc.events else None
+        self.g_a2 = ga2 if sc.split_done else None
+        self.graph = ga
+        self.losses = [loss.detach() if isinstance(loss, torch.Tensor) else loss]
+        self.loss = self.losses[0]
+        self._next = 0
+        self.stream = None
+
+    def _replay_split(self) -> torch.Tensor:
+        cur = torch.cuda.current_stream()
+        main, side = self.s_main, self.s_side
+        main.wait_stream(cur)
+        if self.g_side is not None:
+            side.wait_stream(cur)
+        with torch.cuda.stream(main):
+            self.graphs[0].replay()
+        if self.g_side is not None:
+            with torch.cuda.stream(side):
+                self.g_side.replay()
+            main.wait_stream(side)
+        if self.g_a2 is not None:
+            with torch.cuda.stream(main):
+                self.g_a2.replay()
+        cur.wait_stream(main)
+        if _SYNC_EACH:
+            torch.cuda.synchronize()
+        return self.loss
+
     def __call__(self) -> torch.Tensor:
         _health.check()
+        if self.split:
+            return self._replay_split()
         i = self._next
         self._next = (i + 1) % len(self.graphs)
         if self.stream is not None:

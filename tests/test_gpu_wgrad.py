@@ -94,9 +94,12 @@ def test_side_stream_grads_equal_inline():
             _close(a, b, msg=n)
 
 
-def test_engine_graph_with_side_stream_wgrad(bn_deterministic):
+@pytest.mark.parametrize("split", [False, True])
+def test_engine_graph_with_side_stream_wgrad(bn_deterministic, split):
     """an engine step captured in a whole-step graph with the wgrad forks (parallel graph
-    branches, joined before the bucket gather) matches the eager steps (parameters after 4 steps)"""
+    branches, joined before the bucket gather) matches the eager steps (parameters after 4 steps);
+    split=True: captured as two linear graphs (critical / side stream) joined by external event
+    nodes plus the post-join graph (parallel/graph.py GraphedStep split)"""
     from grace_amd import grace_from_params
     from grace_amd.parallel import DistributedOptimizer, FusedSGD
     from grace_amd.parallel.graph import GraphedStep
@@ -127,7 +130,9 @@ def test_engine_graph_with_side_stream_wgrad(bn_deterministic):
     for _ in range(7):
         s1()
     m2, o2 = build()
-    g = GraphedStep(make_step(m2, o2), warmup=3)  # 3 eager warm-up steps + capture (not a step)
+    g = GraphedStep(make_step(m2, o2), warmup=3, split=split)  # 3 eager warm-up steps + capture (not a step)
+    if split:
+        assert g.g_side is not None and g.g_a2 is not None and len(g._sc.events) >= 3
     for _ in range(4):
         g()
     torch.cuda.synchronize()
@@ -139,9 +144,10 @@ def test_engine_graph_with_side_stream_wgrad(bn_deterministic):
         assert err <= 1e-3 * float(b.abs().max()) + 2e-5, f"{n}: max abs err {err:.3g}"
 
 
-def test_topk_graph_with_side_stream_runs():
+@pytest.mark.parametrize("split", [False, True])
+def test_topk_graph_with_side_stream_runs(split):
     """ResNet-50 Top-K 1 % whole-step graph with the wgrad forks: replays are finite and the
-    exchange leaves ~1 % non-zero gradients"""
+    exchange leaves ~1 % non-zero gradients (one forked graph, or the split A / B / A2 graphs)"""
     from grace_amd import grace_from_params
     from grace_amd.models import resnet50
     from grace_amd.parallel import DistributedOptimizer, FusedSGD
@@ -163,7 +169,7 @@ def test_topk_graph_with_side_stream_runs():
         opt.step()
         return loss
 
-    g = GraphedStep(step, warmup=3)
+    g = GraphedStep(step, warmup=3, split=split)
     for _ in range(3):
         loss = g()
     torch.cuda.synchronize()

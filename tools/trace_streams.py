@@ -47,6 +47,16 @@ def main(argv=None):
     print(f"{args.steps} steps, {(t1 - t0) / 1e6 / args.steps:.3f} ms/step between markers ({qkey})")
     for q, (c, t) in sorted(per_q.items(), key=lambda kv: -kv[1][1]):
         print(f"  queue {q:>6}: {c / args.steps:6.1f} kernels/step, {t / 1e6 / args.steps:7.3f} ms/step of kernel time")
+    # per queue: idle gaps between consecutive kernels (dependency waits, launch / marker latency)
+    byq = collections.defaultdict(list)
+    for s_, e_, _, q in win:
+        byq[q].append((s_, e_))
+    for q, iv in sorted(byq.items()):
+        iv.sort()
+        gaps = [b[0] - a[1] for a, b in zip(iv, iv[1:]) if b[0] > a[1]]
+        big = [g for g in gaps if g > 3000]
+        print(f"  queue {q:>6}: idle between kernels {sum(gaps) / 1e6 / args.steps:7.3f} ms/step; "
+              f"{len(big) / args.steps:5.1f} gaps/step > 3 us totalling {sum(big) / 1e6 / args.steps:7.3f} ms/step")
     # union busy time and the time two or more queues run at once
     ev = []
     for s, e, _, _ in win:
