@@ -10,3 +10,9 @@ from .layout import SegmentLayout, layout_for  # noqa: F401
 
 def native_available() -> bool:
     return _native.available()
+
+
+# the ``grace`` dispatcher operators (torch.ops.grace.*: csrc/ops_library.cpp + ops/library.py)
+from . import library as _library  # noqa: E402
+
+_library.register()
