@@ -976,35 +976,6 @@ void gather_segments(const std::vector<Tensor>& srcs, const std::vector<int64_t>
 }
 
 // dsts[i] (contiguous) <- srcs[i] (any strides, same shape, <= 4 dims), fp32, one launch per 40 tensors.
-void strided_copy(const std::vector<Tensor>& srcs, const std::vector<Tensor>& dsts) {
-  TORCH_CHECK(srcs.size() == dsts.size(), "strided_copy: srcs/dsts length");
-  if (srcs.empty()) return;
-  const size_t n = srcs.size();
-  std::vector<const float*> sp(n);
-  std::vector<float*> dp(n);
-  std::vector<std::array<int32_t, 4>> sz(n);
-  std::vector<std::array<int64_t, 4>> st(n);
-  for (size_t i = 0; i < n; ++i) {
-    const Tensor& a = srcs[i];
-    const Tensor& b = dsts[i];
-    CHECK_DEV(a);
-    CHECK_F32(b);
-    TORCH_CHECK(a.scalar_type() == at::kFloat, "strided_copy: fp32 sources");
-    TORCH_CHECK(a.sizes() == b.sizes() && a.dim() <= 4, "strided_copy: equal shapes of <= 4 dims");
-    TORCH_CHECK(a.device() == b.device(), "strided_copy: device mismatch");
-    TORCH_CHECK(a.numel() < (int64_t(1) << 31), "strided_copy: < 2^31 elements");
-    const int pad = 4 - (int)a.dim();
-    for (int k = 0; k < 4; ++k) {
-      sz[i][k] = k < pad ? 1 : (int32_t)a.size(k - pad);
-      st[i][k] = k < pad ? 0 : a.stride(k - pad);
-    }
-    sp[i] = a.data_ptr<float>();
-    dp[i] = b.data_ptr<float>();
-  }
-  DevGuard guard(dsts[0].device());
-  grace::strided_copy_segments(sp.data(), dp.data(), reinterpret_cast<const int32_t(*)[4]>(sz.data()),
-                               reinterpret_cast<const int64_t(*)[4]>(st.data()), (int)n, cur_stream());
-}
 
 // dsts[i] <- bf16(srcs[i]) (round to nearest even), memory images, one launch per 120 tensors.
 void cast_segments_bf16(const std::vector<Tensor>& srcs, const std::vector<Tensor>& dsts) {
@@ -1266,6 +1237,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("axpby", &axpby);
   m.def("scale_", &scale_);
   m.def("gather_segments", &gather_segments);
-  m.def("strided_copy", &strided_copy);
   m.def("cast_segments_bf16", &cast_segments_bf16);
 }

@@ -215,11 +215,6 @@ void adaq_decode(int n_groups, const float* means, const int32_t* counts, const 
 
 // ---------------------------------------------------------------- ef.hip (bucket gather)
 constexpr int kGatherSegs = 120;
-constexpr int kCopySegs = 40;  // strided_copy_segments: 40 x 80-B table entries in the kernel arguments
-// dst[i] (contiguous, shape size[i]) <- src[i] read with strides stride[i] (<= 4 dims, padded with
-// leading 1s); one launch per kCopySegs tensors
-void strided_copy_segments(const float* const* src, float* const* dst, const int32_t (*size)[4],
-                           const int64_t (*stride)[4], int n_seg, hipStream_t stream);
 void gather_segments(const void* const* src, bool bf16, const int64_t* dst_off, const int64_t* len, int n_seg,
                      float* dst, hipStream_t stream);
 void cast_segments_bf16(const float* const* src, uint16_t* const* dst, const int64_t* len, int n_seg,

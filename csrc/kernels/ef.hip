@@ -128,37 +128,6 @@ __global__ __launch_bounds__(kBlock) void cast_segments_kernel(CastTable t) {
   for (int64_t i = tail + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) d[i] = f32_to_bf16_rne(src[i]);
 }
 
-// Layout-converting batched copy: up to kCopySegs tensors of <= 4 dims, each into a CONTIGUOUS
-// destination of the same shape, from any strided source (a MIOpen channels_last weight gradient
-// into DDP's NCHW bucket view) -- ONE launch instead of one copy kernel per tensor.  Element i of
-// the destination reads the source at the strided offset of its 4-d index (gather reads,
-// coalesced writes).  blockIdx.y = tensor.
-struct StridedTable {
-  const float* src[kCopySegs];
-  float* dst[kCopySegs];
-  int32_t size[kCopySegs][4];      // outermost first, padded with leading 1s
-  int64_t stride[kCopySegs][4];    // source strides (elements)
-};
-
-__global__ __launch_bounds__(kBlock) void strided_copy_kernel(StridedTable t) {
-  // one thread per (i0, i1) row of the destination, looping its n2 x n3 inner elements (a conv
-  // weight's kh x kw taps): one 32-bit division per row instead of three 64-bit ones per element;
-  // consecutive threads read consecutive i1 (a channels_last source's contiguous channel axis)
-  const int s = blockIdx.y;
-  const int n1 = t.size[s][1], n2 = t.size[s][2], n3 = t.size[s][3];
-  const int rows = t.size[s][0] * n1;
-  const float* __restrict__ src = t.src[s];
-  float* __restrict__ d = t.dst[s];
-  const int64_t s0 = t.stride[s][0], s1 = t.stride[s][1], s2 = t.stride[s][2], s3 = t.stride[s][3];
-  for (int r = blockIdx.x * kBlock + threadIdx.x; r < rows; r += gridDim.x * kBlock) {
-    const int i0 = r / n1, i1 = r - i0 * n1;
-    const float* sp = src + i0 * s0 + i1 * s1;
-    float* dp = d + (int64_t)r * n2 * n3;
-    for (int i2 = 0; i2 < n2; ++i2)
-      for (int i3 = 0; i3 < n3; ++i3) dp[i2 * n3 + i3] = sp[i2 * s2 + i3 * s3];
-  }
-}
-
 inline unsigned seg_grid(int64_t maxn) {
   int64_t gx = (maxn / 4 + kBlock - 1) / kBlock;
   if (gx > 512) gx = 512;
@@ -188,34 +157,6 @@ void gather_segments(const void* const* src, bool bf16, const int64_t* dst_off, 
   }
 }
 
-void strided_copy_segments(const float* const* src, float* const* dst, const int32_t (*size)[4],
-                           const int64_t (*stride)[4], int n_seg, hipStream_t stream) {
-  for (int g0 = 0; g0 < n_seg; g0 += kCopySegs) {
-    const int ng = n_seg - g0 < kCopySegs ? n_seg - g0 : kCopySegs;
-    StridedTable t;
-    int64_t maxn = 0;
-    for (int i = 0; i < ng; ++i) {
-      t.src[i] = src[g0 + i];
-      t.dst[i] = dst[g0 + i];
-      int64_t n = 1;
-      for (int k = 0; k < 4; ++k) {
-        t.size[i][k] = size[g0 + i][k];
-        t.stride[i][k] = stride[g0 + i][k];
-        n *= size[g0 + i][k];
-      }
-      if (n > maxn) maxn = n;
-    }
-    if (maxn == 0) continue;
-    int64_t maxrows = 0;
-    for (int i = 0; i < ng; ++i) {
-      const int64_t r = (int64_t)t.size[i][0] * t.size[i][1];
-      if (r > maxrows) maxrows = r;
-    }
-    int64_t gx = (maxrows + kBlock - 1) / kBlock;
-    if (gx > 1024) gx = 1024;
-    strided_copy_kernel<<<dim3((unsigned)gx, (unsigned)ng), kBlock, 0, stream>>>(t);
-  }
-}
 
 void cast_segments_bf16(const float* const* src, uint16_t* const* dst, const int64_t* len, int n_seg,
                         hipStream_t stream) {

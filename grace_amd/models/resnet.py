@@ -18,7 +18,7 @@ from ..ops.bnact import BatchNormAct2d, bn_relu_maxpool
 from ..ops.bnconv import basic_main, bottleneck_main
 from ..ops.conv import Conv1x1F32, conv_bn_act
 from ..ops.pool import GlobalAvgPoolFlat, MaxPool2dNHWC
-from ..ops.wgrad import Conv2dSplitGrad, branch
+from ..ops.wgrad import Conv2dSplitGrad
 
 
 def _conv3x3(cin, cout, stride=1):
@@ -81,27 +81,17 @@ class Bottleneck(nn.Module):
         # two gradients are summed inside the fused BN backward, not by an autograd add), or a
         # plain tensor for the first block
         xm, xs = x if isinstance(x, tuple) else (x, x)
-        if self.downsample is None:
-            idt, br = xs, None
-        else:  # projection shortcut on a second stream, beside the main path (ops/wgrad.py branch)
-            with branch(xs) as br:
-                idt = _down(self.downsample, xs)
-        # the main path with bn1 / bn2 applied inside conv2 / conv3's GEMMs (ops/bnconv.py);
-        # not with the shortcut on its own stream (opt-in branch: merged at the end)
-        if br is None or not br.on:
-            idt = br.merge(idt) if br is not None else idt
-            br = None
-            out = bottleneck_main(self, xm, idt)
-            if out is not None:
-                return out
+        idt = xs if self.downsample is None else _down(self.downsample, xs)
+        # the main path with bn1 / bn2 applied inside conv2 / conv3's GEMMs (ops/bnconv.py)
+        out = bottleneck_main(self, xm, idt)
+        if out is not None:
+            return out
         # 1x1 conv -> BN pairs: the BN statistics may come from the conv GEMM's epilogue
         # (ops/conv.py conv_bn_act, autotuned; otherwise exactly bn(conv(x)))
         # bn1 / bn2 outputs feed exactly one conv each: their backward reductions come from the
         # consuming conv's data-grad GEMM epilogue (ops/bnact.py BNHandoff)
         y = conv_bn_act(self.conv1, self.bn1, xm, handoff=True)
         y = conv_bn_act(self.conv2, self.bn2, y, handoff=True)
-        if br is not None:
-            idt = br.merge(idt)
         return conv_bn_act(self.conv3, self.bn3, y, idt, dual=True)
 
 

@@ -255,17 +255,7 @@ class _Conv1x1AutoFn(torch.autograd.Function):
         dx = dw = None
         f = None
         if ctx.needs_input_grad[1]:
-            tgt = _wg.grad_target(ctx.weight) if _wg._DEFER else None
-            if tgt is not None:
-                be = _pick("wgrad", x, wt, dy, ctx.wshape)
-                wshape = ctx.wshape
-
-                def late(dy=dy, x=x, wt=wt, tgt=tgt, be=be):
-                    _wg.into_target(_run("wgrad", be, x, wt, dy, wshape, out=tgt.reshape(wt.shape)).view(wshape), tgt)
-            if tgt is not None and _wg.defer(dy.device, late):
-                dw = tgt.view_as(tgt)
-            else:
-                f = _wg.fork(dy, ctx.weight)
+            f = _wg.fork(dy, ctx.weight)
 
         def wg():
             be = _pick("wgrad", x, wt, dy, ctx.wshape)  # autotuned on the current stream, never on the side one
@@ -280,12 +270,8 @@ class _Conv1x1AutoFn(torch.autograd.Function):
                     _wg.tag(dy, s)
                     _wg.tag(x, s)
                     _wg.tag(d, f.main)
-                elif tgt is None:
-                    d = _wg.ddp_batched(d, ctx.weight)  # DDP: one batched copy instead of the reducer's
             return d
 
-        if f is not None and _wg._WG_FIRST:
-            dw = wg()
         if ctx.needs_input_grad[0]:
             be = _pick("dgrad", x, wt, dy, ctx.wshape)
             # the producing BN's reduction in the epilogue -- only where the MFMA GEMM is already the
@@ -294,7 +280,7 @@ class _Conv1x1AutoFn(torch.autograd.Function):
                 if be.startswith("mfma") else None
             if dx is None:
                 dx = _run("dgrad", be, x, wt, dy, ctx.wshape)
-        if f is not None and not _wg._WG_FIRST:
+        if f is not None:
             dw = wg()
         return dx, dw
 
@@ -612,15 +598,7 @@ class _Conv3x3Fn(torch.autograd.Function):
         dx = dw = None
         f = None
         if ctx.needs_input_grad[1]:
-            be = _pick3("wgrad", x, w, dy, stride)
-            tgt = _wg.grad_target(ctx.weight) if _wg._DEFER else None
-            if tgt is not None:
-                def late(dy=dy, x=x, w=w, tgt=tgt, be=be):
-                    _wg.into_target(_run3("wgrad", be, x, w, dy, stride, out=tgt), tgt)
-            if tgt is not None and _wg.defer(dy.device, late):
-                dw = tgt.view_as(tgt)
-            else:
-                f = _wg.fork(dy, ctx.weight)
+            f = _wg.fork(dy, ctx.weight)
 
         def wg():
             be = _pick3("wgrad", x, w, dy, stride)  # autotuned on the current stream
@@ -632,19 +610,15 @@ class _Conv3x3Fn(torch.autograd.Function):
                     _wg.tag(dy, s)
                     _wg.tag(x, s)
                     _wg.tag(d, f.main)
-                elif tgt is None:
-                    d = _wg.ddp_batched(d, ctx.weight)  # DDP: one batched copy instead of the reducer's
             return d
 
-        if f is not None and _wg._WG_FIRST:
-            dw = wg()
         if ctx.needs_input_grad[0]:
             be = _pick3("dgrad", x, w, dy, stride)
             dx = _dgrad_handoff(getattr(ctx, "bn_h", None), x, w, dy, 3, _tile_of(be)) \
                 if be.startswith("mfma") and _mfma_cfg(be)[1] <= 1 else None
             if dx is None:
                 dx = _run3("dgrad", be, x, w, dy, stride)
-        if f is not None and not _wg._WG_FIRST:
+        if f is not None:
             dw = wg()
         return dx, dw, None
 

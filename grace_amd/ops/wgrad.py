@@ -40,10 +40,6 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 _ENABLED = os.environ.get("GRACE_WGRAD_STREAM", "1") == "1"
-# issue (capture) the side-stream wgrad before the in-line dgrad of the same conv: measured
-# 2677 -> 2394-2468 img/s (the wgrads then compete with the dgrad chain from its start;
-# profiles/r3_graph_fork_knobs.txt), so off
-_WG_FIRST = os.environ.get("GRACE_WGRAD_FIRST", "0") == "1"
 _streams: Dict[int, "torch.cuda.Stream"] = {}
 _pending: Dict[int, bool] = {}  # device -> side work issued since the last join
 _lock = threading.Lock()
@@ -227,43 +223,6 @@ def joinable(param: torch.Tensor) -> bool:
     return bool(getattr(param, "_grace_wgrad_join", False))
 
 
-# ---------------------------------------------------------------- deferred weight gradients
-# GRACE_WGRAD_DEFER=1: a weight gradient whose destination is an engine bucket view is not
-# computed when its conv's backward runs; its closure is queued and every queued one runs, in
-# order, on the compute stream at the join (the engine's bucket launch / the end of backward).
-# The dgrad chain then runs uninterrupted and the weight gradients back to back after it, in a
-# single-stream graph.  Measured at the in-line speed (2516 vs 2708 img/s for the side stream,
-# profiles/r3_graph_fork_knobs.txt): the side stream's gain is the overlap of its wgrads with
-# the tail of the dgrad chain, not the reordering -- so opt-in.  The fresh alias of the bucket view handed to AccumulateGrad is only
-# READ after the join, so the late write is invisible to the engine.
-_DEFER = os.environ.get("GRACE_WGRAD_DEFER", "0") == "1"
-_deferred: Dict[int, list] = {}
-
-
-def defer(device: torch.device, fn) -> bool:
-    """Queue ``fn`` (computes and stores one weight gradient) for the next join; False when
-    deferral is off or impossible (no backward to attach the final callback to)."""
-    if not (_DEFER and _ENABLED):
-        return False
-    idx = device.index
-    q = _deferred.setdefault(idx, [])
-    if not q and not _pending.get(idx):
-        try:
-            torch.autograd.Variable._execution_engine.queue_callback(_final_join)
-        except RuntimeError:
-            return False
-    q.append(fn)
-    return True
-
-
-def _run_deferred(idx: int) -> None:
-    q = _deferred.get(idx)
-    if q:
-        _deferred[idx] = []
-        for fn in q:
-            fn()
-
-
 class fork:
     """``f = fork(t)`` marks the current stream's position NOW (before the caller issues its
     critical-path kernels); ``with f as go:`` then runs the body on the side stream of ``t``'s
@@ -359,58 +318,6 @@ def into_target(dw: torch.Tensor, tgt: Optional[torch.Tensor]) -> torch.Tensor:
     return tgt.view_as(tgt)
 
 
-# ---------------------------------------------------------------- DDP: one batched copy for library wgrads
-# A DDP-managed parameter (parallel/ddp_hook.py, gradient_as_bucket_view) whose weight gradient
-# comes from a library kernel (MIOpen returns its own channels_last tensor) made DDP's reducer copy
-# it into its NCHW bucket view: one layout-converting copy per parameter on the critical stream
-# (38 per ResNet-50 step, 0.26 ms; profiles/r5_ddp_batched_copy.txt).  ``ddp_batched`` queues the (gradient -> view)
-# pair and hands autograd an alias of the view (the reducer then finds its bucket already
-# aliased); the GRACE comm hook runs every queued copy in ONE multi-tensor launch before it reads
-# a bucket (``flush_copies``), and the end of backward flushes anything left.
-# Measured on the graphed DDP step: 2441-2450 vs 2469-2470 img/s with the reducer's copies
-# (profiles/r5_ddp_batched_copy.txt) -- the one launch at the hook's entry lands on the critical
-# path the scattered copies were not -- so opt-in: GRACE_DDP_BATCH_COPY=1.
-_DDP_BATCH = os.environ.get("GRACE_DDP_BATCH_COPY", "0") == "1"
-_copies: Dict[int, list] = {}
-
-
-def ddp_batched(d: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
-    if not (_DDP_BATCH and d.is_cuda and getattr(weight, "_grace_ddp", False)
-            and getattr(weight, "_grace_view_stable", False)):
-        return d
-    tgt = grad_target(weight)
-    # any source layout (MIOpen's channels_last weight gradients against DDP's NCHW bucket views:
-    # the batched copy converts), a contiguous fp32 destination of the same shape
-    if (tgt is None or d.shape != tgt.shape or d.dtype != torch.float32 or tgt.dtype != torch.float32
-            or d.dim() > 4 or not tgt.is_contiguous()):
-        return d
-    idx = d.device.index
-    q = _copies.setdefault(idx, [])
-    if not q:
-        try:
-            torch.autograd.Variable._execution_engine.queue_callback(lambda idx=idx: flush_copies(idx))
-        except RuntimeError:  # not inside a backward pass: copy now
-            tgt.copy_(d)
-            return tgt.view_as(tgt)
-    q.append((d, tgt))
-    return tgt.view_as(tgt)
-
-
-def flush_copies(device=None) -> None:
-    """Run the queued DDP gradient copies of ``device`` (default: current) on the current stream."""
-    if not _copies:
-        return
-    idx = device if isinstance(device, int) else (torch.device(device).index if device is not None
-                                                  else torch.cuda.current_device())
-    q = _copies.get(idx)
-    if not q:
-        return
-    _copies[idx] = []
-    from . import _native
-
-    _native.lib().strided_copy([s for s, _ in q], [t for _, t in q])  # one launch per 40 tensors
-
-
 def tag(t: Optional[torch.Tensor], stream: "torch.cuda.Stream") -> None:
     """The caching allocator must not recycle ``t`` before ``stream``'s work on it ran."""
     if t is not None and t.is_cuda:
@@ -419,8 +326,8 @@ def tag(t: Optional[torch.Tensor], stream: "torch.cuda.Stream") -> None:
 
 def join(stream: Optional["torch.cuda.Stream"] = None, device=None) -> None:
     """Make ``stream`` (default: the current stream) wait for every side-stream wgrad issued so
-    far, after running the deferred ones (on ``stream``)."""
-    if not _pending and not _deferred:
+    far."""
+    if not _pending:
         return
     if stream is not None:
         devs = [stream.device.index]
@@ -440,12 +347,6 @@ def join(stream: Optional["torch.cuda.Stream"] = None, device=None) -> None:
             sc.split()  # ends graphs A and B, A2 captures from here; the replay joins B into A2
             _pending[idx] = False
             continue
-        if _deferred.get(idx):
-            if stream is not None:
-                with torch.cuda.stream(stream):
-                    _run_deferred(idx)
-            else:
-                _run_deferred(idx)
         if _pending.get(idx):
             tgt = stream if stream is not None else torch.cuda.current_stream(idx)
             tgt.wait_stream(_streams[idx])
@@ -531,17 +432,7 @@ class _ConvSplitFn(torch.autograd.Function):
         stride, padding, dilation, groups = ctx.conf
         cb = torch.ops.aten.convolution_backward
         dx = dw = None
-        f = None
-        if ctx.needs_input_grad[1]:
-            tgt = grad_target(w) if _DEFER and dy.is_cuda else None
-            if tgt is not None:
-                def late(dy=dy, x=x, w=w, tgt=tgt):
-                    into_target(cb(dy, x, w, None, stride, padding, dilation, False, [0, 0], groups,
-                                   [False, True, False])[1], tgt)
-            if tgt is not None and defer(dy.device, late):
-                dw = tgt.view_as(tgt)
-            else:
-                f = fork(dy, w)
+        f = fork(dy, w) if ctx.needs_input_grad[1] else None
 
         def wg():
             # MIOpen returns its own gradient tensor: writing it into the bucket view would be one
@@ -554,15 +445,11 @@ class _ConvSplitFn(torch.autograd.Function):
                     tag(dy, s)
                     tag(x, s)
                     tag(d, f.main)
-                else:
-                    d = ddp_batched(d, w)  # DDP: one batched copy instead of the reducer's
             return d
 
-        if f is not None and _WG_FIRST:
-            dw = wg()
         if ctx.needs_input_grad[0]:
             dx = _dgrad(dy, x, w, stride, padding, dilation, groups)
-        if f is not None and not _WG_FIRST:
+        if f is not None:  # issued after the in-line dgrad (before it measured slower, r3_graph_fork_knobs)
             dw = wg()
         return dx, dw, None, None, None, None
 
@@ -596,64 +483,3 @@ class Conv2dSplitGrad(nn.Conv2d):
                 return _ConvSplitFn.apply(x, w, _as2(self.stride), _as2(self.padding), _as2(self.dilation),
                                           self.groups)
         return super().forward(x)
-
-
-# ---------------------------------------------------------------- forward branches
-# A ResNet stage's first block has two independent branches from its input: the main path
-# (1x1 -> BN -> 3x3 -> BN -> 1x1) and the projection shortcut (strided 1x1 -> BN).  ``branch``
-# runs the shortcut on a second per-device stream that waits for the block input; ``merge``
-# makes the current stream wait for it before the residual add consumes it.  Autograd runs each
-# backward op on its forward op's stream and syncs the two where gradients cross, so the
-# shortcut's backward also runs beside the main path's.  Measured on the fp32 ResNet-50 headline
-# (profiles/r3_wgrad_side_stream_ab.txt): 2647 -> 2590 img/s with the branch -- the autograd
-# cross-stream event pairs around every shortcut gradient cost more than the overlap hides --
-# so it is opt-in (GRACE_BRANCH_STREAM=1).
-_bstreams: Dict[int, "torch.cuda.Stream"] = {}
-
-
-def _branch_stream(device: torch.device) -> "torch.cuda.Stream":
-    idx = device.index
-    s = _bstreams.get(idx)
-    if s is None:
-        with _lock:
-            s = _bstreams.get(idx)
-            if s is None:
-                with torch.cuda.device(idx):
-                    s = torch.cuda.Stream()
-                _bstreams[idx] = s
-    return s
-
-
-_BRANCH = os.environ.get("GRACE_BRANCH_STREAM", "0") == "1"
-
-
-class branch:
-    """``with branch(x) as b: y = f(x)`` then ``y = b.merge(y)`` before the current stream uses y."""
-
-    def __init__(self, x: torch.Tensor):
-        self.x = x
-        self.on = _ENABLED and _BRANCH and x.is_cuda and not torch.is_autocast_enabled()
-        self.main = self.ctx = None
-
-    def __enter__(self):
-        if self.on:
-            self.main = torch.cuda.current_stream(self.x.device)
-            s = _branch_stream(self.x.device)
-            s.wait_stream(self.main)
-            self.ctx = torch.cuda.stream(s)
-            self.ctx.__enter__()
-            tag(self.x, s)
-        return self
-
-    def __exit__(self, *exc):
-        if self.ctx is not None:
-            self.ctx.__exit__(*exc)
-        return False
-
-    def merge(self, y):
-        if not self.on:
-            return y
-        self.main.wait_stream(_branch_stream(self.x.device))
-        for t in (y if isinstance(y, (tuple, list)) else (y,)):
-            tag(t, self.main)
-        return y

@@ -67,7 +67,6 @@ class GraceHookState:
         self._loc: Dict[int, Tuple[str, int, int, int]] = {}
         self._gen: Dict[int, int] = {}
         self._views: Dict[int, int] = {}  # bucket index -> buffer address its gradient targets point into
-        self._stable = set()  # bucket indices whose buffer was seen unchanged on consecutive calls
 
     def layout_for(self, bucket) -> Tuple[str, Optional[torch.Tensor]]:
         """(registered layout name, None | int64 index of the packed elements in the buffer)."""
@@ -99,20 +98,7 @@ class GraceHookState:
             self._migrate(key, params, lay)
             ent = (lay, pidx, buf.numel(), key, sig)
             self.layouts[idx] = ent
-        if self._views.get(idx) == buf.data_ptr():
-            if idx not in self._stable:
-                # the same bucket buffer on two consecutive calls: DDP's one-time bucket rebuild
-                # (after the first iteration) is behind us, the marked views stay valid -- from
-                # now on library weight gradients may defer their copy into them
-                # (ops/wgrad.py ddp_batched; a deferral into a view DDP has just replaced would
-                # let the reducer copy the stale view's old contents)
-                self._stable.add(idx)
-                for p in params:
-                    p._grace_view_stable = True
-        else:  # new layout, or DDP rebuilt the same one
-            self._stable.discard(idx)
-            for p in params:
-                p._grace_view_stable = False
+        if self._views.get(idx) != buf.data_ptr():  # new layout, or DDP rebuilt the same one
             self._views[idx] = buf.data_ptr()
             # with gradient_as_bucket_view DDP makes each .grad a view of the bucket: mark those
             # views as the parameters' gradient targets, so weight-gradient producers
@@ -203,7 +189,6 @@ def grace_comm_hook(state: GraceHookState, bucket: dist.GradBucket) -> torch.fut
     dev = buf.device
     from ..ops import wgrad as _wg
 
-    _wg.flush_copies(dev.index)  # queued library weight gradients into their bucket views (one launch)
     cs, ds = state._streams(dev)
     cur = torch.cuda.current_stream(dev)
     cs.wait_stream(cur)

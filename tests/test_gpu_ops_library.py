@@ -47,15 +47,15 @@ def test_randomk_and_sign_gpu_equal_cpu():
 
 
 def test_qsgd_and_natural_gpu_in_distribution():
-    g = _g(1 << 16).cuda()
+    g = _g(4096).cuda()  # small n: |x| / ||x|| spans a few levels, so 128 roundings average well
     codes, norm = G.qsgd_compress(g, 127, 5)
     assert codes.dtype == torch.int8 and int(codes.abs().max()) <= 127
     torch.testing.assert_close(norm, torch.linalg.vector_norm(g).reshape(1))
     acc = torch.zeros_like(g)
-    for s in range(32):
+    for s in range(128):
         c, n = G.qsgd_compress(g, 127, s)
         acc += G.qsgd_decompress(c, n, 127, [g.numel()])
-    assert float((acc / 32 - g).abs().mean() / g.abs().mean()) < 0.05
+    assert float((acc / 128 - g).abs().mean() / g.abs().mean()) < 0.05  # ~2 % expected
     x = g.abs() + 0.1
     dec = G.natural_decompress(G.natural_compress(x, 1), [x.numel()])
     lo = torch.exp2(torch.floor(torch.log2(x)))
