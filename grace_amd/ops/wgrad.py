@@ -223,6 +223,24 @@ def joinable(param: torch.Tensor) -> bool:
     return bool(getattr(param, "_grace_wgrad_join", False))
 
 
+# GRACE_WGRAD_FORK: which weight gradients may leave the critical stream (A/B of where the side
+# stream's gain comes from; every fork point costs the critical stream a dependency marker in a
+# split capture).  Comma list of selectors, a conv forks when one matches: "all" (default),
+# "k3" / "k1" (kernel size), "hN" (the output gradient's height, e.g. h56 = ResNet stage 1).
+_FORK_SEL = tuple(v.strip() for v in os.environ.get("GRACE_WGRAD_FORK", "all").split(",") if v.strip())
+
+
+def fork_selected(dy: torch.Tensor, w: torch.Tensor) -> bool:
+    if "all" in _FORK_SEL:
+        return True
+    for sel in _FORK_SEL:
+        if sel in ("k3", "k1") and w.dim() == 4 and w.shape[-1] == int(sel[1]):
+            return True
+        if sel.startswith("h") and dy.dim() == 4 and sel[1:].isdigit() and dy.shape[2] == int(sel[1:]):
+            return True
+    return False
+
+
 class fork:
     """``f = fork(t)`` marks the current stream's position NOW (before the caller issues its
     critical-path kernels); ``with f as go:`` then runs the body on the side stream of ``t``'s
@@ -244,7 +262,8 @@ class fork:
         # parameter whose gradient a DistributedDataParallel reducer consumes (parallel/ddp_hook.py
         # clears the tag: the reducer reads it from its AccumulateGrad hook, mid-backward).
         self.sc = None
-        if (_ENABLED and t.is_cuda and param is not None and param.grad is None and joinable(param)):
+        if (_ENABLED and t.is_cuda and param is not None and param.grad is None and joinable(param)
+                and fork_selected(t, param)):
             sc = _split.get(t.device.index)
             if sc is not None and sc.split_done:
                 return  # after the split's join (A2): nothing may fork any more, stay in line
