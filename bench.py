@@ -140,6 +140,10 @@ def parse():
                          "external event nodes between them) plus the post-join graph, instead of one forked "
                          "graph (parallel/graph.py GraphedStep split); engine surface without overlap only; "
                          "auto = GRACE_GRAPH_SPLIT")
+    ap.add_argument("--ddp-defer", choices=["auto", "on", "off"], default="auto",
+                    help="--surface ddp: the GRACE comm hook hands DDP its bucket back and runs the exchange "
+                         "after backward (GraceHookState(defer=True)): DDP-managed weight gradients may then run "
+                         "on the side stream and the step may be a split graph; auto = on under a whole-step graph")
     ap.add_argument("--deterministic", action="store_true",
                     help="bitwise-reproducible BN backward (fixed-order fp64 tree instead of atomic fp32 "
                          "totals; GRACE_BN_DETERMINISTIC=1)")
@@ -428,7 +432,8 @@ def main() -> int:
         with torch.cuda.stream(ddp_stream) if ddp_stream is not None else contextlib.nullcontext():
             model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], bucket_cap_mb=args.bucket_mb,
                                                               gradient_as_bucket_view=True, broadcast_buffers=False)
-        ddp_state = GraceHookState(grc, model=model)
+        ddp_defer = args.ddp_defer == "on" or (args.ddp_defer == "auto" and mode == "full")
+        ddp_state = GraceHookState(grc, model=model, defer=ddp_defer)
         model.register_comm_hook(ddp_state, grace_comm_hook)
         if ddp_stream is not None and hasattr(torch.autograd.graph, "set_warn_on_accumulate_grad_stream_mismatch"):
             # intentional: DDP's reducer keeps AccumulateGrad nodes created on the capture stream (see
@@ -442,6 +447,7 @@ def main() -> int:
                 base_opt.zero_grad(set_to_none=set_to_none)
 
             def step(self):
+                ddp_state.flush()  # the deferred GRACE exchange (no-op for the immediate hook)
                 base_opt.step()
 
             def abort_step(self):
@@ -478,8 +484,12 @@ def main() -> int:
             # first 10 iterations: capture only after those
             cap_warm = max(3, args.warmup // 2) if args.surface == "engine" else max(11, args.warmup)
             split = None if args.graph_split == "auto" else args.graph_split == "on"
-            if args.surface != "engine" or overlap:
-                split = False
+            if split is None and args.surface == "ddp" and ddp_state.defer:
+                # the DDP step as ONE forked graph is host-bound (11.0 ms of issue per 13.6 ms step,
+                # 2352 img/s) -- split graphs: 2558 img/s at 0.27 ms of issue (profiles/r6_ddp_deferred.txt)
+                split = True
+            if overlap or (args.surface == "ddp" and not ddp_state.defer):
+                split = False  # the side stream must be joined on the capture stream after backward
             run = GraphedStep(step, warmup=cap_warm, stream=ddp_stream,
                               capture_error_mode="thread_local" if world > 1 else None, split=split)
             graph_note = "full (split: A / side B / A2)" if run.split else "full"
@@ -657,7 +667,8 @@ def main() -> int:
                 "hip_graph": graph_note,
                 "comm": comm_kind,
                 "grad_mode": args.grad_mode,
-                "surface": args.surface + (f" ({len(ddp_state.layouts)} DDP buckets)" if ddp_state else ""),
+                "surface": args.surface + (f" ({len(ddp_state.layouts)} DDP buckets, "
+                                           f"{'deferred' if ddp_state.defer else 'immediate'} hook)" if ddp_state else ""),
                 "bf16_weights": weights is not None,
                 "optimizer": f"{'FusedSGD' if args.optimizer == 'fused' else 'torch.optim.SGD'}(lr={0.01 * world:g}, momentum=0.5)",
             },

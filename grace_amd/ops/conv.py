@@ -261,7 +261,7 @@ class _Conv1x1AutoFn(torch.autograd.Function):
             be = _pick("wgrad", x, wt, dy, ctx.wshape)  # autotuned on the current stream, never on the side one
             # the engine's bucket view, written in place by the GEMM backends (MIOpen's own output
             # would need a copy kernel on the side stream's critical tail: left to the gather)
-            tgt = _wg.grad_target(ctx.weight) if be != "miopen" else None
+            tgt = _wg.grad_target(ctx.weight) if (be != "miopen" or _wg.must_alias(ctx.weight)) else None
             with f as side:  # wgrad off the critical path (ops/wgrad.py)
                 o2 = tgt.reshape(wt.shape) if tgt is not None else None
                 d = _wg.into_target(_as_param_layout(_run("wgrad", be, x, wt, dy, ctx.wshape, out=o2), ctx.weight), tgt)
@@ -602,7 +602,7 @@ class _Conv3x3Fn(torch.autograd.Function):
 
         def wg():
             be = _pick3("wgrad", x, w, dy, stride)  # autotuned on the current stream
-            tgt = _wg.grad_target(ctx.weight) if be != "miopen" else None
+            tgt = _wg.grad_target(ctx.weight) if (be != "miopen" or _wg.must_alias(ctx.weight)) else None
             with f as side:
                 d = _wg.into_target(_run3("wgrad", be, x, w, dy, stride, out=tgt), tgt)
                 if side:

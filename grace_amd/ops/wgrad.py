@@ -327,6 +327,14 @@ def grad_target(weight: torch.Tensor) -> Optional[torch.Tensor]:
     return v
 
 
+def must_alias(weight: torch.Tensor) -> bool:
+    """The gradient's consumer reads it mid-backward from the parameter's bucket view -- a DDP
+    reducer with the GRACE comm hook deferred (parallel/ddp_hook.py ``defer``): a side-stream
+    gradient must then be written INTO that view (the reducer finds an alias and copies
+    nothing), whatever produced it, library kernels included."""
+    return bool(getattr(weight, "_grace_alias_grad", False))
+
+
 def into_target(dw: torch.Tensor, tgt: Optional[torch.Tensor]) -> torch.Tensor:
     """dw written into tgt (if given; a no-op when dw already is tgt's memory), returned as a FRESH
     alias of tgt (no other reference: AccumulateGrad steals it instead of cloning)."""
@@ -459,6 +467,8 @@ class _ConvSplitFn(torch.autograd.Function):
             # once the dgrad chain is done); the engine's single gather launch copies these
             with f as side:
                 d = cb(dy, x, w, None, stride, padding, dilation, False, [0, 0], groups, [False, True, False])[1]
+                if must_alias(w):
+                    d = into_target(d, grad_target(w))
                 if side:
                     s = torch.cuda.current_stream(dy.device)
                     tag(dy, s)

@@ -31,15 +31,19 @@ from ..core import Communicator, register_layout
 from ..ops.layout import SegmentLayout
 
 
-def mark_ddp_params(params) -> None:
-    """Weight gradients of these parameters are computed in line (ops/wgrad.py): DDP's reducer
-    reads each gradient from its AccumulateGrad hook, during backward, on the current stream."""
+def mark_ddp_params(params, defer: bool = False) -> None:
+    """Immediate hook: weight gradients of these parameters are computed in line (ops/wgrad.py):
+    DDP's reducer reads each gradient from its AccumulateGrad hook, during backward, on the
+    current stream.  Deferred hook: they may run on the side stream, written INTO their bucket
+    views (the reducer then finds aliases and reads nothing); ``flush`` joins the side stream
+    before the exchange reads a bucket."""
     from ..ops import wgrad as _wg
 
     params = list(params)
     for p in params:
         p._grace_ddp = True
-    _wg.mark_joinable(params, on=False)
+        p._grace_alias_grad = bool(defer)
+    _wg.mark_joinable(params, on=bool(defer))
 
 
 # DDP-managed weight gradients stay in line.  Side-stream weight gradients for stable DDP buckets
@@ -49,15 +53,26 @@ def mark_ddp_params(params) -> None:
 
 
 class GraceHookState:
-    def __init__(self, grc: Communicator, name: str = "ddp", model: Optional[torch.nn.Module] = None):
+    def __init__(self, grc: Communicator, name: str = "ddp", model: Optional[torch.nn.Module] = None,
+                 defer: bool = False):
         """``model``: the DistributedDataParallel module the hook is registered on -- pass it so
         its parameters are marked before the first backward (otherwise they are marked by the
         hook's first call, and the first backward may compute weight gradients on a side stream
-        that the reducer does not wait for)."""
+        that the reducer does not wait for).
+
+        ``defer``: the hook hands DDP the bucket buffer itself as an already-completed result and
+        queues the bucket; :meth:`flush` (call it after ``backward()``, before the optimizer
+        step -- ``GraceDDPOptimizer`` does) runs the GRACE exchange of every queued bucket on the
+        current stream, decoding in place into the buffers the parameters' gradients alias.  No
+        overlap of the exchange with backward (as the engine without overlap), but weight
+        gradients may run on the side stream, and the step can be captured as a split graph
+        (parallel/graph.py): the first join is in ``flush``, on the capture stream."""
         self.grc = grc
         self.name = name
+        self.defer = bool(defer)
+        self.pending = []  # deferred buckets: (GradBucket buffer, GRACE name, packed index)
         if model is not None:
-            mark_ddp_params(model.parameters())
+            mark_ddp_params(model.parameters(), defer=self.defer)
         # bucket index -> (layout, packed index or None, buffer numel, GRACE name, param signature)
         self.layouts: Dict[int, tuple] = {}
         self.streams: Dict[int, Tuple[torch.cuda.Stream, torch.cuda.Stream]] = {}
@@ -74,7 +89,7 @@ class GraceHookState:
         buf = bucket.buffer()
         params = bucket.parameters()
         sig = tuple(id(p) for p in params)
-        mark_ddp_params(params)
+        mark_ddp_params(params, defer=self.defer)
         ent = self.layouts.get(idx)
         if ent is None or ent[2] != buf.numel() or ent[4] != sig:
             from ..ops.randomk import fnv1a64
@@ -140,6 +155,20 @@ class GraceHookState:
                 new.view(-1)[lay.offsets[i]:lay.offsets[i] + on].copy_(src.reshape(-1)[ooff:ooff + on])
         self.migrations += 1
 
+    def flush(self) -> None:
+        """Run the GRACE exchange of every deferred bucket, in backward order, on the current
+        stream: join the weight-gradient side stream, compress + collective + decode straight
+        into the bucket buffer (every parameter's gradient aliases it)."""
+        if not self.pending:
+            return
+        from ..ops import wgrad as _wg
+
+        pend, self.pending = self.pending, []
+        for buf, name, pidx in pend:
+            if buf.is_cuda:
+                _wg.join(torch.cuda.current_stream(buf.device))
+            _exchange_into(self.grc, buf, name, pidx)
+
     def _streams(self, dev):
         st = self.streams.get(dev.index)
         if st is None:
@@ -164,10 +193,35 @@ def _record(obj, stream, depth=0):
             _record(o, stream, depth + 1)
 
 
+def _exchange_into(grc: Communicator, buf: torch.Tensor, name: str, pidx) -> None:
+    """Synchronous GRACE step of one bucket on the current stream, result written into ``buf``."""
+    g = buf if (pidx is None and buf.dtype == torch.float32) else \
+        (buf.float() if pidx is None else buf.float().index_select(0, pidx))
+    handles, ctx = grc.send_step(g, name)
+    in_place = pidx is None and buf.dtype == torch.float32
+    if in_place and hasattr(ctx, "out"):
+        ctx.out = buf  # decode straight into the bucket (compress has consumed it)
+    out = grc.receive_step(handles, ctx).reshape(-1)
+    if pidx is None:
+        if out.data_ptr() != buf.data_ptr():
+            buf.copy_(out.view_as(buf))
+    else:
+        full = torch.zeros_like(buf)
+        full.index_copy_(0, pidx, out.to(buf.dtype))
+        buf.copy_(full)
+
+
 def grace_comm_hook(state: GraceHookState, bucket: dist.GradBucket) -> torch.futures.Future[torch.Tensor]:
     buf = bucket.buffer()
     name, pidx = state.layout_for(bucket)
     grc = state.grc
+    if state.defer:
+        # the exchange runs in state.flush(); DDP gets its own buffer back (no copy-back), which
+        # flush() then overwrites in place with the decoded gradient
+        state.pending.append((buf, name, pidx))
+        fut = torch.futures.Future(devices=[buf.device]) if buf.is_cuda else torch.futures.Future()
+        fut.set_result(buf)
+        return fut
 
     def packed(t):
         g = t if t.dtype == torch.float32 else t.float()
@@ -222,3 +276,37 @@ def grace_comm_hook(state: GraceHookState, bucket: dist.GradBucket) -> torch.fut
         g.record_stream(ds)
         fut.set_result(out)
     return fut
+
+
+class GraceDDPOptimizer:
+    """``optimizer`` whose ``step()`` first runs the deferred GRACE exchange of a
+    ``GraceHookState(defer=True)`` (``state.flush()``), then the wrapped optimizer's step.
+
+        ddp = DistributedDataParallel(model, gradient_as_bucket_view=True)
+        state = GraceHookState(grc, model=ddp, defer=True)
+        ddp.register_comm_hook(state, grace_comm_hook)
+        opt = GraceDDPOptimizer(torch.optim.SGD(ddp.parameters(), lr=0.1), state)
+    """
+
+    def __init__(self, optimizer, state: GraceHookState):
+        self.optimizer = optimizer
+        self.state = state
+
+    def step(self, closure=None):
+        self.state.flush()
+        return self.optimizer.step(closure) if closure is not None else self.optimizer.step()
+
+    def zero_grad(self, set_to_none: bool = True):
+        if self.state.pending:
+            raise AssertionError("zero_grad() with deferred GRACE buckets pending -- call step() first")
+        self.optimizer.zero_grad(set_to_none=set_to_none)
+
+    @property
+    def param_groups(self):
+        return self.optimizer.param_groups
+
+    def state_dict(self):
+        return self.optimizer.state_dict()
+
+    def load_state_dict(self, sd):
+        self.optimizer.load_state_dict(sd)

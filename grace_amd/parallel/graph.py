@@ -112,14 +112,16 @@ class GraphedStep:
         import os
 
         self.fn = fn
+        self._stream_arg = stream
         if capture_error_mode is None:
             capture_error_mode = "thread_local" if _nccl_group_up() else "global"
         # split: capture the critical stream and the weight-gradient side stream as separate
-        # linear graphs joined by external event nodes (ops/wgrad.py SplitCapture); the step must
-        # join the side stream only through the GRACE engine (no DDP reducer, no overlap stream)
+        # linear graphs joined by flag words / event nodes (ops/wgrad.py SplitCapture); the step
+        # must join the side stream only on the capture stream after backward: the GRACE engine
+        # without overlap, or DDP with the deferred comm hook (GraceHookState(defer=True))
         if split is None:
             split = os.environ.get("GRACE_GRAPH_SPLIT", "0") == "1"
-        self.split = bool(split) and stream is None
+        self.split = bool(split)
         # ``stream``: warm up, capture and replay on this stream.  Needed when long-lived autograd
         # nodes were created under it -- DDP's reducer keeps the parameters' AccumulateGrad nodes,
         # which run on the stream current at DDP's construction; a capture on any other stream
@@ -173,7 +175,10 @@ class GraphedStep:
         dev = torch.cuda.current_device()
         # GRACE_SPLIT_MAIN_PRIO=-1: the critical chain's queue outranks the side queue in the
         # command processor's dispatch arbitration
-        main = torch.cuda.Stream(dev, priority=int(os.environ.get("GRACE_SPLIT_MAIN_PRIO", "0")))
+        # the caller's stream when given (DDP: the reducer's AccumulateGrad nodes run on the stream
+        # the model was wrapped under)
+        main = self._stream_arg if self._stream_arg is not None else \
+            torch.cuda.Stream(dev, priority=int(os.environ.get("GRACE_SPLIT_MAIN_PRIO", "0")))
         side = _wg._side(torch.device("cuda", dev))
         ga, gb, ga2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         open_ = {"a": False, "b": False, "a2": False}

@@ -223,15 +223,16 @@ def _ddp_net(seed=0):
                          nn.Linear(16, 4), nn.ReLU(), nn.Linear(4, 3))
 
 
-def _ddp_value_body(rank, world, params, kind):
+def _ddp_value_body(rank, world, params, kind, defer=False):
     """DDP comm hook == the reference's per-parameter loop ``grc.step(p.grad, name)``
-    (examples/dist/CIFAR10-dawndist/core.py:203-206) on the same gradients, 3 steps with memory."""
+    (examples/dist/CIFAR10-dawndist/core.py:203-206) on the same gradients, 3 steps with memory.
+    ``defer``: the hook queues each bucket and ``flush()`` runs the exchanges after backward."""
     from grace_amd import grace_from_params
     from grace_amd.parallel import GraceHookState, grace_comm_hook
 
     m = _ddp_net()
-    ddp = nn.parallel.DistributedDataParallel(m, bucket_cap_mb=0.0002)  # several buckets
-    st = GraceHookState(grace_from_params(dict(params, world_size=world)))
+    ddp = nn.parallel.DistributedDataParallel(m, bucket_cap_mb=0.0002, gradient_as_bucket_view=defer)
+    st = GraceHookState(grace_from_params(dict(params, world_size=world)), model=ddp, defer=defer)
     ddp.register_comm_hook(st, grace_comm_hook)
     ref = _ddp_net()
     grc_ref = grace_from_params(dict(params, world_size=world))
@@ -242,6 +243,10 @@ def _ddp_value_body(rank, world, params, kind):
         for p in ddp.parameters():
             p.grad = None
         F.cross_entropy(ddp(x), y).backward()
+        if defer:
+            assert len(st.pending) >= (1 if s == 0 else 2), (s, len(st.pending))  # queued, not yet exchanged
+            st.flush()
+            assert not st.pending
         ref.zero_grad()
         F.cross_entropy(ref(x), y).backward()
         exp = [grc_ref.step(p.grad.clone(), n) for n, p in named]  # per-parameter loop (reverse not needed)
@@ -277,6 +282,16 @@ def _ddp_value_body(rank, world, params, kind):
 @pytest.mark.parametrize("world", [2, 3])
 def test_ddp_hook_matches_per_parameter_loop_gloo(params, kind, world):
     run_distributed(_ddp_value_body, world, params, kind)
+
+
+@pytest.mark.parametrize("params,kind", [
+    ({"compressor": "topk", "compress_ratio": 0.3, "memory": "residual", "communicator": "allgather"}, "exact"),
+    ({"compressor": "powersgd", "compress_rank": 4, "memory": "powersgd", "communicator": "allreduce"}, "lowrank"),
+])
+def test_deferred_ddp_hook_matches_per_parameter_loop_gloo(params, kind):
+    """GraceHookState(defer=True): same gradients as the immediate hook / the per-parameter loop,
+    with every bucket's exchange run by flush() after backward (gradient_as_bucket_view)."""
+    run_distributed(_ddp_value_body, 2, params, kind, True)
 
 
 def test_ddp_hook_padded_bucket_keeps_per_parameter_layout():

@@ -295,48 +295,51 @@ def _split_net(seed=0):
                          nn.AdaptiveAvgPool2d(1), nn.Flatten(), nn.Linear(32, 10)).cuda()
 
 
-@pytest.mark.parametrize("batch_copy", [False, True])
-def test_ddp_hook_split_grad_convs_match_plain_model(nccl_group, batch_copy):
-    """DDP + hook over split-gradient convs (ops/wgrad.py): the reducer reads gradients mid-backward,
-    so DDP-managed weights compute their gradients in line, and (gradient_as_bucket_view) straight
-    into the bucket once the hook has seen it -- gradients equal a plain model's, every step."""
+@pytest.mark.parametrize("defer", [False, True])
+def test_ddp_hook_split_grad_convs_match_plain_model(nccl_group, defer):
+    """DDP + hook over split-gradient convs (ops/wgrad.py).  Immediate hook: the reducer reads
+    gradients mid-backward, so DDP-managed weights compute their gradients in line, and
+    (gradient_as_bucket_view) straight into the bucket once the hook has seen it.  Deferred hook
+    (GraceHookState(defer=True)): weight gradients run on the side stream, written INTO the bucket
+    views (library kernels included), and flush() joins before the exchange.  Either way the
+    gradients equal a plain model's, every step."""
     from grace_amd import grace_from_params
     from grace_amd.parallel import GraceHookState, grace_comm_hook
 
     m, ref = _split_net(), _split_net()
     ddp = nn.parallel.DistributedDataParallel(m, device_ids=[0], gradient_as_bucket_view=True,
                                               broadcast_buffers=False)
-    ddp.register_comm_hook(GraceHookState(grace_from_params({"compressor": "none", "communicator": "allreduce"}),
-                                          model=ddp), grace_comm_hook)
-    from grace_amd.ops import wgrad as _wg
-
-    old_batch = _wg._DDP_BATCH
-    _wg._DDP_BATCH = batch_copy
+    st = GraceHookState(grace_from_params({"compressor": "none", "communicator": "allreduce"}), model=ddp,
+                        defer=defer)
+    ddp.register_comm_hook(st, grace_comm_hook)
     g = torch.Generator().manual_seed(3)
-    for step in range(6):  # steps >= 3: MIOpen weight gradients take the batched-copy path when on
+    for step in range(6):
         x = torch.randn(16, 3, 24, 24, generator=g).cuda()
         y = torch.randint(0, 10, (16,), generator=g).cuda()
         for p in list(m.parameters()) + list(ref.parameters()):
             p.grad = None
         F.cross_entropy(ddp(x), y).backward()
+        st.flush()
         F.cross_entropy(ref(x), y).backward()
         torch.cuda.synchronize()
         for a, b in zip(m.parameters(), ref.parameters()):
             assert a._grace_ddp
             tol = 1e-4 * float(b.grad.abs().max()) + 1e-6
             assert float((a.grad - b.grad).abs().max()) <= tol, step
-    _wg._DDP_BATCH = old_batch
     conv_w = [mod.weight for mod in m if hasattr(mod, "kernel_size")]
     for w in conv_w:  # the gradient IS the bucket view the hook marked (no reducer copy)
         assert w._grace_grad_view.data_ptr() == w.grad.data_ptr()
 
 
-def test_ddp_hook_graph_capture(nccl_group):
+@pytest.mark.parametrize("mode", ["immediate", "deferred", "deferred-split"])
+def test_ddp_hook_graph_capture(nccl_group, mode):
     """A whole DDP step (forward, backward with the comm hook, optimizer) captured in a HIP graph:
     DDP is built under the capture stream (its AccumulateGrad nodes run there) and warmed up past
-    its runtime-logging iterations; replays equal the same steps run eagerly."""
+    its runtime-logging iterations; replays equal the same steps run eagerly.  ``deferred``: the
+    hook queues the buckets and GraceDDPOptimizer.step() flushes them (weight gradients forked
+    onto the side stream); ``deferred-split``: that step captured as split graphs."""
     from grace_amd import grace_from_params
-    from grace_amd.parallel import GraceHookState, grace_comm_hook
+    from grace_amd.parallel import GraceDDPOptimizer, GraceHookState, grace_comm_hook
     from grace_amd.parallel.graph import GraphedStep
 
     g = torch.Generator().manual_seed(5)
@@ -349,9 +352,10 @@ def test_ddp_hook_graph_capture(nccl_group):
         with torch.cuda.stream(s):
             ddp = nn.parallel.DistributedDataParallel(m, device_ids=[0], gradient_as_bucket_view=True,
                                                       broadcast_buffers=False)
-        ddp.register_comm_hook(GraceHookState(grace_from_params({"compressor": "none", "communicator": "allreduce"}),
-                                              model=ddp), grace_comm_hook)
-        opt = torch.optim.SGD(m.parameters(), lr=0.05, momentum=0.5)
+        st = GraceHookState(grace_from_params({"compressor": "none", "communicator": "allreduce"}), model=ddp,
+                            defer=mode != "immediate")
+        ddp.register_comm_hook(st, grace_comm_hook)
+        opt = GraceDDPOptimizer(torch.optim.SGD(m.parameters(), lr=0.05, momentum=0.5), st)
 
         def step():
             opt.zero_grad(set_to_none=True)
@@ -361,7 +365,10 @@ def test_ddp_hook_graph_capture(nccl_group):
             return loss
 
         if graphed:
-            run = GraphedStep(step, warmup=11, stream=s)  # DDP logs runtime stats in its first 10 steps
+            # DDP logs runtime stats in its first 10 steps
+            run = GraphedStep(step, warmup=11, stream=s, split=mode == "deferred-split")
+            if mode == "deferred-split":
+                assert run.g_side is not None and run.g_a2 is not None
             for _ in range(4):
                 run()
         else:
@@ -370,8 +377,10 @@ def test_ddp_hook_graph_capture(nccl_group):
                     step()
         torch.cuda.synchronize()
         finals.append([p.detach().clone() for p in m.parameters()])
-    for a, b in zip(*finals):
-        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
+    for i, (a, b) in enumerate(zip(*finals)):
+        err = float((a - b).abs().max())
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5,
+                                   msg=f"{mode}: parameter {i} {tuple(a.shape)} max abs err {err:.3g}")
 
 
 def _masked_reference(recorded):
