@@ -129,6 +129,9 @@ class SplitCapture:
         self.side = side
         self.on_split = on_split   # ends the A / B captures, begins A2 on ``main``
         self.sync = sync
+        # one flag per 2 fork points: 2601 -> 2684-2689 img/s (every 3: 2680, 4: 2652, 8: 2662, 13: 2627,
+        # 27: 2565; DDP 2558 -> 2649 at 2), profiles/r6_graph_split.txt
+        self.every = max(1, int(os.environ.get("GRACE_SPLIT_SYNC_EVERY", "2")))
         self.spin_limit = int(spin_limit)
         self.events = []           # fork-point tokens (ExtEvents stay alive as long as the graphs)
         self.split_done = False
@@ -152,7 +155,11 @@ class SplitCapture:
             self._lib.xs_bump(self.gen[1:2], self.side.cuda_stream)
 
     def signal(self, stream: "torch.cuda.Stream"):
-        """Fork point on the critical stream: side work issued after ``wait(token)`` may start."""
+        """Fork point on the critical stream: side work issued after ``wait(token)`` may start.
+        Flag sync with ``every = k > 1``: one flag per group of k fork points, published at the
+        group's LAST fork (every dy of the group is ready by then); the side stream waits once,
+        at the group's first fork -- k times fewer kernels on the critical chain, the side work
+        starting up to k - 1 layers later."""
         i = len(self.events)
         if self.sync == "events":
             tok = self._lib.ExtEvent(self.idx)
@@ -160,23 +167,31 @@ class SplitCapture:
         else:
             if i >= self.MAX_FORKS:
                 raise RuntimeError(f"split capture: more than {self.MAX_FORKS} fork points")
-            self._lib.xs_signal(self.flags, i, self.gen[0:1], stream.cuda_stream, self.times)
             tok = i
+            if i % self.every == self.every - 1:
+                self._lib.xs_signal(self.flags, i // self.every, self.gen[0:1], stream.cuda_stream, self.times)
         self.events.append(tok)
         return tok
 
     def wait(self, tok, stream: "torch.cuda.Stream") -> None:
         if self.sync == "events":
             tok.wait(stream.cuda_stream)
-        else:
-            self._lib.xs_wait(self.flags, tok, self.gen[1:2], self.spin_limit, stream.cuda_stream, self.times)
+        elif tok % self.every == 0:  # later forks of the group: already behind that wait
+            self._lib.xs_wait(self.flags, tok // self.every, self.gen[1:2], self.spin_limit, stream.cuda_stream,
+                              self.times)
+
+    def close_group(self) -> None:
+        """Before the critical stream's graph ends: publish a partly filled last group."""
+        n = len(self.events)
+        if self.sync == "flags" and n % self.every:
+            self._lib.xs_signal(self.flags, n // self.every, self.gen[0:1], self.main.cuda_stream, self.times)
 
     def timeline(self):
         """[(fork, A signalled (us, from fork 0), B's wait returned (us), B lag (us))] of the last
         replay (GRACE_SPLIT_TRACE=1; the device clock runs at 100 MHz)."""
         if self.times is None:
             return []
-        n = len(self.events)
+        n = -(-len(self.events) // self.every)
         t = self.times[: 2 * n].view(n, 2).cpu().tolist()
         base = t[0][0]
         return [(i, (a - base) / 100.0, (b - base) / 100.0, (b - a) / 100.0) for i, (a, b) in enumerate(t)]
@@ -184,6 +199,7 @@ class SplitCapture:
     def split(self):
         if not self.split_done:
             self.split_done = True
+            self.close_group()
             self.on_split()
 
 

@@ -218,6 +218,7 @@ class GraphedStep:
             if open_["a2"]:
                 end(ga2, main, "a2")
             else:  # no join on the critical stream: A and B only
+                sc.close_group()
                 end(gb, side, "b")
                 end(ga, main, "a")
         except BaseException:
@@ -241,21 +242,19 @@ class GraphedStep:
         self.stream = None
 
     def _replay_split(self) -> torch.Tensor:
+        # a graph is not bound to its capture stream: A and A2 replay on the caller's stream (two
+        # cross-stream joins per step instead of four), B on the side stream
         cur = torch.cuda.current_stream()
-        main, side = self.s_main, self.s_side
-        main.wait_stream(cur)
+        side = self.s_side
         if self.g_side is not None:
-            side.wait_stream(cur)
-        with torch.cuda.stream(main):
-            self.graphs[0].replay()
+            side.wait_stream(cur)  # after the previous step's A2
+        self.graphs[0].replay()
         if self.g_side is not None:
             with torch.cuda.stream(side):
                 self.g_side.replay()
-            main.wait_stream(side)
+            cur.wait_stream(side)
         if self.g_a2 is not None:
-            with torch.cuda.stream(main):
-                self.g_a2.replay()
-        cur.wait_stream(main)
+            self.g_a2.replay()
         if _SYNC_EACH:
             torch.cuda.synchronize()
         return self.loss
