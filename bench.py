@@ -137,9 +137,9 @@ def parse():
                          "off = RCCL's default; 'MIN/MAX' = fixed")
     ap.add_argument("--graph-split", choices=["auto", "on", "off"], default="auto",
                     help="whole-step graph as two LINEAR graphs (critical stream / weight-gradient side stream, "
-                         "external event nodes between them) plus the post-join graph, instead of one forked "
-                         "graph (parallel/graph.py GraphedStep split); engine surface without overlap only; "
-                         "auto = GRACE_GRAPH_SPLIT")
+                         "flag-word sync between them) plus the post-join graph, instead of one forked graph "
+                         "(parallel/graph.py GraphedStep split): ~0.3 ms of host issue per step instead of ~9; "
+                         "auto = on (engine without overlap, DDP with the deferred hook)")
     ap.add_argument("--ddp-defer", choices=["auto", "on", "off"], default="auto",
                     help="--surface ddp: the GRACE comm hook hands DDP its bucket back and runs the exchange "
                          "after backward (GraceHookState(defer=True)): DDP-managed weight gradients may then run "
@@ -484,9 +484,10 @@ def main() -> int:
             # first 10 iterations: capture only after those
             cap_warm = max(3, args.warmup // 2) if args.surface == "engine" else max(11, args.warmup)
             split = None if args.graph_split == "auto" else args.graph_split == "on"
-            if split is None and args.surface == "ddp" and ddp_state.defer:
-                # the DDP step as ONE forked graph is host-bound (11.0 ms of issue per 13.6 ms step,
-                # 2352 img/s) -- split graphs: 2558 img/s at 0.27 ms of issue (profiles/r6_ddp_deferred.txt)
+            if split is None:
+                # split graphs (critical / side stream, flag sync every 2 fork points): 2720 img/s at
+                # 0.28 ms of host issue vs the forked graph's 2708 at 9.2 ms; DDP 2690 (forked: 2352,
+                # host-bound); W = 2 sharing one GPU 3104 vs 2463 (profiles/r6_graph_split.txt)
                 split = True
             if overlap or (args.surface == "ddp" and not ddp_state.defer):
                 split = False  # the side stream must be joined on the capture stream after backward
