@@ -40,6 +40,9 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 _ENABLED = os.environ.get("GRACE_WGRAD_STREAM", "1") == "1"
+# debug / race detector: a spin of this many GPU cycles at every fork on the side stream, so any
+# consumer that reads a side-stream weight gradient without joining reads a stale one
+_SIDE_DELAY = int(os.environ.get("GRACE_WGRAD_SIDE_DELAY", "0"))
 _streams: Dict[int, "torch.cuda.Stream"] = {}
 _pending: Dict[int, bool] = {}  # device -> side work issued since the last join
 _lock = threading.Lock()
@@ -279,7 +282,10 @@ class fork:
         # clears the tag: the reducer reads it from its AccumulateGrad hook, mid-backward).
         self.sc = None
         if (_ENABLED and t.is_cuda and param is not None and param.grad is None and joinable(param)
-                and fork_selected(t, param)):
+                and fork_selected(t, param) and (not must_alias(param) or grad_target(param) is not None)):
+            # (a gradient its consumer reads mid-backward from a bucket view -- the deferred DDP
+            # hook's reducer -- may leave the critical stream only once that view is known and
+            # stable: the side stream then writes INTO it and the reducer reads nothing)
             sc = _split.get(t.device.index)
             if sc is not None and sc.split_done:
                 return  # after the split's join (A2): nothing may fork any more, stay in line
@@ -304,6 +310,8 @@ class fork:
             side.wait_event(self.ev)
         self.ctx = torch.cuda.stream(side)
         self.ctx.__enter__()
+        if _SIDE_DELAY:  # race detector: the side stream lags far behind the critical stream
+            torch.cuda._sleep(_SIDE_DELAY)
         idx = t.device.index
         if self.sc is not None:  # the split's join (``join`` on the critical stream) ends it
             _pending[idx] = True
@@ -339,6 +347,10 @@ def grad_target(weight: torch.Tensor) -> Optional[torch.Tensor]:
         return None
     v = getattr(weight, "_grace_grad_view", None)
     if v is None or weight.grad is not None or v.dtype != weight.dtype or v.device != weight.device:
+        return None
+    if must_alias(weight) and not getattr(weight, "_grace_view_stable", False):
+        # a DDP bucket view seen on only one hook call may be replaced by DDP's bucket rebuild
+        # (after the first iteration): the reducer would then find no alias and copy mid-backward
         return None
     return v
 

@@ -82,6 +82,7 @@ class GraceHookState:
         self._loc: Dict[int, Tuple[str, int, int, int]] = {}
         self._gen: Dict[int, int] = {}
         self._views: Dict[int, int] = {}  # bucket index -> buffer address its gradient targets point into
+        self._stable = set()  # bucket indices whose buffer was seen unchanged on consecutive calls
 
     def layout_for(self, bucket) -> Tuple[str, Optional[torch.Tensor]]:
         """(registered layout name, None | int64 index of the packed elements in the buffer)."""
@@ -113,7 +114,18 @@ class GraceHookState:
             self._migrate(key, params, lay)
             ent = (lay, pidx, buf.numel(), key, sig)
             self.layouts[idx] = ent
-        if self._views.get(idx) != buf.data_ptr():  # new layout, or DDP rebuilt the same one
+        if self._views.get(idx) == buf.data_ptr():
+            if idx not in self._stable:
+                # the same bucket buffer on two consecutive calls: DDP's one-time bucket rebuild
+                # (after the first iteration) is behind us and the marked views stay valid -- from
+                # now on side-stream weight gradients may be written into them (deferred hook)
+                self._stable.add(idx)
+                for p in params:
+                    p._grace_view_stable = True
+        else:  # new layout, or DDP rebuilt the same one
+            self._stable.discard(idx)
+            for p in params:
+                p._grace_view_stable = False
             self._views[idx] = buf.data_ptr()
             # with gradient_as_bucket_view DDP makes each .grad a view of the bucket: mark those
             # views as the parameters' gradient targets, so weight-gradient producers

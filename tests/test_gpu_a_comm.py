@@ -295,8 +295,21 @@ def _split_net(seed=0):
                          nn.AdaptiveAvgPool2d(1), nn.Flatten(), nn.Linear(32, 10)).cuda()
 
 
+@pytest.fixture
+def side_delay(request):
+    """Race detector: every side-stream fork first spins ~0.1 ms (ops/wgrad.py _SIDE_DELAY), so a
+    consumer that reads a side-stream weight gradient without joining reads a stale one."""
+    from grace_amd.ops import wgrad as _wg
+
+    old = _wg._SIDE_DELAY
+    _wg._SIDE_DELAY = getattr(request, "param", 0)
+    yield _wg._SIDE_DELAY
+    _wg._SIDE_DELAY = old
+
+
+@pytest.mark.parametrize("side_delay", [0, 200000], indirect=True)
 @pytest.mark.parametrize("defer", [False, True])
-def test_ddp_hook_split_grad_convs_match_plain_model(nccl_group, defer):
+def test_ddp_hook_split_grad_convs_match_plain_model(nccl_group, defer, side_delay):
     """DDP + hook over split-gradient convs (ops/wgrad.py).  Immediate hook: the reducer reads
     gradients mid-backward, so DDP-managed weights compute their gradients in line, and
     (gradient_as_bucket_view) straight into the bucket once the hook has seen it.  Deferred hook
@@ -331,8 +344,9 @@ def test_ddp_hook_split_grad_convs_match_plain_model(nccl_group, defer):
         assert w._grace_grad_view.data_ptr() == w.grad.data_ptr()
 
 
+@pytest.mark.parametrize("side_delay", [0, 200000], indirect=True)
 @pytest.mark.parametrize("mode", ["immediate", "deferred", "deferred-split"])
-def test_ddp_hook_graph_capture(nccl_group, mode):
+def test_ddp_hook_graph_capture(nccl_group, mode, side_delay):
     """A whole DDP step (forward, backward with the comm hook, optimizer) captured in a HIP graph:
     DDP is built under the capture stream (its AccumulateGrad nodes run there) and warmed up past
     its runtime-logging iterations; replays equal the same steps run eagerly.  ``deferred``: the

@@ -94,12 +94,15 @@ def test_side_stream_grads_equal_inline():
             _close(a, b, msg=n)
 
 
+@pytest.mark.parametrize("delay", [0, 200000])
 @pytest.mark.parametrize("split", [False, True])
-def test_engine_graph_with_side_stream_wgrad(bn_deterministic, split):
+def test_engine_graph_with_side_stream_wgrad(bn_deterministic, split, delay, monkeypatch):
     """an engine step captured in a whole-step graph with the wgrad forks (parallel graph
     branches, joined before the bucket gather) matches the eager steps (parameters after 4 steps);
-    split=True: captured as two linear graphs (critical / side stream) joined by external event
-    nodes plus the post-join graph (parallel/graph.py GraphedStep split)"""
+    split=True: captured as two linear graphs (critical / side stream) joined by flag words plus
+    the post-join graph (parallel/graph.py GraphedStep split); delay > 0: the race detector (every
+    fork spins first on the side stream, so a missing join reads stale gradients)"""
+    monkeypatch.setattr(wgrad, "_SIDE_DELAY", delay)
     from grace_amd import grace_from_params
     from grace_amd.parallel import DistributedOptimizer, FusedSGD
     from grace_amd.parallel.graph import GraphedStep
