@@ -140,6 +140,11 @@ def parse():
                          "flag-word sync between them) plus the post-join graph, instead of one forked graph "
                          "(parallel/graph.py GraphedStep split): ~0.3 ms of host issue per step instead of ~9; "
                          "auto = on (engine without overlap, DDP with the deferred hook)")
+    ap.add_argument("--tail-bucket", choices=["on", "off"], default="off",
+                    help="engine: the first layer's weight (its gradient is the last one backward produces) in a "
+                         "bucket of its own, exchanged last -- under split graphs the other buckets' exchange "
+                         "overlaps that weight gradient on the side stream (measured neutral: the Top-K "
+                         "histogram and the stem's weight-gradient GEMM contend, profiles/r6_graph_split.txt)")
     ap.add_argument("--ddp-defer", choices=["auto", "on", "off"], default="auto",
                     help="--surface ddp: the GRACE comm hook hands DDP its bucket back and runs the exchange "
                          "after backward (GraceHookState(defer=True)): DDP-managed weight gradients may then run "
@@ -171,7 +176,7 @@ def _grace_split(args, run, opt, base_opt, named, weights, w, model, data, amp, 
     noop = DistributedOptimizer(base_opt, grace_from_params({"compressor": "none", "communicator": "allreduce"},
                                                             comm=LocalComm()),
                                 named_parameters=named, bucket_cap_mb=args.bucket_mb, overlap=False,
-                                weights=weights)
+                                weights=weights, tail_bucket=args.tail_bucket == "on")
 
     def noop_step():
         noop.zero_grad(set_to_none=set_to_none)
@@ -456,7 +461,8 @@ def main() -> int:
         opt = _DdpOpt()
     else:
         opt = DistributedOptimizer(base_opt, grc, named_parameters=named,
-                                   bucket_cap_mb=args.bucket_mb, overlap=overlap, weights=weights)
+                                   bucket_cap_mb=args.bucket_mb, overlap=overlap, weights=weights,
+                                   tail_bucket=args.tail_bucket == "on")
     data = w.make_batch(batch, dev)
     if w.channels_last and isinstance(data, tuple) and data[0].dim() == 4:
         data = (data[0].contiguous(memory_format=torch.channels_last),) + tuple(data[1:])
@@ -560,7 +566,7 @@ def main() -> int:
     step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
     if os.environ.get("GRACE_SPLIT_TRACE", "0") == "1" and getattr(run, "split", False):
         for row in run._sc.timeline():  # (fork, A signalled us, B's wait returned us, lag us)
-            print("[split-trace] fork %3d  A %9.1f  B %9.1f  lag %8.1f" % row, file=sys.stderr)
+            print("[split-trace] fork %3s  A %9.1f  B %9.1f  lag %8.1f" % row, file=sys.stderr)
     if rec is not None:
         print("[bench] losses " + " ".join(f"{v:.4f}" for v in rec.tolist()), file=sys.stderr, flush=True)
     final_loss = float(loss.float().item())
@@ -663,6 +669,7 @@ def main() -> int:
                 if dist.is_initialized() else "none (W=1, no process group: local comm)",
                 "grace": w.grace,
                 "bucket_mb": args.bucket_mb,
+                "buckets": len(opt.engine.buckets) if hasattr(opt.engine, "buckets") else None,
                 "overlap": overlap,
                 **({"overlap_rule": overlap_note} if overlap_note else {}),
                 "hip_graph": graph_note,

@@ -141,6 +141,13 @@ class SplitCapture:
         self._lib = _native.lib()
         dev = torch.device("cuda", device_idx)
         self.flags = torch.zeros(self.MAX_FORKS, dtype=torch.int64, device=dev)
+        # the side stream's PROGRESS: bflags[g] = B's generation once every weight gradient of
+        # fork group g is done -- the post-join graph A2 waits on these per bucket instead of on
+        # the whole side graph (``wait_params``), so one bucket's exchange overlaps the last
+        # group's weight gradients
+        self.bflags = torch.zeros(self.MAX_FORKS, dtype=torch.int64, device=dev)
+        self.group_of = {}     # id(param) -> fork group of its weight gradient
+        self.waited = -1       # highest progress group A2 already waited for
         self.gen = torch.zeros(2, dtype=torch.int64, device=dev)  # [A's generation, B's generation]
         # GRACE_SPLIT_TRACE=1: per fork point, the device clock when A signalled it and when B's
         # wait returned (``timeline()``): the two graphs' overlap without a profiler
@@ -176,12 +183,39 @@ class SplitCapture:
         self.events.append(tok)
         return tok
 
-    def wait(self, tok, stream: "torch.cuda.Stream") -> None:
+    def wait(self, tok, stream: "torch.cuda.Stream", param=None) -> None:
+        if param is not None and self.sync == "flags":
+            self.group_of[id(param)] = tok // self.every
         if self.sync == "events":
             tok.wait(stream.cuda_stream)
         elif tok % self.every == 0:  # later forks of the group: already behind that wait
+            if tok:  # everything of the previous group is enqueued on B: its progress flag
+                self._lib.xs_signal(self.bflags, tok // self.every - 1, self.gen[1:2], stream.cuda_stream, None)
             self._lib.xs_wait(self.flags, tok // self.every, self.gen[1:2], self.spin_limit, stream.cuda_stream,
                               self.times)
+
+    def close_progress(self) -> None:
+        """Before the side graph ends: the last group's progress flag."""
+        n = len(self.events)
+        if self.sync == "flags" and n:
+            self._lib.xs_signal(self.bflags, (n - 1) // self.every, self.gen[1:2], self.side.cuda_stream, None)
+
+    def n_groups(self) -> int:
+        return -(-len(self.events) // self.every) if self.sync == "flags" else len(self.events)
+
+    def wait_params(self, params, stream: "torch.cuda.Stream") -> None:
+        """In A2: wait until the side stream finished the weight gradients of ``params`` (all
+        groups up to the latest one holding any of them; ``params=None``: all of them)."""
+        if self.sync != "flags":
+            raise RuntimeError("per-bucket waits need the flag sync")
+        if params is None:
+            g = self.n_groups() - 1
+        else:
+            gs = [self.group_of[id(p)] for p in params if id(p) in self.group_of]
+            g = max(gs) if gs else -1
+        if g > self.waited:  # progress is monotone: one wait covers every earlier group
+            self._lib.xs_wait(self.bflags, g, self.gen[0:1], self.spin_limit, stream.cuda_stream, None)
+            self.waited = g
 
     def close_group(self) -> None:
         """Before the critical stream's graph ends: publish a partly filled last group."""
@@ -197,12 +231,28 @@ class SplitCapture:
         n = -(-len(self.events) // self.every)
         t = self.times[: 2 * n].view(n, 2).cpu().tolist()
         base = t[0][0]
-        return [(i, (a - base) / 100.0, (b - base) / 100.0, (b - a) / 100.0) for i, (a, b) in enumerate(t)]
+        rows = [(i, (a - base) / 100.0, (b - base) / 100.0, (b - a) / 100.0) for i, (a, b) in enumerate(t)]
+        # markers (when recorded): the side graph's end and the post-join graph's start
+        m = self.times[2 * (self.MAX_FORKS - 2):].view(2, 2)[:, 0].cpu().tolist()
+        if m[0] and m[1]:
+            rows.append(("B end / A2 start", (m[0] - base) / 100.0, (m[1] - base) / 100.0, (m[1] - m[0]) / 100.0))
+        return rows
+
+    def mark(self, which: str) -> None:
+        """GRACE_SPLIT_TRACE: device-clock marker at the side graph's end ("b_end", on the side
+        stream) or the post-join graph's start ("a2_start", on the critical stream)."""
+        if self.times is None or self.sync != "flags":
+            return
+        idx, st = (self.MAX_FORKS - 2, self.side) if which == "b_end" else (self.MAX_FORKS - 1, self.main)
+        self._lib.xs_signal(self.flags, idx, self.gen[0:1], st.cuda_stream, self.times)
 
     def split(self):
         if not self.split_done:
             self.split_done = True
             self.close_group()
+            if self.sync == "flags":
+                with torch.cuda.stream(self.side):
+                    self.close_progress()
             self.on_split()
 
 
@@ -268,6 +318,7 @@ class fork:
 
     def __init__(self, t: torch.Tensor, param: Optional[torch.Tensor] = None):
         self.t = t
+        self.param = param
         self.ctx = None
         self.main = None
         self.ev = None
@@ -305,7 +356,7 @@ class fork:
         t = self.t
         side = _side(t.device)
         if self.sc is not None:
-            self.sc.wait(self.ev, side)
+            self.sc.wait(self.ev, side, self.param)
         else:
             side.wait_event(self.ev)
         self.ctx = torch.cuda.stream(side)
@@ -379,9 +430,27 @@ def tag(t: Optional[torch.Tensor], stream: "torch.cuda.Stream") -> None:
         t.record_stream(stream)
 
 
-def join(stream: Optional["torch.cuda.Stream"] = None, device=None) -> None:
+def join(stream: Optional["torch.cuda.Stream"] = None, device=None, params=None) -> None:
     """Make ``stream`` (default: the current stream) wait for every side-stream wgrad issued so
-    far."""
+    far.  In a split capture the first join on the capture stream ends graphs A and B; from
+    then on (graph A2) a join is a device-side wait for the side stream's progress -- of the
+    weight gradients of ``params`` only, when given (the engine's per-bucket launch)."""
+    if _split:
+        idx = (stream.device.index if stream is not None else
+               (torch.device(device).index if device is not None and not isinstance(device, int) else
+                device if device is not None else torch.cuda.current_device()))
+        sc = _split.get(idx)
+        if sc is not None and (sc.split_done or _pending.get(idx)):
+            cur = stream if stream is not None else torch.cuda.current_stream(idx)
+            if cur.cuda_stream != sc.main.cuda_stream:
+                raise RuntimeError("split capture: side-stream weight gradients must be joined on the capture "
+                                   "stream (the engine's bucket launch; no overlap stream, no DDP reducer)")
+            if not sc.split_done:
+                sc.split()  # ends graphs A and B, A2 captures from here
+                _pending[idx] = False
+            if sc.events and sc.sync == "flags":
+                sc.wait_params(params, cur)
+            return
     if not _pending:
         return
     if stream is not None:
@@ -391,17 +460,6 @@ def join(stream: Optional["torch.cuda.Stream"] = None, device=None) -> None:
     else:
         devs = [torch.cuda.current_device()]
     for idx in devs:
-        sc = _split.get(idx)
-        if sc is not None and not sc.split_done:
-            if not _pending.get(idx):
-                continue
-            cur = stream if stream is not None else torch.cuda.current_stream(idx)
-            if cur.cuda_stream != sc.main.cuda_stream:
-                raise RuntimeError("split capture: side-stream weight gradients must be joined on the capture "
-                                   "stream (the engine's bucket launch; no overlap stream, no DDP reducer)")
-            sc.split()  # ends graphs A and B, A2 captures from here; the replay joins B into A2
-            _pending[idx] = False
-            continue
         if _pending.get(idx):
             tgt = stream if stream is not None else torch.cuda.current_stream(idx)
             tgt.wait_stream(_streams[idx])

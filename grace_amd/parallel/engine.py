@@ -100,7 +100,12 @@ class GraceEngine:
                  bucket_cap_mb: float = 64.0, backward_passes_per_step: int = 1, overlap: bool = True,
                  sparse_params: Sequence[str] = (), debug: Optional[bool] = None,
                  grad_sources: Optional[Dict[int, torch.Tensor]] = None,
-                 group_collectives: Optional[bool] = None, watchdog=None):
+                 group_collectives: Optional[bool] = None, watchdog=None, tail_bucket: bool = False):
+        """``tail_bucket``: the model's first layer weight (its weight gradient is the LAST one
+        backward produces -- e.g. ResNet's 7x7 stem on the side stream) gets a bucket of its own,
+        exchanged last: under a split-graph capture the other buckets' exchange then overlaps that
+        weight gradient (each bucket launch waits only for the side-stream work of its own
+        parameters).  Per-tensor codecs give identical results with any bucketing."""
         from ..utils import debug as _dbg
         from .comm import GroupedComm
 
@@ -152,7 +157,8 @@ class GraceEngine:
         groups: List[List[Tuple[str, torch.nn.Parameter]]] = []
         cur: List[Tuple[str, torch.nn.Parameter]] = []
         size = 0
-        for n, p in reversed(named):  # backward order
+        tail = named[:1] if (tail_bucket and named[0][1].dim() == 4 and len(named) > 1) else []
+        for n, p in reversed(named[len(tail):]):  # backward order
             if cur and size + p.numel() > cap:
                 groups.append(cur)
                 cur, size = [], 0
@@ -160,6 +166,8 @@ class GraceEngine:
             size += p.numel()
         if cur:
             groups.append(cur)
+        if tail:
+            groups.append(tail)
         # deterministic bucket names (same on every rank and across restarts, so GRACE state
         # in checkpoints -- residuals, momenta, step counters -- maps back to its bucket)
         self.buckets: List[Bucket] = []
@@ -334,7 +342,8 @@ class GraceEngine:
                 b.handles, b.ctx = self.grc.send_step(b.flat, b.name)
         else:
             if self.device.type == "cuda":
-                _wgrad.join(torch.cuda.current_stream(self.device))
+                # (a split capture waits only for the side-stream work of this bucket's parameters)
+                _wgrad.join(torch.cuda.current_stream(self.device), params=b.srcs)
             self._gather(b)
             b.handles, b.ctx = self.grc.send_step(b.flat, b.name)
         self.in_flight += 1

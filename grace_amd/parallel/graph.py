@@ -189,11 +189,16 @@ class GraphedStep:
             open_[key] = False
 
         def on_split():
+            sc.mark("b_end")
             end(gb, side, "b")
             end(ga, main, "a")
+            # A2 gets its OWN pool: with flag sync it may start while graph B still runs (each
+            # bucket waits on the side stream's progress on the device), so it must not reuse
+            # blocks graph A freed that B may still read
             with torch.cuda.stream(main):
-                ga2.capture_begin(pool=ga.pool(), capture_error_mode=mode)
+                ga2.capture_begin(capture_error_mode=mode)
             open_["a2"] = True
+            sc.mark("a2_start")
 
         _health.init()  # the flag waits' timeout raises the process-wide fault words
         sc = _wg.SplitCapture(dev, main, side, on_split, sync=os.environ.get("GRACE_GRAPH_SPLIT_SYNC", "flags"))
@@ -252,9 +257,12 @@ class GraphedStep:
         if self.g_side is not None:
             with torch.cuda.stream(side):
                 self.g_side.replay()
-            cur.wait_stream(side)
+            if self._sc.sync != "flags":  # event sync: A2 has no device-side waits on B
+                cur.wait_stream(side)
         if self.g_a2 is not None:
-            self.g_a2.replay()
+            self.g_a2.replay()  # (flag sync: every bucket launch waits on B's progress inside A2)
+        if self.g_side is not None:
+            cur.wait_stream(side)
         if _SYNC_EACH:
             torch.cuda.synchronize()
         return self.loss

@@ -23,7 +23,7 @@ from .engine import GraceEngine
 class _DistributedOptimizer:
     def __init__(self, optimizer, grace, named_parameters=None, backward_passes_per_step: int = 1,
                  bucket_cap_mb: float = 64.0, overlap: bool = True, sparse_params=(), weights=None,
-                 group_collectives=None, watchdog=None):
+                 group_collectives=None, watchdog=None, tail_bucket: bool = False):
         self._opt = optimizer
         if named_parameters is None:
             params = [p for g in optimizer.param_groups for p in g["params"]]
@@ -37,7 +37,8 @@ class _DistributedOptimizer:
                                   backward_passes_per_step=backward_passes_per_step, overlap=overlap,
                                   sparse_params=sparse_params,
                                   grad_sources=weights.grad_sources() if weights is not None else None,
-                                  group_collectives=group_collectives, watchdog=watchdog)
+                                  group_collectives=group_collectives, watchdog=watchdog,
+                                  tail_bucket=tail_bucket)
         self.weights = weights  # parallel/precision.BF16Weights: refreshed after every step
         # FusedSGD writes the bf16 working copies inside its update kernel (no refresh pass)
         self._fused_refresh = False

@@ -378,3 +378,33 @@ def _ddp_views_body(rank, world):
 
 def test_ddp_hook_marks_current_bucket_views_gloo():
     run_distributed(_ddp_views_body, 2)
+
+
+def test_tail_bucket_same_result_as_one_bucket():
+    """GraceEngine(tail_bucket=True): the first layer's weight gets a bucket of its own, exchanged
+    last; per-tensor Top-K gives the same gradients as with one bucket."""
+    from grace_amd import grace_from_params
+    from grace_amd.parallel import DistributedOptimizer
+
+    def run(tail):
+        torch.manual_seed(0)
+        m = torch.nn.Sequential(torch.nn.Conv2d(3, 8, 3), torch.nn.ReLU(), torch.nn.Flatten(),
+                                torch.nn.Linear(8 * 6 * 6, 4))
+        grc = grace_from_params({"compressor": "topk", "compress_ratio": 0.1, "memory": "residual",
+                                 "communicator": "allgather"})
+        opt = DistributedOptimizer(torch.optim.SGD(m.parameters(), lr=0.1), grc,
+                                   named_parameters=list(m.named_parameters()), overlap=False, tail_bucket=tail)
+        g = torch.Generator().manual_seed(1)
+        for _ in range(3):
+            x = torch.randn(5, 3, 8, 8, generator=g)
+            opt.zero_grad()
+            m(x).square().mean().backward()
+            opt.step()
+        return opt, [p.detach().clone() for p in m.parameters()]
+
+    o1, a = run(False)
+    o2, b = run(True)
+    assert len(o1.engine.buckets) == 1 and len(o2.engine.buckets) == 2
+    assert o2.engine.buckets[-1].params[0].dim() == 4  # conv weight alone, last
+    for x, y in zip(a, b):
+        torch.testing.assert_close(x, y, rtol=0, atol=0)

@@ -94,9 +94,10 @@ def test_side_stream_grads_equal_inline():
             _close(a, b, msg=n)
 
 
+@pytest.mark.parametrize("tail", [False, True])
 @pytest.mark.parametrize("delay", [0, 200000])
 @pytest.mark.parametrize("split", [False, True])
-def test_engine_graph_with_side_stream_wgrad(bn_deterministic, split, delay, monkeypatch):
+def test_engine_graph_with_side_stream_wgrad(bn_deterministic, split, delay, tail, monkeypatch):
     """an engine step captured in a whole-step graph with the wgrad forks (parallel graph
     branches, joined before the bucket gather) matches the eager steps (parameters after 4 steps);
     split=True: captured as two linear graphs (critical / side stream) joined by flag words plus
@@ -113,7 +114,9 @@ def test_engine_graph_with_side_stream_wgrad(bn_deterministic, split, delay, mon
         grc = grace_from_params({"compressor": "none", "memory": "none", "communicator": "allreduce",
                                  "world_size": 1})
         opt = DistributedOptimizer(FusedSGD(list(m.parameters()), lr=0.05, momentum=0.5), grc,
-                                   named_parameters=list(m.named_parameters()), overlap=False)
+                                   named_parameters=list(m.named_parameters()), overlap=False, tail_bucket=tail)
+        if tail:  # the first conv's weight alone in the last bucket
+            assert len(opt.engine.buckets) == 2 and len(opt.engine.buckets[-1].params) == 1
         return m, opt
 
     x = torch.randn(16, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
