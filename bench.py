@@ -437,7 +437,9 @@ def main() -> int:
         with torch.cuda.stream(ddp_stream) if ddp_stream is not None else contextlib.nullcontext():
             model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], bucket_cap_mb=args.bucket_mb,
                                                               gradient_as_bucket_view=True, broadcast_buffers=False)
-        ddp_defer = args.ddp_defer == "on" or (args.ddp_defer == "auto" and mode == "full")
+        # deferred hook only where the step becomes split graphs (below: not with the native RCCL
+        # runtime in the graph); a forked DDP graph is host-bound (2352 vs 2468 img/s immediate)
+        ddp_defer = args.ddp_defer == "on" or (args.ddp_defer == "auto" and mode == "full" and rccl_obj is None)
         ddp_state = GraceHookState(grc, model=model, defer=ddp_defer)
         model.register_comm_hook(ddp_state, grace_comm_hook)
         if ddp_stream is not None and hasattr(torch.autograd.graph, "set_warn_on_accumulate_grad_stream_mismatch"):
@@ -493,8 +495,10 @@ def main() -> int:
             if split is None:
                 # split graphs (critical / side stream, flag sync every 2 fork points): 2720 img/s at
                 # 0.28 ms of host issue vs the forked graph's 2708 at 9.2 ms; DDP 2690 (forked: 2352,
-                # host-bound); W = 2 sharing one GPU 3104 vs 2463 (profiles/r6_graph_split.txt)
-                split = True
+                # host-bound); W = 2 sharing one GPU 3104 vs 2463 (profiles/r6_graph_split.txt).
+                # NOT with the native RCCL runtime's collectives in the graph: measured at W = 1
+                # (--force-dist) 2515 split vs 2719 forked -- the forked graph stays the RCCL default
+                split = rccl_obj is None
             if overlap or (args.surface == "ddp" and not ddp_state.defer):
                 split = False  # the side stream must be joined on the capture stream after backward
             run = GraphedStep(step, warmup=cap_warm, stream=ddp_stream,
@@ -564,6 +568,15 @@ def main() -> int:
     if callable(_chk):
         _chk()
     step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
+    if os.environ.get("GRACE_GRAPH_CENSUS", "0") == "1" and hasattr(run, "graphs"):
+        from grace_amd.ops import _native as _nat
+
+        names = ("kernel", "memcpy", "memset", "host", "graph", "empty", "wait_event", "event_record")
+        for tag, g in (("A", run.graphs[0]), ("B", getattr(run, "g_side", None)), ("A2", getattr(run, "g_a2", None))):
+            if g is not None:
+                c = _nat.lib().graph_node_types(g.raw_cuda_graph())
+                print(f"[graph-census] {tag}: " + " ".join(f"{n}={c[i]}" for i, n in enumerate(names) if c[i])
+                      + f" multi_dep={c[15]}", file=sys.stderr)
     if os.environ.get("GRACE_SPLIT_TRACE", "0") == "1" and getattr(run, "split", False):
         for row in run._sc.timeline():  # (fork, A signalled us, B's wait returned us, lag us)
             print("[split-trace] fork %3s  A %9.1f  B %9.1f  lag %8.1f" % row, file=sys.stderr)

@@ -210,6 +210,30 @@ std::vector<uint32_t> stream_cu_mask(uintptr_t stream, int words) {
   return m;
 }
 
+// Node-type census of a captured graph (torch.cuda.CUDAGraph.raw_cuda_graph()): a graph with
+// anything but kernel / memset / memcpy nodes in one chain (host nodes, event nodes, branches)
+// leaves the runtime's packet fast path -- the split-capture diagnostics use this.
+std::vector<int64_t> graph_node_types(uintptr_t graph) {
+  auto g = reinterpret_cast<hipGraph_t>(graph);
+  size_t n = 0;
+  hip_ok(hipGraphGetNodes(g, nullptr, &n), "hipGraphGetNodes");
+  std::vector<hipGraphNode_t> nodes(n);
+  if (n) hip_ok(hipGraphGetNodes(g, nodes.data(), &n), "hipGraphGetNodes");
+  std::vector<int64_t> counts(16, 0);
+  int64_t multi_dep = 0;
+  for (auto nd : nodes) {
+    hipGraphNodeType t;
+    hip_ok(hipGraphNodeGetType(nd, &t), "hipGraphNodeGetType");
+    const int ti = (int)t;
+    if (ti >= 0 && ti < 15) counts[ti]++;
+    size_t nd_deps = 0;
+    hip_ok(hipGraphNodeGetDependencies(nd, nullptr, &nd_deps), "hipGraphNodeGetDependencies");
+    if (nd_deps > 1) multi_dep++;
+  }
+  counts[15] = multi_dep;  // nodes joining more than one predecessor (branches)
+  return counts;
+}
+
 }  // namespace grace_rt
 
 void grace_bind_runtime(py::module& m) {
@@ -223,6 +247,9 @@ void grace_bind_runtime(py::module& m) {
   m.def("stream_capturing", &grace_rt::stream_capturing, py::arg("stream"));
   m.def("create_stream", &grace_rt::create_stream, py::arg("device"), py::arg("priority") = 0,
         py::arg("cu_mask") = std::vector<uint32_t>{});
+  m.def("graph_node_types", &grace_rt::graph_node_types, py::arg("graph"),
+        "counts by hipGraphNodeType (0 kernel, 1 memcpy, 2 memset, 3 host, 4 graph, 5 empty, 6 wait event, "
+        "7 event record, ...); [15] = nodes with more than one dependency");
   m.def("stream_cu_mask", &grace_rt::stream_cu_mask, py::arg("stream"), py::arg("words") = 8);
   m.def("xs_bump", &grace_rt::xs_bump, py::arg("gen"), py::arg("stream"));
   m.def("xs_signal", &grace_rt::xs_signal, py::arg("flags"), py::arg("idx"), py::arg("gen"), py::arg("stream"),
