@@ -571,7 +571,8 @@ def main() -> int:
     if os.environ.get("GRACE_GRAPH_CENSUS", "0") == "1" and hasattr(run, "graphs"):
         from grace_amd.ops import _native as _nat
 
-        names = ("kernel", "memcpy", "memset", "host", "graph", "empty", "wait_event", "event_record")
+        names = ("kernel", "memcpy", "memset", "host", "graph", "empty", "wait_event", "event_record",
+                 "sem_signal", "sem_wait", "mem_alloc", "mem_free", "t12", "t13", "t14")
         for tag, g in (("A", run.graphs[0]), ("B", getattr(run, "g_side", None)), ("A2", getattr(run, "g_a2", None))):
             if g is not None:
                 c = _nat.lib().graph_node_types(g.raw_cuda_graph())

@@ -56,6 +56,16 @@ def graph_safe(grc, allow_static_seeds: bool = False) -> Optional[str]:
     return None
 
 
+def _new_graph() -> "torch.cuda.CUDAGraph":
+    """GRACE_GRAPH_CENSUS=1 keeps the raw hipGraph_t inspectable after capture (instantiated on
+    the first replay instead of at capture end) for the bench's node census."""
+    import os
+
+    if os.environ.get("GRACE_GRAPH_CENSUS", "0") == "1":
+        return torch.cuda.CUDAGraph(keep_graph=True)
+    return torch.cuda.CUDAGraph()
+
+
 def _is_rccl_backend(name) -> bool:
     """True for any backend string that includes RCCL: "nccl", and the per-device forms such as
     "cpu:gloo,cuda:nccl" (what ``init_process_group()`` without a backend reports on a GPU box)."""
@@ -150,7 +160,7 @@ class GraphedStep:
         self.graphs = []
         self.losses = []
         for i in range(max(1, copies)):
-            g = torch.cuda.CUDAGraph()
+            g = _new_graph()
             with torch.cuda.graph(g, pool=pool, stream=self.stream, capture_error_mode=capture_error_mode):
                 loss = fn()
             torch.cuda.synchronize()
@@ -180,7 +190,7 @@ class GraphedStep:
         main = self._stream_arg if self._stream_arg is not None else \
             torch.cuda.Stream(dev, priority=int(os.environ.get("GRACE_SPLIT_MAIN_PRIO", "0")))
         side = _wg._side(torch.device("cuda", dev))
-        ga, gb, ga2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        ga, gb, ga2 = _new_graph(), _new_graph(), _new_graph()
         open_ = {"a": False, "b": False, "a2": False}
 
         def end(g, st, key):
