@@ -589,7 +589,9 @@ void dgc_compensate(const Tensor& g, const Tensor& u, const Tensor& v, double mo
 void powersgd_mq(const Tensor& x, const Tensor& small, const Tensor& out, const Tensor& mats, const Tensor& tiles,
                  int64_t mode, const c10::optional<Tensor>& comp_r, double beta, double gamma,
                  const c10::optional<Tensor>& xout, int64_t max_r, const c10::optional<Tensor>& lazy_p,
-                 const c10::optional<Tensor>& lazy_q, double lazy_scale) {
+                 const c10::optional<Tensor>& lazy_q, double lazy_scale, bool zeroed,
+                 const c10::optional<Tensor>& bump, const c10::optional<Tensor>& vec,
+                 const c10::optional<Tensor>& vec_idx) {
   CHECK_F32(x);
   CHECK_F32(small);
   CHECK_F32(out);
@@ -608,15 +610,31 @@ void powersgd_mq(const Tensor& x, const Tensor& small, const Tensor& out, const 
     TORCH_CHECK(lazy_p->numel() == out.numel() && lazy_q->numel() == small.numel(), "lazy P / Q sizes");
     TORCH_CHECK(lazy_p->data_ptr() != out.data_ptr(), "lazy P must not alias the P being written");
   }
+  int64_t* bp = nullptr;
+  if (bump.has_value()) {
+    CHECK_I64((*bump));
+    TORCH_CHECK(mode == 0 && tiles.numel() >= 3, "the step counter advances in a P = M Q launch with tiles");
+    bp = bump->data_ptr<int64_t>();
+  }
+  TORCH_CHECK(vec.has_value() == vec_idx.has_value(), "vec and vec_idx go together");
+  if (vec.has_value()) {
+    CHECK_F32((*vec));
+    CHECK_I64((*vec_idx));
+    TORCH_CHECK(mode == 0 && tiles.numel() >= 3 && vec->numel() == vec_idx->numel(),
+                "the 1-D segments are packed by a P = M Q launch with tiles (vec / vec_idx of one size)");
+  }
   DevGuard guard(x.device());
   grace::powersgd_mq(x.data_ptr<float>(), small.data_ptr<float>(), out.data_ptr<float>(), out.numel(),
                      mats.data_ptr<int64_t>(), tiles.data_ptr<int32_t>(), (int)(tiles.numel() / 3), (int)mode,
                      opt_f32(comp_r), (float)beta, (float)gamma, opt_f32_mut(xout), (int)max_r, cur_stream(),
-                     opt_f32(lazy_p), opt_f32(lazy_q), (float)lazy_scale);
+                     opt_f32(lazy_p), opt_f32(lazy_q), (float)lazy_scale, zeroed, bp, opt_f32_mut(vec),
+                     vec_idx.has_value() ? vec_idx->data_ptr<int64_t>() : nullptr,
+                     vec.has_value() ? vec->numel() : 0);
 }
 
 void gram_orthonormalize(const Tensor& buf, const Tensor& mats, int64_t which, int64_t n_mat, const Tensor& gtiles,
-                         const Tensor& gtile_begin, int64_t passes, int64_t max_r) {
+                         const Tensor& gtile_begin, int64_t passes, int64_t max_r,
+                         const c10::optional<Tensor>& zero) {
   CHECK_F32(buf);
   CHECK_I64(mats);
   CHECK_I32(gtiles);
@@ -628,11 +646,14 @@ void gram_orthonormalize(const Tensor& buf, const Tensor& mats, int64_t which, i
   auto T = at::empty({std::max<int64_t>(n_mat, 1) * 256}, buf.options());
   grace::gram_orthonormalize(buf.data_ptr<float>(), mats.data_ptr<int64_t>(), (int)n_mat, (int)which,
                              gtiles.data_ptr<int32_t>(), (int)nt, gtile_begin.data_ptr<int32_t>(),
-                             part.data_ptr<double>(), T.data_ptr<float>(), (int)passes, (int)max_r, cur_stream());
+                             part.data_ptr<double>(), T.data_ptr<float>(), (int)passes, (int)max_r, opt_f32_mut(zero),
+                             zero.has_value() ? zero->numel() : 0, cur_stream());
 }
 
 void powersgd_pqt(const Tensor& P, const Tensor& Q, const c10::optional<Tensor>& out, const Tensor& mats,
-                  const Tensor& tiles, const c10::optional<Tensor>& resid, int64_t max_r, double scale) {
+                  const Tensor& tiles, const c10::optional<Tensor>& resid, int64_t max_r, double scale,
+                  const c10::optional<Tensor>& save_p, const c10::optional<Tensor>& save_q,
+                  const c10::optional<Tensor>& vec, const c10::optional<Tensor>& vec_idx, double vec_scale) {
   CHECK_F32(P);
   CHECK_F32(Q);
   CHECK_I64(mats);
@@ -641,16 +662,34 @@ void powersgd_pqt(const Tensor& P, const Tensor& Q, const c10::optional<Tensor>&
   if (out.has_value()) CHECK_F32((*out));
   if (resid.has_value()) CHECK_F32((*resid));
   if (resid.has_value() && out.has_value()) TORCH_CHECK(resid->numel() == out->numel(), "resid size");
+  TORCH_CHECK(save_p.has_value() == save_q.has_value(), "save_p and save_q go together");
+  if (save_p.has_value()) {
+    CHECK_F32((*save_p));
+    CHECK_F32((*save_q));
+    TORCH_CHECK(save_p->numel() == P.numel() && save_q->numel() == Q.numel(), "save_p / save_q sizes");
+  }
+  TORCH_CHECK(vec.has_value() == vec_idx.has_value(), "vec and vec_idx go together");
+  if (vec.has_value()) {
+    CHECK_F32((*vec));
+    CHECK_I64((*vec_idx));
+    TORCH_CHECK(out.has_value() && tiles.numel() >= 3 && vec->numel() == vec_idx->numel(),
+                "the 1-D segments are scattered by a P Q^T launch with tiles into out");
+  }
   DevGuard guard(P.device());
   grace::powersgd_pqt(P.data_ptr<float>(), Q.data_ptr<float>(), opt_f32_mut(out), mats.data_ptr<int64_t>(),
                       tiles.data_ptr<int32_t>(), (int)(tiles.numel() / 3), opt_f32_mut(resid), (float)scale,
-                      (int)max_r, cur_stream());
+                      (int)max_r, opt_f32_mut(save_p), opt_f32_mut(save_q), opt_f32(vec),
+                      vec_idx.has_value() ? vec_idx->data_ptr<int64_t>() : nullptr,
+                      vec.has_value() ? vec->numel() : 0, (float)vec_scale, cur_stream());
 }
 
-void philox_normal(const Tensor& out, int64_t seed, const c10::optional<Tensor>& step) {
+void philox_normal(const Tensor& out, int64_t seed, const c10::optional<Tensor>& step,
+                   const c10::optional<Tensor>& zero) {
   CHECK_F32(out);
+  if (zero.has_value()) CHECK_F32((*zero));
   DevGuard guard(out.device());
-  grace::philox_normal(out.data_ptr<float>(), out.numel(), seed_arg(seed, step), cur_stream());
+  grace::philox_normal(out.data_ptr<float>(), out.numel(), seed_arg(seed, step), cur_stream(), opt_f32_mut(zero),
+                       zero.has_value() ? zero->numel() : 0);
 }
 
 // ------------------------------------------------------------------------------ 16-bit cast, sketch
@@ -1204,8 +1243,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dgc_compensate", &dgc_compensate);
   m.def("powersgd_mq", &powersgd_mq, py::arg("x"), py::arg("small"), py::arg("out"), py::arg("mats"), py::arg("tiles"),
         py::arg("mode"), py::arg("comp_r"), py::arg("beta"), py::arg("gamma"), py::arg("xout"), py::arg("max_r"),
-        py::arg("lazy_p") = py::none(), py::arg("lazy_q") = py::none(), py::arg("lazy_scale") = 0.0);
-  m.def("gram_orthonormalize", &gram_orthonormalize);
+        py::arg("lazy_p") = py::none(), py::arg("lazy_q") = py::none(), py::arg("lazy_scale") = 0.0,
+        py::arg("zeroed") = false, py::arg("bump") = py::none(), py::arg("vec") = py::none(),
+        py::arg("vec_idx") = py::none());
+  m.def("gram_orthonormalize", &gram_orthonormalize, py::arg("buf"), py::arg("mats"), py::arg("which"),
+        py::arg("n_mat"), py::arg("gtiles"), py::arg("gtile_begin"), py::arg("passes"), py::arg("max_r"),
+        py::arg("zero") = py::none());
   m.def("adaq_sample", &adaq_sample);
   m.def("adaq_prepare", &adaq_prepare);
   m.def("adaq_refine", &adaq_refine);
@@ -1217,8 +1260,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("inceptionn_encode", &inceptionn_encode);
   m.def("inceptionn_decode", &inceptionn_decode);
   m.def("powersgd_pqt", &powersgd_pqt, py::arg("P"), py::arg("Q"), py::arg("out"), py::arg("mats"), py::arg("tiles"),
-        py::arg("resid"), py::arg("max_r"), py::arg("scale") = 1.0);
-  m.def("philox_normal", &philox_normal);
+        py::arg("resid"), py::arg("max_r"), py::arg("scale") = 1.0, py::arg("save_p") = py::none(),
+        py::arg("save_q") = py::none(), py::arg("vec") = py::none(), py::arg("vec_idx") = py::none(),
+        py::arg("vec_scale") = 1.0);
+  m.def("philox_normal", &philox_normal, py::arg("out"), py::arg("seed"), py::arg("step") = py::none(),
+        py::arg("zero") = py::none());
   m.def("cast16", &cast16);
   m.def("decode16_sum", &decode16_sum);
   m.def("sketch_encode", &sketch_encode);

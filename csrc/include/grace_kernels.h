@@ -115,15 +115,22 @@ void dgc_compensate(const float* g, float* u, float* v, float momentum, int64_t 
 void powersgd_mq(const float* x, const float* small, float* out, int64_t out_len, const int64_t* mats,
                  const int32_t* tiles, int n_tiles, int mode, const float* comp_r, float beta, float gamma,
                  float* xout, int max_r, hipStream_t stream, const float* lazy_p = nullptr,
-                 const float* lazy_q = nullptr, float lazy_scale = 0.f);  // lazy_*: deferred residual (mode 0
-                                                                          // with comp_r): r = comp_r - s P Q^T
+                 const float* lazy_q = nullptr, float lazy_scale = 0.f, bool zeroed = false,
+                 int64_t* bump = nullptr, float* vec = nullptr, const int64_t* vec_idx = nullptr,
+                 int64_t n_vec = 0);  // lazy_*: deferred residual (mode 0 with comp_r): r = comp_r - s P Q^T;
+                                      // zeroed: out already cleared; bump: step counter += 1 (mode 0);
+                                      // vec[e] = x[vec_idx[e]] (mode 0: the 1-D segments, packed)
 // max_r: largest rank r of the matrices (<= 4 selects the one-launch, one-workgroup-per-matrix form)
 void gram_orthonormalize(float* buf, const int64_t* mats, int n_mat, int which, const int32_t* gtiles,
                          int n_gtiles, const int32_t* gtile_begin, double* partials, float* T, int passes,
-                         int max_r, hipStream_t stream);
+                         int max_r, float* zero, int64_t zn, hipStream_t stream);  // also clears zero[0, zn)
+// out may be null (resid only); save_p / save_q: copies of P and Q (same offsets), may be null
 void powersgd_pqt(const float* P, const float* Q, float* out, const int64_t* mats, const int32_t* tiles, int n_tiles,
-                  float* resid, float scale, int max_r, hipStream_t stream);  // out may be null (resid only)
-void philox_normal(float* out, int64_t n, SeedArg seed, hipStream_t stream);
+                  float* resid, float scale, int max_r, float* save_p, float* save_q, const float* vec,
+                  const int64_t* vec_idx, int64_t n_vec, float vec_scale,
+                  hipStream_t stream);  // + out[vec_idx[e]] = vec_scale * vec[e]
+void philox_normal(float* out, int64_t n, SeedArg seed, hipStream_t stream, float* zero = nullptr,
+                   int64_t zn = 0);  // also clears zero[0, zn)
 
 // ---------------------------------------------------------------- cast_sketch.hip
 void cast16(const float* x, uint16_t* y, int64_t n, bool bf16, hipStream_t stream);

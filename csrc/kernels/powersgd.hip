@@ -84,11 +84,28 @@ struct Lazy {
   float s;
 };
 
+// the 1-D segments of a bucket (biases) travel uncompressed: packed into vec by the P = M Q launch,
+// scattered back (times scale) by the P Q^T launch -- no gather / scatter launches of their own
+struct VecMove {
+  float* vec;
+  const int64_t* idx;
+  int64_t n;
+  float scale;
+};
+
 template <int R, int COMP>
 __global__ __launch_bounds__(kBlock) void ps_mq_kernel(const float* __restrict__ x, const float* __restrict__ Qall,
                                                        float* __restrict__ Pall, const int64_t* __restrict__ mats,
                                                        const int32_t* __restrict__ tiles, const float* cr, float beta,
-                                                       float gamma, float* xout, Lazy lz) {
+                                                       float gamma, float* xout, Lazy lz, int64_t* bump,
+                                                       VecMove vm) {
+  // the caller's device step counter advances here (read by the philox launch that produced Q,
+  // which has completed: stream order) -- one launch fewer per bucket than a separate add
+  if (bump != nullptr && blockIdx.x == 0 && threadIdx.x == 0) bump[0] = bump[0] + 1;
+  // the bucket's 1-D segments packed for the communicator: vec[e] = x[idx[e]] (grid-stride over
+  // every block: replaces a separate gather launch)
+  for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < vm.n; e += (int64_t)gridDim.x * kBlock)
+    vm.vec[e] = x[vm.idx[e]];
   const int* tl = tiles + 3 * blockIdx.x;
   const Mat mt = load_mat(mats, tl[0]);
   const int64_t n = mt.n, m = mt.m;
@@ -345,7 +362,10 @@ template <int R>
 __global__ __launch_bounds__(kBlock) void ps_pqt_kernel(const float* __restrict__ Pall, const float* __restrict__ Qall,
                                                         float* out, const int64_t* __restrict__ mats,
                                                         const int32_t* __restrict__ tiles, float* __restrict__ resid,
-                                                        float scale) {  // out == nullptr: residual update only
+                                                        float scale, float* __restrict__ save_p,
+                                                        float* __restrict__ save_q, VecMove vm) {  // out == nullptr: residual update only
+  for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < vm.n; e += (int64_t)gridDim.x * kBlock)
+    out[vm.idx[e]] = vm.vec[e] * vm.scale;
   const int* tl = tiles + 3 * blockIdx.x;
   const Mat mt = load_mat(mats, tl[0]);
   const int64_t n = mt.n, m = mt.m;
@@ -354,12 +374,24 @@ __global__ __launch_bounds__(kBlock) void ps_pqt_kernel(const float* __restrict_
   const float* Q = Qall + mt.q_off;
   const int64_t r0 = (int64_t)tl[1] * kRSP;
   const int64_t r1 = r0 + kRSP < n ? r0 + kRSP : n;
+  // save_p / save_q (the deferred residual's copies of this step's P and Q, same offsets): the
+  // first column block of every row strip stores the strip's P rows, the first row strip stores
+  // Q below (each element exactly once; replaces two copy launches per bucket)
+  if (save_p != nullptr && tl[2] == 0)
+    for (int64_t e = threadIdx.x; e < (r1 - r0) * r; e += kBlock) save_p[mt.p_off + r0 * r + e] = P[r0 * r + e];
+  const bool save_q_here = save_q != nullptr && tl[1] == 0;
   if (mat_vec(mt)) {
     const int64_t c = (int64_t)tl[2] * kCBV + 4 * threadIdx.x;
     if (c >= m) return;
     float q[4][R];
 #pragma unroll
     for (int t = 0; t < 4; ++t) load_small_row<R>(Q, c + t, r, q[t]);
+    if (save_q_here)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+          if (j < r) save_q[mt.q_off + (c + t) * r + j] = q[t][j];
     for (int64_t rb = r0; rb < r1; rb += kPB) {
       float4 rv[kPB];
       if (resid != nullptr) {
@@ -393,6 +425,10 @@ __global__ __launch_bounds__(kBlock) void ps_pqt_kernel(const float* __restrict_
     if (c >= m) return;
     float q[R];
     load_small_row<R>(Q, c, r, q);
+    if (save_q_here)
+#pragma unroll
+      for (int j = 0; j < R; ++j)
+        if (j < r) save_q[mt.q_off + c * r + j] = q[j];
     for (int64_t row = r0; row < r1; ++row) {
       float p[R];
       load_small_row<R>(P, row, r, p);
@@ -567,7 +603,11 @@ __global__ __launch_bounds__(kBlock) void gram_apply_kernel(float* __restrict__ 
 constexpr int kSmallR = 4;
 constexpr int kGramLds = 16384;  // floats of a block staged in LDS (64 KB)
 __global__ __launch_bounds__(kBlock) void gram_small_kernel(float* __restrict__ buf, const int64_t* __restrict__ mats,
-                                                            int which, int passes) {
+                                                            int which, int passes, float* __restrict__ zero,
+                                                            int64_t zn) {
+  // zero[0, zn): the Q arena the following M^T P launches accumulate into (their memsets folded
+  // into this launch, which precedes them)
+  for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < zn; e += (int64_t)gridDim.x * kBlock) zero[e] = 0.f;
   const Mat mt = load_mat(mats, blockIdx.x);
   const int64_t len = blk_len(mt, which);
   const int r = (int)mt.r;
@@ -686,7 +726,10 @@ __global__ __launch_bounds__(kBlock) void gram_small_kernel(float* __restrict__ 
   }
 }
 
-__global__ __launch_bounds__(kBlock) void philox_normal_kernel(float* __restrict__ out, int64_t n, SeedArg sa) {
+__global__ __launch_bounds__(kBlock) void philox_normal_kernel(float* __restrict__ out, int64_t n, SeedArg sa,
+                                                              float* __restrict__ zero, int64_t zn) {
+  // zero[0, zn): the P buffer the following M Q launch accumulates into (its memset folded here)
+  for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < zn; e += (int64_t)gridDim.x * kBlock) zero[e] = 0.f;
   const uint64_t seed = sa.get();
   const int64_t stride = (int64_t)gridDim.x * kBlock * 4;
   for (int64_t base = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 4; base < n; base += stride) {
@@ -710,42 +753,54 @@ __global__ __launch_bounds__(kBlock) void philox_normal_kernel(float* __restrict
 
 template <int R>
 void launch_mq(const float* x, const float* small, float* out, const int64_t* mats, const int32_t* tiles, int n_tiles,
-               int mode, const float* comp_r, float beta, float gamma, float* xout, Lazy lz, hipStream_t stream) {
+               int mode, const float* comp_r, float beta, float gamma, float* xout, Lazy lz, int64_t* bump,
+               VecMove vm, hipStream_t stream) {
   const Lazy none{nullptr, nullptr, 0.f};
   if (mode == 1)  // (16 rows per batch measured slower: 0.855 vs 0.755 ms VGG-16 exchange)
     ps_mtp_kernel<R, kPB><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles);
   else if (xout == nullptr)
-    ps_mq_kernel<R, 0><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles, nullptr, 0.f, 0.f, nullptr, none);
+    ps_mq_kernel<R, 0><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles, nullptr, 0.f, 0.f, nullptr, none,
+                                                       bump, vm);
   else if (comp_r == nullptr)
-    ps_mq_kernel<R, 1><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles, nullptr, 0.f, 0.f, xout, none);
+    ps_mq_kernel<R, 1><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles, nullptr, 0.f, 0.f, xout, none, bump,
+                                                       vm);
   else if (lz.p == nullptr)
-    ps_mq_kernel<R, 2><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles, comp_r, beta, gamma, xout, none);
+    ps_mq_kernel<R, 2><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles, comp_r, beta, gamma, xout, none,
+                                                       bump, vm);
   else
-    ps_mq_kernel<R, 3><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles, comp_r, beta, gamma, xout, lz);
+    ps_mq_kernel<R, 3><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles, comp_r, beta, gamma, xout, lz, bump,
+                                                       vm);
 }
 
 void powersgd_mq(const float* x, const float* small, float* out, int64_t out_len, const int64_t* mats,
                  const int32_t* tiles, int n_tiles, int mode, const float* comp_r, float beta, float gamma,
                  float* xout, int max_r, hipStream_t stream, const float* lazy_p, const float* lazy_q,
-                 float lazy_scale) {
-  GRACE_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(float) * out_len, stream));
-  if (n_tiles <= 0) return;
+                 float lazy_scale, bool zeroed, int64_t* bump, float* vec, const int64_t* vec_idx,
+                 int64_t n_vec) {
+  // zeroed: an earlier launch on this stream (philox Q / the Gram launch) already cleared out
+  if (!zeroed) GRACE_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(float) * out_len, stream));
+  if (n_tiles <= 0) return;  // (the binding refuses a step counter without tiles to advance it)
   const Lazy lz{lazy_p, lazy_q, lazy_scale};
-  if (max_r <= 1) launch_mq<1>(x, small, out, mats, tiles, n_tiles, mode, comp_r, beta, gamma, xout, lz, stream);
-  else if (max_r <= 2) launch_mq<2>(x, small, out, mats, tiles, n_tiles, mode, comp_r, beta, gamma, xout, lz, stream);
-  else if (max_r <= 4) launch_mq<4>(x, small, out, mats, tiles, n_tiles, mode, comp_r, beta, gamma, xout, lz, stream);
-  else if (max_r <= 8) launch_mq<8>(x, small, out, mats, tiles, n_tiles, mode, comp_r, beta, gamma, xout, lz, stream);
-  else launch_mq<16>(x, small, out, mats, tiles, n_tiles, mode, comp_r, beta, gamma, xout, lz, stream);
+  const VecMove vm{vec, vec_idx, vec != nullptr ? n_vec : 0, 1.f};
+  if (max_r <= 1) launch_mq<1>(x, small, out, mats, tiles, n_tiles, mode, comp_r, beta, gamma, xout, lz, bump, vm, stream);
+  else if (max_r <= 2) launch_mq<2>(x, small, out, mats, tiles, n_tiles, mode, comp_r, beta, gamma, xout, lz, bump, vm, stream);
+  else if (max_r <= 4) launch_mq<4>(x, small, out, mats, tiles, n_tiles, mode, comp_r, beta, gamma, xout, lz, bump, vm, stream);
+  else if (max_r <= 8) launch_mq<8>(x, small, out, mats, tiles, n_tiles, mode, comp_r, beta, gamma, xout, lz, bump, vm, stream);
+  else launch_mq<16>(x, small, out, mats, tiles, n_tiles, mode, comp_r, beta, gamma, xout, lz, bump, vm, stream);
 }
 
 void gram_orthonormalize(float* buf, const int64_t* mats, int n_mat, int which, const int32_t* gtiles,
                          int n_gtiles, const int32_t* gtile_begin, double* partials, float* T, int passes,
-                         int max_r, hipStream_t stream) {
-  if (n_mat <= 0 || n_gtiles <= 0) return;
-  if (max_r <= kSmallR) {
-    gram_small_kernel<<<n_mat, kBlock, 0, stream>>>(buf, mats, which, passes);
+                         int max_r, float* zero, int64_t zn, hipStream_t stream) {
+  if (n_mat <= 0 || n_gtiles <= 0) {
+    if (zn > 0) GRACE_HIP_CHECK(hipMemsetAsync(zero, 0, sizeof(float) * zn, stream));
     return;
   }
+  if (max_r <= kSmallR) {
+    gram_small_kernel<<<n_mat, kBlock, 0, stream>>>(buf, mats, which, passes, zero, zn);
+    return;
+  }
+  if (zn > 0) GRACE_HIP_CHECK(hipMemsetAsync(zero, 0, sizeof(float) * zn, stream));
   for (int p = 0; p < passes; ++p) {
     gram_partial_kernel<<<n_gtiles, kBlock, 0, stream>>>(buf, mats, gtiles, which, partials);
     gram_fix_kernel<<<n_mat, kWave, 0, stream>>>(mats, gtile_begin, partials, T);
@@ -754,20 +809,25 @@ void gram_orthonormalize(float* buf, const int64_t* mats, int n_mat, int which, 
 }
 
 void powersgd_pqt(const float* P, const float* Q, float* out, const int64_t* mats, const int32_t* tiles, int n_tiles,
-                  float* resid, float scale, int max_r, hipStream_t stream) {
-  if (n_tiles <= 0) return;
-  if (max_r <= 1) ps_pqt_kernel<1><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid, scale);
-  else if (max_r <= 2) ps_pqt_kernel<2><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid, scale);
-  else if (max_r <= 4) ps_pqt_kernel<4><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid, scale);
-  else if (max_r <= 8) ps_pqt_kernel<8><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid, scale);
-  else ps_pqt_kernel<16><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid, scale);
+                  float* resid, float scale, int max_r, float* save_p, float* save_q, const float* vec,
+                  const int64_t* vec_idx, int64_t n_vec, float vec_scale, hipStream_t stream) {
+  if (n_tiles <= 0) return;  // (the binding refuses vector segments without tiles)
+  const VecMove vm{const_cast<float*>(vec), vec_idx, vec != nullptr ? n_vec : 0, vec_scale};
+  if (max_r <= 1) ps_pqt_kernel<1><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid, scale, save_p, save_q, vm);
+  else if (max_r <= 2) ps_pqt_kernel<2><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid, scale, save_p, save_q, vm);
+  else if (max_r <= 4) ps_pqt_kernel<4><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid, scale, save_p, save_q, vm);
+  else if (max_r <= 8) ps_pqt_kernel<8><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid, scale, save_p, save_q, vm);
+  else ps_pqt_kernel<16><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid, scale, save_p, save_q, vm);
 }
 
-void philox_normal(float* out, int64_t n, SeedArg seed, hipStream_t stream) {
-  if (n <= 0) return;
+void philox_normal(float* out, int64_t n, SeedArg seed, hipStream_t stream, float* zero, int64_t zn) {
+  if (n <= 0) {
+    if (zn > 0) GRACE_HIP_CHECK(hipMemsetAsync(zero, 0, sizeof(float) * zn, stream));
+    return;
+  }
   int64_t b = (n + 4 * kBlock - 1) / (4 * kBlock);
   if (b > 2048) b = 2048;
-  philox_normal_kernel<<<(int)b, kBlock, 0, stream>>>(out, n, seed);
+  philox_normal_kernel<<<(int)b, kBlock, 0, stream>>>(out, n, seed, zero, zn);
 }
 
 }  // namespace grace

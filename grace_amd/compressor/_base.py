@@ -41,23 +41,29 @@ class DeviceSteps:
 
     def __init__(self):
         self._t: Dict[str, torch.Tensor] = {}
+        self._post: set = set()
 
-    def bump(self, name: str, device: torch.device, host_value: int) -> torch.Tensor:
+    def bump(self, name: str, device: torch.device, host_value: int, post: bool = False) -> torch.Tensor:
+        """``post=True``: the caller's kernel advances the counter itself AFTER its readers ran
+        (PowerSGD's P = M Q launch, one launch fewer than the ``add_``): the counter is created
+        at ``host_value`` and not advanced here, and holds step + 1 between steps."""
         t = self._t.get(name)
-        if t is None or t.device != device:
+        if t is None or t.device != device or (name in self._post) != post:
             t = torch.full((1,), host_value, dtype=torch.int64, device=device)
             self._t[name] = t
-        else:
+            (self._post.add if post else self._post.discard)(name)
+        elif not post:
             t.add_(1)
         return t
 
     def sync_to(self, steps: Dict[str, int]) -> None:
         """Copy the device counters (advanced by graph replays) back into the host dict."""
         for name, t in self._t.items():
-            steps[name] = int(t.item())
+            steps[name] = int(t.item()) - (1 if name in self._post else 0)
 
     def reset(self) -> None:
         self._t.clear()
+        self._post.clear()
 
 
 class StepState:
@@ -67,12 +73,13 @@ class StepState:
         self.steps: Dict[str, int] = {}
         self._dsteps = DeviceSteps()
 
-    def advance(self, name: str, device) -> Tuple[int, Any]:
-        """Advance ``name``'s step.  Returns (host step, device counter or None)."""
+    def advance(self, name: str, device, post: bool = False) -> Tuple[int, Any]:
+        """Advance ``name``'s step.  Returns (host step, device counter or None); ``post``: see
+        :meth:`DeviceSteps.bump` (the caller MUST advance the device counter after using it)."""
         step = self.steps.get(name, 0) + 1
         self.steps[name] = step
         if _native.native_on(device):
-            return step, self._dsteps.bump(name, torch.device(device), step)
+            return step, self._dsteps.bump(name, torch.device(device), step, post=post)
         return step, None
 
     def state_dict(self):

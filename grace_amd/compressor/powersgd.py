@@ -144,24 +144,35 @@ class PowerSGDCompressor(BucketCompressor):
         the P/Q collectives run now (manual path) or in :meth:`step_flush`.  ``x`` feeds the
         first product (compensated on the fly when ``xout`` is given, which then holds x);
         ``x_after`` is what the second product reads."""
-        step, step_t = self.advance(name, x.device)
+        native = PS._native.use_native(x)
+        # native: the P = M Q launch advances the device step counter (post-bump, no add kernel)
+        step, step_t = self.advance(name, x.device, post=native)
+        p_out = self._arena_slice(name, plan) if defer else None
+        if native and p_out is None:
+            p_out = torch.empty(plan.p_total, dtype=torch.float32, device=x.device)
+        zeroed = False
         q = self.q_memory.get(name) if self.warm_start else None
         if q is None or q.numel() != plan.q_total:
             # identical on every rank (no rank in the seed); the device step counter keeps a fresh
             # Q per HIP-graph replay when warm_start is off
             seed = fnv1a64(name.encode())
+            # the same launch clears P for the accumulating P = M Q launch (no memset)
             q = PS.randn_shared(plan.q_total, seed if step_t is not None else mix_step(seed, step), x.device,
-                                step=step_t)
+                                step=step_t, zero=p_out if native else None)
+            zeroed = native
             # The reference orthogonalises this fresh Gaussian Q (dist/compressor/powersgd.py:43).  That cannot
             # change the result: MGS gives Q R^-1 with R upper triangular, so P = M Q R^-1 = P R^-1
             # and the orthonormal factor of P R^-1 is that of P -- orthogonalize(P) below yields the
             # same P-hat, hence the same Q = M^T P-hat and P-hat Q^T (up to rounding; a Gaussian Q is
             # well conditioned).  Skipped: it was a 400 KB single-workgroup pass per step for
             # VGG-16's 25088 x 4 Q.  (A warm-start Q is used as is, as in the reference.)
-        p_out = self._arena_slice(name, plan) if defer else None
-        p = PS.mq(x, q, plan, comp_r=comp_r, xout=xout, out=p_out, lazy=lazy)  # P = M Q, every matrix, one launch
+        # 1-D segments, sent through the communicator: packed by the P = M Q launch (native)
+        vec = torch.empty(plan.v_total, dtype=torch.float32, device=x.device) if native else None
+        p = PS.mq(x, q, plan, comp_r=comp_r, xout=xout, out=p_out, lazy=lazy, zeroed=zeroed,
+                  bump=step_t if native else None, vec=vec)  # P = M Q, every matrix, one launch
         ctx.extra.update(plan=plan, p=p)
-        vec = PS.gather_vectors(x, plan)  # 1-D segments, sent through the communicator
+        if vec is None:
+            vec = PS.gather_vectors(x, plan)
         entry = (name, x_after, ctx)
         if defer:
             self._pending.append(entry)
@@ -196,6 +207,35 @@ class PowerSGDCompressor(BucketCompressor):
         self._arena = {"key": key, "off": off, "p": torch.empty(po, dtype=torch.float32, device=dev),
                        "q": torch.empty(qo, dtype=torch.float32, device=dev), "orth": orth}
 
+    def _merged_mtp(self, entries):
+        """(base tensor, plan) of one Q = M^T P launch over every bucket of the arena: each
+        matrix's x offset is taken relative to the lowest bucket address (the buckets are separate
+        allocations of one device; the kernel addresses them from that base).  None when it does
+        not apply (one bucket, CPU, misaligned or mixed-device buffers)."""
+        if len(entries) < 2:
+            return None
+        xs = [x for _, x, _ in entries]
+        if not all(PS._native.use_native(x) and x.dtype == torch.float32 and x.is_contiguous()
+                   and x.device == xs[0].device for x in xs):
+            return None
+        ptrs = tuple(x.data_ptr() for x in xs)
+        if any(p_ % 16 for p_ in ptrs):
+            return None
+        a = self._arena
+        cached = a.get("mtp")
+        if cached is not None and cached[0] == ptrs:
+            return cached[1], cached[2]
+        bi = min(range(len(xs)), key=lambda i: ptrs[i])
+        base = xs[bi]
+        mats = []
+        for (name, _, ctx), ptr in zip(entries, ptrs):
+            bpo, bqo = a["off"][name]
+            d = (ptr - ptrs[bi]) // 4
+            mats += [(xo + d, n, m, r, mpo + bpo, mqo + bqo) for (xo, n, m, r, mpo, mqo) in ctx.extra["plan"].mats]
+        plan_all = PS.Plan(self.rank_r, mats, [], a["p"].numel(), a["q"].numel(), 0)
+        a["mtp"] = (ptrs, base, plan_all)
+        return base, plan_all
+
     def _exchange(self, entries, arena: bool = False):
         W = self.world_size or 1
         comm = self.comm if (self.comm is not None and W > 1) else None
@@ -222,12 +262,20 @@ class PowerSGDCompressor(BucketCompressor):
             comm.all_reduce(p_all)  # SUM over ranks: the orthonormalisation is scale invariant
             self.matrix_collectives += 1
         if arena:
-            PS.orthogonalize(p_all, self._arena["orth"], which="p")  # all buckets, one launch
+            # all buckets, one launch -- which also clears the Q arena for the M^T P launches
+            PS.orthogonalize(p_all, self._arena["orth"], which="p", zero=q_all)
         else:
             for _, _, ctx in entries:
                 PS.orthogonalize(ctx.extra["p"], ctx.extra["plan"], which="p")
-        for _, x_after, ctx in entries:
-            PS.mtp(x_after, ctx.extra["p"], ctx.extra["plan"], out=ctx.extra["q"])  # Q = M^T P
+        merged = self._merged_mtp(entries) if arena else None
+        if merged is not None:
+            # Q = M^T P of every bucket in ONE launch: the small buckets' tiles fill in beside the
+            # big ones (per-bucket launches of the small conv buckets ran at ~2 TB/s)
+            base, plan_all = merged
+            PS.mtp(base, p_all, plan_all, out=q_all, zeroed=True)
+        else:
+            for _, x_after, ctx in entries:
+                PS.mtp(x_after, ctx.extra["p"], ctx.extra["plan"], out=ctx.extra["q"], zeroed=arena)  # Q = M^T P
         if comm is not None:
             comm.all_reduce(q_all)  # SUM; the 1/W is applied inside the P Q^T pass
             self.matrix_collectives += 1
@@ -249,26 +297,28 @@ class PowerSGDCompressor(BucketCompressor):
         resid = ctx.extra.pop("resid", None)
         mem = ctx.extra.pop("lazy_mem", None)
         scale = ctx.extra.get("q_scale", 1.0)
+        # the 1-D segments go back into out inside the P Q^T launch
+        vec = tensors[0] if tensors and tensors[0].numel() == plan.v_total else None
+        if vec is None and tensors:
+            raise RuntimeError(f"PowerSGD: 1-D payload of {tensors[0].numel()} elements, plan has {plan.v_total}")
         if mem is not None and resid is not None:
             # deferred residual: the residual buffer keeps x, and (P, Q, scale) go to the memory
             # for the next step's P = M Q pass -- as copies in persistent per-name buffers: the
             # next P = M Q pass rewrites the step-level P arena slice while reading the previous P,
             # and a HIP graph replays fixed pointers (the manual path's P / Q are fresh tensors)
-            PS.pqt(ctx.extra["p"], ctx.extra["q"], plan, out, resid=None, scale=scale)
             name = ctx.extra["name"]
             prev = self._pq_prev.get(name)
             dev = ctx.extra["p"].device
             if prev is None or prev.numel() != plan.p_total + plan.q_total or prev.device != dev:
                 prev = self._pq_prev[name] = torch.empty(plan.p_total + plan.q_total, dtype=torch.float32, device=dev)
             pp, qp = prev[:plan.p_total], prev[plan.p_total:]
-            pp.copy_(ctx.extra["p"])
-            qp.copy_(ctx.extra["q"])
+            # the copies are stored by the decompress launch itself (it reads P and Q anyway)
+            PS.pqt(ctx.extra["p"], ctx.extra["q"], plan, out, resid=None, scale=scale, save=(pp, qp), vec=vec,
+                   vec_scale=vec_scale)
             mem.lazy[name] = (pp, qp, scale, plan)
         else:
             # fused eager form / unfused: the residual buffer holds x; this pass leaves r = x - P Q^T
-            PS.pqt(ctx.extra["p"], ctx.extra["q"], plan, out, resid=resid, scale=scale)
-        if tensors:
-            PS.scatter_vectors(tensors[0], plan, out, vec_scale)
+            PS.pqt(ctx.extra["p"], ctx.extra["q"], plan, out, resid=resid, scale=scale, vec=vec, vec_scale=vec_scale)
         return self.finish(out, ctx)
 
     def decompress(self, tensors, ctx):

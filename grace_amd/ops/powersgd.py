@@ -121,14 +121,18 @@ def plan_for(layout: SegmentLayout, rank: int) -> Plan:
     return p
 
 
-def randn_shared(n: int, seed: int, device, step: Optional[torch.Tensor] = None) -> torch.Tensor:
+def randn_shared(n: int, seed: int, device, step: Optional[torch.Tensor] = None,
+                 zero: Optional[torch.Tensor] = None) -> torch.Tensor:
     """N(0,1) vector identical on every rank for the same seed (and device ``step`` counter,
-    mixed in by the kernel when given)."""
+    mixed in by the kernel when given).  ``zero``: a buffer cleared by the same launch (the P
+    that the following :func:`mq` accumulates into: ``mq(..., zeroed=True)``)."""
     if _native.use_native(torch.empty(0, device=device)):
         out = torch.empty(n, dtype=torch.float32, device=device)
         sd = seed & 0xFFFFFFFFFFFFFFFF
-        _native.lib().philox_normal(out, sd - (1 << 64) if sd >= (1 << 63) else sd, step)
+        _native.lib().philox_normal(out, sd - (1 << 64) if sd >= (1 << 63) else sd, step, zero)
         return out
+    if zero is not None:
+        zero.zero_()
     g = torch.Generator(device=device)
     g.manual_seed(seed & 0x7FFFFFFFFFFFFFFF)
     return torch.randn(n, generator=g, device=device)
@@ -144,19 +148,23 @@ def _views(buf, plan, which):
     return out
 
 
-def orthogonalize(buf: torch.Tensor, plan: Plan, which: str) -> None:
+def orthogonalize(buf: torch.Tensor, plan: Plan, which: str, zero: Optional[torch.Tensor] = None) -> None:
     """In-place Gram-Schmidt of the columns of every P_i (or Q_i) -- reference
     dist/compressor/powersgd.py:7-18.  Zero columns stay zero instead of becoming NaN, and a
     column that is numerically dependent on the previous ones (residual below 1e-5 of its norm:
     a rank-deficient P) becomes zero instead of normalised rounding noise (the reference's
-    ``col / (norm + 1e-8)`` turns it into an arbitrary non-orthogonal direction)."""
+    ``col / (norm + 1e-8)`` turns it into an arbitrary non-orthogonal direction).
+    ``zero``: a buffer cleared by the same launch (the Q arena the following :func:`mtp` calls
+    accumulate into: ``mtp(..., zeroed=True)``)."""
+    if zero is not None and not _native.use_native(buf):
+        zero.zero_()
     if _native.use_native(buf):
         # Gram-matrix MGS on MFMA, two passes (CholQR2): csrc/kernels/powersgd.hip
         t = plan.tables(buf.device)
         # P = M Q can be ill-conditioned (near-low-rank gradients): CholQR2; the Gaussian Q
         # (condition number ~1) needs one pass
         _native.lib().gram_orthonormalize(buf, t["mat"], 0 if which == "p" else 1, plan.n_mat, t["gt_" + which],
-                                          t["gtb_" + which], 2 if which == "p" else 1, plan.rank)
+                                          t["gtb_" + which], 2 if which == "p" else 1, plan.rank, zero)
         return
     for a in _views(buf, plan, which):
         r = a.shape[1]
@@ -177,7 +185,8 @@ def orthogonalize(buf: torch.Tensor, plan: Plan, which: str) -> None:
 
 def mq(x: torch.Tensor, q: torch.Tensor, plan: Plan, comp_r: Optional[torch.Tensor] = None, beta: float = 1.0,
        gamma: float = 1.0, xout: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-       lazy: Optional[Tuple[torch.Tensor, torch.Tensor, float]] = None) -> torch.Tensor:
+       lazy: Optional[Tuple[torch.Tensor, torch.Tensor, float]] = None, zeroed: bool = False,
+       bump: Optional[torch.Tensor] = None, vec: Optional[torch.Tensor] = None) -> torch.Tensor:
     """P_i = M_i Q_i for every matrix (flat P buffer; ``out``: a caller-owned [p_total] view,
     e.g. this bucket's slice of the step-level P arena).
 
@@ -185,7 +194,10 @@ def mq(x: torch.Tensor, q: torch.Tensor, plan: Plan, comp_r: Optional[torch.Tens
     ``xout`` for the matrix segments -- the error-feedback compensate fused into this pass.
     ``lazy = (P', Q', s)``: ``comp_r`` holds the previous step's M and the residual is
     comp_r - s P' Q'^T (the previous step's final P and summed Q; the deferred residual update,
-    formed here with ``pqt``'s float ops instead of written by it and read back)."""
+    formed here with ``pqt``'s float ops instead of written by it and read back).
+    ``zeroed``: ``out`` was already cleared (by :func:`randn_shared`'s launch).  ``bump``: a device
+    step counter advanced by this launch (native only).  ``vec`` [v_total]: receives the bucket's
+    1-D segments, packed (:func:`gather_vectors`, in the same launch)."""
     p = out if out is not None else torch.empty(plan.p_total, dtype=torch.float32, device=x.device)
     if lazy is not None and comp_r is None:
         raise ValueError("a deferred residual needs comp_r (the previous M)")
@@ -193,8 +205,14 @@ def mq(x: torch.Tensor, q: torch.Tensor, plan: Plan, comp_r: Optional[torch.Tens
         t = plan.tables(x.device)
         lp, lq, ls = lazy if lazy is not None else (None, None, 0.0)
         _native.lib().powersgd_mq(x, q, p, t["mat"], t["tiles0"], 0, comp_r, beta, gamma, xout, plan.rank,
-                                  lazy_p=lp, lazy_q=lq, lazy_scale=float(ls))
+                                  lazy_p=lp, lazy_q=lq, lazy_scale=float(ls), zeroed=bool(zeroed) and out is not None,
+                                  bump=bump, vec=vec if plan.v_total else None,
+                                  vec_idx=t["vec_idx"] if vec is not None and plan.v_total else None)
         return p
+    if bump is not None:
+        bump.add_(1)
+    if vec is not None:
+        vec.copy_(gather_vectors(x, plan))
     for (xo, n, m, r, po, qo) in plan.mats:
         mx = x[xo:xo + n * m]
         if xout is not None:
@@ -210,12 +228,15 @@ def mq(x: torch.Tensor, q: torch.Tensor, plan: Plan, comp_r: Optional[torch.Tens
     return p
 
 
-def mtp(x: torch.Tensor, p: torch.Tensor, plan: Plan, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Q_i = M_i^T P_i for every matrix (flat Q buffer, or ``out``)."""
+def mtp(x: torch.Tensor, p: torch.Tensor, plan: Plan, out: Optional[torch.Tensor] = None,
+        zeroed: bool = False) -> torch.Tensor:
+    """Q_i = M_i^T P_i for every matrix (flat Q buffer, or ``out``; ``zeroed``: ``out`` was
+    already cleared, by :func:`orthogonalize`'s launch)."""
     q = out if out is not None else torch.empty(plan.q_total, dtype=torch.float32, device=x.device)
     if _native.use_native(x):
         t = plan.tables(x.device)
-        _native.lib().powersgd_mq(x, p, q, t["mat"], t["tiles1"], 1, None, 1.0, 1.0, None, plan.rank)
+        _native.lib().powersgd_mq(x, p, q, t["mat"], t["tiles1"], 1, None, 1.0, 1.0, None, plan.rank,
+                                  zeroed=bool(zeroed) and out is not None)
         return q
     for (xo, n, m, r, po, qo) in plan.mats:
         torch.mm(x[xo:xo + n * m].view(n, m).t(), p[po:po + n * r].view(n, r), out=q[qo:qo + m * r].view(m, r))
@@ -223,16 +244,30 @@ def mtp(x: torch.Tensor, p: torch.Tensor, plan: Plan, out: Optional[torch.Tensor
 
 
 def pqt(p: torch.Tensor, q: torch.Tensor, plan: Plan, out: Optional[torch.Tensor], resid: Optional[torch.Tensor] = None,
-        scale: float = 1.0) -> None:
+        scale: float = 1.0, save: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+        vec: Optional[torch.Tensor] = None, vec_scale: float = 1.0) -> None:
     """out[matrix i] = scale * P_i Q_i^T (vector segments untouched); with ``resid`` (holding x)
     also resid[matrix i] -= out in the same pass (PowerSGD residual update).  ``scale`` = 1/W
     folds the average of the summed Q into this pass (no separate division kernel).
-    ``out=None``: only the residual update (materialising a deferred residual)."""
+    ``out=None``: only the residual update (materialising a deferred residual).
+    ``save = (P', Q')``: copies of ``p`` and ``q`` stored by the same launch.  ``vec``: the
+    packed 1-D segments, scattered into ``out`` times ``vec_scale`` (:func:`scatter_vectors`)."""
     ref = out if out is not None else resid
+    if vec is not None and out is None:
+        raise ValueError("pqt: the 1-D segments need out")
     if _native.use_native(ref):
         t = plan.tables(ref.device)
-        _native.lib().powersgd_pqt(p, q, out, t["mat"], t["tilesp"], resid, plan.rank, float(scale))
+        sp, sq = save if save is not None else (None, None)
+        fv = vec is not None and plan.v_total > 0
+        _native.lib().powersgd_pqt(p, q, out, t["mat"], t["tilesp"], resid, plan.rank, float(scale), save_p=sp,
+                                   save_q=sq, vec=vec.float().contiguous() if fv else None,
+                                   vec_idx=t["vec_idx"] if fv else None, vec_scale=float(vec_scale))
         return
+    if save is not None:
+        save[0].copy_(p)
+        save[1].copy_(q)
+    if vec is not None:
+        scatter_vectors(vec, plan, out, vec_scale)
     for (xo, n, m, r, po, qo) in plan.mats:
         o = torch.mm(p[po:po + n * r].view(n, r), q[qo:qo + m * r].view(m, r).t())
         if scale != 1.0:

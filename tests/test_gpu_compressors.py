@@ -237,10 +237,12 @@ def test_powersgd_fused_memory_gpu_matches_cpu_unfused(monkeypatch):
 
     real = PS.randn_shared
 
-    def shared_q(n, seed, device, step=None):
+    def shared_q(n, seed, device, step=None, zero=None):
         if torch.device(device).type == "cpu":
+            if zero is not None:
+                zero.zero_()
             return real(n, seed, "cuda").cpu()
-        return real(n, seed, device, step=step)
+        return real(n, seed, device, step=step, zero=zero)
 
     monkeypatch.setattr(PS, "randn_shared", shared_q)
 
@@ -633,3 +635,59 @@ def test_dgc_sample_select_is_exact_kth_largest():
         ref = torch.topk(samp[o:o + n_s].abs(), k).values.min()
         assert torch.equal(thr[s], ref), (s, float(thr[s]), float(ref))
         o += n_s
+
+
+def test_powersgd_step_level_gpu_merged_launches_match_per_bucket_and_cpu():
+    """Several buckets on the GPU: the step-level exchange (one M^T P launch over every bucket,
+    fused P / Q clears, fused P / Q copies, 1-D segments moved inside the product launches,
+    device step counter advanced inside P = M Q) trains like the per-bucket immediate exchange
+    and like the CPU reference path (same Q: the Philox draw is host/device identical)."""
+    import torch.nn as nn
+    import torch.nn.functional as F
+
+    from grace_amd import grace_from_params
+    from grace_amd.ops import powersgd as PS
+    from grace_amd.parallel import DistributedOptimizer
+    from grace_amd.parallel.comm import LocalComm
+
+    real = PS.randn_shared
+
+    def train(dev, step_level, steps=3):
+        torch.manual_seed(0)
+        model = nn.Sequential(nn.Conv2d(3, 8, 3, padding=1), nn.ReLU(), nn.Conv2d(8, 16, 3, padding=1), nn.ReLU(),
+                              nn.AdaptiveAvgPool2d(2), nn.Flatten(), nn.Linear(64, 300), nn.ReLU(),
+                              nn.Linear(300, 200), nn.ReLU(), nn.Linear(200, 10)).to(dev)
+        grc = grace_from_params({"compressor": "powersgd", "compress_rank": 2, "memory": "powersgd",
+                                 "communicator": "allreduce", "world_size": 1}, comm=LocalComm())
+        opt = DistributedOptimizer(torch.optim.SGD(model.parameters(), lr=0.05, momentum=0.5), grc,
+                                   named_parameters=model.named_parameters(), bucket_cap_mb=0.1,
+                                   overlap=False, group_collectives=False)
+        grc.compressor.enable_step_level(step_level)
+        assert len(opt.engine.buckets) >= 3
+        for s in range(steps):
+            g = torch.Generator().manual_seed(100 * s)
+            x, y = torch.randn(4, 3, 8, 8, generator=g).to(dev), torch.randint(0, 10, (4,), generator=g).to(dev)
+            opt.zero_grad()
+            F.cross_entropy(model(x), y).backward()
+            opt.step()
+        if dev == "cuda" and step_level:
+            assert grc.compressor._arena.get("mtp") is not None  # the merged launch ran
+        return [p.detach().cpu() for p in model.parameters()]
+
+    def shared_q(n, seed, device, step=None, zero=None):  # CPU path: the device generator's draw
+        if torch.device(device).type == "cpu":
+            if zero is not None:
+                zero.zero_()
+            return real(n, seed, "cuda").cpu()
+        return real(n, seed, device, step=step, zero=zero)
+
+    PS.randn_shared = shared_q
+    try:
+        a = train("cuda", True)
+        b = train("cuda", False)
+        c = train("cpu", True)
+    finally:
+        PS.randn_shared = real
+    for pa, pb, pc in zip(a, b, c):
+        torch.testing.assert_close(pa, pb, rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(pa, pc, rtol=1e-4, atol=1e-5)

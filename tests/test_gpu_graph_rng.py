@@ -119,3 +119,28 @@ def test_graph_replay_randomk_roundtrip_consistent():
         masks.append(nz.clone())
     assert not torch.equal(masks[0], masks[1])
     assert int(masks[0].sum()) == int(masks[2].sum())
+
+
+def test_graph_replay_powersgd_post_bump_counter():
+    """PowerSGD advances its device step counter inside the P = M Q launch (no add_ kernel):
+    every replay still draws a fresh Q (a new P) and state_dict() reports executed steps."""
+    x, _ = _bucket()
+    comp = Z.PowerSGDCompressor(rank=2)
+
+    def fn():
+        payload, ctx = comp.compress(x, "rng_bucket")
+        return ctx.extra["p"]
+
+    g, out = _capture(fn)
+    seen = []
+    for _ in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        seen.append(out.clone())
+    assert not torch.equal(seen[0], seen[1]) and not torch.equal(seen[1], seen[2])
+    comp.state_dict()
+    assert comp.steps["rng_bucket"] == 5
+    # the next eager step continues the sequence: the same Q as a fresh compressor at step 6
+    ref = Z.PowerSGDCompressor(rank=2)
+    ref.steps["rng_bucket"] = 5
+    torch.testing.assert_close(fn(), ref.compress(x, "rng_bucket")[1].extra["p"], rtol=0, atol=0)
