@@ -653,7 +653,8 @@ void gram_orthonormalize(const Tensor& buf, const Tensor& mats, int64_t which, i
 void powersgd_pqt(const Tensor& P, const Tensor& Q, const c10::optional<Tensor>& out, const Tensor& mats,
                   const Tensor& tiles, const c10::optional<Tensor>& resid, int64_t max_r, double scale,
                   const c10::optional<Tensor>& save_p, const c10::optional<Tensor>& save_q,
-                  const c10::optional<Tensor>& vec, const c10::optional<Tensor>& vec_idx, double vec_scale) {
+                  const c10::optional<Tensor>& vec, const c10::optional<Tensor>& vec_idx, double vec_scale,
+                  const c10::optional<Tensor>& T) {
   CHECK_F32(P);
   CHECK_F32(Q);
   CHECK_I64(mats);
@@ -675,12 +676,33 @@ void powersgd_pqt(const Tensor& P, const Tensor& Q, const c10::optional<Tensor>&
     TORCH_CHECK(out.has_value() && tiles.numel() >= 3 && vec->numel() == vec_idx->numel(),
                 "the 1-D segments are scattered by a P Q^T launch with tiles into out");
   }
+  if (T.has_value()) {
+    CHECK_F32((*T));
+    TORCH_CHECK(max_r <= 4 && T->numel() * 6 >= mats.numel() * 16, "T: fp32 [n_mat][16], r <= 4");
+  }
   DevGuard guard(P.device());
   grace::powersgd_pqt(P.data_ptr<float>(), Q.data_ptr<float>(), opt_f32_mut(out), mats.data_ptr<int64_t>(),
                       tiles.data_ptr<int32_t>(), (int)(tiles.numel() / 3), opt_f32_mut(resid), (float)scale,
                       (int)max_r, opt_f32_mut(save_p), opt_f32_mut(save_q), opt_f32(vec),
                       vec_idx.has_value() ? vec_idx->data_ptr<int64_t>() : nullptr,
-                      vec.has_value() ? vec->numel() : 0, (float)vec_scale, cur_stream());
+                      vec.has_value() ? vec->numel() : 0, (float)vec_scale, opt_f32(T), cur_stream());
+}
+
+void powersgd_mtp_gram(const Tensor& x, const Tensor& P, const Tensor& Q, const Tensor& mats, const Tensor& tiles,
+                       int64_t n_mat, const Tensor& T, int64_t passes, int64_t max_r) {
+  CHECK_F32(x);
+  CHECK_F32(P);
+  CHECK_F32(Q);
+  CHECK_F32(T);
+  CHECK_I64(mats);
+  CHECK_I32(tiles);
+  TORCH_CHECK(max_r <= 4, "powersgd_mtp_gram: r <= 4 (larger ranks orthonormalise with the MFMA Gram kernels)");
+  TORCH_CHECK(mats.numel() >= 6 * n_mat && T.numel() >= 16 * n_mat, "powersgd_mtp_gram: table sizes");
+  TORCH_CHECK(passes >= 1 && passes <= 4, "powersgd_mtp_gram: 1..4 passes");
+  DevGuard guard(x.device());
+  grace::powersgd_mtp_gram(x.data_ptr<float>(), P.data_ptr<float>(), Q.data_ptr<float>(), mats.data_ptr<int64_t>(),
+                           tiles.data_ptr<int32_t>(), (int)(tiles.numel() / 3), (int)n_mat, T.data_ptr<float>(),
+                           (int)passes, (int)max_r, cur_stream());
 }
 
 void philox_normal(const Tensor& out, int64_t seed, const c10::optional<Tensor>& step,
@@ -1262,7 +1284,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("powersgd_pqt", &powersgd_pqt, py::arg("P"), py::arg("Q"), py::arg("out"), py::arg("mats"), py::arg("tiles"),
         py::arg("resid"), py::arg("max_r"), py::arg("scale") = 1.0, py::arg("save_p") = py::none(),
         py::arg("save_q") = py::none(), py::arg("vec") = py::none(), py::arg("vec_idx") = py::none(),
-        py::arg("vec_scale") = 1.0);
+        py::arg("vec_scale") = 1.0, py::arg("T") = py::none());
+  m.def("powersgd_mtp_gram", &powersgd_mtp_gram);
   m.def("philox_normal", &philox_normal, py::arg("out"), py::arg("seed"), py::arg("step") = py::none(),
         py::arg("zero") = py::none());
   m.def("cast16", &cast16);

@@ -127,8 +127,12 @@ void gram_orthonormalize(float* buf, const int64_t* mats, int n_mat, int which, 
 // out may be null (resid only); save_p / save_q: copies of P and Q (same offsets), may be null
 void powersgd_pqt(const float* P, const float* Q, float* out, const int64_t* mats, const int32_t* tiles, int n_tiles,
                   float* resid, float scale, int max_r, float* save_p, float* save_q, const float* vec,
-                  const int64_t* vec_idx, int64_t n_vec, float vec_scale,
-                  hipStream_t stream);  // + out[vec_idx[e]] = vec_scale * vec[e]
+                  const int64_t* vec_idx, int64_t n_vec, float vec_scale, const float* T,
+                  hipStream_t stream);  // + out[vec_idx[e]] = vec_scale * vec[e]; T (r <= 4): P T, Q T
+// Q = M^T P (P un-normalised) plus, in the same launch, T_i (fp32 [n_mat][16]) with P_i T_i orthonormal
+// (r <= 4; n_mat workgroups ahead of the product tiles); Q must be cleared beforehand
+void powersgd_mtp_gram(const float* x, const float* P, float* Q, const int64_t* mats, const int32_t* tiles,
+                       int n_tiles, int n_mat, float* T, int passes, int max_r, hipStream_t stream);
 void philox_normal(float* out, int64_t n, SeedArg seed, hipStream_t stream, float* zero = nullptr,
                    int64_t zn = 0);  // also clears zero[0, zn)
 

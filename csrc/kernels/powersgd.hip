@@ -54,7 +54,7 @@ __device__ __forceinline__ Mat load_mat(const int64_t* __restrict__ mats, int i)
 // ran at 2.6-4.4 TB/s; MFMA utilisation 0.25-1.8 %, profiles/r1_pmc_powersgd.txt.)
 constexpr int kRB0 = 16, kCS0 = 2048;     // ps_mq: rows per block, columns per strip
 constexpr int kCBV = 1024, kCBS = 256;    // ps_mtp / ps_pqt: columns per block (16-B / 4-B path)
-constexpr int kRSP = 32;                  // rows per strip: ps_pqt (ps_mtp: per-matrix, from the tile table)
+constexpr int kRSP = 32;                  // rows per strip, at most: ps_pqt (the tile gives its strip; ps_mtp: per-matrix)
 constexpr int kPB = 8;                    // rows per batch: independent 16-B loads in flight per thread
 
 
@@ -289,12 +289,27 @@ __global__ __launch_bounds__(kBlock) void ps_mq_kernel(const float* __restrict__
 // loads in flight, the block's partial Q is transposed through LDS into address order, and the
 // strip's atomics go out as contiguous wave-wide runs (per-lane atomics 64 B apart measured 1.8
 // TB/s for VGG-16 fc6; a block covering only 1 KB of each row read slower than one covering 4 KB).
+template <int SR>
+__device__ void gram_t_block(const float* __restrict__ A, int64_t len, int r, int passes, float* __restrict__ Tout,
+                             float4* __restrict__ stage);
+
+// gram: the first n_gram workgroups do not multiply -- workgroup i computes the orthonormalising
+// transform T_i of P_i (r <= 4, gram_t_block) while the others stream M: the Gram work hides
+// under this bandwidth-bound launch instead of idling the chip in a launch of its own.  Q is then
+// M^T P_raw, and Q T / P T are formed where they are consumed (ps_pqt).
 template <int R, int kPBm>  // kPBm: rows per batch (independent 16-B loads in flight per thread)
 __global__ __launch_bounds__(kBlock) void ps_mtp_kernel(const float* __restrict__ x, const float* __restrict__ Pall,
                                                         float* __restrict__ Qall, const int64_t* __restrict__ mats,
-                                                        const int32_t* __restrict__ tiles) {
-  __shared__ float red[kCBV * R];
-  const int* tl = tiles + 3 * blockIdx.x;
+                                                        const int32_t* __restrict__ tiles, int n_gram,
+                                                        float* __restrict__ Tout, int passes) {
+  __shared__ __align__(16) float red[kCBV * R];
+  if ((int)blockIdx.x < n_gram) {  // block-uniform; red doubles as its row staging buffer
+    const Mat g = load_mat(mats, blockIdx.x);
+    gram_t_block<(kCBV * R) / (kBlock * 4)>(Pall + g.p_off, g.n, (int)g.r, passes, Tout + 16 * (int64_t)blockIdx.x,
+                                            reinterpret_cast<float4*>(red));
+    return;
+  }
+  const int* tl = tiles + 3 * (blockIdx.x - n_gram);
   const Mat mt = load_mat(mats, tl[0]);
   const int64_t n = mt.n, m = mt.m;
   const int r = (int)mt.r;
@@ -363,29 +378,73 @@ __global__ __launch_bounds__(kBlock) void ps_pqt_kernel(const float* __restrict_
                                                         float* out, const int64_t* __restrict__ mats,
                                                         const int32_t* __restrict__ tiles, float* __restrict__ resid,
                                                         float scale, float* __restrict__ save_p,
-                                                        float* __restrict__ save_q, VecMove vm) {  // out == nullptr: residual update only
+                                                        float* __restrict__ save_q, VecMove vm,
+                                                        const float* __restrict__ Tall) {  // out == nullptr: residual update only
   for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < vm.n; e += (int64_t)gridDim.x * kBlock)
     out[vm.idx[e]] = vm.vec[e] * vm.scale;
   const int* tl = tiles + 3 * blockIdx.x;
   const Mat mt = load_mat(mats, tl[0]);
+  // Tall (r <= 4): the orthonormalising transform of matrix tl[0] (ps_mtp's gram workgroups): the
+  // P / Q rows read here are P_raw / M^T P_raw, and P T / (M^T P_raw) T = M^T (P T) are formed in
+  // registers
+  float tt[(R <= 4) ? 4 : 1][(R <= 4) ? 4 : 1];
+  const bool use_t = R <= 4 && Tall != nullptr;
+  if constexpr (R <= 4) {
+    if (use_t) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) tt[i][j] = Tall[16 * (int64_t)tl[0] + 4 * i + j];
+    }
+  }
+  auto xform = [&](float (&v)[R]) {
+    if constexpr (R <= 4) {
+      if (use_t) {
+        float o[R];
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+          float a = 0.f;
+#pragma unroll
+          for (int i = 0; i < R; ++i) a = fmaf(v[i], tt[i][j], a);
+          o[j] = a;
+        }
+#pragma unroll
+        for (int j = 0; j < R; ++j) v[j] = o[j];
+      }
+    }
+  };
   const int64_t n = mt.n, m = mt.m;
   const int r = (int)mt.r;
   const float* P = Pall + mt.p_off;
   const float* Q = Qall + mt.q_off;
-  const int64_t r0 = (int64_t)tl[1] * kRSP;
-  const int64_t r1 = r0 + kRSP < n ? r0 + kRSP : n;
+  // tl[1] = first row, tl[2] = column block | rows in the strip (<= kRSP) << 20: short strips
+  // (more workgroups) for buckets of small matrices, chosen on the host
+  const int64_t rows = tl[2] >> 20;
+  const int64_t r0 = tl[1];
+  const int64_t r1 = r0 + rows < n ? r0 + rows : n;
+  const int cblk = tl[2] & 0xfffff;
   // save_p / save_q (the deferred residual's copies of this step's P and Q, same offsets): the
   // first column block of every row strip stores the strip's P rows, the first row strip stores
   // Q below (each element exactly once; replaces two copy launches per bucket)
-  if (save_p != nullptr && tl[2] == 0)
-    for (int64_t e = threadIdx.x; e < (r1 - r0) * r; e += kBlock) save_p[mt.p_off + r0 * r + e] = P[r0 * r + e];
+  if (save_p != nullptr && cblk == 0)
+    for (int64_t row = r0 + threadIdx.x; row < r1; row += kBlock) {
+      float p[R];
+      load_small_row<R>(P, row, r, p);
+      xform(p);
+#pragma unroll
+      for (int j = 0; j < R; ++j)
+        if (j < r) save_p[mt.p_off + row * r + j] = p[j];
+    }
   const bool save_q_here = save_q != nullptr && tl[1] == 0;
   if (mat_vec(mt)) {
-    const int64_t c = (int64_t)tl[2] * kCBV + 4 * threadIdx.x;
+    const int64_t c = (int64_t)cblk * kCBV + 4 * threadIdx.x;
     if (c >= m) return;
     float q[4][R];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) load_small_row<R>(Q, c + t, r, q[t]);
+    for (int t = 0; t < 4; ++t) {
+      load_small_row<R>(Q, c + t, r, q[t]);
+      xform(q[t]);
+    }
     if (save_q_here)
 #pragma unroll
       for (int t = 0; t < 4; ++t)
@@ -405,6 +464,7 @@ __global__ __launch_bounds__(kBlock) void ps_pqt_kernel(const float* __restrict_
         if (row >= r1) break;
         float p[R];
         load_small_row<R>(P, row, r, p);
+        xform(p);
         float o[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -421,10 +481,11 @@ __global__ __launch_bounds__(kBlock) void ps_pqt_kernel(const float* __restrict_
       }
     }
   } else {
-    const int64_t c = (int64_t)tl[2] * kCBS + threadIdx.x;
+    const int64_t c = (int64_t)cblk * kCBS + threadIdx.x;
     if (c >= m) return;
     float q[R];
     load_small_row<R>(Q, c, r, q);
+    xform(q);
     if (save_q_here)
 #pragma unroll
       for (int j = 0; j < R; ++j)
@@ -432,6 +493,7 @@ __global__ __launch_bounds__(kBlock) void ps_pqt_kernel(const float* __restrict_
     for (int64_t row = r0; row < r1; ++row) {
       float p[R];
       load_small_row<R>(P, row, r, p);
+      xform(p);
       float v = 0.f;
 #pragma unroll
       for (int j = 0; j < R; ++j) v = fmaf(p[j], q[j], v);
@@ -536,6 +598,144 @@ __device__ __forceinline__ void mgs_gram_metric_reg(const double (&G)[4][4], dou
 #pragma unroll
       for (int a = 0; a <= i; ++a) Tm[a][j] -= pr * Tm[a][i];
     }
+  }
+}
+
+// The orthonormalising transform of one n x r block A (r <= 4) WITHOUT rewriting A: T = T_1 T_2
+// (CholQR2 in the Gram metric, fp64 Gram sums, as gram_small_kernel) such that A T has orthonormal
+// columns; pass 2's rows fl(A T_1) are formed on the fly from A.  Tout: fp32 4 x 4, row-major,
+// zero outside r x r.  Whole workgroup; block-uniform control flow.
+template <int SR>  // rows per thread staged per round (the stage holds kBlock * SR rows of 16 B)
+__device__ void gram_t_block(const float* __restrict__ A, int64_t len, int r, int passes, float* __restrict__ Tout,
+                             float4* __restrict__ stage) {
+  __shared__ double red[kBlock / kWave][10];
+  __shared__ float tcur[4][4];
+  __shared__ double tacc[4][4];
+  __shared__ double gG[8][4], gT[4][4];
+  const bool vec = r == 4 && (reinterpret_cast<uintptr_t>(A) & 15) == 0;
+  if (threadIdx.x < 16) {
+    const int i = threadIdx.x >> 2, j = threadIdx.x & 3;
+    tcur[i][j] = i == j ? 1.f : 0.f;
+    tacc[i][j] = i == j ? 1.0 : 0.0;
+  }
+  __syncthreads();
+  for (int pass = 0; pass < passes; ++pass) {
+    float t[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) t[i][j] = tcur[i][j];
+    double s[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) s[k] = 0.0;
+    // rounds of kBlock * SR rows: the SR 16-B loads of a thread go out together and land in the
+    // thread's own slots of the stage (no barrier: each thread reads back only what it wrote),
+    // then the rows are consumed one at a time -- latency of one round trip per round while the
+    // fp64 math stays rolled (VGPRs: this workgroup's register budget is the whole launch's)
+#pragma unroll 1
+    for (int64_t base = 0; base < len; base += (int64_t)kBlock * SR) {
+      if (vec) {
+#pragma unroll
+        for (int u = 0; u < SR; ++u) {
+          const int64_t row = base + (int64_t)u * kBlock + threadIdx.x;
+          stage[u * kBlock + threadIdx.x] =
+              row < len ? reinterpret_cast<const float4*>(A)[row] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+#pragma unroll 1
+    for (int u = 0; u < SR; ++u) {
+      const int64_t row = base + (int64_t)u * kBlock + threadIdx.x;
+      float a[4];
+      if (vec) {
+        const float4 v = stage[u * kBlock + threadIdx.x];
+        a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = i < r && row < len ? A[row * r + i] : 0.f;
+      }
+      float o[4];
+      if (pass == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = a[j];
+      } else {  // the row of A T_acc, with gram_small_kernel's apply float ops
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float v = 0.f;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v = fmaf(a[i], t[i][j], v);
+          o[j] = v;
+        }
+      }
+      int k = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = i; j < 4; ++j) s[k++] += (double)o[i] * (double)o[j];
+    }
+    }
+#pragma unroll
+    for (int k = 0; k < 10; ++k) s[k] = wave_sum(s[k]);
+    if (lane_id() == 0)
+#pragma unroll
+      for (int k = 0; k < 10; ++k) red[wave_id()][k] = s[k];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      // the Gram and the MGS coefficients in LDS (mgs_gram_metric, runtime loops): this workgroup
+      // runs beside the bandwidth-bound product, so its latency is hidden, while register arrays
+      // here (mgs_gram_metric_reg) would set the WHOLE launch's VGPR budget (200, occupancy 2)
+      // (loops kept rolled: unrolled, this one lane's fp64 temporaries set the register budget)
+#pragma unroll 1
+      for (int e = 0; e < 16; ++e) {
+        const int i = e >> 2, j = e & 3, lo = i < j ? i : j, hi = i < j ? j : i;
+        const int k = lo * 4 - (lo * (lo - 1)) / 2 + (hi - lo);  // packed upper-triangle index
+        double v = 0.0;
+#pragma unroll 1
+        for (int w = 0; w < kBlock / kWave; ++w) v += red[w][k];  // fixed order: deterministic
+        gG[i][j] = v;
+        gT[i][j] = i == j ? 1.0 : 0.0;
+      }
+#pragma unroll 1
+      for (int i = 0; i < r; ++i) {  // mgs_gram_metric on the 4 x 4 corner
+        double nn = 0.0;
+#pragma unroll 1
+        for (int a = 0; a <= i; ++a)
+#pragma unroll 1
+          for (int b = 0; b <= i; ++b) nn += gT[a][i] * gG[a][b] * gT[b][i];
+        const double nrm = nn > 1e-10 * gG[i][i] && nn > 0.0 ? sqrt(nn) : 0.0;
+        const double inv = nrm > 1e-30 ? 1.0 / nrm : 0.0;
+#pragma unroll 1
+        for (int a = 0; a <= i; ++a) gT[a][i] *= inv;
+#pragma unroll 1
+        for (int j = i + 1; j < r; ++j) {
+          double pr = 0.0;
+#pragma unroll 1
+          for (int a = 0; a <= i; ++a)
+#pragma unroll 1
+            for (int b = 0; b <= j; ++b) pr += gT[a][i] * gG[a][b] * gT[b][j];
+#pragma unroll 1
+          for (int a = 0; a <= i; ++a) gT[a][j] -= pr * gT[a][i];
+        }
+      }
+#pragma unroll 1
+      for (int e = 0; e < 16; ++e) {  // T_acc <- T_acc T_pass (fp64; gG reused as scratch)
+        const int i = e >> 2, j = e & 3;
+        double v = 0.0;
+#pragma unroll 1
+        for (int l = 0; l < 4; ++l) v += tacc[i][l] * gT[l][j];
+        gG[4 + i][j] = v;
+      }
+#pragma unroll 1
+      for (int e = 0; e < 16; ++e) {
+        const int i = e >> 2, j = e & 3;
+        tacc[i][j] = gG[4 + i][j];
+        tcur[i][j] = (float)gG[4 + i][j];
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < 16) {
+    const int i = threadIdx.x >> 2, j = threadIdx.x & 3;
+    Tout[threadIdx.x] = i < r && j < r ? tcur[i][j] : 0.f;
   }
 }
 
@@ -757,7 +957,7 @@ void launch_mq(const float* x, const float* small, float* out, const int64_t* ma
                VecMove vm, hipStream_t stream) {
   const Lazy none{nullptr, nullptr, 0.f};
   if (mode == 1)  // (16 rows per batch measured slower: 0.855 vs 0.755 ms VGG-16 exchange)
-    ps_mtp_kernel<R, kPB><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles);
+    ps_mtp_kernel<R, kPB><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles, 0, nullptr, 0);
   else if (xout == nullptr)
     ps_mq_kernel<R, 0><<<n_tiles, kBlock, 0, stream>>>(x, small, out, mats, tiles, nullptr, 0.f, 0.f, nullptr, none,
                                                        bump, vm);
@@ -789,6 +989,15 @@ void powersgd_mq(const float* x, const float* small, float* out, int64_t out_len
   else launch_mq<16>(x, small, out, mats, tiles, n_tiles, mode, comp_r, beta, gamma, xout, lz, bump, vm, stream);
 }
 
+void powersgd_mtp_gram(const float* x, const float* P, float* Q, const int64_t* mats, const int32_t* tiles,
+                       int n_tiles, int n_mat, float* T, int passes, int max_r, hipStream_t stream) {
+  const int nb = n_tiles + n_mat;
+  if (nb <= 0) return;
+  if (max_r <= 1) ps_mtp_kernel<1, kPB><<<nb, kBlock, 0, stream>>>(x, P, Q, mats, tiles, n_mat, T, passes);
+  else if (max_r <= 2) ps_mtp_kernel<2, kPB><<<nb, kBlock, 0, stream>>>(x, P, Q, mats, tiles, n_mat, T, passes);
+  else ps_mtp_kernel<4, kPB><<<nb, kBlock, 0, stream>>>(x, P, Q, mats, tiles, n_mat, T, passes);
+}
+
 void gram_orthonormalize(float* buf, const int64_t* mats, int n_mat, int which, const int32_t* gtiles,
                          int n_gtiles, const int32_t* gtile_begin, double* partials, float* T, int passes,
                          int max_r, float* zero, int64_t zn, hipStream_t stream) {
@@ -810,14 +1019,14 @@ void gram_orthonormalize(float* buf, const int64_t* mats, int n_mat, int which, 
 
 void powersgd_pqt(const float* P, const float* Q, float* out, const int64_t* mats, const int32_t* tiles, int n_tiles,
                   float* resid, float scale, int max_r, float* save_p, float* save_q, const float* vec,
-                  const int64_t* vec_idx, int64_t n_vec, float vec_scale, hipStream_t stream) {
+                  const int64_t* vec_idx, int64_t n_vec, float vec_scale, const float* T, hipStream_t stream) {
   if (n_tiles <= 0) return;  // (the binding refuses vector segments without tiles)
   const VecMove vm{const_cast<float*>(vec), vec_idx, vec != nullptr ? n_vec : 0, vec_scale};
-  if (max_r <= 1) ps_pqt_kernel<1><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid, scale, save_p, save_q, vm);
-  else if (max_r <= 2) ps_pqt_kernel<2><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid, scale, save_p, save_q, vm);
-  else if (max_r <= 4) ps_pqt_kernel<4><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid, scale, save_p, save_q, vm);
-  else if (max_r <= 8) ps_pqt_kernel<8><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid, scale, save_p, save_q, vm);
-  else ps_pqt_kernel<16><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid, scale, save_p, save_q, vm);
+  if (max_r <= 1) ps_pqt_kernel<1><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid, scale, save_p, save_q, vm, T);
+  else if (max_r <= 2) ps_pqt_kernel<2><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid, scale, save_p, save_q, vm, T);
+  else if (max_r <= 4) ps_pqt_kernel<4><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid, scale, save_p, save_q, vm, T);
+  else if (max_r <= 8) ps_pqt_kernel<8><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid, scale, save_p, save_q, vm, T);
+  else ps_pqt_kernel<16><<<n_tiles, kBlock, 0, stream>>>(P, Q, out, mats, tiles, resid, scale, save_p, save_q, vm, T);
 }
 
 void philox_normal(float* out, int64_t n, SeedArg seed, hipStream_t stream, float* zero, int64_t zn) {

@@ -61,6 +61,7 @@ class PowerSGDCompressor(BucketCompressor):
         self._arena = None
         self.matrix_collectives = 0  # matrix all-reduces issued (tests / monitoring)
         self._pq_prev = {}  # name -> [P | Q] of the last step (deferred residual), persistent
+        self._q_cleared = False  # the step's first P-clearing launch also cleared the Q arena
 
     def enable_step_level(self, on: bool = True):
         """Defer the P/Q exchange of every bucket to :meth:`step_flush` (called by the engine)."""
@@ -147,9 +148,17 @@ class PowerSGDCompressor(BucketCompressor):
         native = PS._native.use_native(x)
         # native: the P = M Q launch advances the device step counter (post-bump, no add kernel)
         step, step_t = self.advance(name, x.device, post=native)
-        p_out = self._arena_slice(name, plan) if defer else None
+        sl = p_out = self._arena_slice(name, plan) if defer else None
         if native and p_out is None:
             p_out = torch.empty(plan.p_total, dtype=torch.float32, device=x.device)
+        zero = p_out
+        a = self._arena
+        if native and sl is not None and not self._pending and not self.warm_start and a["off"][name][0] == 0:
+            # the step's first bucket: [Q arena | P arena] is one buffer and this bucket's P slice
+            # leads the P arena, so the launch that clears P clears the Q arena too (no memset
+            # before the step's M^T P launch)
+            zero = a["qp"][:a["q"].numel() + plan.p_total]
+            self._q_cleared = True
         zeroed = False
         q = self.q_memory.get(name) if self.warm_start else None
         if q is None or q.numel() != plan.q_total:
@@ -158,8 +167,10 @@ class PowerSGDCompressor(BucketCompressor):
             seed = fnv1a64(name.encode())
             # the same launch clears P for the accumulating P = M Q launch (no memset)
             q = PS.randn_shared(plan.q_total, seed if step_t is not None else mix_step(seed, step), x.device,
-                                step=step_t, zero=p_out if native else None)
+                                step=step_t, zero=zero if native else None)
             zeroed = native
+        elif zero is not p_out:
+            self._q_cleared = False
             # The reference orthogonalises this fresh Gaussian Q (dist/compressor/powersgd.py:43).  That cannot
             # change the result: MGS gives Q R^-1 with R upper triangular, so P = M Q R^-1 = P R^-1
             # and the orthonormal factor of P R^-1 is that of P -- orthogonalize(P) below yields the
@@ -204,16 +215,15 @@ class PowerSGDCompressor(BucketCompressor):
             plan = ctx.extra["plan"]
             mats += [(xo, n, m, r, mpo + bpo, mqo + bqo) for (xo, n, m, r, mpo, mqo) in plan.mats]
         orth = PS.Plan(self.rank_r, mats, [], po, qo, 0)
-        self._arena = {"key": key, "off": off, "p": torch.empty(po, dtype=torch.float32, device=dev),
-                       "q": torch.empty(qo, dtype=torch.float32, device=dev), "orth": orth}
+        qp = torch.empty(qo + po, dtype=torch.float32, device=dev)  # [Q arena | P arena]
+        self._arena = {"key": key, "off": off, "qp": qp, "p": qp[qo:], "q": qp[:qo], "orth": orth,
+                       "T": torch.empty(max(1, len(mats)) * 16, dtype=torch.float32, device=dev)}
 
     def _merged_mtp(self, entries):
         """(base tensor, plan) of one Q = M^T P launch over every bucket of the arena: each
         matrix's x offset is taken relative to the lowest bucket address (the buckets are separate
         allocations of one device; the kernel addresses them from that base).  None when it does
         not apply (one bucket, CPU, misaligned or mixed-device buffers)."""
-        if len(entries) < 2:
-            return None
         xs = [x for _, x, _ in entries]
         if not all(PS._native.use_native(x) and x.dtype == torch.float32 and x.is_contiguous()
                    and x.device == xs[0].device for x in xs):
@@ -243,6 +253,7 @@ class PowerSGDCompressor(BucketCompressor):
             key = tuple((name, ctx.extra["plan"].p_total, ctx.extra["plan"].q_total) for name, _, ctx in entries)
             if self._arena is None or self._arena["key"] != key:
                 self._build_arena(entries)  # first step (or a changed bucket set): re-home P
+                self._q_cleared = False  # (a clear, if any, went to the previous arena)
             a = self._arena
             p_all, q_all = a["p"], a["q"]
             for name, _, ctx in entries:
@@ -261,21 +272,36 @@ class PowerSGDCompressor(BucketCompressor):
         if comm is not None:
             comm.all_reduce(p_all)  # SUM over ranks: the orthonormalisation is scale invariant
             self.matrix_collectives += 1
-        if arena:
-            # all buckets, one launch -- which also clears the Q arena for the M^T P launches
-            PS.orthogonalize(p_all, self._arena["orth"], which="p", zero=q_all)
-        else:
-            for _, _, ctx in entries:
-                PS.orthogonalize(ctx.extra["p"], ctx.extra["plan"], which="p")
+        cleared, self._q_cleared = self._q_cleared, False
         merged = self._merged_mtp(entries) if arena else None
-        if merged is not None:
-            # Q = M^T P of every bucket in ONE launch: the small buckets' tiles fill in beside the
-            # big ones (per-bucket launches of the small conv buckets ran at ~2 TB/s)
+        if merged is not None and self.rank_r <= 4:
+            # ONE launch for the whole step: Q = M^T P of every bucket (the small buckets' tiles fill
+            # in beside the big ones) with the orthonormalising transforms T of every P computed by
+            # extra workgroups of the same launch; P stays as reduced, and P T / Q T are formed by
+            # the decompress launches (the Gram work hides under the bandwidth-bound product)
             base, plan_all = merged
-            PS.mtp(base, p_all, plan_all, out=q_all, zeroed=True)
+            if not cleared:
+                q_all.zero_()
+            T = self._arena["T"]
+            PS.mtp_gram(base, p_all, plan_all, q_all, T)
+            i = 0
+            for _, _, ctx in entries:
+                k = ctx.extra["plan"].n_mat
+                ctx.extra["T"] = T[16 * i:16 * (i + k)]
+                i += k
         else:
-            for _, x_after, ctx in entries:
-                PS.mtp(x_after, ctx.extra["p"], ctx.extra["plan"], out=ctx.extra["q"], zeroed=arena)  # Q = M^T P
+            if arena:
+                # all buckets, one launch -- which also clears the Q arena for the M^T P launches
+                PS.orthogonalize(p_all, self._arena["orth"], which="p", zero=None if cleared else q_all)
+            else:
+                for _, _, ctx in entries:
+                    PS.orthogonalize(ctx.extra["p"], ctx.extra["plan"], which="p")
+            if merged is not None:
+                base, plan_all = merged
+                PS.mtp(base, p_all, plan_all, out=q_all, zeroed=True)
+            else:
+                for _, x_after, ctx in entries:
+                    PS.mtp(x_after, ctx.extra["p"], ctx.extra["plan"], out=ctx.extra["q"], zeroed=arena)  # Q = M^T P
         if comm is not None:
             comm.all_reduce(q_all)  # SUM; the 1/W is applied inside the P Q^T pass
             self.matrix_collectives += 1
@@ -314,11 +340,12 @@ class PowerSGDCompressor(BucketCompressor):
             pp, qp = prev[:plan.p_total], prev[plan.p_total:]
             # the copies are stored by the decompress launch itself (it reads P and Q anyway)
             PS.pqt(ctx.extra["p"], ctx.extra["q"], plan, out, resid=None, scale=scale, save=(pp, qp), vec=vec,
-                   vec_scale=vec_scale)
+                   vec_scale=vec_scale, T=ctx.extra.pop("T", None))
             mem.lazy[name] = (pp, qp, scale, plan)
         else:
             # fused eager form / unfused: the residual buffer holds x; this pass leaves r = x - P Q^T
-            PS.pqt(ctx.extra["p"], ctx.extra["q"], plan, out, resid=resid, scale=scale, vec=vec, vec_scale=vec_scale)
+            PS.pqt(ctx.extra["p"], ctx.extra["q"], plan, out, resid=resid, scale=scale, vec=vec, vec_scale=vec_scale,
+                   T=ctx.extra.pop("T", None))
         return self.finish(out, ctx)
 
     def decompress(self, tensors, ctx):

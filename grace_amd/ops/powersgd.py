@@ -18,7 +18,14 @@ from .layout import SegmentLayout
 
 # ps_mq column strip (power of two, 512..65536) and the ps_mtp workgroup target per matrix
 # (row strips x 1024-column blocks): tuning knobs, GRACE_PS_MQ_COLS / GRACE_PS_MTP_WG
+_MQ_COLS_SET = "GRACE_PS_MQ_COLS" in os.environ
 _MQ_COLS = int(os.environ.get("GRACE_PS_MQ_COLS", "2048"))
+# workgroups a P = M Q launch should have before its column strips stop shrinking
+_MIN_WG = int(os.environ.get("GRACE_PS_MIN_WG", "4096"))
+# rows per P Q^T workgroup strip (1..32)
+_PQT_ROWS = int(os.environ.get("GRACE_PS_PQT_ROWS", "32"))
+if not 1 <= _PQT_ROWS <= 32:
+    raise ValueError("GRACE_PS_PQT_ROWS must be in [1, 32]")
 _MTP_WG = int(os.environ.get("GRACE_PS_MTP_WG", "1024"))
 if _MQ_COLS < 512 or _MQ_COLS > 65536 or _MQ_COLS & (_MQ_COLS - 1):
     raise ValueError("GRACE_PS_MQ_COLS must be a power of two in [512, 65536]")
@@ -38,6 +45,10 @@ class Plan:
     def n_mat(self) -> int:
         return len(self.mats)
 
+    def _mq_blocks(self, cs: int) -> int:
+        return sum(-(-n // 16) * -(-m // cs) for (_, n, m, _, _, _) in self.mats)
+
+
     def tables(self, device):
         key = str(device)
         t = self._dev.get(key)
@@ -45,7 +56,13 @@ class Plan:
             # work tables of csrc/kernels/powersgd.hip (ps_mq: 16 rows x 2048 columns; ps_mtp:
             # 1024 / 256 columns x per-matrix row strips; ps_pqt: 32 rows x 1024 / 256 columns)
             t0, t1, tp = [], [], []
-            cs = _MQ_COLS
+            cs, prs = _MQ_COLS, _PQT_ROWS
+            if not _MQ_COLS_SET:
+                # P = M Q runs faster with more workgroups: shorter column strips until the launch
+                # has _MIN_WG of them (VGG-16 fc6: 248 -> 234 us at 1024 columns; the P Q^T
+                # launches measured SLOWER with shorter row strips: 70 -> 75 us -- they stay at 32)
+                while cs > 512 and self._mq_blocks(cs) < _MIN_WG:
+                    cs //= 2
             lg = cs.bit_length() - 1
             for i, (xo, n, m, r, po, qo) in enumerate(self.mats):
                 cb = 1024 if (xo % 4 == 0 and m % 4 == 0) else 256
@@ -62,9 +79,9 @@ class Plan:
                 for c in range(ncb):
                     for s0 in range(0, n32, per):
                         t1.append((i, c, (s0 << 16) | min(per, n32 - s0)))
-                for rb in range((n + 31) // 32):
+                for r0 in range(0, n, prs):
                     for c in range((m + cb - 1) // cb):
-                        tp.append((i, rb, c))
+                        tp.append((i, r0, c | (min(prs, n - r0) << 20)))
 
             def it(lst):
                 return torch.tensor(lst, dtype=torch.int32, device=device).view(-1) if lst else \
@@ -243,15 +260,27 @@ def mtp(x: torch.Tensor, p: torch.Tensor, plan: Plan, out: Optional[torch.Tensor
     return q
 
 
+def mtp_gram(x: torch.Tensor, p: torch.Tensor, plan: Plan, out: torch.Tensor, T: torch.Tensor,
+             passes: int = 2) -> None:
+    """Native, rank <= 4: ``out`` (cleared beforehand) += M_i^T P_i with P_i as it is (NOT
+    orthonormalised), and in the same launch T [n_mat * 16] with P_i T_i orthonormal (CholQR2 in
+    the Gram metric, :func:`orthogonalize`'s numerics).  Consumers apply T: the orthonormal factor
+    is P T and the PowerSGD Q is (M^T P) T = M^T (P T) (:func:`pqt` ``T=``)."""
+    t = plan.tables(x.device)
+    _native.lib().powersgd_mtp_gram(x, p, out, t["mat"], t["tiles1"], plan.n_mat, T, int(passes), plan.rank)
+
+
 def pqt(p: torch.Tensor, q: torch.Tensor, plan: Plan, out: Optional[torch.Tensor], resid: Optional[torch.Tensor] = None,
         scale: float = 1.0, save: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
-        vec: Optional[torch.Tensor] = None, vec_scale: float = 1.0) -> None:
+        vec: Optional[torch.Tensor] = None, vec_scale: float = 1.0, T: Optional[torch.Tensor] = None) -> None:
     """out[matrix i] = scale * P_i Q_i^T (vector segments untouched); with ``resid`` (holding x)
     also resid[matrix i] -= out in the same pass (PowerSGD residual update).  ``scale`` = 1/W
     folds the average of the summed Q into this pass (no separate division kernel).
     ``out=None``: only the residual update (materialising a deferred residual).
     ``save = (P', Q')``: copies of ``p`` and ``q`` stored by the same launch.  ``vec``: the
-    packed 1-D segments, scattered into ``out`` times ``vec_scale`` (:func:`scatter_vectors`)."""
+    packed 1-D segments, scattered into ``out`` times ``vec_scale`` (:func:`scatter_vectors`).
+    ``T`` [n_mat * 16] (from :func:`mtp_gram`): ``p`` / ``q`` are taken as P T / Q T (the saved
+    copies too)."""
     ref = out if out is not None else resid
     if vec is not None and out is None:
         raise ValueError("pqt: the 1-D segments need out")
@@ -261,8 +290,14 @@ def pqt(p: torch.Tensor, q: torch.Tensor, plan: Plan, out: Optional[torch.Tensor
         fv = vec is not None and plan.v_total > 0
         _native.lib().powersgd_pqt(p, q, out, t["mat"], t["tilesp"], resid, plan.rank, float(scale), save_p=sp,
                                    save_q=sq, vec=vec.float().contiguous() if fv else None,
-                                   vec_idx=t["vec_idx"] if fv else None, vec_scale=float(vec_scale))
+                                   vec_idx=t["vec_idx"] if fv else None, vec_scale=float(vec_scale), T=T)
         return
+    if T is not None:
+        p, q = p.clone(), q.clone()
+        for i, (xo, n, m, r, po, qo) in enumerate(plan.mats):
+            ti = T[16 * i:16 * i + 16].view(4, 4)[:r, :r]
+            p[po:po + n * r] = (p[po:po + n * r].view(n, r) @ ti).reshape(-1)
+            q[qo:qo + m * r] = (q[qo:qo + m * r].view(m, r) @ ti).reshape(-1)
     if save is not None:
         save[0].copy_(p)
         save[1].copy_(q)
