@@ -2,7 +2,7 @@
 """GRACE exchange microbenchmark: the compress -> communicate -> decompress part of one
 training step, in isolation, on the real parameter shapes of a model.
 
-The model's parameters are bucketed exactly as in training (``GraceEngine``, 64 MB buckets);
+The model's parameters are bucketed exactly as in training (``GraceEngine``, 128 MB buckets as in bench.py);
 their gradient buckets are filled with N(0,1) data and ``engine.synchronize()`` -- every
 bucket's fused error-feedback compress, the collective, and the one-pass decode into the
 bucket -- is timed with HIP events (captured in a HIP graph when the pipeline is graph-safe,
@@ -58,7 +58,7 @@ PIPELINES = {
 }
 
 
-def run(name, model_name=None, iters=20, bucket_mb=64.0, graph=True, dev=None):
+def run(name, model_name=None, iters=20, bucket_mb=128.0, graph=True, dev=None):
     dev = dev or torch.device("cuda", 0)
     mname, params = PIPELINES[name]
     mname = model_name or mname
@@ -125,7 +125,8 @@ def main():
                     help=f"comma list of {sorted(PIPELINES)} or 'all'")
     ap.add_argument("--model", default=None)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--bucket-mb", type=float, default=128.0,
+                    help="GraceEngine bucket cap (128 MB: the training default of bench.py)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--json", action="store_true")
     a = ap.parse_args()
