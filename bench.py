@@ -423,6 +423,21 @@ def main() -> int:
             else:
                 comm_kind = "torch (native comm failed)"
     grc = grace_from_params(dict(w.grace, world_size=world))
+    # split graphs (critical stream A / side stream B / A2; see the capture below) unless the step
+    # overlaps its exchange with backward or DDP's hook runs immediately
+    ddp_defer = args.ddp_defer == "on" or (args.ddp_defer == "auto" and mode == "full")
+    split_planned = mode == "full" and (args.graph_split == "on" or (
+        args.graph_split == "auto" and not overlap and not (args.surface == "ddp" and not ddp_defer)))
+    main_stream = None
+    if split_planned:
+        # A and B must sit on DIFFERENT hardware queues: HIP deals streams of one priority to a few
+        # HW queues (GPU_MAX_HW_QUEUES, 4), and once the native RCCL runtime had created its
+        # streams the side stream shared the replay stream's queue -- the two graphs serialised
+        # (2494-2515 img/s at W = 1 vs 2746-2752 with the step on a high-priority stream, whose
+        # queue pool holds nothing else; profiles/r6_graph_split.txt)
+        main_stream = torch.cuda.Stream(dev, priority=-1)
+        main_stream.wait_stream(torch.cuda.current_stream(dev))
+        torch.cuda.set_stream(main_stream)
     ddp_state = ddp_stream = None
     if args.surface == "ddp":
         from grace_amd.parallel import GraceHookState, grace_comm_hook
@@ -433,13 +448,12 @@ def main() -> int:
         # reference's Horovod harness, not before every forward
         # a captured DDP step: the reducer's AccumulateGrad nodes take the stream current at
         # construction, so build DDP under the stream the step is captured and replayed on
-        ddp_stream = torch.cuda.Stream(dev) if mode == "full" else None
+        ddp_stream = (main_stream if main_stream is not None else torch.cuda.Stream(dev)) if mode == "full" else None
         with torch.cuda.stream(ddp_stream) if ddp_stream is not None else contextlib.nullcontext():
             model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], bucket_cap_mb=args.bucket_mb,
                                                               gradient_as_bucket_view=True, broadcast_buffers=False)
-        # deferred hook only where the step becomes split graphs (below: not with the native RCCL
-        # runtime in the graph); a forked DDP graph is host-bound (2352 vs 2468 img/s immediate)
-        ddp_defer = args.ddp_defer == "on" or (args.ddp_defer == "auto" and mode == "full" and rccl_obj is None)
+        # deferred hook where the step becomes split graphs (a forked DDP graph is host-bound:
+        # 2352 vs 2468 img/s immediate)
         ddp_state = GraceHookState(grc, model=model, defer=ddp_defer)
         model.register_comm_hook(ddp_state, grace_comm_hook)
         if ddp_stream is not None and hasattr(torch.autograd.graph, "set_warn_on_accumulate_grad_stream_mismatch"):
@@ -491,16 +505,12 @@ def main() -> int:
             # DDP records runtime-logging events (and reads them back with a host sync) in its
             # first 10 iterations: capture only after those
             cap_warm = max(3, args.warmup // 2) if args.surface == "engine" else max(11, args.warmup)
-            split = None if args.graph_split == "auto" else args.graph_split == "on"
-            if split is None:
-                # split graphs (critical / side stream, flag sync every 2 fork points): 2720 img/s at
-                # 0.28 ms of host issue vs the forked graph's 2708 at 9.2 ms; DDP 2690 (forked: 2352,
-                # host-bound); W = 2 sharing one GPU 3104 vs 2463 (profiles/r6_graph_split.txt).
-                # NOT with the native RCCL runtime's collectives in the graph: measured at W = 1
-                # (--force-dist) 2515 split vs 2719 forked -- the forked graph stays the RCCL default
-                split = rccl_obj is None
-            if overlap or (args.surface == "ddp" and not ddp_state.defer):
-                split = False  # the side stream must be joined on the capture stream after backward
+            # split graphs (critical / side stream, flag sync every 2 fork points): 2730-2750 img/s
+            # at 0.2 ms of host issue vs the forked graph's 2700-2720 at 9.2 ms, also with the native
+            # RCCL runtime in the step (--force-dist); DDP (deferred hook) 0.99 of the engine; W = 2
+            # sharing one GPU 3104 vs 2463 (profiles/r6_graph_split.txt).  Forked: overlap, or an
+            # immediate DDP hook (the side stream must be joined on the capture stream after backward)
+            split = split_planned
             run = GraphedStep(step, warmup=cap_warm, stream=ddp_stream,
                               capture_error_mode="thread_local" if world > 1 else None, split=split)
             graph_note = "full (split: A / side B / A2)" if run.split else "full"

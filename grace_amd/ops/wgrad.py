@@ -89,7 +89,8 @@ def _side(device: torch.device) -> "torch.cuda.Stream":
                     s = torch.cuda.ExternalStream(ptr, device=torch.device("cuda", idx))
                 else:
                     with torch.cuda.device(idx):
-                        s = torch.cuda.Stream()  # a high-priority side stream measured 20 ms/step (r3_graph_fork_knobs)
+                        # a high-priority side stream measured 20 ms/step (r3_graph_fork_knobs)
+                        s = torch.cuda.Stream(priority=int(os.environ.get("GRACE_SIDE_PRIO", "0")))
                 _streams[idx] = s
     return s
 
