@@ -149,6 +149,7 @@ class GraphedStep:
         # cannot be re-submitted while its previous launch still runs; alternating copies lets
         # the host submit step N+1 while step N executes.
         self.g_side = self.g_a2 = None
+        self._hp = None  # private high-priority replay stream (split, normal-priority callers)
         if self.split:
             self._capture_split(fn, pool, capture_error_mode)
             return
@@ -258,8 +259,26 @@ class GraphedStep:
 
     def _replay_split(self) -> torch.Tensor:
         # a graph is not bound to its capture stream: A and A2 replay on the caller's stream (two
-        # cross-stream joins per step instead of four), B on the side stream
-        cur = torch.cuda.current_stream()
+        # cross-stream joins per step instead of four), B on the side stream -- when the caller's
+        # stream is high priority.  A and B must sit on different HARDWARE queues, and HIP deals the
+        # streams of one priority to a few of them (GPU_MAX_HW_QUEUES): with more streams alive
+        # (the native RCCL runtime's) the side stream shared the caller's queue and the two graphs
+        # serialised (ResNet-50 2494 vs 2746 img/s, profiles/r6_graph_split.txt).  A normal-priority
+        # caller gets its replay moved to a private high-priority stream (bench.py runs the whole
+        # step on one, avoiding the two extra joins)
+        caller = torch.cuda.current_stream()
+        if caller.priority < 0:
+            return self._replay_split_on(caller)
+        hp = self._hp
+        if hp is None:
+            hp = self._hp = torch.cuda.Stream(caller.device, priority=-1)
+        hp.wait_stream(caller)
+        with torch.cuda.stream(hp):
+            loss = self._replay_split_on(hp)
+        caller.wait_stream(hp)
+        return loss
+
+    def _replay_split_on(self, cur) -> torch.Tensor:
         side = self.s_side
         if self.g_side is not None:
             side.wait_stream(cur)  # after the previous step's A2
