@@ -435,7 +435,9 @@ def main() -> int:
         # streams the side stream shared the replay stream's queue -- the two graphs serialised
         # (2494-2515 img/s at W = 1 vs 2746-2752 with the step on a high-priority stream, whose
         # queue pool holds nothing else; profiles/r6_graph_split.txt)
-        main_stream = torch.cuda.Stream(dev, priority=-1)
+        from grace_amd.ops.wgrad import dedicated_stream
+
+        main_stream = dedicated_stream(local, -1, "bench-main")
         main_stream.wait_stream(torch.cuda.current_stream(dev))
         torch.cuda.set_stream(main_stream)
     ddp_state = ddp_stream = None

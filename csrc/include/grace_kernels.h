@@ -293,7 +293,8 @@ void bias_act_backward(const void* dy, const void* y, bool fp32, int64_t M, int 
 void maxpool_forward(const void* x, bool fp32, int N, int H, int W, int C, int OH, int OW, int k, int s, int pad,
                      void* y, uint8_t* code, hipStream_t stream);
 void maxpool_backward(const void* dy, const uint8_t* code, bool fp32, int N, int H, int W, int C, int OH, int OW,
-                      int k, int s, int pad, void* dx, hipStream_t stream);
+                      int k, int s, int pad, void* dx, hipStream_t stream,
+                      const void* dy2 = nullptr);
 // global average pool backward over channels_last: dx[n, h, w, c] = dy[n, c] / HW (C % 8 == 0)
 void global_avgpool_backward(const void* dy, bool fp32, int N, int HW, int C, void* dx, hipStream_t stream);
 

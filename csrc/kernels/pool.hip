@@ -124,8 +124,12 @@ __device__ __forceinline__ int fdiv(int m, int d, float inv, int* r) {
 // four 64-bit integer divisions per element (the ResNet-50 stem's backward: 101 us -> see
 // profiles/r4_final_headline_graph_kernels.txt)
 template <typename T, bool SMALL>
-__global__ __launch_bounds__(kPB) void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ code,
-                                                          T* __restrict__ dx, PoolGeom g, int64_t n_vec) {
+__global__ __launch_bounds__(kPB) void maxpool_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ dy2,
+                                                          const uint8_t* __restrict__ code, T* __restrict__ dx,
+                                                          PoolGeom g, int64_t n_vec) {
+  // dy2 (may be null): a second gradient of the same pooled output (two consumers: the first
+  // bottleneck's main path and shortcut), summed here as autograd's add would -- dy + dy2 per
+  // element, then the window accumulation -- without that add kernel's extra pass
   const int cv = g.C >> 3;
   const float inv_cv = 1.f / (float)cv, inv_w = 1.f / (float)g.W, inv_h = 1.f / (float)g.H;
   for (int64_t i = (int64_t)blockIdx.x * kPB + threadIdx.x; i < n_vec; i += (int64_t)gridDim.x * kPB) {
@@ -160,7 +164,12 @@ __global__ __launch_bounds__(kPB) void maxpool_bwd_kernel(const T* __restrict__ 
 #pragma unroll
         for (int j = 0; j < 8; ++j) any |= ((cw[j >> 2] >> (8 * (j & 3))) & 0xffu) == pos;
         if (!any) continue;
-        const V8 d = ldv(dy + o);
+        V8 d = ldv(dy + o);
+        if (dy2 != nullptr) {
+          const V8 d2 = ldv(dy2 + o);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) d.v[j] = d.v[j] + d2.v[j];
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           if (((cw[j >> 2] >> (8 * (j & 3))) & 0xffu) == pos) acc[j] += d.v[j];
@@ -220,14 +229,14 @@ void global_avgpool_backward(const void* dy, bool fp32, int N, int HW, int C, vo
 }
 
 void maxpool_backward(const void* dy, const uint8_t* code, bool fp32, int N, int H, int W, int C, int OH, int OW,
-                      int k, int s, int pad, void* dx, hipStream_t stream) {
+                      int k, int s, int pad, void* dx, hipStream_t stream, const void* dy2) {
   const PoolGeom g{N, H, W, C, OH, OW, k, s, pad};
   const int64_t n_vec = (int64_t)N * H * W * (C / 8);
   if (n_vec == 0) return;
   const bool small = n_vec < (int64_t(1) << 24);
 #define GRACE_POOL_BWD(T, S)                                                                             \
   hipLaunchKernelGGL((maxpool_bwd_kernel<T, S>), dim3(pool_grid(n_vec)), dim3(kPB), 0, stream,          \
-                     static_cast<const T*>(dy), code, static_cast<T*>(dx), g, n_vec)
+                     static_cast<const T*>(dy), static_cast<const T*>(dy2), code, static_cast<T*>(dx), g, n_vec)
   if (fp32 && small) GRACE_POOL_BWD(float, true);
   else if (fp32) GRACE_POOL_BWD(float, false);
   else if (small) GRACE_POOL_BWD(uint16_t, true);

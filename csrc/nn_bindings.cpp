@@ -380,7 +380,13 @@ std::vector<Tensor> maxpool_fwd(const Tensor& x, int64_t k, int64_t s, int64_t p
   return {y, code};
 }
 
-Tensor maxpool_bwd(const Tensor& dy, const Tensor& code, int64_t H, int64_t W, int64_t k, int64_t s, int64_t pad) {
+Tensor maxpool_bwd(const Tensor& dy, const Tensor& code, int64_t H, int64_t W, int64_t k, int64_t s, int64_t pad,
+                   const c10::optional<Tensor>& dy2) {
+  if (dy2.has_value())
+    TORCH_CHECK(dy2->sizes() == dy.sizes() && dy2->scalar_type() == dy.scalar_type() &&
+                    dy2->is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                    (reinterpret_cast<uintptr_t>(dy2->data_ptr()) & 15) == 0,
+                "maxpool backward: dy2 like dy (channels_last, 16-B aligned)");
   TORCH_CHECK(dy.is_cuda() && dy.dim() == 4 && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
                   (reinterpret_cast<uintptr_t>(dy.data_ptr()) & 15) == 0,
               "maxpool backward: channels_last 16-B aligned grad");
@@ -390,7 +396,8 @@ Tensor maxpool_bwd(const Tensor& dy, const Tensor& code, int64_t H, int64_t W, i
   DevGuard guard(dy.device());
   Tensor dx = at::empty({N, C, H, W}, dy.options(), at::MemoryFormat::ChannelsLast);
   grace::maxpool_backward(dy.data_ptr(), code.data_ptr<uint8_t>(), dy.scalar_type() == at::kFloat, (int)N, (int)H,
-                          (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)pad, dx.data_ptr(), cur_stream());
+                          (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)pad, dx.data_ptr(), cur_stream(),
+                          dy2.has_value() ? dy2->data_ptr() : nullptr);
   return dx;
 }
 
@@ -400,7 +407,8 @@ void grace_bind_nn(py::module& m) {
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("gap_bwd", &gap_bwd);
   m.def("bn_act_pool_fwd", &bn_act_pool_fwd);
-  m.def("maxpool_bwd", &maxpool_bwd);
+  m.def("maxpool_bwd", &maxpool_bwd, py::arg("dy"), py::arg("code"), py::arg("H"), py::arg("W"), py::arg("k"),
+        py::arg("s"), py::arg("pad"), py::arg("dy2") = py::none());
   m.def("bias_act_fwd", &bias_act_fwd);
   m.def("bias_act_bwd", &bias_act_bwd);
   m.def("sgd_step", &sgd_step);

@@ -132,7 +132,9 @@ class ResNet(nn.Module):
 
     def forward(self, x):
         # stem: BN + ReLU + max pool fused (the BN output is never written; ops/bnact.py)
-        x = bn_relu_maxpool(self.conv1(x), self.bn1, self.maxpool)
+        # dual: the first block reads the pooled output twice (main path + shortcut); the two
+        # gradients are summed inside the max-pool backward
+        x = bn_relu_maxpool(self.conv1(x), self.bn1, self.maxpool, dual=True)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         if isinstance(x, tuple):
             x = x[0]

@@ -73,25 +73,51 @@ def side_cu_mask(spec: str, n_cu: int):
     return words
 
 
+_dedicated = {}
+
+
+def dedicated_stream(idx: int, priority: int = 0, role: str = "side") -> "torch.cuda.Stream":
+    """A HIP stream of its own (hipStreamCreateWithPriority), one per (device, priority), kept for
+    the process.  torch.cuda.Stream() hands out streams round-robin from a pool of 32 per
+    priority, so two of them can be the SAME stream: a split capture's main stream once came back
+    as the cached side stream (its second concurrent capture then began on a stream already
+    capturing), and a side stream that aliases the caller's serialises the two graphs.  One
+    stream per (device, priority, role)."""
+    key = (idx, priority, role)
+    s = _dedicated.get(key)
+    if s is None:
+        with _lock:
+            s = _dedicated.get(key)
+            if s is None:
+                from . import _native
+
+                if _native.available():
+                    s = torch.cuda.ExternalStream(_native.lib().create_stream(idx, priority),
+                                                  device=torch.device("cuda", idx))
+                else:
+                    with torch.cuda.device(idx):
+                        s = torch.cuda.Stream(priority=priority)
+                _dedicated[key] = s
+    return s
+
+
 def _side(device: torch.device) -> "torch.cuda.Stream":
     idx = device.index if device.index is not None else torch.cuda.current_device()
     s = _streams.get(idx)
     if s is None:
+        mask = side_cu_mask(os.environ.get("GRACE_SIDE_CUS", ""),
+                            torch.cuda.get_device_properties(idx).multi_processor_count)
         with _lock:
             s = _streams.get(idx)
-            if s is None:
-                mask = side_cu_mask(os.environ.get("GRACE_SIDE_CUS", ""),
-                                    torch.cuda.get_device_properties(idx).multi_processor_count)
-                if mask:  # the side GEMMs may not take the CUs the critical chain needs
-                    from . import _native
+            if s is None and mask:  # the side GEMMs may not take the CUs the critical chain needs
+                from . import _native
 
-                    ptr = _native.lib().create_stream(idx, 0, mask)
-                    s = torch.cuda.ExternalStream(ptr, device=torch.device("cuda", idx))
-                else:
-                    with torch.cuda.device(idx):
-                        # a high-priority side stream measured 20 ms/step (r3_graph_fork_knobs)
-                        s = torch.cuda.Stream(priority=int(os.environ.get("GRACE_SIDE_PRIO", "0")))
-                _streams[idx] = s
+                ptr = _native.lib().create_stream(idx, 0, mask)
+                s = _streams[idx] = torch.cuda.ExternalStream(ptr, device=torch.device("cuda", idx))
+        if s is None:
+            # a stream of its own, never one of torch's pooled streams (see dedicated_stream); a
+            # high-priority side stream measured 20 ms/step (r3_graph_fork_knobs)
+            s = _streams[idx] = dedicated_stream(idx, 0, "side")
     return s
 
 

@@ -188,8 +188,9 @@ class GraphedStep:
         # command processor's dispatch arbitration
         # the caller's stream when given (DDP: the reducer's AccumulateGrad nodes run on the stream
         # the model was wrapped under)
+        # (a dedicated stream: a pooled torch.cuda.Stream() may be the side stream itself)
         main = self._stream_arg if self._stream_arg is not None else \
-            torch.cuda.Stream(dev, priority=int(os.environ.get("GRACE_SPLIT_MAIN_PRIO", "0")))
+            _wg.dedicated_stream(dev, int(os.environ.get("GRACE_SPLIT_MAIN_PRIO", "0")), "split-main")
         side = _wg._side(torch.device("cuda", dev))
         ga, gb, ga2 = _new_graph(), _new_graph(), _new_graph()
         open_ = {"a": False, "b": False, "a2": False}
@@ -271,7 +272,9 @@ class GraphedStep:
             return self._replay_split_on(caller)
         hp = self._hp
         if hp is None:
-            hp = self._hp = torch.cuda.Stream(caller.device, priority=-1)
+            from ..ops import wgrad as _wg
+
+            hp = self._hp = _wg.dedicated_stream(caller.device.index, -1, "split-replay")
         hp.wait_stream(caller)
         with torch.cuda.stream(hp):
             loss = self._replay_split_on(hp)

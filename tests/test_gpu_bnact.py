@@ -334,6 +334,39 @@ def test_bn_relu_maxpool_fused_matches_reference(shape, k, s, p, dtype):
         torch.testing.assert_close(m.bias.grad, b.grad, rtol=5e-2, atol=0.5)
 
 
+def test_bn_relu_maxpool_dual_output_sums_two_consumers_exactly():
+    """dual=True: two aliases of the pooled output for two consumers (the first bottleneck's main
+    path and shortcut); the max-pool backward sums their gradients itself -- bitwise the gradient of
+    the single-output op fed with the autograd sum dy1 + dy2."""
+    from grace_amd.ops.bnact import bn_relu_maxpool
+    from grace_amd.ops.pool import MaxPool2dNHWC
+
+    m, x, _, _ = _case(4, 64, 56, 56, relu=True, with_res=False, seed=5, dtype=torch.float32)
+    pool = MaxPool2dNHWC(3, 2, 1)
+    g = torch.Generator(device="cpu").manual_seed(9)
+    shape = (4, 64, 28, 28)
+    d1 = torch.randn(shape, generator=g).to(DEV).contiguous(memory_format=torch.channels_last)
+    d2 = torch.randn(shape, generator=g).to(DEV).contiguous(memory_format=torch.channels_last)
+    xa = x.detach().clone().requires_grad_(True)
+    ya, yb = bn_relu_maxpool(xa, m, pool, dual=True)
+    assert ya.data_ptr() == yb.data_ptr()
+    torch.autograd.backward([ya, yb], [d1, d2])
+    ga, wa = xa.grad.clone(), m.weight.grad.clone()
+    m.weight.grad = None
+    m.bias.grad = None
+    xs = x.detach().clone().requires_grad_(True)
+    y = bn_relu_maxpool(xs, m, pool)
+    y.backward(d1 + d2)
+    assert torch.equal(ga, xs.grad)
+    torch.testing.assert_close(wa, m.weight.grad, rtol=0, atol=0)
+    xo = x.detach().clone().requires_grad_(True)  # one consumer with a gradient, the other none
+    y1, _ = bn_relu_maxpool(xo, m, pool, dual=True)
+    y1.backward(d1)
+    xp = x.detach().clone().requires_grad_(True)
+    bn_relu_maxpool(xp, m, pool).backward(d1)
+    assert torch.equal(xo.grad, xp.grad)
+
+
 @pytest.fixture
 def atomic_bn():
     prev = _native.lib().bn_atomic_chunks()
