@@ -426,8 +426,10 @@ def main() -> int:
     # split graphs (critical stream A / side stream B / A2; see the capture below) unless the step
     # overlaps its exchange with backward or DDP's hook runs immediately
     ddp_defer = args.ddp_defer == "on" or (args.ddp_defer == "auto" and mode == "full")
-    split_planned = mode == "full" and (args.graph_split == "on" or (
-        args.graph_split == "auto" and not overlap and not (args.surface == "ddp" and not ddp_defer)))
+    # (never with overlap or an immediate DDP hook, --graph-split on included: the side stream must
+    # then be joined on the capture stream after backward)
+    split_planned = (mode == "full" and args.graph_split != "off" and not overlap
+                     and not (args.surface == "ddp" and not ddp_defer))
     main_stream = None
     if split_planned:
         # A and B must sit on DIFFERENT hardware queues: HIP deals streams of one priority to a few
