@@ -223,7 +223,7 @@ class PowerSGDCompressor(BucketCompressor):
         """(base tensor, plan) of one Q = M^T P launch over every bucket of the arena: each
         matrix's x offset is taken relative to the lowest bucket address (the buckets are separate
         allocations of one device; the kernel addresses them from that base).  None when it does
-        not apply (one bucket, CPU, misaligned or mixed-device buffers)."""
+        not apply (CPU, misaligned or mixed-device buffers)."""
         xs = [x for _, x, _ in entries]
         if not all(PS._native.use_native(x) and x.dtype == torch.float32 and x.is_contiguous()
                    and x.device == xs[0].device for x in xs):
